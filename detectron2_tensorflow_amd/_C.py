@@ -1,0 +1,158 @@
+"""ctypes binding of libd2mi_hip.so (the C ABI declared in include/d2mi.h).
+
+The library is built in-tree (``detectron2_tensorflow_amd/_build.py``) and is
+the only compute path of the hot ops: if it cannot be loaded, every op raises
+(there is no CPU or eager fallback).  torch is imported first so that the HIP
+runtime torch ships (``libamdhip64.so.7``) is the one the library binds to;
+device pointers and ``hipStream_t`` handles are passed straight from torch.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libd2mi_hip.so")
+
+_lib = None
+_load_error = None
+
+c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+P = c_void_p  # device or host pointer
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "d2mi_version": (c_int, []),
+    "d2mi_last_error": (c_char_p, []),
+    "d2mi_error_word_dev": (c_void_p, []),
+    "d2mi_clear_errors": (c_int, [P]),
+    "d2mi_roi_align_fwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "d2mi_roi_align_bwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_nms_workspace_size": (c_size_t, [c_int, c_int]),
+    "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
+    "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),
+    "d2mi_topk": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, c_size_t, P]),
+    "d2mi_grid_anchors": (c_int, [c_int, c_int, c_float, P, c_int, P, P]),
+    "d2mi_apply_deltas": (c_int, [P, P, c_int, c_int, P, c_float, P, P]),
+    "d2mi_rpn_proposals_workspace_size": (c_size_t, [c_int, c_int, P, c_int, c_int, c_int]),
+    "d2mi_rpn_proposals": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int, c_float,
+                                   c_float, P, c_float, P, P, P, P, c_size_t, P]),
+    "d2mi_fast_rcnn_workspace_size": (c_size_t, [c_int, c_int, c_int, c_float, c_int]),
+    "d2mi_fast_rcnn_inference": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P,
+                                         c_float, c_float, c_float, c_int, P, P, P, P, P, P,
+                                         c_size_t, P]),
+    "d2mi_retinanet_workspace_size": (c_size_t, [c_int, c_int, P, c_int, c_int, c_int]),
+    "d2mi_retinanet_inference": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float,
+                                         c_float, c_int, P, c_float, P, P, P, P, P, c_size_t, P]),
+    "d2mi_matrix_nms_workspace_size": (c_size_t, [c_int]),
+    "d2mi_matrix_nms": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, P, P, c_size_t, P]),
+    "d2mi_conv_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_int, c_int, c_int, P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class D2MIError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load the library (idempotent).  Raises if it is missing or incomplete."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        _load_error = f"{path} not found; run detectron2_tensorflow_amd._build.build()"
+        raise D2MIError(_load_error)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)  # AttributeError if the export is missing
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def last_error():
+    msg = lib().d2mi_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc, what):
+    if rc != 0:
+        raise D2MIError(f"{what} failed (rc={rc}): {last_error()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise ValueError(
+                "detectron2_tensorflow_amd hot-path ops run on the MI355X only: "
+                f"got a tensor on {t.device}")
+
+
+def host_array(ctype, values):
+    arr = (ctype * len(values))(*values)
+    return arr
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+_ERR_BITS = {1: "box index out of range", 2: "NMS candidate capacity exceeded",
+             4: "top-k candidate capacity exceeded"}
+
+
+def error_word(device=None):
+    """Read (synchronising) and decode the device error word."""
+    addr = lib().d2mi_error_word_dev()
+    if not addr:
+        raise D2MIError("cannot resolve the device error word")
+    host = ctypes.c_int32(0)
+    torch.cuda.synchronize(device)
+    # hipMemcpy through torch: wrap the raw device int in a 1-element tensor view
+    buf = torch.empty(1, dtype=torch.int32, device=device or "cuda")
+    _copy_word(addr, buf)
+    v = int(buf.item())
+    return v, [m for b, m in _ERR_BITS.items() if v & b]
+
+
+def _copy_word(addr, dst):
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [c_void_p, c_void_p, c_size_t, c_int]
+    rc = hip.hipMemcpy(c_void_p(dst.data_ptr()), c_void_p(addr), 4, 3)  # DeviceToDevice
+    if rc != 0:
+        raise D2MIError(f"hipMemcpy of the error word failed ({rc})")
+
+
+def clear_errors(device=None):
+    check(lib().d2mi_clear_errors(stream_of(device)), "d2mi_clear_errors")
+
+
+def raise_on_errors(device=None):
+    v, msgs = error_word(device)
+    if v:
+        clear_errors(device)
+        raise D2MIError("device-side error(s): " + ", ".join(msgs))

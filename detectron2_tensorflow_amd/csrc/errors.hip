@@ -1,0 +1,44 @@
+// Thread-local host error string + the device error word (see include/d2mi.h).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+namespace {
+thread_local char g_msg[1024] = "";
+__device__ int32_t g_error_word = 0;
+}  // namespace
+
+namespace d2mi {
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_msg, sizeof(g_msg), fmt, ap);
+  va_end(ap);
+}
+
+int32_t* error_word() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_error_word)) != hipSuccess) return nullptr;
+  return (int32_t*)p;
+}
+
+}  // namespace d2mi
+
+extern "C" {
+
+int d2mi_version(void) { return 1; }
+
+const char* d2mi_last_error(void) { return g_msg; }
+
+int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }
+
+int d2mi_clear_errors(void* stream) {
+  int32_t* w = d2mi::error_word();
+  D2MI_REQUIRE(w != nullptr, "cannot resolve the device error word");
+  D2MI_HIP(hipMemsetAsync(w, 0, sizeof(int32_t), d2mi::as_stream(stream)));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// Library-internal host APIs shared between translation units.
+#pragma once
+#include "common.h"
+
+namespace d2mi {
+
+// Segmented ascending sort of 64-bit keys stored in "capacity layout":
+// segment s owns keys[s*cap, s*cap + lens[s]).  Keys beyond lens[s] are
+// ignored.  cap <= kLdsSortCap uses the in-LDS bitonic kernel, larger
+// capacities go through rocPRIM's segmented radix sort.
+constexpr int kLdsSortCap = 8192;
+size_t sort_workspace_size(int S, int cap);
+int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* lens, int S,
+                        int cap, void* ws, size_t ws_bytes, hipStream_t stream);
+
+// Greedy NMS core over candidates already in capacity layout.
+//   keys   [S*cap] sort keys (desc_key(score, local idx)); lens [S]
+//   boxes  candidate boxes; candidate i of segment s is at
+//          boxes[(box_off ? box_off[s] : s*cap) + i]
+//   keep   [S*max_out] local candidate indices, -1 padded; num_keep [S]
+size_t nms_core_workspace_size(int S, int cap);
+int nms_core(const uint64_t* keys, const int32_t* lens, const float4* boxes,
+             const int32_t* box_off, int S, int cap, int max_out, float iou_thr, int32_t* keep,
+             int32_t* num_keep, void* ws, size_t ws_bytes, hipStream_t stream);
+
+// Mask + scan only, over candidates already sorted and gathered in capacity
+// layout: sboxes[s*cap + i] (boxes used for IoU, e.g. class-offset boxes),
+// sidx[s*cap + i] (the value written to keep for that candidate), count[s]
+// selectable candidates.
+size_t nms_sorted_workspace_size(int S, int cap);
+int nms_sorted(const float4* sboxes, const int32_t* sidx, const int32_t* count, int S, int cap,
+               int max_out, float iou_thr, int32_t* keep, int32_t* num_keep, void* ws,
+               size_t ws_bytes, hipStream_t stream);
+
+// Exact segmented top-k (value desc, index asc).  See d2mi_topk.
+size_t topk_workspace_size(int S, int k);
+int topk_core(const float* values, const int64_t* seg_start, const int32_t* seg_len, int S,
+              int max_len, int k, int key_mode, float* vals_out, int32_t* idx_out,
+              int32_t* count_out, void* ws, size_t ws_bytes, hipStream_t stream);
+// seg_k (device, nullable): per-segment k limit (effective k = min(k, seg_k[s], len)).
+int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* seg_len,
+                 const int32_t* seg_k, int S, int max_len, int k, int key_mode, float* vals_out,
+                 int32_t* idx_out, int32_t* count_out, void* ws, size_t ws_bytes,
+                 hipStream_t stream);
+
+}  // namespace d2mi

@@ -1,0 +1,101 @@
+// Segmented sort of 64-bit (score, index) keys.
+// Small segments (<= 8192 keys: RPN levels, RetinaNet candidates, NMS inputs)
+// are sorted by one 1024-thread workgroup per segment with an in-LDS bitonic
+// network (64 KiB of keys); larger capacities fall back to rocPRIM's
+// segmented radix sort.
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include "internal.h"
+
+namespace d2mi {
+namespace {
+
+__global__ __launch_bounds__(1024) void bitonic_lds_kernel(const uint64_t* __restrict__ in,
+                                                           uint64_t* __restrict__ out,
+                                                           const int32_t* __restrict__ lens,
+                                                           int cap) {
+  extern __shared__ uint64_t s[];
+  const int seg = blockIdx.x;
+  const int len = min(lens[seg], cap);
+  int n = 1;
+  while (n < len) n <<= 1;
+  const uint64_t* src = in + (size_t)seg * cap;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = i < len ? src[i] : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = s[i], b = s[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            s[i] = b;
+            s[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  uint64_t* dst = out + (size_t)seg * cap;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) dst[i] = s[i];
+}
+
+__global__ void seg_bounds_kernel(const int32_t* lens, int S, int cap, int* begin, int* end) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < S) {
+    begin[s] = s * cap;
+    end[s] = s * cap + min(lens[s], cap);
+  }
+}
+
+size_t rocprim_tmp_bytes(int S, int cap) {
+  size_t bytes = 0;
+  rocprim::segmented_radix_sort_keys((void*)nullptr, bytes, (const uint64_t*)nullptr,
+                                     (uint64_t*)nullptr, (unsigned int)((size_t)S * cap),
+                                     (unsigned int)S, (const int*)nullptr, (const int*)nullptr,
+                                     0u, 64u, (hipStream_t)0, false);
+  return bytes;
+}
+
+}  // namespace
+
+size_t sort_workspace_size(int S, int cap) {
+  if (cap <= kLdsSortCap) return 0;
+  WorkspaceSizer z;
+  z.take<int>(S);
+  z.take<int>(S);
+  z.take<char>(rocprim_tmp_bytes(S, cap));
+  return z.off;
+}
+
+int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* lens, int S,
+                        int cap, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (S == 0 || cap == 0) return 0;
+  if (cap <= kLdsSortCap) {
+    int n = 1;
+    while (n < cap) n <<= 1;
+    const int threads = n >= 1024 ? 1024 : (n < 64 ? 64 : n);
+    hipLaunchKernelGGL(bitonic_lds_kernel, dim3(S), dim3(threads), n * sizeof(uint64_t), stream,
+                       keys_in, keys_out, lens, cap);
+    D2MI_LAUNCH_CHECK();
+    return 0;
+  }
+  Workspace w(ws, ws_bytes);
+  int* begin = w.take<int>(S);
+  int* end = w.take<int>(S);
+  size_t tmp_bytes = rocprim_tmp_bytes(S, cap);
+  void* tmp = w.take<char>(tmp_bytes);
+  D2MI_REQUIRE(w.ok(), "sort workspace too small (%zu < %zu)", ws_bytes, w.off);
+  hipLaunchKernelGGL(seg_bounds_kernel, dim3((S + 255) / 256), dim3(256), 0, stream, lens, S, cap,
+                     begin, end);
+  D2MI_LAUNCH_CHECK();
+  D2MI_HIP(rocprim::segmented_radix_sort_keys(tmp, tmp_bytes, keys_in, keys_out,
+                                              (unsigned int)((size_t)S * cap), (unsigned int)S,
+                                              (const int*)begin, (const int*)end, 0u, 64u, stream,
+                                              false));
+  return 0;
+}
+
+}  // namespace d2mi

@@ -1,0 +1,345 @@
+"""torch-facing wrappers of the libd2mi_hip.so hot-path kernels.
+
+Every function here launches hand-written HIP on torch's current stream and
+raises if the library is missing or a tensor is not on the GPU: there is no
+CPU/eager fallback for the hot path.  Shapes and argument meaning follow the
+reference op they replace (cited per function).
+"""
+import math
+
+import torch
+
+from .. import _C
+
+_DEFAULT_SCALE_CLAMP = math.log(1000.0 / 16)  # lib/modeling/box_regression.py:10
+
+BOX_MODE_RAW, BOX_MODE_ALIGNED, BOX_MODE_UNALIGNED = 0, 1, 2
+
+
+def _f32c(t):
+    return t.to(torch.float32).contiguous()
+
+
+def _i32c(t):
+    return t.to(torch.int32).contiguous()
+
+
+# ------------------------------------------------------------------ ROIAlign
+class _RoIAlignFn(torch.autograd.Function):
+    """ROIAlign forward/backward over 1..8 feature levels.  Boxes carry no
+    gradient (crop_and_resize stop_gradient, lib/layers/functional.py:120)."""
+
+    @staticmethod
+    def forward(ctx, boxes, box_ind, params, *feats):
+        feats = [_f32c(f) for f in feats]
+        boxes = _f32c(boxes)
+        box_ind = _i32c(box_ind)
+        _C.require_device(boxes, box_ind, *feats)
+        (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
+         want_level) = params
+        L = len(feats)
+        C = feats[0].shape[-1]
+        R = boxes.shape[0]
+        out = torch.empty((R, out_h, out_w, C), dtype=torch.float32, device=boxes.device)
+        level = torch.empty((R,), dtype=torch.int32, device=boxes.device) if want_level else None
+        fp = _C.host_array(_C.c_void_p, [f.data_ptr() for f in feats])
+        dims = _C.host_array(_C.ctypes.c_int32,
+                             [v for f in feats for v in (f.shape[0], f.shape[1], f.shape[2])])
+        sc = _C.host_array(_C.c_float, list(scales))
+        rc = _C.lib().d2mi_roi_align_fwd(fp, dims, sc, L, C, _C.ptr(boxes), _C.ptr(box_ind), R,
+                                         out_h, out_w, sr, mode, pad, assign, min_l, max_l,
+                                         canon_s, canon_l, _C.ptr(level), _C.ptr(out),
+                                         _C.stream_of(boxes.device))
+        _C.check(rc, "d2mi_roi_align_fwd")
+        ctx.params = params
+        ctx.shapes = [f.shape for f in feats]
+        ctx.save_for_backward(boxes, box_ind)
+        if level is not None:
+            ctx.mark_non_differentiable(level)
+        return out, level
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_level):
+        boxes, box_ind = ctx.saved_tensors
+        (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
+         _) = ctx.params
+        grads = [torch.zeros(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
+        g = _f32c(grad_out)
+        gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
+        dims = _C.host_array(_C.ctypes.c_int32, [v for s in ctx.shapes for v in (s[0], s[1], s[2])])
+        sc = _C.host_array(_C.c_float, list(scales))
+        rc = _C.lib().d2mi_roi_align_bwd(gp, dims, sc, len(grads), ctx.shapes[0][-1],
+                                         _C.ptr(boxes), _C.ptr(box_ind), boxes.shape[0], out_h,
+                                         out_w, sr, mode, pad, assign, min_l, max_l, canon_s,
+                                         canon_l, _C.ptr(g), _C.stream_of(boxes.device))
+        _C.check(rc, "d2mi_roi_align_bwd")
+        return (None, None, None, *grads)
+
+
+def roi_align(features, boxes, box_ind, output_size, scales, sampling_ratio=0, aligned=True,
+              pad_border=True, assign_levels=True, min_level=None, max_level=None,
+              canonical_box_size=224, canonical_level=4, return_levels=False,
+              box_mode=None):
+    """Multi-level ROIAlign (poolers.py:134-180 + roi_align.py:45-66 +
+    functional.py:100-166) in one launch; output rows in input order."""
+    if not isinstance(features, (list, tuple)):
+        features = [features]
+    L = len(features)
+    if min_level is None:
+        min_level = int(round(-math.log2(scales[0]))) if L > 1 else 0
+        max_level = int(round(-math.log2(scales[-1]))) if L > 1 else 0
+    if box_mode is None:
+        box_mode = BOX_MODE_ALIGNED if aligned else BOX_MODE_UNALIGNED
+    oh, ow = (output_size, output_size) if isinstance(output_size, int) else output_size
+    params = (int(oh), int(ow), tuple(float(s) for s in scales), int(sampling_ratio),
+              int(box_mode), int(bool(pad_border)), int(bool(assign_levels and L > 1)),
+              int(min_level), int(max_level), int(canonical_box_size), int(canonical_level),
+              bool(return_levels))
+    out, level = _RoIAlignFn.apply(boxes, box_ind, params, *features)
+    return (out, level) if return_levels else out
+
+
+# ----------------------------------------------------------------------- NMS
+def nms_segments(boxes, scores, seg_offsets, max_output_size, iou_threshold, seg_capacity=None):
+    """Segmented TF NonMaxSuppressionV3.  boxes [T,4], scores [T], seg_offsets
+    int [S+1] (device).  Returns keep [S, max_out] int32 (segment-relative,
+    -1 padded) and num_keep [S] int32."""
+    if not 0.0 <= float(iou_threshold) <= 1.0:
+        raise ValueError("iou_threshold must be in [0, 1], got %r" % (iou_threshold,))
+    if max_output_size < 0:
+        raise ValueError("max_output_size must be non-negative, got %r" % (max_output_size,))
+    boxes, scores, seg_offsets = _f32c(boxes), _f32c(scores), _i32c(seg_offsets)
+    _C.require_device(boxes, scores, seg_offsets)
+    S = seg_offsets.shape[0] - 1
+    if seg_capacity is None:
+        seg_capacity = int(boxes.shape[0])
+    dev = boxes.device
+    keep = torch.empty((S, max(int(max_output_size), 1)), dtype=torch.int32, device=dev)
+    num = torch.empty((S,), dtype=torch.int32, device=dev)
+    wsb = _C.lib().d2mi_nms_workspace_size(S, int(seg_capacity))
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_nms(_C.ptr(boxes), _C.ptr(scores), _C.ptr(seg_offsets), S,
+                           int(seg_capacity), int(max_output_size), float(iou_threshold),
+                           _C.ptr(keep), _C.ptr(num), _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_nms")
+    return keep[:, :max_output_size], num
+
+
+def non_max_suppression(boxes, scores, max_output_size, iou_threshold=0.5):
+    """tf.image.non_max_suppression: selected indices (int32, selection order)."""
+    n = boxes.shape[0]
+    off = torch.tensor([0, n], dtype=torch.int32, device=boxes.device)
+    keep, num = nms_segments(boxes, scores, off, max_output_size, iou_threshold, seg_capacity=n)
+    return keep[0, : int(num[0].item())]
+
+
+# --------------------------------------------------------------------- top-k
+def topk_segments(values, seg_start, seg_len, k, max_seg_len, sigmoid=False):
+    """Exact segmented top-k (tf.nn.top_k sorted=True order)."""
+    values = _f32c(values)
+    seg_start = seg_start.to(torch.int64).contiguous()
+    seg_len = _i32c(seg_len)
+    _C.require_device(values, seg_start, seg_len)
+    S = seg_len.shape[0]
+    dev = values.device
+    vals = torch.empty((S, max(k, 1)), dtype=torch.float32, device=dev)
+    idx = torch.empty((S, max(k, 1)), dtype=torch.int32, device=dev)
+    cnt = torch.empty((S,), dtype=torch.int32, device=dev)
+    wsb = _C.lib().d2mi_topk_workspace_size(S, k)
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_topk(_C.ptr(values), _C.ptr(seg_start), _C.ptr(seg_len), S,
+                            int(max_seg_len), int(k), int(bool(sigmoid)), _C.ptr(vals),
+                            _C.ptr(idx), _C.ptr(cnt), _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_topk")
+    return vals[:, :k], idx[:, :k], cnt
+
+
+# ------------------------------------------------------------ anchors/deltas
+def grid_anchors(H, W, stride, cell_anchors, device):
+    """DefaultAnchorGenerator.grid_anchors for one level -> [H*W*A, 4]."""
+    cell = [float(v) for v in torch.as_tensor(cell_anchors, dtype=torch.float32).reshape(-1)]
+    A = len(cell) // 4
+    out = torch.empty((H * W * A, 4), dtype=torch.float32, device=device)
+    rc = _C.lib().d2mi_grid_anchors(int(H), int(W), float(stride),
+                                    _C.host_array(_C.c_float, cell), A, _C.ptr(out),
+                                    _C.stream_of(device))
+    _C.check(rc, "d2mi_grid_anchors")
+    return out
+
+
+def apply_deltas(deltas, boxes, weights, scale_clamp=_DEFAULT_SCALE_CLAMP):
+    """Box2BoxTransform.apply_deltas: deltas [N, K*4], boxes [N, 4]."""
+    deltas, boxes = _f32c(deltas), _f32c(boxes)
+    _C.require_device(deltas, boxes)
+    N = boxes.shape[0]
+    K = deltas.shape[1] // 4
+    out = torch.empty_like(deltas)
+    if N == 0:
+        return out
+    rc = _C.lib().d2mi_apply_deltas(_C.ptr(deltas), _C.ptr(boxes), N, K,
+                                    _C.host_array(_C.c_float, [float(w) for w in weights]),
+                                    float(scale_clamp), _C.ptr(out), _C.stream_of(boxes.device))
+    _C.check(rc, "d2mi_apply_deltas")
+    return out
+
+
+# -------------------------------------------------------------------- convs
+def pack_conv_weights(w_hwio):
+    """HWIO -> [KH, KW, Cout, Cin] for d2mi_conv2d_nhwc."""
+    w = _f32c(w_hwio)
+    _C.require_device(w)
+    KH, KW, Cin, Cout = w.shape
+    out = torch.empty((KH, KW, Cout, Cin), dtype=torch.float32, device=w.device)
+    rc = _C.lib().d2mi_conv_pack_weights(_C.ptr(w), KH, KW, Cin, Cout, _C.ptr(out),
+                                         _C.stream_of(w.device))
+    _C.check(rc, "d2mi_conv_pack_weights")
+    return out
+
+
+def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
+                residual=None):
+    """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin]."""
+    x = _f32c(x)
+    _C.require_device(x, w_packed)
+    N, H, W, Cin = x.shape
+    KH, KW, Cout, Cin2 = w_packed.shape
+    if Cin != Cin2:
+        raise ValueError(f"conv input has {Cin} channels, weights expect {Cin2}")
+    pb, pe = pad
+    OH = (H + pb + pe - KH) // stride + 1
+    OW = (W + pb + pe - KW) // stride + 1
+    y = torch.empty((N, OH, OW, Cout), dtype=torch.float32, device=x.device)
+    if topdown is not None:
+        topdown = _f32c(topdown)
+        if topdown.shape != (N, (OH + 1) // 2, (OW + 1) // 2, Cout):
+            raise ValueError(f"top-down map {tuple(topdown.shape)} does not upsample to "
+                             f"{(N, OH, OW, Cout)}")
+    if residual is not None:
+        residual = _f32c(residual)
+    rc = _C.lib().d2mi_conv2d_nhwc(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias), _C.ptr(topdown),
+                                   _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
+                                   int(stride), int(pb), int(pe), int(bool(relu)),
+                                   _C.stream_of(x.device))
+    _C.check(rc, "d2mi_conv2d_nhwc")
+    return y
+
+
+# -------------------------------------------------------------- matrix NMS
+def matrix_nms_scores(masks, classes, scores, sum_masks=None, kernel="gaussian", sigma=2.0):
+    if kernel not in ("gaussian", "linear"):
+        raise NotImplementedError(f"NMS kernel {kernel} not implemented yet.")
+    M = masks.shape[0]
+    masks2 = _f32c(masks.reshape(M, -1))
+    classes = classes.to(torch.int64).contiguous()
+    scores = _f32c(scores)
+    _C.require_device(masks2, classes, scores)
+    sm = _f32c(sum_masks) if sum_masks is not None else None
+    out = torch.empty_like(scores)
+    wsb = _C.lib().d2mi_matrix_nms_workspace_size(M)
+    ws = _C.workspace(wsb, masks.device)
+    rc = _C.lib().d2mi_matrix_nms(_C.ptr(masks2), _C.ptr(classes), _C.ptr(scores), _C.ptr(sm), M,
+                                  masks2.shape[1], 0 if kernel == "gaussian" else 1, float(sigma),
+                                  _C.ptr(out), _C.ptr(ws), wsb, _C.stream_of(masks.device))
+    _C.check(rc, "d2mi_matrix_nms")
+    return out
+
+
+# ------------------------------------------------------- fused post-processing
+def _level_arrays(tensors, hw, strides, cell_anchors):
+    L = len(tensors)
+    ptrs = _C.host_array(_C.c_void_p, [t.data_ptr() for t in tensors])
+    lhw = _C.host_array(_C.ctypes.c_int32, [v for h, w in hw for v in (int(h), int(w))])
+    st = _C.host_array(_C.c_float, [float(s) for s in strides])
+    cells = [float(v) for c in cell_anchors for v in torch.as_tensor(c, dtype=torch.float32).reshape(-1)]
+    A = len(cells) // (4 * L)
+    return ptrs, lhw, st, _C.host_array(_C.c_float, cells), A
+
+
+def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk, post_nms_topk,
+                  nms_thresh, min_box_side_len=0.0, weights=(1.0, 1.0, 1.0, 1.0),
+                  scale_clamp=_DEFAULT_SCALE_CLAMP):
+    """find_top_rpn_proposals (rpn_outputs.py:29-132) fused with anchor
+    generation and decode.  logits[l] [N,H,W,A], deltas[l] [N,H,W,A*4]."""
+    logits = [_f32c(t) for t in logits]
+    deltas = [_f32c(t) for t in deltas]
+    image_hw = _i32c(image_hw)
+    _C.require_device(image_hw, *logits, *deltas)
+    N = logits[0].shape[0]
+    L = len(logits)
+    hw = [(t.shape[1], t.shape[2]) for t in logits]
+    lp, lhw, st, cells, A = _level_arrays(logits, hw, strides, cell_anchors)
+    dp = _C.host_array(_C.c_void_p, [t.data_ptr() for t in deltas])
+    dev = logits[0].device
+    ob = torch.empty((N, post_nms_topk, 4), dtype=torch.float32, device=dev)
+    os_ = torch.empty((N, post_nms_topk), dtype=torch.float32, device=dev)
+    ov = torch.empty((N, post_nms_topk), dtype=torch.uint8, device=dev)
+    wsb = _C.lib().d2mi_rpn_proposals_workspace_size(N, L, lhw, A, pre_nms_topk, post_nms_topk)
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_rpn_proposals(lp, dp, lhw, st, cells, L, A, N, _C.ptr(image_hw),
+                                     int(pre_nms_topk), int(post_nms_topk), float(nms_thresh),
+                                     float(min_box_side_len),
+                                     _C.host_array(_C.c_float, [float(w) for w in weights]),
+                                     float(scale_clamp), _C.ptr(ob), _C.ptr(os_), _C.ptr(ov),
+                                     _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_rpn_proposals")
+    return ob, os_, ov.bool()
+
+
+def fast_rcnn_inference(logits, deltas, proposals, roi_img, roi_slot, num_images, P, image_hw,
+                        weights, score_thresh, nms_thresh, topk_per_image,
+                        cls_agnostic=False, scale_clamp=_DEFAULT_SCALE_CLAMP):
+    """FastRCNNOutputs.inference + fast_rcnn_inference (fast_rcnn.py:28-187,
+    :359-395): softmax, decode, clip, threshold, class-offset NMS, pad."""
+    logits, deltas, proposals = _f32c(logits), _f32c(deltas), _f32c(proposals)
+    roi_img, roi_slot, image_hw = _i32c(roi_img), _i32c(roi_slot), _i32c(image_hw)
+    _C.require_device(logits, deltas, proposals, roi_img, roi_slot, image_hw)
+    R, K1 = logits.shape
+    K = K1 - 1
+    N = int(num_images)
+    dev = logits.device
+    ob = torch.empty((N, topk_per_image, 4), dtype=torch.float32, device=dev)
+    os_ = torch.empty((N, topk_per_image), dtype=torch.float32, device=dev)
+    oc = torch.empty((N, topk_per_image), dtype=torch.int64, device=dev)
+    ov = torch.empty((N, topk_per_image), dtype=torch.uint8, device=dev)
+    oroi = torch.empty((N, topk_per_image), dtype=torch.int32, device=dev)
+    wsb = _C.lib().d2mi_fast_rcnn_workspace_size(N, int(P), K, float(score_thresh),
+                                                 int(topk_per_image))
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_fast_rcnn_inference(
+        _C.ptr(logits), _C.ptr(deltas), _C.ptr(proposals), _C.ptr(roi_img), _C.ptr(roi_slot), R,
+        N, int(P), K, int(bool(cls_agnostic)), _C.ptr(image_hw),
+        _C.host_array(_C.c_float, [float(w) for w in weights]), float(scale_clamp),
+        float(score_thresh), float(nms_thresh), int(topk_per_image), _C.ptr(ob), _C.ptr(os_),
+        _C.ptr(oc), _C.ptr(ov), _C.ptr(oroi), _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_fast_rcnn_inference")
+    return ob, os_, oc, ov.bool(), oroi
+
+
+def retinanet_inference(box_cls, box_delta, strides, cell_anchors, num_classes, topk_candidates,
+                        score_threshold, nms_threshold, max_detections,
+                        weights=(1.0, 1.0, 1.0, 1.0), scale_clamp=_DEFAULT_SCALE_CLAMP):
+    """RetinaNetHead.inference (retinanet.py:285-387).  box_cls[l] [N,H,W,A*K],
+    box_delta[l] [N,H,W,A*4]."""
+    box_cls = [_f32c(t) for t in box_cls]
+    box_delta = [_f32c(t) for t in box_delta]
+    _C.require_device(*box_cls, *box_delta)
+    N = box_cls[0].shape[0]
+    L = len(box_cls)
+    hw = [(t.shape[1], t.shape[2]) for t in box_cls]
+    cp, lhw, st, cells, A = _level_arrays(box_cls, hw, strides, cell_anchors)
+    bp = _C.host_array(_C.c_void_p, [t.data_ptr() for t in box_delta])
+    dev = box_cls[0].device
+    ob = torch.empty((N, max_detections, 4), dtype=torch.float32, device=dev)
+    os_ = torch.empty((N, max_detections), dtype=torch.float32, device=dev)
+    oc = torch.empty((N, max_detections), dtype=torch.int32, device=dev)
+    ov = torch.empty((N, max_detections), dtype=torch.uint8, device=dev)
+    wsb = _C.lib().d2mi_retinanet_workspace_size(N, L, lhw, A, int(num_classes),
+                                                 int(topk_candidates))
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_retinanet_inference(
+        cp, bp, lhw, st, cells, L, A, int(num_classes), N, int(topk_candidates),
+        float(score_threshold), float(nms_threshold), int(max_detections),
+        _C.host_array(_C.c_float, [float(w) for w in weights]), float(scale_clamp), _C.ptr(ob),
+        _C.ptr(os_), _C.ptr(oc), _C.ptr(ov), _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_retinanet_inference")
+    return ob, os_, oc, ov.bool()

@@ -1,0 +1,220 @@
+/*
+ * d2mi.h — C ABI of libd2mi_hip.so, the MI355X (gfx950) hot path of the
+ * detection stack (ROIAlign, batched greedy NMS, anchor/top-k/decode, FPN convs).
+ *
+ * Every entry point replaces a TensorFlow kernel (or a Python glue function
+ * around one) that SimeonZhang/detectron2_tensorflow calls; the replaced
+ * reference interface is cited above each declaration as path:line into the
+ * reference tree.
+ *
+ * Conventions (all functions):
+ *   - return 0 on success, a negative value on a host-detected argument error
+ *     (message in d2mi_last_error(), thread-local);
+ *   - every pointer argument named *_dev / listed as "device" is a device
+ *     pointer owned by the CALLER (PyTorch allocates inputs, outputs and
+ *     workspace; the library never hipMallocs); host arrays are plain host
+ *     memory read during the call only;
+ *   - `stream` is a hipStream_t passed as void* (torch's current stream);
+ *     nothing synchronises, so every call is graph-capturable;
+ *   - layouts follow the reference: NHWC activations, HWIO conv weights,
+ *     boxes [ymin, xmin, ymax, xmax] (yxyx) in absolute pixels, deltas
+ *     (dy, dx, dh, dw) — lib/data/fields.py, lib/layers/convolutional.py:175,
+ *     lib/modeling/box_regression.py:53-73.
+ *   - run-time data errors the reference raises inside a TF kernel (e.g.
+ *     box_ind out of range in CropAndResize) are recorded in a device error
+ *     word; d2mi_error_word_dev() returns it so the host can check lazily
+ *     without a synchronisation on every call.
+ */
+#ifndef D2MI_H
+#define D2MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define D2MI_MAX_LEVELS 8
+
+/* ------------------------------------------------------------------ misc */
+int d2mi_version(void);
+const char* d2mi_last_error(void);
+/* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
+ * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
+int32_t* d2mi_error_word_dev(void);
+int d2mi_clear_errors(void* stream);
+
+/* -------------------------------------------------------------- ROIAlign
+ * Multi-level ROIAlign / crop_and_resize, one launch for all levels.
+ * Replaces:
+ *   lib/layers/roi_align.py:45-66       ROIAlign.call (scale, SR crop, avg_pool)
+ *   lib/layers/functional.py:100-166    crop_and_resize (SYMMETRIC pad + box transform
+ *                                        + tf.image.crop_and_resize bilinear)
+ *   lib/modeling/poolers.py:11-49       assign_boxes_to_levels (when num_levels > 1)
+ *   lib/modeling/poolers.py:134-180     ROIPooler.call (gather/concat/invert_permutation:
+ *                                        output is written directly in input order)
+ * feats[l]      device NHWC float [N, H_l, W_l, C] (C equal over levels)
+ * dims          host int32 [num_levels][3] = (N, H_l, W_l)
+ * scales        host float [num_levels] spatial_scale per level (1/stride)
+ * boxes         device float [R,4] yxyx, image pixels (before spatial_scale)
+ * box_ind       device int32 [R] image index of each box
+ * box_mode      0 = raw normalised boxes (tf.image.crop_and_resize),
+ *               1 = aligned fpcoor (ROIAlignV2), 2 = unaligned fpcoor (ROIAlign)
+ * assign        1: level per box by the FPN heuristic (min_level..max_level,
+ *               canonical_box_size, canonical_level); 0: every box on level 0
+ * level_out     device int32 [R] (nullable): assigned level index
+ * out           device float [R, out_h, out_w, C]
+ */
+int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims, const float* scales,
+                       int num_levels, int C, const float* boxes, const int32_t* box_ind,
+                       int R, int out_h, int out_w, int sampling_ratio, int box_mode,
+                       int pad_border, int assign, int min_level, int max_level,
+                       int canonical_box_size, int canonical_level, int32_t* level_out,
+                       float* out, void* stream);
+
+/* Gradient of d2mi_roi_align_fwd w.r.t. the feature maps (TF
+ * CropAndResizeGradImage + the pad/avg_pool chain rule; boxes get no gradient,
+ * lib/layers/functional.py:120). grad_feats[l] must be zeroed by the caller;
+ * contributions are accumulated with float atomics. */
+int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims, const float* scales,
+                       int num_levels, int C, const float* boxes, const int32_t* box_ind,
+                       int R, int out_h, int out_w, int sampling_ratio, int box_mode,
+                       int pad_border, int assign, int min_level, int max_level,
+                       int canonical_box_size, int canonical_level, const float* grad_out,
+                       void* stream);
+
+/* ------------------------------------------------------------------- NMS
+ * Segmented greedy NMS with TF NonMaxSuppressionV3 semantics
+ * (score_threshold = -inf; IoU with min/max-normalised corners, 0 when an
+ * area <= 0; suppress when IoU > iou_threshold; score desc, ties lowest index
+ * first; stop at max_output_size).
+ * Replaces tf.image.non_max_suppression at lib/layers/nms.py:23 (batch_nms),
+ * lib/modeling/proposal_generator/rpn_outputs.py:90,
+ * lib/modeling/roi_heads/fast_rcnn.py:145, single_stage_heads/retinanet.py:353.
+ * boxes [total,4], scores [total] device; seg_offsets device int32 [num_segs+1];
+ * seg_capacity = host upper bound of any segment length.
+ * keep device int32 [num_segs, max_out] (segment-relative indices in selection
+ * order, -1 padded); num_keep device int32 [num_segs].
+ */
+size_t d2mi_nms_workspace_size(int num_segs, int seg_capacity);
+int d2mi_nms(const float* boxes, const float* scores, const int32_t* seg_offsets, int num_segs,
+             int seg_capacity, int max_out, float iou_threshold, int32_t* keep,
+             int32_t* num_keep, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------ top-k (segmented)
+ * Exact segmented top-k with TF TopKV2 sorted=True order (value desc, ties
+ * lowest index first).  key_mode 0: keys are the values; 1: keys are
+ * sigmoid(values) (RetinaNet, retinanet.py:321-326); values_out receives the keys.
+ * Segment s = values[seg_start[s] : seg_start[s] + seg_len[s]] (device int64
+ * start, int32 len).  Replaces tf.nn.top_k at rpn_outputs.py:70/:106,
+ * retinanet.py:326.  Output idx is segment-relative. */
+size_t d2mi_topk_workspace_size(int num_segs, int k_max);
+int d2mi_topk(const float* values, const int64_t* seg_start, const int32_t* seg_len,
+              int num_segs, int max_seg_len, int k, int key_mode, float* values_out,
+              int32_t* idx_out, int32_t* count_out, void* workspace, size_t workspace_bytes,
+              void* stream);
+
+/* -------------------------------------------------------- anchors/deltas
+ * DefaultAnchorGenerator.grid_anchors for one level (anchor_generator.py:92-109):
+ * out[(h*W + w)*A + a] = cell[a] + (h*stride, w*stride, h*stride, w*stride). */
+int d2mi_grid_anchors(int H, int W, float stride, const float* cell_anchors_host, int A,
+                      float* out, void* stream);
+
+/* Box2BoxTransform.apply_deltas (box_regression.py:76-123):
+ * deltas [N, K*4] (dy,dx,dh,dw), boxes [N,4] -> out [N, K*4]. */
+int d2mi_apply_deltas(const float* deltas, const float* boxes, int N, int K,
+                      const float* weights4_host, float scale_clamp, float* out, void* stream);
+
+/* ------------------------------------------------------ RPN proposals
+ * Fused find_top_rpn_proposals (rpn_outputs.py:29-132) +
+ * predict_proposals (:403-426) + anchors (anchor_generator.py:92-109):
+ * per (image, level) exact top-k of the objectness logits, decode ONLY the
+ * selected anchors (anchors regenerated from the index), clip to the image,
+ * prune small boxes, per-level NMS, then per-image top-k(post) and zero pad.
+ * logits[l]  device float [N, H_l, W_l, A]; deltas[l] device [N, H_l, W_l, A*4]
+ * level_hw   host int32 [L][2]; strides host float [L]; cell_anchors host [L][A][4]
+ * image_hw   device int32 [N,2] (true image height, width)
+ * out_boxes  device [N, post, 4]; out_scores [N, post]; out_valid uint8 [N, post]
+ */
+size_t d2mi_rpn_proposals_workspace_size(int N, int L, const int32_t* level_hw, int A,
+                                         int pre_nms_topk, int post_nms_topk);
+int d2mi_rpn_proposals(const float* const* logits, const float* const* deltas,
+                       const int32_t* level_hw, const float* strides,
+                       const float* cell_anchors, int L, int A, int N, const int32_t* image_hw,
+                       int pre_nms_topk, int post_nms_topk, float nms_thresh,
+                       float min_box_side_len, const float* weights4_host, float scale_clamp,
+                       float* out_boxes, float* out_scores, uint8_t* out_valid,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------- Fast R-CNN inference
+ * FastRCNNOutputs.predict_boxes/predict_probs + fast_rcnn_inference
+ * (fast_rcnn.py:28-187, :359-379): softmax, class-specific decode, clip to the
+ * true image shape, score > thresh in class-major order, class-offset NMS
+ * (offset = cls * (max clipped coord of the image + 1)), top-k, pad.
+ * logits [R, K+1] (background last), deltas [R, K*4] (or [R,4] when
+ * cls_agnostic), proposals [R,4]; roi_img/roi_slot int32 [R] = (image, dense
+ * slot) of each ROI (SparseBoxList.indices); P = dense slots per image.
+ * Outputs [N, max_det] boxes/scores/classes(int64)/valid(uint8) and
+ * out_roi int32 [N, max_det] (kept ROI row, -1 pad).
+ */
+size_t d2mi_fast_rcnn_workspace_size(int N, int P, int K, float score_thresh, int max_det);
+int d2mi_fast_rcnn_inference(const float* logits, const float* deltas, const float* proposals,
+                             const int32_t* roi_img, const int32_t* roi_slot, int R, int N, int P,
+                             int K, int cls_agnostic, const int32_t* image_hw,
+                             const float* weights4_host, float scale_clamp, float score_thresh,
+                             float nms_thresh, int max_det, float* out_boxes, float* out_scores,
+                             int64_t* out_classes, uint8_t* out_valid, int32_t* out_roi,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------- RetinaNet inference
+ * RetinaNetHead.inference (retinanet.py:285-387): per level sigmoid,
+ * top_k(min(topk_candidates, H*W*A*K)), score > thresh, decode the chosen
+ * anchors (no clipping), concat levels, class-offset NMS, pad to max_det.
+ * cls[l] device [N, H_l, W_l, A*K]; box[l] device [N, H_l, W_l, A*4].
+ */
+size_t d2mi_retinanet_workspace_size(int N, int L, const int32_t* level_hw, int A, int K,
+                                     int topk_candidates);
+int d2mi_retinanet_inference(const float* const* cls, const float* const* box,
+                             const int32_t* level_hw, const float* strides,
+                             const float* cell_anchors, int L, int A, int K, int N,
+                             int topk_candidates, float score_thresh, float nms_thresh,
+                             int max_det, const float* weights4_host, float scale_clamp,
+                             float* out_boxes, float* out_scores, int32_t* out_classes,
+                             uint8_t* out_valid, void* workspace, size_t workspace_bytes,
+                             void* stream);
+
+/* ------------------------------------------------------------ Matrix NMS
+ * lib/layers/nms.py:29-83 (SOLOv2 Matrix-NMS).  masks [M, HW] float,
+ * classes int64 [M], scores [M], sum_masks [M] (nullable: computed);
+ * kernel 0 = gaussian, 1 = linear.  out_scores [M]. */
+size_t d2mi_matrix_nms_workspace_size(int M);
+int d2mi_matrix_nms(const float* masks, const int64_t* classes, const float* scores,
+                    const float* sum_masks, int M, int HW, int kernel, float sigma,
+                    float* out_scores, void* workspace, size_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------- conv2d
+ * NHWC implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32),
+ * lib/layers/convolutional.py:12-23 (fix_padding: symmetric pad) and
+ * :198-263 (Conv2D.call: conv + bias + activation), with the FPN top-down
+ * merge fused into the epilogue (lib/modeling/necks/fpn.py:138-149):
+ *   y = act(conv(x, w) + bias) + (topdown ? up2_nearest(topdown) : 0)
+ *        [+ residual]
+ * x [N,H,W,Cin]; w_packed [KH,KW,Cout,Cin] (d2mi_conv_pack_weights of the
+ * reference's HWIO [KH,KW,Cin,Cout] variable); bias [Cout] (nullable);
+ * topdown [N, ceil(OH/2), ceil(OW/2), Cout] (nullable);
+ * residual [N,OH,OW,Cout] (nullable); y [N,OH,OW,Cout].
+ * act: 0 none, 1 relu.  pad_beg/pad_end: explicit spatial padding
+ * (fix_padding gives pad_beg = (k-1)//2, pad_end = k-1-pad_beg).
+ */
+int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout,
+                           float* w_packed, void* stream);
+int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const float* bias,
+                     const float* topdown, const float* residual, float* y, int N, int H, int W,
+                     int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
+                     int act, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* D2MI_H */

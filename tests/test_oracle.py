@@ -1,0 +1,141 @@
+"""CPU tests: the oracle against the reference's golden vectors and
+hand-computed known answers (no GPU)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "nms_golden.npz")
+F32 = np.float32
+
+
+def test_nms_matches_reference_numpy_nms():
+    """oracle NMS == lib/structures/np_box_list_ops.py:146-217 on every golden case."""
+    d = np.load(GOLDEN)
+    for i in range(int(d["num_cases"])):
+        thr, max_out = d[f"c{i}_params"]
+        got = oracle.nms(d[f"c{i}_boxes"], d[f"c{i}_scores"], int(max_out), float(thr))
+        np.testing.assert_array_equal(got, d[f"c{i}_keep"], err_msg=f"case {i}")
+
+
+def test_nms_kat_threshold_is_strict():
+    # IoU(box0, box1) = 0.69, IoU(box0, box2) = 0.71: thr 0.7 keeps 0,1 and drops 2
+    b0 = [0, 0, 10, 10]
+    # box1: shift in x so that IoU = 0.69 -> inter = 100*(1-d/10), IoU = (10-d)/(10+d)
+    d1 = 10 * (1 - 0.69) / (1 + 0.69)
+    d2 = 10 * (1 - 0.71) / (1 + 0.71)
+    boxes = np.array([b0, [0, d1, 10, 10 + d1], [0, d2, 10, 10 + d2]], F32)
+    scores = np.array([0.9, 0.8, 0.7], F32)
+    assert list(oracle.nms(boxes, scores, 10, 0.7)) == [0, 1]
+    # equal IoU to the threshold is NOT suppressed (IOU > thr)
+    boxes = np.array([[0, 0, 10, 10], [0, 0, 10, 5]], F32)  # IoU 0.5
+    assert list(oracle.nms(boxes, np.array([1.0, 0.5], F32), 10, 0.5)) == [0, 1]
+
+
+def test_nms_tie_rule_and_degenerate_boxes():
+    boxes = np.array([[0, 0, 1, 1], [0, 0, 1, 1], [5, 5, 6, 6]], F32)
+    # equal scores: lowest index first
+    assert list(oracle.nms(boxes, np.array([0.5, 0.5, 0.1], F32), 10, 0.5)) == [0, 2]
+    # zero-area boxes never suppress (IoU := 0)
+    z = np.array([[1, 1, 1, 1], [1, 1, 1, 1]], F32)
+    assert list(oracle.nms(z, np.array([0.9, 0.8], F32), 10, 0.0)) == [0, 1]
+    # corners are min/max normalised
+    flipped = np.array([[0, 0, 10, 10], [10, 10, 0, 0]], F32)
+    assert list(oracle.nms(flipped, np.array([0.9, 0.8], F32), 10, 0.5)) == [0]
+    # NaN / -inf scores are never selected, max_output_size caps
+    s = np.array([np.nan, -np.inf, 0.3], F32)
+    assert list(oracle.nms(np.array([[0, 0, 1, 1], [2, 2, 3, 3], [4, 4, 5, 5]], F32), s, 10, 0.5)) == [2]
+    assert len(oracle.nms(boxes, np.array([0.5, 0.4, 0.3], F32), 1, 0.5)) == 1
+    with pytest.raises(ValueError):
+        oracle.nms(boxes, np.ones(3, F32), 10, 1.5)
+
+
+def test_crop_and_resize_kat():
+    """tf.image.crop_and_resize sample positions: in_y = y1*(H-1) + y*(y2-y1)*(H-1)/(ch-1)."""
+    H, W = 5, 7
+    img = (np.arange(H)[:, None] * 100 + np.arange(W)[None, :]).astype(F32)[None, :, :, None]
+    box = np.array([[0.25, 0.5, 0.75, 1.0]], F32)
+    out = oracle.crop_and_resize_tf(img, box, [0], (3, 4))[0, :, :, 0]
+    ys = 0.25 * 4 + np.arange(3) * (0.5 * 4 / 2)
+    xs = 0.5 * 6 + np.arange(4) * (0.5 * 6 / 3)
+    np.testing.assert_allclose(out, ys[:, None] * 100 + xs[None, :], rtol=0, atol=1e-4)
+    # outside [0, H-1] -> extrapolation value 0; crop 1 -> centre sample
+    out = oracle.crop_and_resize_tf(img, np.array([[-1.0, 0, -0.5, 1]], F32), [0], (2, 2))
+    assert np.all(out == 0)
+    c = oracle.crop_and_resize_tf(img, np.array([[0, 0, 1, 1]], F32), [0], (1, 1))[0, 0, 0, 0]
+    assert abs(c - (2 * 100 + 3)) < 1e-5
+    with pytest.raises(ValueError):
+        oracle.crop_and_resize_tf(img, box, [1], (2, 2))
+
+
+def test_roi_align_aligned_bin_centres():
+    """ROIAlignV2 with SR=0 samples bin centres: ymin*s + (i+0.5)*h*s/oh - 0.5
+    (functional.py:138-152 on the SYMMETRIC-padded map)."""
+    H, W = 16, 20
+    yy, xx = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+    img = (yy * 1000 + xx).astype(F32)[None, :, :, None]
+    box = np.array([[2.0, 3.0, 10.0, 15.0]], F32) * 4  # image px, stride 4
+    out = oracle.roi_align(img, box, [0], (4, 6), 0.25, 0, aligned=True)[0, :, :, 0]
+    cy = 2 + (np.arange(4) + 0.5) * 8 / 4 - 0.5
+    cx = 3 + (np.arange(6) + 0.5) * 12 / 6 - 0.5
+    np.testing.assert_allclose(out, cy[:, None] * 1000 + cx[None, :], rtol=0, atol=2e-3)
+    # edge replicate through the SYMMETRIC pad: a box hanging off the top-left
+    out = oracle.roi_align(img, np.array([[-2.0, -2.0, 2.0, 2.0]], F32), [0], (2, 2), 1.0, 0)[0, :, :, 0]
+    assert out[0, 0] == img[0, 0, 0, 0]
+
+
+def test_roi_align_sampling_ratio_is_mean_of_samples():
+    rng = np.random.default_rng(0)
+    img = rng.normal(size=(1, 12, 12, 3)).astype(F32)
+    box = np.array([[8.0, 4.0, 40.0, 44.0]], F32)
+    a = oracle.roi_align(img, box, [0], (2, 2), 0.25, 2)
+    b = oracle.roi_align(img, box, [0], (4, 4), 0.25, 0)
+    np.testing.assert_allclose(a, b.reshape(1, 2, 2, 2, 2, 3).mean(axis=(2, 4)), atol=1e-6)
+
+
+def test_cell_anchor_kat():
+    """size 32, ratio 0.5: w = sqrt(1024/0.5) = 45.25, h = 22.63 (anchor_generator.py:132-143)."""
+    cell = oracle.generate_cell_anchors([32], [0.5, 1.0, 2.0])
+    w = math.sqrt(1024 / 0.5)
+    np.testing.assert_allclose(cell[0], [-0.25 * w, -w / 2, 0.25 * w, w / 2], rtol=1e-6)
+    grid = oracle.grid_anchors(3, 4, 4, cell)
+    assert grid.shape == (3 * 4 * 3, 4)
+    # anchor k at (i, j) = cell + [4i, 4j, 4i, 4j], order [H, W, A]
+    i, j, a = 2, 3, 1
+    np.testing.assert_array_equal(grid[(i * 4 + j) * 3 + a], cell[a] + np.array([8, 12, 8, 12], F32))
+
+
+def test_apply_deltas_identity_and_clamp():
+    boxes = np.array([[10, 20, 30, 60]], F32)
+    out = oracle.apply_deltas(np.zeros((1, 8), F32), boxes, (10, 10, 5, 5))
+    np.testing.assert_array_equal(out.reshape(2, 4), np.repeat(boxes, 2, 0))
+    big = oracle.apply_deltas(np.array([[0, 0, 100, 100]], F32), boxes, (1, 1, 1, 1))
+    h = 20 * 1000 / 16
+    np.testing.assert_allclose(big[0, 2] - big[0, 0], h, rtol=1e-5)
+
+
+def test_assign_levels_kat():
+    # sqrt(area) = 224 -> canonical level 4 -> index 2 of [2..5]
+    b = np.array([[0, 0, 224, 224], [0, 0, 112, 112], [0, 0, 10, 10], [0, 0, 2000, 2000],
+                  [0, 0, 0, 0]], F32)
+    lv = oracle.assign_boxes_to_levels(b, 2, 5, 224, 4)
+    assert list(lv) == [2, 1, 0, 3, 0]
+
+
+def test_top_k_order():
+    v = np.array([1.0, 3.0, 3.0, -1.0, 2.0], F32)
+    vals, idx = oracle.top_k(v, 3)
+    assert list(idx) == [1, 2, 4] and list(vals) == [3.0, 3.0, 2.0]
+
+
+def test_matrix_nms_kat():
+    m = np.zeros((3, 4, 4), F32)
+    m[0, :2, :2] = 1
+    m[1, :2, :3] = 1   # overlaps mask 0: inter 4, union 6 -> iou 2/3
+    m[2, 2:, 2:] = 1
+    out = oracle.matrix_nms(m, np.array([0, 0, 0]), np.array([0.9, 0.8, 0.7], F32))
+    iou = 4 / 6
+    np.testing.assert_allclose(out, [0.9, 0.8 * math.exp(-2 * iou ** 2), 0.7], rtol=1e-6)
