@@ -1,0 +1,217 @@
+#!/usr/bin/env python
+"""Benchmark: Mask R-CNN R50-FPN inference at 1333x800 on MI355X (img/s).
+
+One step = one batched forward of the whole model (BASELINE.json metric
+"img/sec whole-node Mask R-CNN R50-FPN @1333x800") over synthetic COCO-shaped
+images already resident in HBM: ResNet-50 (PyTorch-ROCm convs) -> FPN (MFMA
+kernels, fused top-down add) -> RPN head (MFMA) + fused top-k/decode/NMS
+proposals -> multi-level ROIAlign 7x7 -> box head (hipBLASLt GEMMs) -> fused
+Fast R-CNN post-processing (softmax/decode/clip/class-offset NMS) -> ROIAlign
+14x14 on the detections -> mask head (MFMA) -> per-class mask sigmoid.
+
+Weights are random-init with the reference initialisers; as BASELINE.md
+prescribes, the class / objectness logit scales are calibrated once
+(box-head class logits ~ N(0, 3^2), RPN objectness ~ N(0, 1)) so that the
+score thresholds and NMS see realistic survivor counts (reported).
+
+Multi-GPU: one process per GPU (torchrun), each rank runs its own images
+(inference shards by image: "replicas", no data-path collective), barrier +
+synchronize around the timed region, time = max over ranks, value = all
+images / that time (weak scaling).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    "mask_rcnn_R_50_FPN": "configs/COCO-InstanceSegmentation/mask_rcnn_R_50_FPN_1x.yaml",
+    "faster_rcnn_R_50_FPN": "configs/COCO-Detection/faster_rcnn_R_50_FPN_1x.yaml",
+}
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32)
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=2, help="images per GPU per step")
+    p.add_argument("--model", default="mask_rcnn_R_50_FPN", choices=sorted(CONFIGS))
+    p.add_argument("--height", type=int, default=800)
+    p.add_argument("--width", type=int, default=1333)
+    p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
+    p.add_argument("--cpu-images", type=int, default=1)
+    p.add_argument("--no-kernel-timing", action="store_true")
+    return p.parse_args()
+
+
+def build(args, device):
+    from detectron2_tensorflow_amd.config import finalize, get_cfg
+    from detectron2_tensorflow_amd.modeling import build_model
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(ROOT, CONFIGS[args.model]))
+    cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = "raw"
+    cfg.SOLVER.IMS_PER_GPU = args.batch
+    finalize(cfg, training=False, world_size=args.gpus,
+             category_map={"num_thing_classes": 80, "num_stuff_classes": 53,
+                           "stuff_ignore_value": 0})
+    torch.manual_seed(0)
+    model = build_model(cfg).to(device).eval()
+    return cfg, model
+
+
+@torch.no_grad()
+def calibrate_scores(model, batch):
+    """Rescale the class / objectness logit weights so the random-init model
+    emits BASELINE.md's synthetic score distributions."""
+    stats = {}
+
+    def grab(name):
+        def hook(mod, inp, out):
+            x = inp[0]
+            stats[name] = float((x.reshape(-1, x.shape[-1]) ** 2).sum(-1).mean())
+        return hook
+
+    rh = model.roi_heads
+    h1 = rh.box_predictor.register_forward_hook(grab("box"))
+    rpn_head = model.proposal_generator.rpn_head
+    h2 = rpn_head.conv.register_forward_hook(lambda m, i, o: stats.__setitem__(
+        "rpn", float((o.reshape(-1, o.shape[-1]) ** 2).sum(-1).mean())))
+    model.inference(batch)
+    h1.remove()
+    h2.remove()
+    cls = rh.box_predictor.cls_score
+    cls.weights.normal_(0.0, 3.0 / math.sqrt(max(stats["box"], 1e-12)))
+    obj = rpn_head.objectness_logits
+    obj.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["rpn"], 1e-12)))
+
+
+def synthetic_batch(args, device, rank):
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    img = torch.rand(args.batch, args.height, args.width, 3, generator=g) * 255.0
+    shapes = torch.tensor([[args.height, args.width]] * args.batch, dtype=torch.int32)
+    return {"image": img.to(device), "image_shape": shapes.to(device)}
+
+
+def kernel_report(summary):
+    """Roofline objects from the live HIP-event timings of the timed region."""
+    rep = {}
+    if "conv2d_mfma" in summary:
+        n, ms, flops = summary["conv2d_mfma"]
+        ach = flops / (ms * 1e-3) / 1e12
+        rep["conv2d_mfma"] = {"bound": "mfma", "achieved": round(ach, 2),
+                              "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                              "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                              "algorithmic_per_launch": flops / n}
+    if "roi_align_fwd" in summary:
+        n, ms, byts = summary["roi_align_fwd"]
+        ach = byts / (ms * 1e-3) / 1e9
+        rep["roi_align_fwd"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                                "traffic": None, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                                "algorithmic_per_launch": byts / n}
+    return rep
+
+
+def cpu_baseline(args, model, batch):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from cpu_pipeline import CPUReference, cpu_cores
+    cores = cpu_cores()
+    ref = CPUReference(model)
+    n = args.cpu_images
+    imgs = batch["image"][:n].cpu().numpy()
+    shapes = batch["image_shape"][:n].cpu().numpy()
+    ref(imgs[:1, :256, :320], [[256, 320]], threads=cores)  # warm the libraries
+    t0 = time.perf_counter()
+    ref(imgs, shapes, threads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
+            "sample": f"{n} image(s) {args.height}x{args.width}, whole {args.model} inference, "
+                      f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU convs), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    args.gpus = world
+    device = torch.device("cuda", local)
+    from detectron2_tensorflow_amd import _C
+    from detectron2_tensorflow_amd.layers.ops import KernelTimer
+    _C.load()
+    cfg, model = build(args, device)
+    batch = synthetic_batch(args, device, rank)
+    calibrate_scores(model, batch)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = model.inference(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        KernelTimer.reset(enabled=not args.no_kernel_timing)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model.inference(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        KernelTimer.enabled = False
+    summary = KernelTimer.summary()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    _C.raise_on_errors(device)
+    inst = out["instances"]
+    survivors = int(inst["is_valid"].sum().item())
+
+    if rank == 0:
+        kernels = kernel_report(summary)
+        result = {
+            "metric": "img/sec whole-node Mask R-CNN R50-FPN @1333x800"
+                      if args.model.startswith("mask") else "img/sec Faster R-CNN R50-FPN @1333x800",
+            "value": round(world * args.batch * args.steps / elapsed, 3),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U[0,255) images, random-init weights, calibrated logits)",
+            "config": {"workload": f"{args.model} inference {args.width}x{args.height}",
+                       "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                       "parallelism": f"replicas{world}", "mode": "inference",
+                       "detections_per_step_rank0": survivors},
+            "roofline": kernels.get("conv2d_mfma"),
+            "kernels": kernels,
+        }
+        if args.cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline(args, model, batch)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,246 @@
+"""Conv2D / ConvTranspose2D with the reference's constructor surface
+(lib/layers/convolutional.py:119-263, :747-893).
+
+Activations are NHWC, weights are HWIO ``[k, k, in/groups, out]`` (the
+reference variable layout; ConvTranspose2D keeps TF's ``[k, k, out, in]``).
+``impl="mfma"`` runs the forward pass on the hand-written gfx950 MFMA
+implicit-GEMM kernel (d2mi_conv2d_nhwc) — the FPN lateral/output convs, the
+RPN head and the mask head use it — and raises if the tensor is not on the GPU.
+``impl="torch"`` is stock PyTorch-ROCm conv2d in channels_last, used for the
+backbone (a caller of the hot path, outside its scope).
+``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation,
+Cin % 4 == 0) and the input is on the GPU.
+Backward of the mfma path: dgrad/wgrad via torch.nn.grad on the GPU.
+"""
+import torch
+import torch.nn.functional as F
+
+from ..utils.arg_scope import add_arg_scope
+from . import initializers as init
+from . import ops
+from .activation import get_activation, is_relu
+from .base import Layer
+from .normalization import BatchNorm
+
+
+def fix_padding(inputs, kernel_size, padding="SAME", rate=1):
+    """Explicit symmetric 'SAME' padding (convolutional.py:12-23): NHWC zero pad."""
+    if padding == "SAME" and kernel_size != 1:
+        pb, pe = same_pads(kernel_size, rate)
+        inputs = F.pad(inputs, (0, 0, pb, pe, pb, pe))
+    return inputs
+
+
+def same_pads(kernel_size, rate=1):
+    k_eff = kernel_size + (kernel_size - 1) * (rate - 1)
+    pad_total = k_eff - 1
+    pb = pad_total // 2
+    return pb, pad_total - pb
+
+
+class _ConvMFMAFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown):
+        if relu and topdown is not None:
+            raise ValueError("fused relu + top-down add is not differentiable here")
+        y = ops.conv2d_nhwc(x, w_packed, bias, stride, pads, relu, topdown)
+        ctx.save_for_backward(x, w_hwio, y if relu else None)
+        ctx.conf = (stride, pads, relu, bias is not None, topdown is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        stride, (pb, pe), relu, has_bias, has_td = ctx.conf
+        gtd = None
+        if has_td:
+            N, OH, OW, C = gy.shape
+            g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
+            gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
+        if relu:
+            gy = gy * (y > 0).to(gy.dtype)
+        gy_nchw = gy.permute(0, 3, 1, 2)
+        w_oihw = w.permute(3, 2, 0, 1)
+        xin = x
+        if pb != pe:
+            xin = F.pad(x, (0, 0, pb, pe, pb, pe))
+            pad = 0
+        else:
+            pad = pb
+        x_nchw = xin.permute(0, 3, 1, 2)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(x_nchw.shape, w_oihw, gy_nchw, stride, pad)
+            if pb != pe:
+                gx = gx[:, :, pb:gx.shape[2] - pe, pb:gx.shape[3] - pe]
+            gx = gx.permute(0, 2, 3, 1)
+        if ctx.needs_input_grad[1]:
+            gw = torch.nn.grad.conv2d_weight(x_nchw, w_oihw.shape, gy_nchw, stride, pad)
+            gw = gw.permute(2, 3, 1, 0)
+        if has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 1, 2))
+        return gx, gw, gb, None, None, None, None, gtd
+
+
+@add_arg_scope
+class Conv2D(Layer):
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding="SAME", rate=1,
+                 num_groups=1, use_bias=True, activation=None, normalizer=None,
+                 normalizer_params=None, weights_initializer=None, weights_regularizer=None,
+                 bias_initializer=None, bias_regularizer=None, variables_collections=None,
+                 trainable=True, outputs_collections=None, impl="mfma", **kwargs):
+        padding = padding.upper()
+        if padding not in ("SAME", "VALID"):
+            raise ValueError('"padding" must be "SAME" or "VALID."')
+        if in_channels % num_groups != 0:
+            raise ValueError(f'"in_channels" {in_channels} is not divisible by "num_groups" {num_groups}.')
+        if out_channels % num_groups != 0:
+            raise ValueError(f'"out_channels" {out_channels} is not divisible by "num_groups" {num_groups}.')
+        super().__init__(in_channels=in_channels, out_channels=out_channels,
+                         kernel_size=kernel_size, stride=stride, padding=padding, rate=rate,
+                         num_groups=num_groups, use_bias=use_bias, activation=activation,
+                         normalizer=normalizer, normalizer_params=normalizer_params,
+                         weights_initializer=weights_initializer,
+                         weights_regularizer=weights_regularizer,
+                         bias_initializer=bias_initializer, bias_regularizer=bias_regularizer,
+                         trainable=trainable, impl=impl, **kwargs)
+        self.build()
+
+    def build(self):
+        shape = (self.kernel_size, self.kernel_size, self.in_channels // self.num_groups,
+                 self.out_channels)
+        w = torch.empty(shape, dtype=torch.float32)
+        (self.weights_initializer or init.variance_scaling(2.0, distribution="untruncated_normal"))(w)
+        self.weights = torch.nn.Parameter(w, requires_grad=self.trainable)
+        if self.use_bias:
+            b = torch.zeros(self.out_channels)
+            if self.bias_initializer is not None:
+                self.bias_initializer(b)
+            self.bias = torch.nn.Parameter(b, requires_grad=self.trainable)
+        else:
+            self.bias = None
+        self.normalizer_fn = None
+        if self.normalizer is not None:
+            p = dict(self.normalizer_params or {})
+            p["channels"] = self.out_channels
+            self.normalizer_fn = self.normalizer(**p)
+        self.act_fn = get_activation(self.activation)
+        self._packed = None
+        self._packed_key = None
+
+    def _mfma_eligible(self, x):
+        return (x.is_cuda and self.num_groups == 1 and self.rate == 1
+                and self.in_channels % 4 == 0)
+
+    def packed_weights(self):
+        key = (self.weights.data_ptr(), self.weights._version)
+        if self._packed is None or self._packed_key != key:
+            self._packed = ops.pack_conv_weights(self.weights.detach())
+            self._packed_key = key
+        return self._packed
+
+    def call(self, inputs, topdown=None):
+        impl = self.impl
+        if impl == "auto":
+            impl = "mfma" if self._mfma_eligible(inputs) else "torch"
+        if impl == "mfma":
+            if not self._mfma_eligible(inputs):
+                raise ValueError(f"{self.scope}: shape/device not supported by the MFMA conv "
+                                 f"(groups={self.num_groups}, rate={self.rate}, "
+                                 f"Cin={self.in_channels}, device={inputs.device})")
+            pads = same_pads(self.kernel_size, self.rate) if self.padding == "SAME" else (0, 0)
+            fuse_relu = self.normalizer_fn is None and is_relu(self.act_fn)
+            ret = _ConvMFMAFn.apply(inputs, self.weights, self.bias, self.packed_weights(),
+                                    self.stride, pads, fuse_relu, topdown)
+            if self.normalizer_fn is not None:
+                ret = self.normalizer_fn(ret)
+            if self.act_fn is not None and not fuse_relu:
+                ret = self.act_fn(ret)
+            return ret
+        # torch (channels_last) path: backbone / unsupported shapes
+        x = fix_padding(inputs, self.kernel_size, self.padding, self.rate)
+        w = self.weights.permute(3, 2, 0, 1)
+        bias = self.bias
+        norm = self.normalizer_fn
+        if isinstance(norm, BatchNorm):
+            # frozen statistics: fold the affine into the conv (one pass over the map)
+            scale, shift = norm.folded()
+            w = w * scale[:, None, None, None]
+            bias = shift if bias is None else bias * scale + shift
+            norm = None
+        y = F.conv2d(x.permute(0, 3, 1, 2), w.contiguous(memory_format=torch.channels_last),
+                     bias, stride=self.stride, dilation=self.rate, groups=self.num_groups)
+        ret = y.permute(0, 2, 3, 1)
+        if norm is not None:
+            ret = norm(ret)
+        if self.act_fn is not None:
+            ret = self.act_fn(ret)
+        if topdown is not None:
+            N, H, W, C = ret.shape
+            ret = ret + topdown.repeat_interleave(2, 1).repeat_interleave(2, 2)[:, :H, :W]
+        return ret
+
+
+@add_arg_scope
+class ConvTranspose2D(Layer):
+    """Transposed conv (convolutional.py:747-893); weights [k, k, out, in].
+
+    For the kernel == stride case of the mask head (2x2, s2) each input pixel
+    owns a disjoint 2x2 output block, so the op is one GEMM over
+    [pixels, in] x [in, k*k*out]: it runs on the MFMA conv kernel as a 1x1
+    conv whose packed weight is the TF kernel itself, followed by a pixel
+    shuffle."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding="SAME",
+                 use_bias=True, activation=None, normalizer=None, normalizer_params=None,
+                 weights_initializer=None, weights_regularizer=None, bias_initializer=None,
+                 bias_regularizer=None, variables_collections=None, trainable=True,
+                 outputs_collections=None, **kwargs):
+        super().__init__(in_channels=in_channels, out_channels=out_channels,
+                         kernel_size=kernel_size, stride=stride, padding=padding.upper(),
+                         use_bias=use_bias, activation=activation, normalizer=normalizer,
+                         normalizer_params=normalizer_params, weights_initializer=weights_initializer,
+                         bias_initializer=bias_initializer, trainable=trainable, **kwargs)
+        k = kernel_size
+        w = torch.empty((k, k, out_channels, in_channels))
+        # fans of a transposed kernel: tf computes them on [k, k, out, in]
+        (weights_initializer or init.variance_scaling(2.0, distribution="untruncated_normal"))(w)
+        self.weights = torch.nn.Parameter(w, requires_grad=trainable)
+        self.bias = torch.nn.Parameter(torch.zeros(out_channels), requires_grad=trainable) if use_bias else None
+        self.normalizer_fn = None
+        if normalizer is not None:
+            p = dict(normalizer_params or {})
+            p["channels"] = out_channels
+            self.normalizer_fn = normalizer(**p)
+        self.act_fn = get_activation(activation)
+
+    def call(self, inputs):
+        k, s = self.kernel_size, self.stride
+        N, H, W, C = inputs.shape
+        if k == s:  # the mask-head case: MFMA GEMM (raises off-GPU, no CPU fallback)
+            wp = self.weights.reshape(1, 1, k * k * self.out_channels, self.in_channels)
+            b = self.bias.repeat(k * k) if self.bias is not None else None
+            fuse = self.normalizer_fn is None and is_relu(self.act_fn)
+            y = _ConvMFMAFn.apply(inputs, wp.permute(0, 1, 3, 2), b, wp.detach().contiguous(), 1,
+                                  (0, 0), fuse, None)
+            y = y.reshape(N, H, W, k, k, self.out_channels).permute(0, 1, 3, 2, 4, 5)
+            ret = y.reshape(N, H * k, W * k, self.out_channels)
+            if self.normalizer_fn is not None:
+                ret = self.normalizer_fn(ret)
+            if self.act_fn is not None and not fuse:
+                ret = self.act_fn(ret)
+            return ret
+        # general case on torch: conv_transpose2d with TF 'SAME'/'VALID' output size
+        w = self.weights.permute(3, 2, 0, 1)  # [in, out, kh, kw]
+        y = F.conv_transpose2d(inputs.permute(0, 3, 1, 2), w, self.bias, stride=s)
+        OH = H * s + (max(k - s, 0) if self.padding == "VALID" else 0)
+        OW = W * s + (max(k - s, 0) if self.padding == "VALID" else 0)
+        if self.padding == "SAME":
+            ph, pw = max((H - 1) * s + k - OH, 0), max((W - 1) * s + k - OW, 0)
+            y = y[:, :, ph // 2: ph // 2 + OH, pw // 2: pw // 2 + OW]
+        ret = y.permute(0, 2, 3, 1)
+        if self.normalizer_fn is not None:
+            ret = self.normalizer_fn(ret)
+        if self.act_fn is not None:
+            ret = self.act_fn(ret)
+        return ret

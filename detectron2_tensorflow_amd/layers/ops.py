@@ -16,6 +16,46 @@ _DEFAULT_SCALE_CLAMP = math.log(1000.0 / 16)  # lib/modeling/box_regression.py:1
 BOX_MODE_RAW, BOX_MODE_ALIGNED, BOX_MODE_UNALIGNED = 0, 1, 2
 
 
+class KernelTimer:
+    """Opt-in per-launch HIP-event timing of the hot kernels (bench.py's live
+    roofline).  Events are recorded on the launching stream around each call;
+    ``work`` is the op's ALGORITHMIC flops (conv) or bytes (ROIAlign)."""
+
+    enabled = False
+    records = []
+
+    @classmethod
+    def reset(cls, enabled=True):
+        cls.enabled = enabled
+        cls.records = []
+
+    @classmethod
+    def start(cls):
+        if not cls.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        return ev
+
+    @classmethod
+    def stop(cls, ev0, name, work):
+        if ev0 is None:
+            return
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record(torch.cuda.current_stream())
+        cls.records.append((name, ev0, ev1, float(work)))
+
+    @classmethod
+    def summary(cls):
+        """{name: (launches, total_ms, total_work)} (synchronises)."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, w in cls.records:
+            n, t, tw = out.get(name, (0, 0.0, 0.0))
+            out[name] = (n + 1, t + e0.elapsed_time(e1), tw + w)
+        return out
+
+
 def _f32c(t):
     return t.to(torch.float32).contiguous()
 
@@ -46,10 +86,14 @@ class _RoIAlignFn(torch.autograd.Function):
         dims = _C.host_array(_C.ctypes.c_int32,
                              [v for f in feats for v in (f.shape[0], f.shape[1], f.shape[2])])
         sc = _C.host_array(_C.c_float, list(scales))
+        ev = KernelTimer.start()
         rc = _C.lib().d2mi_roi_align_fwd(fp, dims, sc, L, C, _C.ptr(boxes), _C.ptr(box_ind), R,
                                          out_h, out_w, sr, mode, pad, assign, min_l, max_l,
                                          canon_s, canon_l, _C.ptr(level), _C.ptr(out),
                                          _C.stream_of(boxes.device))
+        S = max(sr, 1) ** 2
+        # algorithmic bytes: 4 f32 corner reads per sample + 1 f32 write per output
+        KernelTimer.stop(ev, "roi_align_fwd", R * out_h * out_w * C * (16 * S + 4))
         _C.check(rc, "d2mi_roi_align_fwd")
         ctx.params = params
         ctx.shapes = [f.shape for f in feats]
@@ -216,10 +260,12 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                              f"{(N, OH, OW, Cout)}")
     if residual is not None:
         residual = _f32c(residual)
+    ev = KernelTimer.start()
     rc = _C.lib().d2mi_conv2d_nhwc(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias), _C.ptr(topdown),
                                    _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
                                    int(stride), int(pb), int(pe), int(bool(relu)),
                                    _C.stream_of(x.device))
+    KernelTimer.stop(ev, "conv2d_mfma", 2.0 * N * OH * OW * Cout * KH * KW * Cin)
     _C.check(rc, "d2mi_conv2d_nhwc")
     return y
 

@@ -1,0 +1,137 @@
+"""ResNet backbone (lib/modeling/backbone/resnet.py:22-253, blocks.py:143-186).
+
+A caller of the hot path (out of scope as a rewrite target, SURVEY.md
+section 2): stock PyTorch-ROCm convolutions in channels_last through
+Conv2D(impl="torch"), FrozenBN folded into the conv at run time.
+Structure, strides (STRIDE_IN_1X1), the stem's zero pad + 3x3/2 VALID max
+pool and FREEZE_AT follow the reference.
+"""
+import copy
+from contextlib import ExitStack, contextmanager
+
+import torch
+import torch.nn.functional as F
+
+from ...layers import BatchNorm, Conv2D, Layer, get_norm
+from ...layers import initializers as init
+from ...utils.arg_scope import add_arg_scope, arg_scope
+from .build import BACKBONE_REGISTRY, Backbone
+
+
+@contextmanager
+def resnet_arg_scope(freeze, norm):
+    normalizer = get_norm(norm)
+    with arg_scope([Conv2D], use_bias=False, normalizer=normalizer,
+                   normalizer_params={"scope": "norm"}, activation="relu", impl="torch",
+                   weights_initializer=init.variance_scaling(2.0, mode="fan_out")), ExitStack() as st:
+        if freeze:
+            st.enter_context(arg_scope([Conv2D, BatchNorm], trainable=False))
+        yield
+
+
+@add_arg_scope
+class BottleneckBlock(Layer):
+    def __init__(self, in_channels, out_channels, bottleneck_channels, stride=1, num_groups=1,
+                 stride_in_1x1=False, rate=1, **kwargs):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, **kwargs)
+        self.shortcut = None
+        if in_channels != out_channels:
+            self.shortcut = Conv2D(in_channels, out_channels, 1, stride=stride, activation=None,
+                                   scope="shortcut")
+        s1, s3 = (stride, 1) if stride_in_1x1 else (1, stride)
+        self.conv1 = Conv2D(in_channels, bottleneck_channels, 1, stride=s1, scope="conv1")
+        self.conv2 = Conv2D(bottleneck_channels, bottleneck_channels, 3, stride=s3,
+                            num_groups=num_groups, rate=rate, scope="conv2")
+        self.conv3 = Conv2D(bottleneck_channels, out_channels, 1, activation=None, scope="conv3")
+
+    def call(self, x):
+        out = self.conv3(self.conv2(self.conv1(x)))
+        sc = self.shortcut(x) if self.shortcut is not None else x
+        return torch.relu_(out + sc)
+
+
+@add_arg_scope
+class Stem(Layer):
+    def __init__(self, in_channels, out_channels, **kwargs):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, **kwargs)
+        self.conv1 = Conv2D(in_channels, out_channels, 7, stride=2,
+                            normalizer_params={"channels": out_channels, "scope": "norm"},
+                            scope="conv1")
+
+    def call(self, x):
+        ret = self.conv1(x)
+        ret = F.pad(ret.permute(0, 3, 1, 2), (1, 1, 1, 1))  # tf.pad zeros (resnet.py:80)
+        ret = F.max_pool2d(ret, 3, 2)                        # VALID 3x3/2 (resnet.py:81)
+        return ret.permute(0, 2, 3, 1)
+
+    @property
+    def stride(self):
+        return 4
+
+
+class Stage(Layer):
+    def __init__(self, block_class, block_kwargs, num_blocks, first_stride, **kwargs):
+        super().__init__(**kwargs)
+        self.blocks = torch.nn.ModuleList()
+        for i in range(num_blocks):
+            kw = copy.copy(block_kwargs)
+            kw["scope"] = f"block_{i + 1}"
+            kw["stride"] = first_stride if i == 0 else 1
+            if i > 0:
+                kw["in_channels"] = block_kwargs["out_channels"]
+            self.blocks.append(block_class(**kw))
+
+    def call(self, x):
+        for b in self.blocks:
+            x = b(x)
+        return x
+
+
+@BACKBONE_REGISTRY.register()
+class ResNet(Backbone):
+    def __init__(self, cfg, input_shape, **kwargs):
+        r = cfg.MODEL.RESNETS
+        if r.RES5_DILATION not in (1, 2):
+            raise ValueError(f"res5_dilation cannot be {r.RES5_DILATION}.")
+        if any(r.DEFORM_ON_PER_STAGE):
+            raise NotImplementedError("deformable ResNet stages are outside the hot path")
+        super().__init__(**kwargs)
+        self._out_features = list(r.OUT_FEATURES)
+        freeze_at = cfg.MODEL.BACKBONE.FREEZE_AT
+        out_stage_idx = [{"res2": 2, "res3": 3, "res4": 4, "res5": 5}[f] for f in self._out_features]
+        max_stage_idx = max(out_stage_idx)
+        num_blocks = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}[r.DEPTH]
+        with resnet_arg_scope(freeze_at > 0, r.NORM):
+            self.stem = Stem(input_shape.channels, r.STEM_OUT_CHANNELS, scope="stem")
+        stride = self.stem.stride
+        self._out_feature_strides = {"stem": stride}
+        self._out_feature_channels = {"stem": r.STEM_OUT_CHANNELS}
+        in_ch, out_ch = r.STEM_OUT_CHANNELS, r.RES2_OUT_CHANNELS
+        bott = r.NUM_GROUPS * r.WIDTH_PER_GROUP
+        self.stages = torch.nn.ModuleList()
+        self.stage_names = []
+        for idx, stage_idx in enumerate(range(2, max_stage_idx + 1)):
+            rate = r.RES5_DILATION if stage_idx == 5 else 1
+            first_stride = 1 if (idx == 0 or (stage_idx == 5 and rate == 2)) else 2
+            kw = {"in_channels": in_ch, "out_channels": out_ch, "bottleneck_channels": bott,
+                  "rate": rate, "num_groups": r.NUM_GROUPS, "stride_in_1x1": r.STRIDE_IN_1X1}
+            name = f"res{stage_idx}"
+            with resnet_arg_scope(freeze_at >= stage_idx, r.NORM):
+                self.stages.append(Stage(BottleneckBlock, kw, num_blocks[idx], first_stride,
+                                         scope=name))
+            self.stage_names.append(name)
+            stride = int(stride * first_stride)
+            self._out_feature_strides[name] = stride
+            self._out_feature_channels[name] = out_ch
+            in_ch, out_ch, bott = out_ch, out_ch * 2, bott * 2
+
+    def call(self, x):
+        outputs = {}
+        x = self.stem(x)
+        if "stem" in self._out_features:
+            outputs["stem"] = x
+        for name, stage in zip(self.stage_names, self.stages):
+            x = stage(x)
+            if name in self._out_features:
+                outputs[name] = x
+        return outputs

@@ -1,0 +1,105 @@
+"""GeneralizedRCNN / ProposalNetwork (lib/modeling/meta_arch/rcnn.py:17-224).
+
+batched_inputs is the reference's dict: "image" [N, H, W, 3] float32 0-255
+RGB (NHWC), "image_shape" [N, 2] int32 true (h, w).  Preprocessing
+normalises, THEN flips to BGR when INPUT_FORMAT == "BGR", then zero-pads to
+the neck's size divisibility (rcnn.py:146-157, image_list.py:89-100).
+Inference returns {"instances": {boxes, classes, scores, is_valid[, masks]}}
+as dense [N, DETECTIONS_PER_IMAGE] tensors (fields.ResultFields names).
+"""
+import torch
+
+from ...layers import Layer
+from ...structures import ImageList
+from ..backbone import build_backbone
+from ..necks import build_neck
+from ..proposal_generator import build_proposal_generator
+from ..roi_heads import build_roi_heads
+from .build import META_ARCH_REGISTRY
+
+
+class _Preprocess:
+    def _init_preprocess(self, cfg):
+        assert len(cfg.MODEL.PIXEL_MEAN) == len(cfg.MODEL.PIXEL_STD)
+        self.register_buffer("pixel_mean", torch.tensor(cfg.MODEL.PIXEL_MEAN, dtype=torch.float32),
+                             persistent=False)
+        self.register_buffer("pixel_std", torch.tensor(cfg.MODEL.PIXEL_STD, dtype=torch.float32),
+                             persistent=False)
+        self.input_format = cfg.MODEL.INPUT_FORMAT
+
+    def preprocess_image(self, batched_inputs):
+        images = (batched_inputs["image"] - self.pixel_mean) / self.pixel_std
+        if self.input_format == "BGR":
+            images = images.flip(-1)
+        shapes = batched_inputs["image_shape"].to(device=images.device, dtype=torch.int32)
+        return ImageList.from_tensors(images.contiguous(), shapes, self.neck.size_divisibility)
+
+
+def _check_output_format(fmt):
+    if fmt != "raw":
+        raise NotImplementedError(
+            f"MODEL.SEGMENTATION_OUTPUT.FORMAT={fmt!r}: pasting masks into the image "
+            "(detector_postprocess, lib/modeling/postprocessing.py:9-59) is the next row of "
+            "SURVEY.md section 8f (F1); use 'raw' (28x28 per-box masks)")
+
+
+@META_ARCH_REGISTRY.register()
+class GeneralizedRCNN(_Preprocess, Layer):
+    def __init__(self, cfg, **kwargs):
+        super().__init__(**kwargs)
+        self.backbone = build_backbone(cfg, scope="backbone")
+        self.neck = build_neck(cfg, self.backbone.output_shape(), scope="neck")
+        self.proposal_generator = build_proposal_generator(cfg, self.neck.output_shape(),
+                                                           scope="proposal_generator")
+        self.roi_heads = build_roi_heads(cfg, self.neck.output_shape(), scope="roi_heads")
+        self._init_preprocess(cfg)
+        self.segmentation_output_format = cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT
+        self.segmentation_output_resolution = cfg.MODEL.SEGMENTATION_OUTPUT.FIXED_RESOLUTION
+
+    def call(self, batched_inputs):
+        if not self.training:
+            return self.inference(batched_inputs)
+        raise NotImplementedError("GeneralizedRCNN training step lands with the RPN / ROI-head "
+                                  "losses (SURVEY.md section 8f, F2)")
+
+    def inference(self, batched_inputs, detected_instances=None):
+        assert not self.training
+        _check_output_format(self.segmentation_output_format)
+        images = self.preprocess_image(batched_inputs)
+        features = self.neck(self.backbone(images.tensor))
+        if detected_instances is None:
+            if self.proposal_generator is not None:
+                proposals, *_ = self.proposal_generator(images, features, None)
+            else:
+                proposals = batched_inputs["proposals"]
+            results, _ = self.roi_heads(images, features, proposals, None)
+        else:
+            results = self.roi_heads.forward_with_given_boxes(features, detected_instances)
+        out = {"boxes": results.boxes, "classes": results.get_field("pred_classes"),
+               "scores": results.get_field("scores"), "is_valid": results.get_field("is_valid")}
+        if results.has_field("pred_masks"):
+            out["masks"] = results.get_field("pred_masks")
+        return {"instances": out}
+
+
+@META_ARCH_REGISTRY.register()
+class ProposalNetwork(_Preprocess, Layer):
+    """rcnn.py:161-224: backbone + neck + RPN, returns the proposals."""
+
+    def __init__(self, cfg, **kwargs):
+        super().__init__(**kwargs)
+        self.backbone = build_backbone(cfg, scope="backbone")
+        self.neck = build_neck(cfg, self.backbone.output_shape(), scope="neck")
+        self.proposal_generator = build_proposal_generator(cfg, self.neck.output_shape(),
+                                                           scope="proposal_generator")
+        self._init_preprocess(cfg)
+
+    def call(self, batched_inputs):
+        images = self.preprocess_image(batched_inputs)
+        features = self.neck(self.backbone(images.tensor))
+        proposals, losses, _ = self.proposal_generator(images, features, None)
+        if self.training:
+            return losses
+        return {"proposals": {"boxes": proposals.boxes,
+                              "objectness_logits": proposals.get_field("objectness_logits"),
+                              "is_valid": proposals.get_field("is_valid")}}

@@ -1,0 +1,141 @@
+"""ORACLE — test infrastructure only.  End-to-end CPU restatement of the
+reference's Mask R-CNN / Faster R-CNN R50-FPN inference
+(lib/modeling/meta_arch/rcnn.py:92-157) with the weights of a built model:
+
+  preprocess (rcnn.py:146-157) -> ResNet (the model's own backbone module on
+  CPU torch convs: the backbone is a caller of the hot path) -> FPN with
+  torch-CPU convs + nearest upsample (fpn.py:121-159) -> RPN head convs ->
+  ALL anchors materialised and decoded (anchor_generator.py:92-109,
+  rpn_outputs.py:403-426) -> find_top_rpn_proposals (rpn_outputs.py:29-132)
+  -> per-level ROIAlign with a materialised SYMMETRIC pad (poolers.py:134-180)
+  -> box head GEMMs -> softmax/decode/fast_rcnn_inference (fast_rcnn.py:28-187)
+  -> mask pooler + mask head convs + mask_rcnn_inference (mask_head.py:71-103).
+
+It is what bench.py times as ``cpu_baseline`` (kind "port": a TF-1.15
+semantics restatement, not TensorFlow) and what the end-to-end parity test
+compares the GPU model against.  Never imported by the product path.
+"""
+import copy
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+import oracle
+
+F32 = np.float32
+
+
+def _conv(x_nhwc, layer, relu=None, stride=None):
+    """Reference Conv2D.call on CPU: fix_padding + VALID conv + bias (+ relu)."""
+    k = layer.kernel_size
+    s = stride or layer.stride
+    x = x_nhwc
+    if layer.padding == "SAME" and k != 1:
+        pt = k - 1
+        x = F.pad(x, (0, 0, pt // 2, pt - pt // 2, pt // 2, pt - pt // 2))
+    y = F.conv2d(x.permute(0, 3, 1, 2), layer.weights.permute(3, 2, 0, 1), layer.bias, stride=s)
+    y = y.permute(0, 2, 3, 1)
+    act = layer.act_fn if relu is None else (torch.relu if relu else None)
+    return act(y) if act is not None else y
+
+
+class CPUReference:
+    def __init__(self, model):
+        self.m = copy.deepcopy(model).cpu().eval()
+        for p in self.m.parameters():
+            p.requires_grad_(False)
+
+    def fpn(self, feats):
+        neck = self.m.neck
+        x = [feats[f] for f in neck.in_features[::-1]]
+        prev = _conv(x[0], neck.lateral_convs[0])
+        results = [_conv(prev, neck.output_convs[0])]
+        for f, lat, out in zip(x[1:], neck.lateral_convs[1:], neck.output_convs[1:]):
+            top = prev.repeat_interleave(2, 1).repeat_interleave(2, 2)
+            prev = _conv(f, lat) + top
+            results.insert(0, _conv(prev, out))
+        results.append(results[-1][:, ::2, ::2, :])  # LastLevelMaxPool
+        return dict(zip(neck._out_features, results))
+
+    @torch.no_grad()
+    def __call__(self, images, image_shapes, threads=None):
+        if threads:
+            torch.set_num_threads(threads)
+        m = self.m
+        x = (torch.from_numpy(np.asarray(images, F32)) - m.pixel_mean) / m.pixel_std
+        if m.input_format == "BGR":
+            x = x.flip(-1)
+        H, W = x.shape[1:3]
+        d = m.neck.size_divisibility
+        x = F.pad(x, (0, 0, 0, (-W) % d, 0, (-H) % d))
+        feats = self.fpn(m.backbone(x.contiguous()))
+        rpn = m.proposal_generator
+        head = rpn.rpn_head
+        N = x.shape[0]
+        props, logits = [], []
+        ag = rpn.anchor_generator
+        for lvl, f in enumerate(rpn.in_features):
+            share = _conv(feats[f], head.conv)
+            lg = _conv(share, head.objectness_logits).numpy()
+            dl = _conv(share, head.anchor_deltas).numpy()
+            h, w = lg.shape[1:3]
+            anc = oracle.grid_anchors(h, w, ag.strides[lvl], ag.cell_anchors[lvl].numpy())
+            p = oracle.apply_deltas(dl.reshape(-1, 4), np.tile(anc, (N, 1)),
+                                    rpn.box2box_transform.weights)
+            props.append(p.reshape(N, -1, 4))
+            logits.append(lg.reshape(N, -1))
+        shapes = np.asarray(image_shapes)
+        pb, ps, pv = oracle.find_top_rpn_proposals(props, logits, shapes, rpn.nms_thresh,
+                                                   rpn.pre_nms_topk[False],
+                                                   rpn.post_nms_topk[False],
+                                                   float(rpn.min_box_side_len))
+        rh = m.roi_heads
+        P = pb.shape[1]
+        roi_img, roi_slot = np.nonzero(pv)
+        boxes = pb[roi_img, roi_slot]
+        levels = [feats[f].numpy() for f in rh.in_features]
+        bp = rh.box_pooler
+        pooled, _ = oracle.roi_pooler(levels, boxes, roi_img, bp.output_size, bp.scales,
+                                      bp.sampling_ratio, bp.aligned)
+        xb = torch.from_numpy(pooled).reshape(len(boxes), -1)
+        for fc in rh.box_head.fcs:
+            xb = torch.relu(xb @ fc.weights + fc.bias)
+        cls = (xb @ rh.box_predictor.cls_score.weights + rh.box_predictor.cls_score.bias).numpy()
+        dlt = (xb @ rh.box_predictor.bbox_pred.weights + rh.box_predictor.bbox_pred.bias).numpy()
+        probs = oracle.softmax(cls)
+        dec = oracle.apply_deltas(dlt, boxes, rh.box2box_transform.weights)
+        res = oracle.fast_rcnn_inference(dec, probs, roi_img, roi_slot, P, shapes,
+                                         rh.test_score_thresh, rh.test_nms_thresh,
+                                         rh.test_detections_per_img)
+        out = {"boxes": np.stack([r[0] for r in res]), "scores": np.stack([r[1] for r in res]),
+               "classes": np.stack([r[2] for r in res]), "is_valid": np.stack([r[3] for r in res]),
+               "rpn": (pb, ps, pv)}
+        if rh.mask_on:
+            D = out["boxes"].shape[1]
+            di, ds = np.nonzero(out["is_valid"])
+            mp = rh.mask_pooler
+            pooled, _ = oracle.roi_pooler(levels, out["boxes"][di, ds], di, mp.output_size,
+                                          mp.scales, mp.sampling_ratio, mp.aligned)
+            y = torch.from_numpy(pooled)
+            for c in rh.mask_head.convs:
+                y = _conv(y, c)
+            dc = rh.mask_head.deconv
+            y = F.conv_transpose2d(y.permute(0, 3, 1, 2), dc.weights.permute(3, 2, 0, 1), dc.bias,
+                                   stride=dc.stride)
+            y = torch.relu(y).permute(0, 2, 3, 1)
+            y = _conv(y, rh.mask_head.predictor).numpy()
+            cls_k = out["classes"][di, ds]
+            logit = y[np.arange(len(di)), :, :, cls_k] if y.shape[-1] > 1 else y[..., 0]
+            masks = np.zeros((N, D) + logit.shape[1:], F32)
+            masks[di, ds] = oracle.sigmoid(logit)
+            out["masks"] = masks
+        return out
+
+
+def cpu_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
