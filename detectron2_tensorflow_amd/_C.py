@@ -52,6 +52,9 @@ _SIGS = {
     "d2mi_conv_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_int, P]),
+    "d2mi_conv2d_workspace_size": (c_size_t, [c_int] * 10),
+    "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
 }
 
 EXPORTED = tuple(_SIGS)

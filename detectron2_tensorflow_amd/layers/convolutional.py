@@ -40,25 +40,29 @@ def same_pads(kernel_size, rate=1):
 
 class _ConvMFMAFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown):
-        if relu and topdown is not None:
-            raise ValueError("fused relu + top-down add is not differentiable here")
-        y = ops.conv2d_nhwc(x, w_packed, bias, stride, pads, relu, topdown)
+    def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
+                relu_after=False):
+        has_add = topdown is not None or residual is not None
+        if relu and has_add and not relu_after:
+            raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
+        y = ops.conv2d_nhwc(x, w_packed, bias, stride, pads, relu, topdown, residual,
+                            relu_after_add=relu_after)
         ctx.save_for_backward(x, w_hwio, y if relu else None)
-        ctx.conf = (stride, pads, relu, bias is not None, topdown is not None)
+        ctx.conf = (stride, pads, relu, bias is not None, topdown is not None, residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, (pb, pe), relu, has_bias, has_td = ctx.conf
+        stride, (pb, pe), relu, has_bias, has_td, has_res = ctx.conf
+        if relu:  # relu is the last op whenever an add is fused (relu_after)
+            gy = gy * (y > 0).to(gy.dtype)
         gtd = None
         if has_td:
             N, OH, OW, C = gy.shape
             g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
-        if relu:
-            gy = gy * (y > 0).to(gy.dtype)
+        gres = gy if has_res else None
         gy_nchw = gy.permute(0, 3, 1, 2)
         w_oihw = w.permute(3, 2, 0, 1)
         xin = x
@@ -79,7 +83,7 @@ class _ConvMFMAFn(torch.autograd.Function):
             gw = gw.permute(2, 3, 1, 0)
         if has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 1, 2))
-        return gx, gw, gb, None, None, None, None, gtd
+        return gx, gw, gb, None, None, None, None, gtd, gres, None
 
 
 @add_arg_scope
@@ -132,52 +136,92 @@ class Conv2D(Layer):
         return (x.is_cuda and self.num_groups == 1 and self.rate == 1
                 and self.in_channels % 4 == 0)
 
-    def packed_weights(self):
-        key = (self.weights.data_ptr(), self.weights._version)
+    def _param_key(self):
+        key = [self.weights.data_ptr(), self.weights._version]
+        if self.bias is not None:
+            key.append(self.bias._version)
+        if isinstance(self.normalizer_fn, BatchNorm):
+            n = self.normalizer_fn
+            key += [t._version for t in (n.gamma, n.beta, n.moving_mean, n.moving_variance)
+                    if t is not None]
+        return tuple(key)
+
+    def effective_params(self):
+        """(weights HWIO, bias) with a frozen BatchNorm folded in, plus the
+        normalizer still to apply (None when folded).  Cached while autograd
+        is off (inference); recomputed (differentiably) otherwise."""
+        norm = self.normalizer_fn
+        if not isinstance(norm, BatchNorm):
+            return self.weights, self.bias, norm
+        if not torch.is_grad_enabled() and getattr(self, "_fold_key", None) == self._param_key():
+            return self._fold_w, self._fold_b, None
+        scale, shift = norm.folded()
+        w = self.weights * scale
+        b = shift if self.bias is None else self.bias * scale + shift
+        if not torch.is_grad_enabled():
+            self._fold_w, self._fold_b, self._fold_key = w.contiguous(), b.contiguous(), self._param_key()
+            return self._fold_w, self._fold_b, None
+        return w, b, None
+
+    def packed_weights(self, w_eff=None):
+        key = self._param_key()
         if self._packed is None or self._packed_key != key:
-            self._packed = ops.pack_conv_weights(self.weights.detach())
+            w = self.weights if w_eff is None else w_eff
+            self._packed = ops.pack_conv_weights(w.detach())
             self._packed_key = key
         return self._packed
 
-    def call(self, inputs, topdown=None):
+    def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False):
+        """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
+        relu_after_add: the layer's ReLU runs after those adds; final_relu: an
+        extra ReLU after the adds for a layer without activation (the
+        bottleneck's relu(conv3(x) + shortcut), blocks.py:143-186)."""
         impl = self.impl
         if impl == "auto":
             impl = "mfma" if self._mfma_eligible(inputs) else "torch"
+        w, b, norm = self.effective_params()
+        if final_relu:
+            if self.act_fn is not None:
+                raise ValueError("final_relu is for layers without an activation")
+            if impl == "torch":
+                return torch.relu_(self.call(inputs, topdown, residual))
         if impl == "mfma":
             if not self._mfma_eligible(inputs):
                 raise ValueError(f"{self.scope}: shape/device not supported by the MFMA conv "
                                  f"(groups={self.num_groups}, rate={self.rate}, "
                                  f"Cin={self.in_channels}, device={inputs.device})")
             pads = same_pads(self.kernel_size, self.rate) if self.padding == "SAME" else (0, 0)
-            fuse_relu = self.normalizer_fn is None and is_relu(self.act_fn)
-            ret = _ConvMFMAFn.apply(inputs, self.weights, self.bias, self.packed_weights(),
-                                    self.stride, pads, fuse_relu, topdown)
-            if self.normalizer_fn is not None:
-                ret = self.normalizer_fn(ret)
+            fuse_relu = norm is None and (is_relu(self.act_fn) or final_relu)
+            relu_after_add = relu_after_add or final_relu
+            if (topdown is not None or residual is not None) and fuse_relu and not relu_after_add:
+                raise ValueError("relu(conv) + add cannot be fused; use relu_after_add")
+            ret = _ConvMFMAFn.apply(inputs, w, b, self.packed_weights(w), self.stride, pads,
+                                    fuse_relu, topdown, residual, relu_after_add)
+            if norm is not None:
+                ret = norm(ret)
             if self.act_fn is not None and not fuse_relu:
                 ret = self.act_fn(ret)
+            if final_relu and not fuse_relu:
+                ret = torch.relu(ret)
             return ret
-        # torch (channels_last) path: backbone / unsupported shapes
+        # torch (channels_last) path: backbone 3x3 convs / the stem
         x = fix_padding(inputs, self.kernel_size, self.padding, self.rate)
-        w = self.weights.permute(3, 2, 0, 1)
-        bias = self.bias
-        norm = self.normalizer_fn
-        if isinstance(norm, BatchNorm):
-            # frozen statistics: fold the affine into the conv (one pass over the map)
-            scale, shift = norm.folded()
-            w = w * scale[:, None, None, None]
-            bias = shift if bias is None else bias * scale + shift
-            norm = None
-        y = F.conv2d(x.permute(0, 3, 1, 2), w.contiguous(memory_format=torch.channels_last),
-                     bias, stride=self.stride, dilation=self.rate, groups=self.num_groups)
+        y = F.conv2d(x.permute(0, 3, 1, 2),
+                     w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last), b,
+                     stride=self.stride, dilation=self.rate, groups=self.num_groups)
         ret = y.permute(0, 2, 3, 1)
         if norm is not None:
             ret = norm(ret)
-        if self.act_fn is not None:
+        has_add = topdown is not None or residual is not None
+        if self.act_fn is not None and not (has_add and relu_after_add):
             ret = self.act_fn(ret)
         if topdown is not None:
             N, H, W, C = ret.shape
             ret = ret + topdown.repeat_interleave(2, 1).repeat_interleave(2, 2)[:, :H, :W]
+        if residual is not None:
+            ret = ret + residual
+        if self.act_fn is not None and has_add and relu_after_add:
+            ret = torch.relu_(ret) if is_relu(self.act_fn) else self.act_fn(ret)
         return ret
 
 
@@ -222,7 +266,7 @@ class ConvTranspose2D(Layer):
             b = self.bias.repeat(k * k) if self.bias is not None else None
             fuse = self.normalizer_fn is None and is_relu(self.act_fn)
             y = _ConvMFMAFn.apply(inputs, wp.permute(0, 1, 3, 2), b, wp.detach().contiguous(), 1,
-                                  (0, 0), fuse, None)
+                                  (0, 0), fuse, None, None, False)
             y = y.reshape(N, H, W, k, k, self.out_channels).permute(0, 1, 3, 2, 4, 5)
             ret = y.reshape(N, H * k, W * k, self.out_channels)
             if self.normalizer_fn is not None:

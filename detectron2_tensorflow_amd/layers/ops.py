@@ -241,8 +241,10 @@ def pack_conv_weights(w_hwio):
 
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
-                residual=None):
-    """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin]."""
+                residual=None, relu_after_add=False):
+    """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
+    relu_after_add: relu(conv + bias + residual/topdown) instead of
+    relu(conv + bias) + residual/topdown."""
     x = _f32c(x)
     _C.require_device(x, w_packed)
     N, H, W, Cin = x.shape
@@ -260,11 +262,15 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                              f"{(N, OH, OW, Cout)}")
     if residual is not None:
         residual = _f32c(residual)
+    flags = (1 if relu else 0) | (2 if relu_after_add else 0)
+    wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
+                                              int(pe))
+    ws = _C.workspace(wsb, x.device) if wsb else None
     ev = KernelTimer.start()
-    rc = _C.lib().d2mi_conv2d_nhwc(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias), _C.ptr(topdown),
-                                   _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
-                                   int(stride), int(pb), int(pe), int(bool(relu)),
-                                   _C.stream_of(x.device))
+    rc = _C.lib().d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias), _C.ptr(topdown),
+                                      _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
+                                      int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
+                                      _C.stream_of(x.device))
     KernelTimer.stop(ev, "conv2d_mfma", 2.0 * N * OH * OW * Cout * KH * KW * Cin)
     _C.check(rc, "d2mi_conv2d_nhwc")
     return y

@@ -34,20 +34,24 @@ class BottleneckBlock(Layer):
     def __init__(self, in_channels, out_channels, bottleneck_channels, stride=1, num_groups=1,
                  stride_in_1x1=False, rate=1, **kwargs):
         super().__init__(in_channels=in_channels, out_channels=out_channels, **kwargs)
+        # 1x1 convs run on the MFMA implicit-GEMM kernel with FrozenBN folded
+        # and ReLU / residual fused in its epilogue; the 3x3 stays on MIOpen.
         self.shortcut = None
         if in_channels != out_channels:
             self.shortcut = Conv2D(in_channels, out_channels, 1, stride=stride, activation=None,
-                                   scope="shortcut")
+                                   impl="mfma", scope="shortcut")
         s1, s3 = (stride, 1) if stride_in_1x1 else (1, stride)
-        self.conv1 = Conv2D(in_channels, bottleneck_channels, 1, stride=s1, scope="conv1")
+        self.conv1 = Conv2D(in_channels, bottleneck_channels, 1, stride=s1, impl="mfma",
+                            scope="conv1")
         self.conv2 = Conv2D(bottleneck_channels, bottleneck_channels, 3, stride=s3,
                             num_groups=num_groups, rate=rate, scope="conv2")
-        self.conv3 = Conv2D(bottleneck_channels, out_channels, 1, activation=None, scope="conv3")
+        self.conv3 = Conv2D(bottleneck_channels, out_channels, 1, activation=None, impl="mfma",
+                            scope="conv3")
 
     def call(self, x):
-        out = self.conv3(self.conv2(self.conv1(x)))
         sc = self.shortcut(x) if self.shortcut is not None else x
-        return torch.relu_(out + sc)
+        # relu(conv3(...) + shortcut) in one kernel
+        return self.conv3(self.conv2(self.conv1(x)), residual=sc.contiguous(), final_relu=True)
 
 
 @add_arg_scope

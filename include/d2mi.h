@@ -213,6 +213,18 @@ int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const float* bias,
                      const float* topdown, const float* residual, float* y, int N, int H, int W,
                      int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
                      int act, void* stream);
+/* Extended form: flags bit0 = ReLU, bit1 = apply the ReLU after the
+ * residual / top-down add (ResNet bottleneck: relu(conv3 + bias + shortcut),
+ * lib/modeling/backbone/blocks.py:143-186).  With a workspace of
+ * d2mi_conv2d_workspace_size() bytes, small-M shapes split K over several
+ * workgroups and reduce in a fixed order (deterministic). */
+size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                                  int stride, int pad_beg, int pad_end);
+int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
+                        const float* topdown, const float* residual, float* y, int N, int H,
+                        int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
+                        int pad_end, int flags, void* workspace, size_t workspace_bytes,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,9 @@ F32 = np.float32
 
 
 def _conv(x_nhwc, layer, relu=None, stride=None):
-    """Reference Conv2D.call on CPU: fix_padding + VALID conv + bias (+ relu)."""
+    """Reference Conv2D.call on CPU (convolutional.py:198-263): fix_padding +
+    VALID conv + bias, then the normalizer (FrozenBN: (x - mean) * gamma /
+    sqrt(var + eps) + beta), then the activation."""
     k = layer.kernel_size
     s = stride or layer.stride
     x = x_nhwc
@@ -37,8 +39,26 @@ def _conv(x_nhwc, layer, relu=None, stride=None):
         x = F.pad(x, (0, 0, pt // 2, pt - pt // 2, pt // 2, pt - pt // 2))
     y = F.conv2d(x.permute(0, 3, 1, 2), layer.weights.permute(3, 2, 0, 1), layer.bias, stride=s)
     y = y.permute(0, 2, 3, 1)
+    bn = layer.normalizer_fn
+    if bn is not None:
+        y = (y - bn.moving_mean) * (bn.gamma / torch.sqrt(bn.moving_variance + bn.epsilon)) + bn.beta
     act = layer.act_fn if relu is None else (torch.relu if relu else None)
     return act(y) if act is not None else y
+
+
+def _backbone(bb, x):
+    """ResNet.call (resnet.py:238-253): stem conv + zero pad + 3x3/2 VALID max
+    pool, then bottlenecks relu(conv3(conv2(conv1(x))) + shortcut(x))."""
+    outs = {}
+    y = _conv(x, bb.stem.conv1)
+    y = F.max_pool2d(F.pad(y.permute(0, 3, 1, 2), (1, 1, 1, 1)), 3, 2).permute(0, 2, 3, 1)
+    for name, stage in zip(bb.stage_names, bb.stages):
+        for blk in stage.blocks:
+            sc = _conv(y, blk.shortcut) if blk.shortcut is not None else y
+            y = torch.relu(_conv(_conv(_conv(y, blk.conv1), blk.conv2), blk.conv3) + sc)
+        if name in bb._out_features:
+            outs[name] = y
+    return outs
 
 
 class CPUReference:
@@ -70,7 +90,7 @@ class CPUReference:
         H, W = x.shape[1:3]
         d = m.neck.size_divisibility
         x = F.pad(x, (0, 0, 0, (-W) % d, 0, (-H) % d))
-        feats = self.fpn(m.backbone(x.contiguous()))
+        feats = self.fpn(_backbone(m.backbone, x.contiguous()))
         rpn = m.proposal_generator
         head = rpn.rpn_head
         N = x.shape[0]

@@ -369,3 +369,26 @@ def test_conv2d_fused_topdown_add(dev):
     y = ops().conv2d_nhwc(x.to(dev), ops().pack_conv_weights(w.to(dev)), b.to(dev),
                           topdown=top.to(dev))
     np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 25, 42, 256, 256, 3, 1, 1), (2, 50, 84, 1024, 64, 1, 2, 0),
+                                   (1, 7, 11, 2048, 15, 1, 1, 0)])
+def test_conv2d_residual_relu_after_and_split_k(dev, shape):
+    """relu(conv + bias + residual) fused (bottleneck epilogue); small-M shapes
+    take the split-K path with the fixed-order reduction (deterministic)."""
+    N, H, W, Cin, Cout, k, stride, pad = shape
+    g = torch.Generator().manual_seed(7 + sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
+    b = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(3, 2, 0, 1).double(),
+                                     b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
+    res = torch.randn(ref.shape, generator=g).float()
+    want = torch.relu(ref + res.double())
+    wp = ops().pack_conv_weights(w.to(dev))
+    y1 = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), stride, (pad, pad), relu=True,
+                           residual=res.to(dev), relu_after_add=True)
+    y2 = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), stride, (pad, pad), relu=True,
+                           residual=res.to(dev), relu_after_add=True)
+    assert torch.equal(y1, y2)
+    np.testing.assert_allclose(y1.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
