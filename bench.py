@@ -1,9 +1,15 @@
 #!/usr/bin/env python
-"""Benchmark: Mask R-CNN R50-FPN inference at 1333x800 on MI355X (img/s).
+"""Benchmark: Mask R-CNN R50-FPN at 1333x800 on MI355X (img/s).
 
-One step = one batched forward of the whole model (BASELINE.json metric
-"img/sec whole-node Mask R-CNN R50-FPN @1333x800") over synthetic COCO-shaped
-images already resident in HBM: ResNet-50 (PyTorch-ROCm convs) -> FPN (MFMA
+Default (--mode train, BASELINE.json config C3 / the north_star target): one
+step = one data-parallel training iteration at 2 images per GPU — forward,
+RPN / Fast R-CNN / mask losses, backward with the bucketed RCCL gradient
+all-reduce overlapped, per-tensor clip and the Momentum-SGD update — over
+synthetic COCO-shaped images + GT already resident in HBM.  value = all
+ranks' images / (max-over-ranks time of K steps), weak scaling.
+
+--mode infer: one step = one batched forward of the whole model over
+synthetic images already resident in HBM: ResNet-50 (PyTorch-ROCm convs) -> FPN (MFMA
 kernels, fused top-down add) -> RPN head (MFMA) + fused top-k/decode/NMS
 proposals -> multi-level ROIAlign 7x7 -> box head (hipBLASLt GEMMs) -> fused
 Fast R-CNN post-processing (softmax/decode/clip/class-offset NMS) -> ROIAlign
@@ -15,7 +21,8 @@ prescribes, the class / objectness logit scales are calibrated once
 score thresholds and NMS see realistic survivor counts (reported).
 
 Multi-GPU: one process per GPU (torchrun), each rank runs its own images
-(inference shards by image: "replicas", no data-path collective), barrier +
+(inference: "replicas", no data-path collective; training: DP with one
+gradient all-reduce per step), barrier +
 synchronize around the timed region, time = max over ranks, value = all
 images / that time (weak scaling).
 """
@@ -51,6 +58,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
     p.add_argument("--cpu-images", type=int, default=1)
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--mode", default="train", choices=["train", "infer"])
+    p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
     return p.parse_args()
 
 
@@ -61,11 +70,12 @@ def build(args, device):
     cfg.merge_from_file(os.path.join(ROOT, CONFIGS[args.model]))
     cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = "raw"
     cfg.SOLVER.IMS_PER_GPU = args.batch
-    finalize(cfg, training=False, world_size=args.gpus,
+    finalize(cfg, training=args.mode == "train", world_size=args.gpus,
              category_map={"num_thing_classes": 80, "num_stuff_classes": 53,
                            "stuff_ignore_value": 0})
     torch.manual_seed(0)
-    model = build_model(cfg).to(device).eval()
+    model = build_model(cfg).to(device)
+    model.train(args.mode == "train")
     return cfg, model
 
 
@@ -86,7 +96,10 @@ def calibrate_scores(model, batch):
     rpn_head = model.proposal_generator.rpn_head
     h2 = rpn_head.conv.register_forward_hook(lambda m, i, o: stats.__setitem__(
         "rpn", float((o.reshape(-1, o.shape[-1]) ** 2).sum(-1).mean())))
+    was = model.training
+    model.eval()
     model.inference(batch)
+    model.train(was)
     h1.remove()
     h2.remove()
     cls = rh.box_predictor.cls_score
@@ -96,10 +109,10 @@ def calibrate_scores(model, batch):
 
 
 def synthetic_batch(args, device, rank):
-    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    img = torch.rand(args.batch, args.height, args.width, 3, generator=g) * 255.0
-    shapes = torch.tensor([[args.height, args.width]] * args.batch, dtype=torch.int32)
-    return {"image": img.to(device), "image_shape": shapes.to(device)}
+    from detectron2_tensorflow_amd.utils.synthetic import synthetic_images, synthetic_train_batch
+    if args.mode == "train":
+        return synthetic_train_batch(args.batch, args.height, args.width, 1000 + rank, device)
+    return synthetic_images(args.batch, args.height, args.width, 1000 + rank, device)
 
 
 def kernel_report(summary):
@@ -128,6 +141,7 @@ def cpu_baseline(args, model, batch):
     from cpu_pipeline import CPUReference, cpu_cores
     cores = cpu_cores()
     ref = CPUReference(model)
+    model.eval()
     n = args.cpu_images
     imgs = batch["image"][:n].cpu().numpy()
     shapes = batch["image_shape"][:n].cpu().numpy()
@@ -135,8 +149,10 @@ def cpu_baseline(args, model, batch):
     t0 = time.perf_counter()
     ref(imgs, shapes, threads=cores)
     dt = time.perf_counter() - t0
+    what = ("inference forward only (the CPU restatement has no backward; a training step "
+            "costs more)" if args.mode == "train" else "inference")
     return {"value": round(n / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
-            "sample": f"{n} image(s) {args.height}x{args.width}, whole {args.model} inference, "
+            "sample": f"{n} image(s) {args.height}x{args.width}, whole {args.model} {what}, "
                       f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU convs), "
                       f"{dt:.1f} s"}
 
@@ -158,17 +174,25 @@ def main():
     cfg, model = build(args, device)
     batch = synthetic_batch(args, device, rank)
     calibrate_scores(model, batch)
+    if args.mode == "train":
+        from detectron2_tensorflow_amd.engine import Trainer
+        trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        step = lambda: trainer.step(batch)
+        grad_ctx = torch.enable_grad
+    else:
+        step = lambda: model.inference(batch)
+        grad_ctx = torch.no_grad
 
-    with torch.no_grad():
+    with grad_ctx():
         for _ in range(args.warmup):
-            out = model.inference(batch)
+            out = step()
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         KernelTimer.reset(enabled=not args.no_kernel_timing)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = model.inference(batch)
+            out = step()
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -180,8 +204,10 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     _C.raise_on_errors(device)
-    inst = out["instances"]
-    survivors = int(inst["is_valid"].sum().item())
+    if args.mode == "train":
+        extra = {"losses_last_step_rank0": {k: round(float(v), 4) for k, v in out.items()}}
+    else:
+        extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 
     if rank == 0:
         kernels = kernel_report(summary)
@@ -198,11 +224,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (U[0,255) images, random-init weights, calibrated logits)",
-            "config": {"workload": f"{args.model} inference {args.width}x{args.height}",
-                       "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                       "parallelism": f"replicas{world}", "mode": "inference",
-                       "detections_per_step_rank0": survivors},
+            "data": "synthetic (U[0,255) images, 7 GT boxes/img + 56x56 mini masks for training, "
+                    "random-init weights, calibrated logits)",
+            "config": dict({"workload": f"{args.model} {'training' if args.mode == 'train' else 'inference'} "
+                                        f"{args.width}x{args.height}",
+                            "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                            "parallelism": (f"dp{world}" if args.mode == "train" else f"replicas{world}"),
+                            "mode": args.mode}, **extra),
             "roofline": kernels.get("conv2d_mfma"),
             "kernels": kernels,
         }

@@ -1,0 +1,114 @@
+"""Bucketed gradient all-reduce overlapped with backward.
+
+Replaces the reference's clone scheme (model_deploy.py:253-299, :408-438),
+where every clone's gradients are summed with add_n on CPU:0 and the
+variables travel host <-> device each step.  Here each rank holds its own
+replica and its own shard of the batch; after backward the gradients of all
+ranks are averaged with RCCL all-reduces (torch.distributed "nccl" backend)
+so every replica applies the same update — the same arithmetic as the
+reference's sum of per-clone losses x 1/num_clones.
+
+Overlap: parameters are packed, in reverse registration order (the order
+backward produces their gradients), into flat fp32 buckets of
+``bucket_bytes``.  A post-accumulate-grad hook copies each gradient
+(pre-scaled by 1/world) into its bucket slot; when every gradient of a bucket
+has arrived the bucket's all-reduce is launched asynchronously on the
+communicator's stream while backward continues.  Buckets are launched
+strictly in index order on every rank (a bucket that completes early waits
+for its predecessors), so the collective sequence is identical across ranks.
+``finish()`` waits for the outstanding collectives and points each .grad at
+its slice of the reduced bucket.
+
+Bucket size: the ~44 M trainable fp32 gradients (~177 MB) of Mask R-CNN R50-FPN
+split into 32 MB buckets give 6 collectives per step — large enough that each
+ring all-reduce runs at xGMI link bandwidth, small enough that the first
+launches early in backward.
+"""
+import torch
+import torch.distributed as dist
+
+
+class _Bucket:
+    __slots__ = ("params", "offsets", "numel", "flat", "pending", "work")
+
+    def __init__(self):
+        self.params, self.offsets, self.numel = [], [], 0
+        self.flat, self.pending, self.work = None, 0, None
+
+
+class BucketedAllReduce:
+    def __init__(self, params, bucket_bytes=32 << 20, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.params = [p for p in params if p.requires_grad]
+        self.buckets = []
+        self.where = {}
+        cur = _Bucket()
+        for p in reversed(self.params):
+            if cur.params and (cur.numel + p.numel()) * 4 > bucket_bytes:
+                self.buckets.append(cur)
+                cur = _Bucket()
+            self.where[p] = (len(self.buckets), len(cur.params))
+            cur.params.append(p)
+            cur.offsets.append(cur.numel)
+            cur.numel += p.numel()
+        if cur.params:
+            self.buckets.append(cur)
+        self._next = 0
+        self._hooks = []
+        if self.world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.reset()
+
+    def reset(self):
+        """Arm for the next backward."""
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+        self._next = 0
+
+    def _flat(self, b, like):
+        if b.flat is None:
+            b.flat = torch.empty(b.numel, dtype=torch.float32, device=like.device)
+        return b.flat
+
+    def _on_grad(self, p):
+        bi, k = self.where[p]
+        b = self.buckets[bi]
+        flat = self._flat(b, p)
+        off = b.offsets[k]
+        torch.mul(p.grad.reshape(-1), 1.0 / self.world, out=flat[off: off + p.numel()])
+        b.pending -= 1
+        self._launch_ready()
+
+    def _launch_ready(self):
+        while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+            b = self.buckets[self._next]
+            b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+            self._next += 1
+
+    def finish(self):
+        """Wait for every bucket and expose the averaged gradients as .grad."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            if b.pending:
+                # a parameter got no gradient this step: contribute zeros (all ranks
+                # take the same branch because the graph is the same on every rank)
+                flat = self._flat(b, b.params[0])
+                for p, off in zip(b.params, b.offsets):
+                    if p.grad is None:
+                        flat[off: off + p.numel()].zero_()
+                b.pending = 0
+        self._launch_ready()
+        for b in self.buckets:
+            b.work.wait()
+            for p, off in zip(b.params, b.offsets):
+                p.grad = b.flat[off: off + p.numel()].view_as(p)
+        self.reset()
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,61 @@
+"""Data-parallel training step (lib/engine/trainer.py:43-199, model_deploy.py:122-438).
+
+One process per GPU.  Each rank runs the model on its own shard of the global
+batch (fixing the reference's shared-batch quirk, trainer.py:63 — SURVEY.md
+section 8a), backward overlaps the bucketed RCCL gradient all-reduce
+(engine/reducer.py), and every rank applies the identical Momentum-SGD update
+(solver/optimizer.py) with the host-side LR schedule (solver/learning_rate.py).
+
+A step enqueues work only: the losses come back as device tensors and the
+caller decides when to synchronise (bench.py brackets K steps with one
+barrier + synchronize on each side).
+"""
+import torch
+import torch.distributed as dist
+
+from ..solver import MomentumSGD, build_learning_rate, param_groups
+from .reducer import BucketedAllReduce
+
+
+def get_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def broadcast_parameters(model, src=0, group=None):
+    """Start every replica from rank src's weights (slim's single variable copy)."""
+    if get_world()[0] == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src, group=group)
+
+
+class Trainer:
+    def __init__(self, cfg, model, bucket_bytes=32 << 20, group=None, start_step=0):
+        self.cfg = cfg
+        self.model = model
+        self.world, self.rank = get_world()
+        broadcast_parameters(model, group=group)
+        self.optimizer = MomentumSGD(param_groups(model, cfg), momentum=cfg.SOLVER.MOMENTUM,
+                                     clip_norm=cfg.SOLVER.CLIP_GRADIENTS_BY_NORM)
+        self.reducer = BucketedAllReduce(self.optimizer.params, bucket_bytes, group)
+        self.lr = build_learning_rate(cfg)
+        self.iter = start_step
+
+    def step(self, batched_inputs):
+        """One iteration: forward + losses, backward with the overlapped
+        all-reduce, clip + momentum update.  Returns the loss dict (device)."""
+        self.model.train()
+        self.optimizer.zero_grad()
+        self.reducer.reset()
+        losses = self.model(batched_inputs)
+        total = sum(losses.values())
+        total.backward()
+        self.reducer.finish()
+        self.optimizer.step(self.lr(self.iter))
+        self.iter += 1
+        losses = dict(losses)
+        losses["total_loss"] = total.detach()
+        return losses

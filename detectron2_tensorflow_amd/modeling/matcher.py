@@ -1,0 +1,90 @@
+"""Matcher (lib/modeling/matcher.py:8-173) and subsample_labels
+(lib/modeling/sampling.py:6-45), batched and dense on the GPU.
+
+Everything works on padded [N, G] ground truth with an ``is_valid`` mask and
+fixed-size outputs, so the training step needs no host synchronisation:
+invalid GT rows never match (their IoU row is -inf), and the random subsample
+picks the k smallest of per-element uniform keys among the candidates
+(equivalent in distribution to tf.random_shuffle(...)[:k]).
+"""
+import torch
+
+
+def pairwise_iou(boxes1, boxes2):
+    """box_list_ops.pairwise_iou (:295-372) batched: [N, G, 4] x [N, P, 4] -> [N, G, P];
+    0 where the union is 0."""
+    y1a, x1a, y2a, x2a = boxes1.unbind(-1)
+    y1b, x1b, y2b, x2b = boxes2.unbind(-1)
+    ih = (torch.minimum(y2a[..., :, None], y2b[..., None, :]) -
+          torch.maximum(y1a[..., :, None], y1b[..., None, :])).clamp(min=0.0)
+    iw = (torch.minimum(x2a[..., :, None], x2b[..., None, :]) -
+          torch.maximum(x1a[..., :, None], x1b[..., None, :])).clamp(min=0.0)
+    inter = ih * iw
+    area_a = (y2a - y1a) * (x2a - x1a)
+    area_b = (y2b - y1b) * (x2b - x1b)
+    union = area_a[..., :, None] + area_b[..., None, :] - inter
+    return torch.where(union == 0, torch.zeros_like(union), inter / union)
+
+
+class Matcher:
+    def __init__(self, thresholds, labels, allow_low_quality_matches=False):
+        thresholds = [-float("inf")] + list(thresholds) + [float("inf")]
+        assert all(lo <= hi for lo, hi in zip(thresholds[:-1], thresholds[1:]))
+        assert all(lb in (-1, 0, 1) for lb in labels)
+        assert len(labels) == len(thresholds) - 1
+        self.thresholds = thresholds
+        self.labels = list(labels)
+        self.allow_low_quality_matches = allow_low_quality_matches
+
+    def __call__(self, quality, gt_valid, crowd_quality=None, difficult_quality=None):
+        """quality [N, G, P] (rows of invalid GT are ignored), gt_valid [N, G];
+        crowd_quality / difficult_quality [N, G, P] with zero rows for GT that are
+        not crowd / difficult (matcher.py:114-139).
+        Returns matches [N, P] (int64 GT index) and labels [N, P] in {-1, 0, 1}."""
+        q = torch.where(gt_valid[..., None], quality, torch.full_like(quality, -float("inf")))
+        vals, matches = q.max(dim=1)
+        any_gt = gt_valid.any(dim=1, keepdim=True)
+        labels = torch.zeros_like(matches)
+        for lb, lo, hi in zip(self.labels, self.thresholds[:-1], self.thresholds[1:]):
+            labels = torch.where((vals >= lo) & (vals < hi), torch.full_like(labels, lb), labels)
+        if self.allow_low_quality_matches:
+            best = q.max(dim=2, keepdim=True).values  # [N, G, 1]
+            hit = ((q == best) & gt_valid[..., None]).any(dim=1)
+            labels = torch.where(hit, torch.ones_like(labels), labels)
+        # no valid GT: every prediction is background (matcher.py:119-125)
+        labels = torch.where(any_gt, labels, torch.zeros_like(labels))
+        matches = torch.where(any_gt, matches, torch.zeros_like(matches))
+        if crowd_quality is not None:
+            crowd = (crowd_quality.max(dim=1).values > 1e-3) if crowd_quality.shape[1] else None
+            if crowd is not None:
+                labels = torch.where((labels == 0) & crowd, torch.full_like(labels, -1), labels)
+        if difficult_quality is not None and difficult_quality.shape[1]:
+            diff = difficult_quality.max(dim=1).values > self.thresholds[1]
+            labels = torch.where((labels == 0) & diff, torch.full_like(labels, -1), labels)
+        return matches, labels
+
+
+def subsample_labels(labels, num_samples, positive_fraction, bg_label, generator=None):
+    """Dense subsample_labels over [N, P]: returns (pos_mask, neg_mask) [N, P] bool
+    with min(#pos, int(num_samples * fraction)) positives and
+    min(#neg, num_samples - #pos_taken) negatives chosen uniformly at random."""
+    N, P = labels.shape
+    positive = (labels != -1) & (labels != bg_label)
+    negative = labels == bg_label
+    num_pos = int(num_samples * positive_fraction)
+    keys = torch.rand((N, P), device=labels.device, generator=generator)
+    pos_rank = _rank(keys, positive)
+    pos_sel = positive & (pos_rank < num_pos)
+    n_pos = pos_sel.sum(dim=1, keepdim=True)
+    neg_rank = _rank(torch.rand((N, P), device=labels.device, generator=generator), negative)
+    neg_sel = negative & (neg_rank < (num_samples - n_pos))
+    return pos_sel, neg_sel
+
+
+def _rank(keys, mask):
+    """rank of each masked element among the masked elements by ascending key."""
+    k = torch.where(mask, keys, torch.full_like(keys, 2.0))
+    order = k.argsort(dim=1)
+    rank = torch.empty_like(order)
+    rank.scatter_(1, order, torch.arange(k.shape[1], device=k.device).expand_as(order))
+    return rank

@@ -6,6 +6,12 @@ normalises, THEN flips to BGR when INPUT_FORMAT == "BGR", then zero-pads to
 the neck's size divisibility (rcnn.py:146-157, image_list.py:89-100).
 Inference returns {"instances": {boxes, classes, scores, is_valid[, masks]}}
 as dense [N, DETECTIONS_PER_IMAGE] tensors (fields.ResultFields names).
+
+Training (rcnn.py:62-90) takes batched_inputs["instances"] as a dict of dense
+padded ground truth: gt_boxes [N, G, 4] (y1, x1, y2, x2, absolute),
+gt_classes [N, G] (0-based), is_valid [N, G], optional gt_is_crowd /
+gt_difficult [N, G] and gt_masks [N, G, 56, 56] mini masks (MASK_ON), and
+returns the dict of scalar losses.
 """
 import torch
 
@@ -59,8 +65,18 @@ class GeneralizedRCNN(_Preprocess, Layer):
     def call(self, batched_inputs):
         if not self.training:
             return self.inference(batched_inputs)
-        raise NotImplementedError("GeneralizedRCNN training step lands with the RPN / ROI-head "
-                                  "losses (SURVEY.md section 8f, F2)")
+        images = self.preprocess_image(batched_inputs)
+        gt = batched_inputs.get("instances", batched_inputs.get("targets"))
+        features = self.neck(self.backbone(images.tensor))
+        if self.proposal_generator is not None:
+            proposals, proposal_losses, _ = self.proposal_generator(images, features, gt)
+        else:
+            proposals, proposal_losses = batched_inputs["proposals"], {}
+        _, detector_losses = self.roi_heads(images, features, proposals, gt)
+        losses = {}
+        losses.update(detector_losses)
+        losses.update(proposal_losses)
+        return losses
 
     def inference(self, batched_inputs, detected_instances=None):
         assert not self.training
@@ -97,7 +113,8 @@ class ProposalNetwork(_Preprocess, Layer):
     def call(self, batched_inputs):
         images = self.preprocess_image(batched_inputs)
         features = self.neck(self.backbone(images.tensor))
-        proposals, losses, _ = self.proposal_generator(images, features, None)
+        gt = batched_inputs.get("instances") if self.training else None
+        proposals, losses, _ = self.proposal_generator(images, features, gt)
         if self.training:
             return losses
         return {"proposals": {"boxes": proposals.boxes,

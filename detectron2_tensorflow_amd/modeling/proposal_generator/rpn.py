@@ -11,6 +11,8 @@ import torch
 from ...layers import Conv2D, Layer
 from ...layers import initializers as init
 from ...layers import ops
+from ...layers.loss import smooth_l1_loss
+from ..matcher import Matcher, pairwise_iou, subsample_labels
 from ...structures import BoxList
 from ...utils.arg_scope import arg_scope
 from ...utils.registry import Registry
@@ -89,16 +91,69 @@ class RPN(Layer):
         shapes = [input_shape[f] for f in self.in_features]
         self.anchor_generator = build_anchor_generator(cfg, shapes)
         self.box2box_transform = Box2BoxTransform(weights=r.BBOX_REG_WEIGHTS)
+        self.anchor_matcher = Matcher(r.IOU_THRESHOLDS, r.IOU_LABELS, allow_low_quality_matches=True)
         with arg_scope([Conv2D], weights_initializer=init.random_normal(0.01)):
             self.rpn_head = build_rpn_head(cfg, shapes, scope="rpn_head")
+
+    def _all_anchors(self, feats):
+        """Level-major concatenation of the grid anchors (box_list_ops.concatenate
+        of anchor_generator(features), rpn_outputs.py:253), cached per grid."""
+        key = tuple((f.shape[1], f.shape[2]) for f in feats) + (str(feats[0].device),)
+        if getattr(self, "_anchor_key", None) != key:
+            grids = [(f.shape[1], f.shape[2]) for f in feats]
+            self._anchors = torch.cat(self.anchor_generator.grid_anchors(grids, feats[0].device))
+            self._anchor_key = key
+        return self._anchors
+
+    def losses(self, images, feats, logits, deltas, gt):
+        """RPNOutputs.losses (rpn_outputs.py:306-401): IoU(GT, all anchors),
+        Matcher(0.3/0.7, low-quality), subsample 256 @ 0.5, sigmoid CE + smooth-L1,
+        both summed and normalised by BATCH_SIZE_PER_IMAGE * N."""
+        anchors = self._all_anchors(feats)
+        N = logits[0].shape[0]
+        gt_boxes = gt["gt_boxes"]
+        valid = gt["is_valid"]
+        crowd = gt.get("gt_is_crowd")
+        crowd = crowd.bool() if crowd is not None else torch.zeros_like(valid)
+        iou = pairwise_iou(gt_boxes, anchors[None].expand(N, -1, -1))
+        crowd_q = torch.where(crowd[..., None], iou, torch.zeros_like(iou))
+        matches, labels = self.anchor_matcher(iou, valid & ~crowd, crowd_q)
+        if self.boundary_threshold >= 0:
+            # legacy inside_window filter (rpn_outputs.py:268-277, box_list_ops.py:150)
+            t = float(self.boundary_threshold)
+            hw = images.image_shapes.to(anchors.dtype)
+            inside = ((anchors[None, :, 0] >= -t) & (anchors[None, :, 1] >= -t) &
+                      (anchors[None, :, 2] <= hw[:, :1] + t) & (anchors[None, :, 3] <= hw[:, 1:2] + t))
+            labels = torch.where(inside, labels, torch.full_like(labels, -1))
+        pos, neg = subsample_labels(labels, self.batch_size_per_image, self.positive_fraction, 0)
+        matched = torch.gather(gt_boxes, 1, matches[..., None].expand(-1, -1, 4))
+        gt_deltas = self.box2box_transform.get_deltas(
+            anchors[None].expand(N, -1, -1).reshape(-1, 4), matched.reshape(-1, 4)).reshape(N, -1, 4)
+        # only positive rows carry targets (dynamic_stitch of zeros, rpn_outputs.py:286-290);
+        # other rows may be matched to padded GT whose log-size is -inf
+        gt_deltas = torch.where(pos[..., None], gt_deltas, torch.zeros_like(gt_deltas))
+        pl = torch.cat([x.reshape(N, -1) for x in logits], dim=1)
+        pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
+        sampled = pos | neg
+        obj = torch.nn.functional.binary_cross_entropy_with_logits(
+            pl, pos.to(pl.dtype), reduction="none")
+        loss_cls = torch.where(sampled, obj, torch.zeros_like(obj)).sum()
+        loc = smooth_l1_loss(labels=gt_deltas, predictions=pd, beta=self.smooth_l1_beta)
+        loss_loc = torch.where(pos[..., None], loc, torch.zeros_like(loc)).sum()
+        norm = 1.0 / (self.batch_size_per_image * N)
+        return {"loss_rpn_cls": loss_cls * norm * self.loss_weight,
+                "loss_rpn_loc": loss_loc * norm * self.loss_weight}
 
     def call(self, images, features, gt_instances=None):
         feats = [features[f] for f in self.in_features]
         rpn_features, logits, deltas = self.rpn_head(feats)
-        if self.training:
-            raise NotImplementedError("RPN training losses (matcher/sampler) are a later round "
-                                      "(SURVEY.md section 8f, F2)")
         losses = {}
+        if self.training:
+            if gt_instances is None:
+                raise ValueError("RPN training needs gt_instances")
+            losses = self.losses(images, feats, logits, deltas, gt_instances)
+            logits = [x.detach() for x in logits]
+            deltas = [x.detach() for x in deltas]
         boxes, scores, valid = ops.rpn_proposals(
             logits, deltas, self.anchor_generator.strides, self.anchor_generator.cell_anchors,
             images.image_shapes, self.pre_nms_topk[self.training],

@@ -8,6 +8,7 @@ import numpy as np
 from ...layers import Layer, Linear
 from ...layers import initializers as init
 from ...layers import ops
+from ...layers.loss import smooth_l1_loss
 
 
 class FastRCNNOutputLayers(Layer):
@@ -43,3 +44,29 @@ def fast_rcnn_inference(pred_class_logits, pred_proposal_deltas, proposal_boxes,
                                    box2box_transform.weights, score_thresh, nms_thresh,
                                    topk_per_image, cls_agnostic=agnostic,
                                    scale_clamp=box2box_transform.scale_clamp)
+
+
+def fast_rcnn_losses(pred_class_logits, pred_proposal_deltas, proposal_boxes, gt_classes,
+                     gt_boxes, valid, box2box_transform, smooth_l1_beta):
+    """FastRCNNOutputs.losses on dense rows (fast_rcnn.py:269-357).
+
+    Rows with ``valid`` False are the padding of the fixed [N * BATCH_SIZE_PER_IMAGE]
+    layout and take no part (the reference drops them with SparseBoxList).
+    loss_cls = mean softmax CE over the R valid rows; loss_box_reg = smooth-L1 of
+    the gt-class deltas of foreground rows, summed, / R.  Both 0 when R == 0."""
+    import torch
+    K = pred_class_logits.shape[1] - 1
+    R = valid.sum().clamp(min=1).to(pred_class_logits.dtype)
+    cls = torch.where(valid, gt_classes, torch.zeros_like(gt_classes)).long()
+    ce = torch.nn.functional.cross_entropy(pred_class_logits, cls, reduction="none")
+    loss_cls = torch.where(valid, ce, torch.zeros_like(ce)).sum() / R
+    fg = valid & (gt_classes >= 0) & (gt_classes < K)
+    nreg = pred_proposal_deltas.shape[1] // 4
+    pred = pred_proposal_deltas.reshape(-1, nreg, 4)
+    col = torch.zeros_like(cls) if nreg == 1 else torch.where(fg, cls, torch.zeros_like(cls))
+    pred = torch.gather(pred, 1, col[:, None, None].expand(-1, 1, 4))[:, 0]
+    target = box2box_transform.get_deltas(proposal_boxes, gt_boxes)
+    target = torch.where(fg[:, None], target, torch.zeros_like(target))
+    l1 = smooth_l1_loss(labels=target, predictions=pred, beta=smooth_l1_beta)
+    loss_box = torch.where(fg[:, None], l1, torch.zeros_like(l1)).sum() / R
+    return {"loss_cls": loss_cls, "loss_box_reg": loss_box}

@@ -25,6 +25,38 @@ def mask_rcnn_inference(pred_mask_logits, pred_classes):
     return torch.sigmoid(logits)
 
 
+def mask_rcnn_loss(pred_mask_logits, boxes, gt_boxes, gt_classes, gt_masks, mask_ind, fg,
+                   use_mini_masks):
+    """mask_head.py:17-68 on dense rows.
+
+    pred_mask_logits [B, Hm, Wm, C]; boxes / gt_boxes [B, 4] (proposal, matched GT);
+    gt_classes [B]; gt_masks [M, h, w] (mini masks when use_mini_masks); mask_ind [B]
+    row of gt_masks per ROI; fg [B] rows that count (the foreground proposals).
+    Targets: tf.image.crop_and_resize of the GT mask to Hm x Wm (ROI coordinates
+    normalised to the GT box for mini masks), rounded; loss: mean sigmoid CE of the
+    GT-class channel over fg rows x Hm x Wm (0 with no foreground)."""
+    from ...layers.functional import tf_crop_and_resize
+    B, Hm, Wm, C = pred_mask_logits.shape
+    if use_mini_masks:
+        gy1, gx1, gy2, gx2 = gt_boxes.unbind(-1)
+        gh, gw = gy2 - gy1, gx2 - gx1
+        y1, x1, y2, x2 = boxes.unbind(-1)
+        boxes = torch.stack([(y1 - gy1) / gh, (x1 - gx1) / gw, (y2 - gy1) / gh, (x2 - gx1) / gw], 1)
+    masks = gt_masks.to(torch.float32)[..., None].contiguous()
+    ind = torch.where(fg, mask_ind, torch.zeros_like(mask_ind)).to(torch.int32)
+    with torch.no_grad():
+        target = tf_crop_and_resize(masks, boxes.detach().contiguous(), ind, (Hm, Wm))
+        target = torch.round(target[..., 0])
+    if C == 1:
+        logits = pred_mask_logits[..., 0]
+    else:
+        cls = torch.where(fg, gt_classes, torch.zeros_like(gt_classes)).clamp(0, C - 1).long()
+        logits = torch.gather(pred_mask_logits, 3, cls[:, None, None, None].expand(B, Hm, Wm, 1))[..., 0]
+    bce = torch.nn.functional.binary_cross_entropy_with_logits(logits, target, reduction="none")
+    n = (fg.sum() * (Hm * Wm)).clamp(min=1).to(bce.dtype)
+    return torch.where(fg[:, None, None], bce, torch.zeros_like(bce)).sum() / n
+
+
 @ROI_MASK_HEAD_REGISTRY.register()
 class MaskRCNNConvUpsampleHead(Layer):
     def __init__(self, cfg, input_shape, **kwargs):

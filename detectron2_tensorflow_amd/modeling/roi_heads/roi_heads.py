@@ -1,4 +1,4 @@
-"""ROIHeads / StandardROIHeads (lib/modeling/roi_heads/roi_heads.py:66-605), inference.
+"""ROIHeads / StandardROIHeads (lib/modeling/roi_heads/roi_heads.py:66-605).
 
 Dense, synchronisation-free layout: the RPN hands over [N, P] proposals with
 an is_valid mask; every slot is pooled (invalid slots pool a zero box and are
@@ -15,8 +15,9 @@ from ...utils.registry import Registry
 from ..box_regression import Box2BoxTransform
 from ..poolers import ROIPooler
 from .box_head import build_box_head
-from .fast_rcnn import FastRCNNOutputLayers, fast_rcnn_inference
-from .mask_head import build_mask_head, mask_rcnn_inference
+from ..matcher import Matcher, pairwise_iou, subsample_labels
+from .fast_rcnn import FastRCNNOutputLayers, fast_rcnn_inference, fast_rcnn_losses
+from .mask_head import build_mask_head, mask_rcnn_inference, mask_rcnn_loss
 
 from ...layers import Layer
 
@@ -45,6 +46,55 @@ class ROIHeads(Layer):
         self.cls_agnostic_bbox_reg = cfg.MODEL.ROI_BOX_HEAD.CLS_AGNOSTIC_BBOX_REG
         self.smooth_l1_beta = cfg.MODEL.ROI_BOX_HEAD.SMOOTH_L1_BETA
         self.box2box_transform = Box2BoxTransform(weights=cfg.MODEL.ROI_BOX_HEAD.BBOX_REG_WEIGHTS)
+        self.proposal_matcher = Matcher(h.IOU_THRESHOLDS, h.IOU_LABELS,
+                                        allow_low_quality_matches=False)
+
+    def label_and_sample_proposals(self, proposals, targets):
+        """roi_heads.py:100-232 batched: append GT (proposal_utils.py:7-60), match
+        (crowd -> ignore bg, difficult -> ignore bg above the threshold), gt_classes
+        (fg class / bg = NUM_CLASSES / -1), subsample, fg-first order, pad.
+        Returns a dict of [N, S] tensors: boxes, gt_classes, gt_boxes, gt_index
+        (matched GT row), is_valid."""
+        boxes = proposals.boxes
+        pvalid = proposals.get_field("is_valid")
+        gt_boxes = targets["gt_boxes"]
+        gvalid = targets["is_valid"].bool()
+        N, G = gvalid.shape
+        zeros = torch.zeros_like(gvalid)
+        crowd = targets.get("gt_is_crowd", zeros).bool()
+        difficult = targets.get("gt_difficult", zeros).bool()
+        if self.proposal_append_gt:
+            boxes = torch.cat([boxes, gt_boxes.to(boxes.dtype)], dim=1)
+            pvalid = torch.cat([pvalid, gvalid], dim=1)
+        M = boxes.shape[1]
+        iou = pairwise_iou(gt_boxes, boxes)
+        zq = torch.zeros_like(iou)
+        matches, labels = self.proposal_matcher(
+            iou, gvalid & ~crowd & ~difficult, torch.where(crowd[..., None], iou, zq),
+            torch.where(difficult[..., None], iou, zq))
+        K = self.num_classes
+        gcls = torch.gather(targets["gt_classes"].long(), 1, matches)
+        gt_classes = torch.where(labels == 1, gcls,
+                                 torch.where(labels == 0, torch.full_like(gcls, K),
+                                             torch.full_like(gcls, -1)))
+        gt_classes = torch.where(pvalid, gt_classes, torch.full_like(gt_classes, -1))
+        pos, neg = subsample_labels(gt_classes, self.batch_size_per_image,
+                                    self.positive_sample_fraction, K)
+        S = self.batch_size_per_image
+        ar = torch.arange(M, device=boxes.device)
+        key = torch.where(pos, 0, torch.where(neg, 1, 2)) * M + ar
+        if M < S:
+            key = torch.cat([key, torch.full((N, S - M), 3 * M, dtype=key.dtype,
+                                             device=key.device)], dim=1)
+        key = key.sort(dim=1).values[:, :S]
+        valid = key < 2 * M
+        order = torch.where(valid, key % M, torch.zeros_like(key))
+        take = lambda t: torch.gather(t, 1, order)
+        take4 = lambda t: torch.gather(t, 1, order[..., None].expand(-1, -1, 4))
+        gidx = take(matches)
+        return {"boxes": take4(boxes), "gt_classes": take(gt_classes), "gt_index": gidx,
+                "gt_boxes": torch.gather(gt_boxes, 1, gidx[..., None].expand(-1, -1, 4)),
+                "is_valid": valid}
 
 
 @ROI_HEADS_REGISTRY.register()
@@ -81,10 +131,15 @@ class StandardROIHeads(ROIHeads):
                                                         height=m.POOLER_RESOLUTION), scope="mask_head")
 
     def call(self, images, features, proposals, targets=None):
-        if self.training:
-            raise NotImplementedError("ROI-head training (label_and_sample_proposals, losses) is "
-                                      "a later round (SURVEY.md section 8f, F2)")
         feats = [features[f] for f in self.in_features]
+        if self.training:
+            if targets is None:
+                raise ValueError("ROI-head training needs targets")
+            sampled = self.label_and_sample_proposals(proposals, targets)
+            losses = self._box_losses(feats, sampled)
+            if self.mask_on:
+                losses["loss_mask"] = self._mask_loss(feats, sampled, targets)
+            return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
         pred = self.forward_with_given_boxes(features, pred)
         return pred, {}
@@ -110,6 +165,35 @@ class StandardROIHeads(ROIHeads):
         res.add_field("is_valid", ov)
         res.set_tracking("image_shape", image_shapes)
         return res
+
+    def _box_losses(self, feats, sampled):
+        boxes = sampled["boxes"]
+        N, S = boxes.shape[:2]
+        img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(S)
+        x = self.box_pooler.pool(feats, boxes.reshape(-1, 4).contiguous(), img)
+        logits, deltas = self.box_predictor(self.box_head(x))
+        return fast_rcnn_losses(logits, deltas, boxes.reshape(-1, 4), sampled["gt_classes"].reshape(-1),
+                                sampled["gt_boxes"].reshape(-1, 4), sampled["is_valid"].reshape(-1),
+                                self.box2box_transform, self.smooth_l1_beta)
+
+    def _mask_loss(self, feats, sampled, targets):
+        """_forward_mask training branch (roi_heads.py:594-600) over the first
+        int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
+        foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
+        F_ = int(self.batch_size_per_image * self.positive_sample_fraction)
+        boxes = sampled["boxes"][:, :F_].contiguous()
+        N = boxes.shape[0]
+        cls = sampled["gt_classes"][:, :F_]
+        fg = sampled["is_valid"][:, :F_] & (cls >= 0) & (cls < self.num_classes)
+        img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(F_)
+        x = self.mask_pooler.pool(feats, boxes.reshape(-1, 4), img)
+        _, logits = self.mask_head(x)
+        gm = targets["gt_masks"]
+        G = gm.shape[1]
+        mind = sampled["gt_index"][:, :F_] + torch.arange(N, device=boxes.device)[:, None] * G
+        return mask_rcnn_loss(logits, boxes.reshape(-1, 4), sampled["gt_boxes"][:, :F_].reshape(-1, 4),
+                              cls.reshape(-1), gm.reshape(N * G, *gm.shape[2:]), mind.reshape(-1),
+                              fg.reshape(-1), self.use_mini_masks)
 
     def forward_with_given_boxes(self, features, instances, image_shape=None):
         assert not self.training

@@ -1,0 +1,48 @@
+"""Synthetic COCO-shaped batches for bench / tests.
+
+Images U[0, 255) at the padded-to-/32 size, and for training 7 GT boxes per
+image with log-uniform sqrt(area) in [32, 512], log-uniform aspect ratio in
+[0.5, 2], centres uniform inside the image (boxes clipped to it), classes
+U{0..K-1}, and box-filled 56x56 mini masks (all ones, the shape
+TRANSFORM.RESIZE.USE_MINI_MASKS produces).  Seeded; generated on the host
+once and moved to the device, so the timed region reads it from HBM.
+"""
+import numpy as np
+import torch
+
+
+def synthetic_images(batch, height, width, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    img = torch.rand(batch, height, width, 3, generator=g) * 255.0
+    shapes = torch.tensor([[height, width]] * batch, dtype=torch.int32)
+    return {"image": img.to(device), "image_shape": shapes.to(device)}
+
+
+def synthetic_instances(batch, height, width, seed, device, num_gt=7, num_classes=80,
+                        mask_size=56, sqrt_area=(32.0, 512.0)):
+    rng = np.random.default_rng(seed)
+    n = batch * num_gt
+    s = np.exp(rng.uniform(np.log(sqrt_area[0]), np.log(sqrt_area[1]), n))
+    r = np.exp(rng.uniform(np.log(0.5), np.log(2.0), n))  # h / w
+    h, w = s * np.sqrt(r), s / np.sqrt(r)
+    cy, cx = rng.uniform(0, height, n), rng.uniform(0, width, n)
+    boxes = np.stack([np.clip(cy - h / 2, 0, height), np.clip(cx - w / 2, 0, width),
+                      np.clip(cy + h / 2, 0, height), np.clip(cx + w / 2, 0, width)], 1)
+    # keep every box at least 4 px on a side after clipping
+    boxes[:, 2] = np.maximum(boxes[:, 2], boxes[:, 0] + 4)
+    boxes[:, 3] = np.maximum(boxes[:, 3], boxes[:, 1] + 4)
+    inst = {
+        "gt_boxes": torch.from_numpy(boxes.astype(np.float32).reshape(batch, num_gt, 4)),
+        "gt_classes": torch.from_numpy(rng.integers(0, num_classes, (batch, num_gt))),
+        "is_valid": torch.ones(batch, num_gt, dtype=torch.bool),
+        "gt_is_crowd": torch.zeros(batch, num_gt, dtype=torch.bool),
+        "gt_difficult": torch.zeros(batch, num_gt, dtype=torch.bool),
+        "gt_masks": torch.ones(batch, num_gt, mask_size, mask_size, dtype=torch.uint8),
+    }
+    return {k: v.to(device) for k, v in inst.items()}
+
+
+def synthetic_train_batch(batch, height, width, seed, device, **kw):
+    out = synthetic_images(batch, height, width, seed, device)
+    out["instances"] = synthetic_instances(batch, height, width, seed, device, **kw)
+    return out

@@ -1,0 +1,187 @@
+"""ORACLE (training targets and losses) — test infrastructure only.
+
+Per-image numpy restatement of the reference's training-target glue, written
+the way the reference writes it (boolean_mask of the valid GT, one image at a
+time, dynamic_stitch of label groups), so the batched/dense GPU versions in
+detectron2_tensorflow_amd.modeling can be checked against it.  float32
+throughout.  Randomness (subsample_labels' random_shuffle) is not restated:
+tests use inputs where every candidate is sampled, which makes the reference
+deterministic.
+
+Parity status: restated from the reference source (cited per function);
+unpinned by reference-run vectors (TensorFlow cannot run here).
+"""
+import numpy as np
+
+from oracle import crop_and_resize_tf
+
+F32 = np.float32
+
+
+def pairwise_iou(b1, b2):
+    """box_list_ops.py:295-331 (iou_type 'iou')."""
+    b1 = np.asarray(b1, F32).reshape(-1, 4)
+    b2 = np.asarray(b2, F32).reshape(-1, 4)
+    ih = np.maximum(F32(0), np.minimum(b1[:, None, 2], b2[None, :, 2]) -
+                    np.maximum(b1[:, None, 0], b2[None, :, 0]))
+    iw = np.maximum(F32(0), np.minimum(b1[:, None, 3], b2[None, :, 3]) -
+                    np.maximum(b1[:, None, 1], b2[None, :, 1]))
+    inter = ih * iw
+    a1 = (b1[:, 2] - b1[:, 0]) * (b1[:, 3] - b1[:, 1])
+    a2 = (b2[:, 2] - b2[:, 0]) * (b2[:, 3] - b2[:, 1])
+    union = a1[:, None] + a2[None, :] - inter
+    with np.errstate(divide="ignore", invalid="ignore"):
+        iou = np.where(union == 0, F32(0), inter / union).astype(F32)
+    return iou
+
+
+def matcher(quality, thresholds, labels, allow_low_quality_matches, crowd=None, difficult=None):
+    """Matcher.__call__ (matcher.py:55-139) on an [M, N] matrix of VALID GT."""
+    thr = [-np.inf] + list(thresholds) + [np.inf]
+    M, N = quality.shape
+    if M > 0:
+        matches = np.argmax(quality, axis=0).astype(np.int64)
+        vals = quality.max(axis=0)
+        lab = np.zeros(N, np.int64)
+        for lb, lo, hi in zip(labels, thr[:-1], thr[1:]):
+            lab[(vals >= lo) & (vals < hi)] = lb
+        if allow_low_quality_matches:
+            # get_low_quality_matches_ (matcher.py:141-173), ties included
+            best = quality.max(axis=1)
+            _, preds = np.nonzero(quality == best[:, None])
+            lab[preds] = 1
+    else:
+        matches = np.zeros(N, np.int64)
+        lab = np.zeros(N, np.int64)
+    if crowd is not None and crowd.shape[0] > 0:
+        lab[(lab == 0) & (crowd.max(axis=0) > 1e-3)] = -1
+    if difficult is not None and difficult.shape[0] > 0:
+        lab[(lab == 0) & (difficult.max(axis=0) > thr[1])] = -1
+    return matches, lab
+
+
+def get_deltas(src, tgt, weights):
+    """Box2BoxTransform.get_deltas (box_regression.py:38-74)."""
+    src = np.asarray(src, F32)
+    tgt = np.asarray(tgt, F32)
+    sh = src[:, 2] - src[:, 0]
+    sw = src[:, 3] - src[:, 1]
+    scy = src[:, 0] + F32(0.5) * sh
+    scx = src[:, 1] + F32(0.5) * sw
+    th = tgt[:, 2] - tgt[:, 0]
+    tw = tgt[:, 3] - tgt[:, 1]
+    tcy = tgt[:, 0] + F32(0.5) * th
+    tcx = tgt[:, 1] + F32(0.5) * tw
+    wy, wx, wh, ww = [F32(w) for w in weights]
+    return np.stack([wy * (tcy - scy) / sh, wx * (tcx - scx) / sw,
+                     wh * np.log(th / sh), ww * np.log(tw / sw)], 1).astype(F32)
+
+
+def rpn_targets(anchors, gt_boxes, is_valid, is_crowd, weights, thresholds, labels,
+                image_shape=None, boundary_threshold=-1):
+    """RPNOutputs._get_ground_truth, one image (rpn_outputs.py:255-290)."""
+    valid = is_valid & ~is_crowd
+    vgt = gt_boxes[valid]
+    iou = pairwise_iou(vgt, anchors)
+    crowd = pairwise_iou(gt_boxes[is_crowd], anchors)
+    matches, lab = matcher(iou, thresholds, labels, True, crowd)
+    if boundary_threshold >= 0:
+        t = boundary_threshold
+        inside = ~((anchors[:, 0] < -t) | (anchors[:, 1] < -t) |
+                   (anchors[:, 2] > image_shape[0] + t) | (anchors[:, 3] > image_shape[1] + t))
+        lab = np.where(inside, lab, -1)
+    deltas = np.zeros_like(anchors, dtype=F32)
+    pos = np.nonzero(lab > 0)[0]
+    if len(pos):
+        deltas[pos] = get_deltas(anchors[pos], vgt[matches[pos]], weights)
+    return lab, deltas
+
+
+def rpn_losses(labels, gt_deltas, pred_logits, pred_deltas, num_images, batch_size_per_image):
+    """rpn_losses (rpn_outputs.py:135-185) with beta = 0 plus the normaliser
+    (:396-399); labels already subsampled (-1 = not sampled)."""
+    pos = labels == 1
+    loc = np.abs(gt_deltas[pos] - pred_deltas[pos]).astype(np.float64).sum()
+    v = labels >= 0
+    x = pred_logits[v].astype(np.float64)
+    z = labels[v].astype(np.float64)
+    # sigmoid_cross_entropy_with_logits: max(x, 0) - x * z + log(1 + exp(-|x|))
+    obj = (np.maximum(x, 0) - x * z + np.log1p(np.exp(-np.abs(x)))).sum()
+    norm = 1.0 / (batch_size_per_image * num_images)
+    return obj * norm, loc * norm
+
+
+def label_proposals(proposals, p_valid, gt_boxes, gt_classes, is_valid, is_crowd, difficult,
+                    num_classes, iou_threshold, append_gt=True):
+    """label_and_sample_proposals before sampling, one image (roi_heads.py:130-180).
+    Returns (kept proposal boxes, gt_classes per proposal, matched GT box)."""
+    if append_gt:  # proposal_utils.py:31-45 (all GT rows appended, validity kept)
+        proposals = np.concatenate([proposals, gt_boxes])
+        p_valid = np.concatenate([p_valid, is_valid])
+    vb = is_valid & ~is_crowd & ~difficult
+    vgt, vcls = gt_boxes[vb], gt_classes[vb]
+    props = proposals[p_valid]
+    iou = pairwise_iou(vgt, props)
+    matches, lab = matcher(iou, [iou_threshold], [0, 1], False,
+                           pairwise_iou(gt_boxes[is_crowd], props),
+                           pairwise_iou(gt_boxes[difficult], props))
+    cls = np.full(len(props), -1, np.int64)
+    cls[lab == 1] = vcls[matches[lab == 1]] if len(vcls) else 0
+    cls[lab == 0] = num_classes
+    mgt = vgt[matches] if len(vgt) else np.zeros_like(props)
+    return props, cls, mgt
+
+
+def fast_rcnn_losses(logits, deltas, proposals, gt_classes, gt_boxes, weights):
+    """FastRCNNOutputs.losses (fast_rcnn.py:269-357), beta = 0, over the valid rows."""
+    R = len(gt_classes)
+    if R == 0:
+        return 0.0, 0.0
+    x = logits.astype(np.float64)
+    m = x.max(axis=1, keepdims=True)
+    lse = (m[:, 0] + np.log(np.exp(x - m).sum(axis=1)))
+    loss_cls = (lse - x[np.arange(R), gt_classes]).mean()
+    K = logits.shape[1] - 1
+    fg = (gt_classes >= 0) & (gt_classes < K)
+    if not fg.any():
+        return loss_cls, 0.0
+    nreg = deltas.shape[1] // 4
+    d = deltas.reshape(R, nreg, 4)
+    col = gt_classes[fg] if nreg > 1 else np.zeros(fg.sum(), np.int64)
+    pred = d[np.nonzero(fg)[0], col]
+    tgt = get_deltas(proposals[fg], gt_boxes[fg], weights)
+    return loss_cls, np.abs(tgt - pred).astype(np.float64).sum() / R
+
+
+def mask_rcnn_loss(logits, boxes, gt_boxes, gt_classes, gt_masks):
+    """mask_rcnn_loss (mask_head.py:17-68) with mini masks: logits [B, Hm, Wm, C],
+    boxes / gt_boxes [B, 4], gt_masks [B, h, w] (the matched mini mask per row)."""
+    B, Hm, Wm, C = logits.shape
+    if B == 0:
+        return 0.0
+    y1, x1, y2, x2 = [boxes[:, i] for i in range(4)]
+    gy1, gx1, gy2, gx2 = [gt_boxes[:, i] for i in range(4)]
+    gh, gw = gt_boxes[:, 2] - gy1, gt_boxes[:, 3] - gx1
+    nb = np.stack([(y1 - gy1) / gh, (x1 - gx1) / gw, (y2 - gy1) / gh, (x2 - gx1) / gw],
+                  1).astype(F32)
+    tgt = crop_and_resize_tf(gt_masks.astype(F32)[..., None], nb, np.arange(B, dtype=np.int32),
+                             (Hm, Wm))[..., 0]
+    tgt = np.round(tgt).astype(np.float64)
+    ch = gt_classes if C > 1 else np.zeros(B, np.int64)
+    x = logits[np.arange(B), :, :, ch].astype(np.float64)
+    return (np.maximum(x, 0) - x * tgt + np.log1p(np.exp(-np.abs(x)))).mean()
+
+
+def sgd_step(params, grads, accums, lr, momentum, weight_decays, clip_norm):
+    """One reference update: grad of loss + sum(wd * |w|^2 / 2), per-tensor
+    clip_by_norm (slim.learning.clip_gradient_norms), MomentumOptimizer."""
+    out_p, out_a = [], []
+    for p, g, a, wd in zip(params, grads, accums, weight_decays):
+        g = g.astype(np.float64) + wd * p.astype(np.float64)
+        n = np.sqrt((g * g).sum())
+        if clip_norm > 0:
+            g = g * clip_norm / max(n, clip_norm)
+        a = momentum * a + g
+        out_a.append(a)
+        out_p.append(p - lr * a)
+    return out_p, out_a
