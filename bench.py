@@ -126,13 +126,15 @@ def kernel_report(summary):
                               "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
                               "launches": n, "avg_us": round(ms * 1e3 / n, 2),
                               "algorithmic_per_launch": flops / n}
-    if "roi_align_fwd" in summary:
-        n, ms, byts = summary["roi_align_fwd"]
+    for name in ("roi_align_fwd", "roi_align_bwd"):
+        if name not in summary:
+            continue
+        n, ms, byts = summary[name]
         ach = byts / (ms * 1e-3) / 1e9
-        rep["roi_align_fwd"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                                "traffic": None, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
-                                "algorithmic_per_launch": byts / n}
+        rep[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                     "traffic": None, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                     "algorithmic_per_launch": byts / n}
     return rep
 
 
@@ -190,6 +192,7 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         KernelTimer.reset(enabled=not args.no_kernel_timing)
+        torch.cuda.nvtx.range_push("timed_region")  # roctx: tools/prof_window.py
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = step()
@@ -197,6 +200,7 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
+        torch.cuda.nvtx.range_pop()
         KernelTimer.enabled = False
     summary = KernelTimer.summary()
     if world > 1:
@@ -205,7 +209,7 @@ def main():
         elapsed = float(t.item())
     _C.raise_on_errors(device)
     if args.mode == "train":
-        extra = {"losses_last_step_rank0": {k: round(float(v), 4) for k, v in out.items()}}
+        extra = {"losses_last_step_rank0": {k: round(float(v.detach()), 4) for k, v in out.items()}}
     else:
         extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 

@@ -29,8 +29,9 @@ _SIGS = {
     "d2mi_clear_errors": (c_int, [P]),
     "d2mi_roi_align_fwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "d2mi_roi_align_bwd_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int]),
     "d2mi_roi_align_bwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
-                                   c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+                                   c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_size_t, P]),
     "d2mi_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
     "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),

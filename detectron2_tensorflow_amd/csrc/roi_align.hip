@@ -16,6 +16,7 @@
 // one 1 KiB store. A 256-thread workgroup = 4 waves walks up to 64 bins of one
 // ROI, so the per-ROI geometry (level, normalised box) stays in scalar registers.
 #include "common.h"
+#include "internal.h"
 
 namespace d2mi {
 namespace {
@@ -224,49 +225,245 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
   }
 }
 
-// Backward: TF CropAndResizeGradImage scatter (+ AvgPoolGrad's 1/count and
-// MirrorPadGrad folding the pad rows onto the edge rows, both implicit here).
-// Channel mapping c = lane + 64 k keeps every atomic wave-instruction on 256
-// contiguous bytes (the full-rate atomic shape on gfx950).
-__global__ __launch_bounds__(256) void roi_align_bwd_kernel(RoiArgs a) {
-  const int r = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const RoiGeom g = roi_geom(a, r);
-  if (!g.ok) return;
-  const int nbins = a.out_h * a.out_w;
+// ---------------------------------------------------------------- backward
+// TF CropAndResizeGradImage (+ AvgPoolGrad's 1/count and MirrorPadGrad folding
+// the pad rows onto the edge rows, implicit in the clamped taps) as a GATHER:
+// device-scope float atomics on gfx950 resolve beyond the XCD-private L2 and a
+// scatter of them ran at ~120 GB/s.  Instead:
+//   1. geom: per-ROI geometry (level, image, normalised box, tap scales);
+//   2. emit: for every (ROI, sample, corner) contribution a 64-bit key
+//      pixel << low_bits | slot, slot = (roi * samples + sample) * 4 + corner,
+//      and its (grad_out row, y_lerp, x_lerp) record at index slot;
+//   3. radix-sort the keys: pixel-major, then the TF loop order;
+//   4. runs: first / end key of every touched pixel;
+//   5. pixels with more than kSeg contributions are split into kSeg-long
+//      segments (exclusive scan of their segment counts) summed by one wave
+//      each into a partial row — bounded work per wave however many ROIs pile
+//      onto one pixel (collapsed proposals at the image border do);
+//   6. one wave per feature-map pixel, lanes over channels (float4): sum its
+//      contributions (or its segments' partials) in order and store it —
+//      every element of every grad map is written exactly once.
+// Summation order per pixel is (box, y, x, corner), the TF kernel's loop order
+// (partials regroup it for pixels past kSeg): deterministic run to run, and
+// bit-identical to the TF scatter for pixels with at most kSeg contributions
+// and no folded pad row.
+constexpr int kSeg = 64;    // contributions per wave before a pixel is split
+constexpr int kBatch = 8;   // contributions in flight per wave
+
+struct PixMap {
+  long long base[D2MI_MAX_LEVELS + 1];  // first global pixel id per level
+};
+
+struct Contrib {
+  int32_t row;  // grad_out row index r * nbins + bin
+  float yl, xl;
+  int32_t pad;
+};
+
+__global__ void roi_bwd_geom_kernel(RoiArgs a, RoiGeom* geo) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < a.R) geo[r] = roi_geom(a, r);
+}
+
+__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, const RoiGeom* __restrict__ geo,
+                                    int low_bits, uint64_t* __restrict__ keys,
+                                    Contrib* __restrict__ rec) {
   const int S = a.sr > 0 ? a.sr : 1;
-  const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
-  float* base = a.gfeat[g.lvl] + (size_t)g.n * g.H * g.W * a.C;
+  const long long nsamp = (long long)a.out_h * a.out_w * S * S;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)a.R * nsamp) return;
+  const int r = (int)(t / nsamp);
+  const int s = (int)(t - (long long)r * nsamp);
+  const RoiGeom g = geo[r];
+  const uint64_t slot = (uint64_t)t * 4u;
+  uint64_t* k = keys + slot;
+  bool ok = g.ok;
+  Tap ty = {}, tx = {};
+  int iy = 0, ix = 0;
+  if (ok) {
+    const bool pad = a.pad_border != 0;
+    iy = s / g.cw;
+    ix = s - iy * g.cw;
+    ty = make_tap(in_coord(g.y1, g.y2, g.hs, iy, g.ch, g.Hp), g.Hp, g.H, pad);
+    tx = make_tap(in_coord(g.x1, g.x2, g.ws, ix, g.cw, g.Wp), g.Wp, g.W, pad);
+    ok = ty.valid && tx.valid;
+  }
+  if (!ok) {
+    k[0] = k[1] = k[2] = k[3] = ~0ull;
+    return;
+  }
+  Contrib c;
+  c.row = r * (a.out_h * a.out_w) + (iy / S) * a.out_w + ix / S;
+  c.yl = ty.lerp;
+  c.xl = tx.lerp;
+  c.pad = 0;
+  rec[t] = c;  // shared by the 4 corners: slot >> 2
+  const uint64_t img = (uint64_t)pm.base[g.lvl] + (uint64_t)g.n * g.H * g.W;
+  k[0] = ((img + (uint64_t)ty.r0 * g.W + tx.r0) << low_bits) | (slot + 0);
+  k[1] = ((img + (uint64_t)ty.r0 * g.W + tx.r1) << low_bits) | (slot + 1);
+  k[2] = ((img + (uint64_t)ty.r1 * g.W + tx.r0) << low_bits) | (slot + 2);
+  k[3] = ((img + (uint64_t)ty.r1 * g.W + tx.r1) << low_bits) | (slot + 3);
+}
+
+// run_start[p] = first sorted index of pixel p (-1 untouched), run_end[p] = one past its last.
+__global__ void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
+                                    long long total_pixels, int32_t* __restrict__ run_start,
+                                    int32_t* __restrict__ run_end) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = keys[i] >> low_bits;
+  if ((long long)p >= total_pixels) return;  // invalid contributions sort last
+  if (i == 0 || (keys[i - 1] >> low_bits) != p) run_start[p] = (int32_t)i;
+  if (i == n - 1 || (keys[i + 1] >> low_bits) != p) run_end[p] = (int32_t)(i + 1);
+}
+
+// nseg[p] = number of kSeg segments of pixel p when it has more than kSeg
+// contributions, else 0; nseg[total_pixels] = 0 (scan sentinel).
+__global__ void roi_bwd_nseg_kernel(const int32_t* __restrict__ run_start,
+                                    const int32_t* __restrict__ run_end, long long total_pixels,
+                                    int32_t* __restrict__ nseg) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > total_pixels) return;
+  int v = 0;
+  if (p < total_pixels && run_start[p] >= 0) {
+    const int len = run_end[p] - run_start[p];
+    v = len > kSeg ? (len + kSeg - 1) / kSeg : 0;
+  }
+  nseg[p] = v;
+}
+
+__global__ void roi_bwd_segpix_kernel(const int32_t* __restrict__ nseg,
+                                      const int32_t* __restrict__ seg_first, long long total_pixels,
+                                      int32_t* __restrict__ seg_pixel) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= total_pixels) return;
+  const int k = nseg[p];
+  const int f = seg_first[p];
+  for (int j = 0; j < k; ++j) seg_pixel[f + j] = (int32_t)p;
+}
+
+// TF order of operations: dtop = (1 - y_lerp) * g, dbot = y_lerp * g, then
+// (1 - x_lerp) * d or x_lerp * d.
+__device__ __forceinline__ float weigh(int corner, float yl, float xl, float v) {
+  const float d = (corner < 2) ? (1.f - yl) * v : yl * v;
+  return (corner & 1) ? xl * d : (1.f - xl) * d;
+}
+
+// Sum of sorted contributions [i0, i1) for the lane's channel(s) c.
+template <bool VEC4>
+__device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __restrict__ keys,
+                                          const Contrib* __restrict__ rec, uint64_t low_mask,
+                                          int i0, int i1, int c, bool live, float inv, bool avg) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int C = a.C;
-  const bool pad = a.pad_border != 0;
-  const int b_end = min(nbins, (int)(blockIdx.y + 1) * kBinsPerBlock);
-  for (int bin = blockIdx.y * kBinsPerBlock + wave; bin < b_end; bin += 4) {
-    const int oy = bin / a.out_w, ox = bin - oy * a.out_w;
-    const float* src = a.gout + ((size_t)r * nbins + bin) * C;
-    for (int sy = 0; sy < S; ++sy) {
-      const Tap ty = make_tap(in_coord(g.y1, g.y2, g.hs, oy * S + sy, g.ch, g.Hp), g.Hp, g.H,
-                              pad);
-      if (!ty.valid) continue;
-      for (int sx = 0; sx < S; ++sx) {
-        const Tap tx = make_tap(in_coord(g.x1, g.x2, g.ws, ox * S + sx, g.cw, g.Wp), g.Wp,
-                                g.W, pad);
-        if (!tx.valid) continue;
-        float* tl = base + ((size_t)ty.r0 * g.W + tx.r0) * C;
-        float* tr = base + ((size_t)ty.r0 * g.W + tx.r1) * C;
-        float* bl = base + ((size_t)ty.r1 * g.W + tx.r0) * C;
-        float* br = base + ((size_t)ty.r1 * g.W + tx.r1) * C;
-        for (int c = lane; c < C; c += 64) {
-          float gv = src[c];
-          if (S > 1) gv = gv / inv;
-          const float dtop = (1.f - ty.lerp) * gv;
-          const float dbot = ty.lerp * gv;
-          atomicAdd(tl + c, (1.f - tx.lerp) * dtop);
-          atomicAdd(tr + c, tx.lerp * dtop);
-          atomicAdd(bl + c, (1.f - tx.lerp) * dbot);
-          atomicAdd(br + c, tx.lerp * dbot);
+  for (int i = i0; i < i1; i += kBatch) {
+    int corner[kBatch];
+    Contrib e[kBatch];
+    const int m = min(kBatch, i1 - i);
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      if (u < m) {
+        const uint64_t slot = keys[i + u] & low_mask;
+        corner[u] = (int)(slot & 3u);
+        e[u] = rec[slot >> 2];
+      }
+    }
+    float4 v[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      if (u < m && live) {
+        const float* src = a.gout + (size_t)e[u].row * C + c;
+        if (VEC4) v[u] = *reinterpret_cast<const float4*>(src);
+        else v[u].x = *src;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      if (u < m) {
+        float4 g = v[u];
+        if (avg) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
+        acc.x += weigh(corner[u], e[u].yl, e[u].xl, g.x);
+        if (VEC4) {
+          acc.y += weigh(corner[u], e[u].yl, e[u].xl, g.y);
+          acc.z += weigh(corner[u], e[u].yl, e[u].xl, g.z);
+          acc.w += weigh(corner[u], e[u].yl, e[u].xl, g.w);
         }
       }
+    }
+  }
+  return acc;
+}
+
+// One wave per split segment: partial[seg] (C floats).
+template <bool VEC4>
+__global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
+    RoiArgs a, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec, int low_bits,
+    const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
+    const int32_t* __restrict__ seg_first, const int32_t* __restrict__ seg_pixel,
+    const int32_t* __restrict__ total_segs, float* __restrict__ partial) {
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (seg >= *total_segs) return;
+  const int p = seg_pixel[seg];
+  const int k = seg - seg_first[p];
+  const int i0 = run_start[p] + k * kSeg;
+  const int i1 = min(i0 + kSeg, run_end[p]);
+  const uint64_t low_mask = (1ull << low_bits) - 1ull;
+  const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
+  const int step = VEC4 ? 256 : 64;
+  for (int c0 = 0; c0 < a.C; c0 += step) {
+    const int c = c0 + (VEC4 ? lane * 4 : lane);
+    const bool live = c < a.C;
+    const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
+    if (live) {
+      float* dst = partial + (size_t)seg * a.C + c;
+      if (VEC4) *reinterpret_cast<float4*>(dst) = acc;
+      else *dst = acc.x;
+    }
+  }
+}
+
+// One wave per feature-map pixel.
+template <bool VEC4>
+__global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
+    RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
+    int low_bits, const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
+    const int32_t* __restrict__ nseg, const int32_t* __restrict__ seg_first,
+    const float* __restrict__ partial, long long total_pixels) {
+  const long long pix = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pix >= total_pixels) return;
+  int l = 0;
+  while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
+  const int C = a.C;
+  float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
+  const int i0 = run_start[pix];
+  const int i1 = i0 >= 0 ? run_end[pix] : i0;
+  const int ns = i0 >= 0 ? nseg[pix] : 0;
+  const int f = ns ? seg_first[pix] : 0;
+  const uint64_t low_mask = (1ull << low_bits) - 1ull;
+  const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
+  const int step = VEC4 ? 256 : 64;
+  for (int c0 = 0; c0 < C; c0 += step) {
+    const int c = c0 + (VEC4 ? lane * 4 : lane);
+    const bool live = c < C;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ns == 0 && i0 >= 0) {
+      acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
+    } else if (ns > 0 && live) {
+      for (int j = 0; j < ns; ++j) {
+        const float* src = partial + (size_t)(f + j) * C + c;
+        if (VEC4) {
+          const float4 v = *reinterpret_cast<const float4*>(src);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        } else {
+          acc.x += *src;
+        }
+      }
+    }
+    if (live) {
+      if (VEC4) *reinterpret_cast<float4*>(dst + c) = acc;
+      else dst[c] = acc.x;
     }
   }
 }
@@ -348,23 +545,154 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   return 0;
 }
 
+namespace d2mi {
+namespace {
+
+int bits_for(unsigned long long v) {  // smallest b with 2^b > v
+  int b = 0;
+  while (b < 64 && (v >> b) != 0) ++b;
+  return b;
+}
+
+struct BwdPlan {
+  long long total_pixels, n_keys, n_samples, max_segs;
+  int low_bits, end_bit;
+  PixMap pm;
+};
+
+int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, int sr,
+             BwdPlan* p) {
+  const long long S = sr > 0 ? sr : 1;
+  p->n_samples = (long long)R * out_h * out_w * S * S;
+  p->n_keys = p->n_samples * 4;
+  long long t = 0;
+  for (int l = 0; l < num_levels; ++l) {
+    p->pm.base[l] = t;
+    t += (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2];
+  }
+  p->pm.base[num_levels] = t;
+  p->total_pixels = t;
+  // every split pixel has > kSeg contributions: segments <= 2 * n / kSeg
+  p->max_segs = 2 * (p->n_keys / kSeg) + 1;
+  p->low_bits = max(1, bits_for(p->n_keys > 0 ? (unsigned long long)(p->n_keys - 1) : 0ull));
+  p->end_bit = p->low_bits + bits_for((unsigned long long)t);
+  D2MI_REQUIRE(p->end_bit <= 64, "ROIAlign backward key space too large (%d bits)", p->end_bit);
+  D2MI_REQUIRE(p->n_keys < (1LL << 31) && t < (1LL << 31), "ROIAlign backward too large");
+  return 0;
+}
+
+template <typename WS>
+void bwd_layout(WS& w, int R, int C, const BwdPlan& p) {
+  w.template take<RoiGeom>((size_t)R + 1);
+  w.template take<uint64_t>((size_t)p.n_keys + 1);          // keys
+  w.template take<uint64_t>((size_t)p.n_keys + 1);          // sorted keys
+  w.template take<Contrib>((size_t)p.n_samples + 1);        // records
+  w.template take<int32_t>((size_t)p.total_pixels + 1);     // run_start
+  w.template take<int32_t>((size_t)p.total_pixels + 1);     // run_end
+  w.template take<int32_t>((size_t)p.total_pixels + 1);     // nseg
+  w.template take<int32_t>((size_t)p.total_pixels + 1);     // seg_first
+  w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
+  w.template take<float>((size_t)p.max_segs * C);           // partial rows
+  w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
+                            exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1)));
+}
+
+}  // namespace
+}  // namespace d2mi
+
+extern "C" size_t d2mi_roi_align_bwd_workspace_size(const int32_t* dims, int num_levels, int C,
+                                                    int R, int out_h, int out_w,
+                                                    int sampling_ratio) {
+  if (!dims || num_levels < 1 || num_levels > D2MI_MAX_LEVELS || R < 0 || C < 1) return 0;
+  BwdPlan p;
+  if (bwd_plan(dims, num_levels, R, out_h, out_w, sampling_ratio, &p)) return 0;
+  WorkspaceSizer w;
+  bwd_layout(w, R, C, p);
+  return w.off;
+}
+
 extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
                                   const float* scales, int num_levels, int C, const float* boxes,
                                   const int32_t* box_ind, int R, int out_h, int out_w,
                                   int sampling_ratio, int box_mode, int pad_border, int assign,
                                   int min_level, int max_level, int canonical_box_size,
-                                  int canonical_level, const float* grad_out, void* stream) {
+                                  int canonical_level, const float* grad_out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
   RoiArgs a = {};
   int rc = fill_args(a, dims, scales, num_levels, C, boxes, box_ind, R, out_h, out_w,
                      sampling_ratio, box_mode, pad_border, assign, min_level, max_level,
                      canonical_box_size, canonical_level);
   if (rc) return rc;
-  for (int l = 0; l < num_levels; ++l) a.gfeat[l] = grad_feats[l];
+  bool vec4 = (C % 4) == 0 && ((uintptr_t)grad_out & 15) == 0;
+  for (int l = 0; l < num_levels; ++l) {
+    a.gfeat[l] = grad_feats[l];
+    vec4 = vec4 && (((uintptr_t)grad_feats[l] & 15) == 0);
+  }
   a.gout = grad_out;
-  if (R == 0) return 0;
-  const int nbins = out_h * out_w;
-  dim3 grid(R, (nbins + kBinsPerBlock - 1) / kBinsPerBlock);
-  hipLaunchKernelGGL(roi_align_bwd_kernel, grid, dim3(256), 0, as_stream(stream), a);
+  BwdPlan p;
+  rc = bwd_plan(dims, num_levels, R, out_h, out_w, sampling_ratio, &p);
+  if (rc) return rc;
+  const size_t need = d2mi_roi_align_bwd_workspace_size(dims, num_levels, C, R, out_h, out_w,
+                                                        sampling_ratio);
+  D2MI_REQUIRE(workspace_bytes >= need && (workspace || need == 0),
+               "ROIAlign backward workspace too small: %zu < %zu", workspace_bytes, need);
+  if (p.total_pixels == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  Workspace w(workspace, workspace_bytes);
+  RoiGeom* geo = w.take<RoiGeom>((size_t)R + 1);
+  uint64_t* keys = w.take<uint64_t>((size_t)p.n_keys + 1);
+  uint64_t* sorted = w.take<uint64_t>((size_t)p.n_keys + 1);
+  Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
+  int32_t* run_start = w.take<int32_t>((size_t)p.total_pixels + 1);
+  int32_t* run_end = w.take<int32_t>((size_t)p.total_pixels + 1);
+  int32_t* nseg = w.take<int32_t>((size_t)p.total_pixels + 1);
+  int32_t* seg_first = w.take<int32_t>((size_t)p.total_pixels + 1);
+  int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
+  float* partial = w.take<float>((size_t)p.max_segs * C);
+  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
+                               exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1));
+  void* tmp = w.take<char>(tmp_bytes);
+  const long long TP = p.total_pixels;
+  D2MI_HIP(hipMemsetAsync(run_start, 0xff, (size_t)TP * sizeof(int32_t), st));
+  if (p.n_keys > 0) {
+    hipLaunchKernelGGL(roi_bwd_geom_kernel, dim3((R + 255) / 256), dim3(256), 0, st, a, geo);
+    D2MI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((p.n_samples + 255) / 256)), dim3(256),
+                       0, st, a, p.pm, geo, p.low_bits, keys, rec);
+    D2MI_LAUNCH_CHECK();
+    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.end_bit, tmp, tmp_bytes, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256),
+                       0, st, sorted, p.n_keys, p.low_bits, TP, run_start, run_end);
+    D2MI_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(roi_bwd_nseg_kernel, dim3((unsigned)((TP + 1 + 255) / 256)), dim3(256), 0, st,
+                     run_start, run_end, TP, nseg);
+  D2MI_LAUNCH_CHECK();
+  rc = exclusive_scan_i32(nseg, seg_first, (size_t)TP + 1, tmp, tmp_bytes, st);
+  if (rc) return rc;
+  if (p.n_keys > 0) {
+    hipLaunchKernelGGL(roi_bwd_segpix_kernel, dim3((unsigned)((TP + 255) / 256)), dim3(256), 0, st,
+                       nseg, seg_first, TP, seg_pixel);
+    D2MI_LAUNCH_CHECK();
+    const dim3 sgrid((unsigned)((p.max_segs + 3) / 4));
+    if (vec4)
+      hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted, rec,
+                         p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TP,
+                         partial);
+    else
+      hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted, rec,
+                         p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TP,
+                         partial);
+    D2MI_LAUNCH_CHECK();
+  }
+  const dim3 grid((unsigned)((TP + 3) / 4));
+  if (vec4)
+    hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
+                       p.low_bits, run_start, run_end, nseg, seg_first, partial, TP);
+  else
+    hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
+                       p.low_bits, run_start, run_end, nseg, seg_first, partial, TP);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

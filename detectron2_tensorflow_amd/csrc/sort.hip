@@ -3,6 +3,8 @@
 // are sorted by one 1024-thread workgroup per segment with an in-LDS bitonic
 // network (64 KiB of keys); larger capacities fall back to rocPRIM's
 // segmented radix sort.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "internal.h"
@@ -95,6 +97,40 @@ int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32
                                               (unsigned int)((size_t)S * cap), (unsigned int)S,
                                               (const int*)begin, (const int*)end, 0u, 64u, stream,
                                               false));
+  return 0;
+}
+
+size_t radix_sort_u64_workspace_size(size_t n, int end_bit) {
+  size_t bytes = 0;
+  rocprim::radix_sort_keys((void*)nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, n,
+                           0u, (unsigned)end_bit, (hipStream_t)0, false);
+  return bytes;
+}
+
+int radix_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, size_t n, int end_bit, void* ws,
+                   size_t ws_bytes, hipStream_t stream) {
+  if (n == 0) return 0;
+  size_t need = radix_sort_u64_workspace_size(n, end_bit);
+  D2MI_REQUIRE(ws_bytes >= need, "radix sort workspace too small (%zu < %zu)", ws_bytes, need);
+  D2MI_HIP(rocprim::radix_sort_keys(ws, need, keys_in, keys_out, n, 0u, (unsigned)end_bit, stream,
+                                    false));
+  return 0;
+}
+
+size_t exclusive_scan_i32_workspace_size(size_t n) {
+  size_t bytes = 0;
+  rocprim::exclusive_scan((void*)nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                          (int32_t)0, n, rocprim::plus<int32_t>(), (hipStream_t)0, false);
+  return bytes;
+}
+
+int exclusive_scan_i32(const int32_t* in, int32_t* out, size_t n, void* ws, size_t ws_bytes,
+                       hipStream_t stream) {
+  if (n == 0) return 0;
+  size_t need = exclusive_scan_i32_workspace_size(n);
+  D2MI_REQUIRE(ws_bytes >= need, "scan workspace too small (%zu < %zu)", ws_bytes, need);
+  D2MI_HIP(rocprim::exclusive_scan(ws, need, in, out, (int32_t)0, n, rocprim::plus<int32_t>(),
+                                   stream, false));
   return 0;
 }
 

@@ -107,15 +107,23 @@ class _RoIAlignFn(torch.autograd.Function):
         boxes, box_ind = ctx.saved_tensors
         (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
          _) = ctx.params
-        grads = [torch.zeros(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
+        # every element is written by the kernel: no zero-fill
+        grads = [torch.empty(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
         g = _f32c(grad_out)
         gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
         dims = _C.host_array(_C.ctypes.c_int32, [v for s in ctx.shapes for v in (s[0], s[1], s[2])])
         sc = _C.host_array(_C.c_float, list(scales))
-        rc = _C.lib().d2mi_roi_align_bwd(gp, dims, sc, len(grads), ctx.shapes[0][-1],
-                                         _C.ptr(boxes), _C.ptr(box_ind), boxes.shape[0], out_h,
-                                         out_w, sr, mode, pad, assign, min_l, max_l, canon_s,
-                                         canon_l, _C.ptr(g), _C.stream_of(boxes.device))
+        R, C = boxes.shape[0], ctx.shapes[0][-1]
+        wsb = _C.lib().d2mi_roi_align_bwd_workspace_size(dims, len(grads), C, R, out_h, out_w, sr)
+        ws = _C.workspace(wsb, boxes.device)
+        ev = KernelTimer.start()
+        rc = _C.lib().d2mi_roi_align_bwd(gp, dims, sc, len(grads), C, _C.ptr(boxes),
+                                         _C.ptr(box_ind), R, out_h, out_w, sr, mode, pad, assign,
+                                         min_l, max_l, canon_s, canon_l, _C.ptr(g), _C.ptr(ws), wsb,
+                                         _C.stream_of(boxes.device))
+        # algorithmic bytes: one read of grad_out + one write of every grad map element
+        KernelTimer.stop(ev, "roi_align_bwd",
+                         4 * (R * out_h * out_w * C + sum(math.prod(s) for s in ctx.shapes)))
         _C.check(rc, "d2mi_roi_align_bwd")
         return (None, None, None, *grads)
 

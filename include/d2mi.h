@@ -75,14 +75,21 @@ int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims, const flo
 
 /* Gradient of d2mi_roi_align_fwd w.r.t. the feature maps (TF
  * CropAndResizeGradImage + the pad/avg_pool chain rule; boxes get no gradient,
- * lib/layers/functional.py:120). grad_feats[l] must be zeroed by the caller;
- * contributions are accumulated with float atomics. */
+ * lib/layers/functional.py:120). Every element of every grad_feats[l] is
+ * WRITTEN (not accumulated; no zero-fill needed): the scatter is computed as a
+ * gather — contributions radix-sorted by destination pixel, one wave per pixel
+ * summing them in the TF kernel's (box, y, x, corner) order (pixels with more
+ * than 64 contributions are split into 64-long partial sums first).
+ * Deterministic, no atomics. Workspace from d2mi_roi_align_bwd_workspace_size
+ * (same dims / C / R / crop arguments). */
+size_t d2mi_roi_align_bwd_workspace_size(const int32_t* dims, int num_levels, int C, int R,
+                                         int out_h, int out_w, int sampling_ratio);
 int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims, const float* scales,
                        int num_levels, int C, const float* boxes, const int32_t* box_ind,
                        int R, int out_h, int out_w, int sampling_ratio, int box_mode,
                        int pad_border, int assign, int min_level, int max_level,
                        int canonical_box_size, int canonical_level, const float* grad_out,
-                       void* stream);
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------- NMS
  * Segmented greedy NMS with TF NonMaxSuppressionV3 semantics

@@ -104,7 +104,72 @@ def test_roi_align_backward_raw_matches_tf_grad(dev):
     out = ops().roi_align([x], torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
                           (6, 5), [1.0], 0, pad_border=False, box_mode=ops().BOX_MODE_RAW)
     out.backward(torch.from_numpy(g).to(dev))
-    np.testing.assert_allclose(x.grad.cpu().numpy(), want, rtol=1e-5, atol=1e-4)
+    # the tiled gather sums each pixel in the TF kernel's (box, y, x, corner) order
+    np.testing.assert_array_equal(x.grad.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("C,crop,sr", [(300, (14, 14), 0), (64, (7, 7), 2), (3, (28, 20), 0)])
+def test_roi_align_backward_raw_large_crops_and_ragged_channels(dev, C, crop, sr):
+    """More samples than one 64-lane block, channel counts off the 64-chunk grid,
+    boxes spanning many 8x8 tiles (and flipped ones)."""
+    rng = np.random.default_rng(C)
+    img = rng.normal(size=(3, 40, 52, C)).astype(F32)
+    boxes = rng.uniform(-0.2, 1.2, size=(25, 4)).astype(F32)
+    bimg = rng.integers(0, 3, size=25).astype(np.int32)
+    x = torch.from_numpy(img).to(dev).requires_grad_(True)
+    out = ops().roi_align([x], torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
+                          crop, [1.0], sr, pad_border=False, box_mode=ops().BOX_MODE_RAW)
+    g = rng.normal(size=tuple(out.shape)).astype(F32)
+    out.backward(torch.from_numpy(g).to(dev))
+    if sr == 0:
+        want = oracle.crop_and_resize_grad_image(g, boxes, bimg, (3, 40, 52))
+        np.testing.assert_array_equal(x.grad.cpu().numpy(), want)
+    else:
+        lhs = (out.double() * torch.from_numpy(g).to(dev).double()).sum().item()
+        rhs = (x.double() * x.grad.double()).sum().item()
+        assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
+
+
+def test_roi_align_backward_hot_pixels(dev):
+    """Hundreds of ROIs collapsed onto the same pixels (degenerate proposals at
+    the border): the split-segment path, against the TF scatter."""
+    rng = np.random.default_rng(9)
+    img = rng.normal(size=(2, 24, 30, 64)).astype(F32)
+    boxes = np.concatenate([np.tile([[0.5, 0.5, 0.5, 0.5]], (300, 1)),
+                            rng.uniform(0, 1, size=(50, 4))]).astype(F32)
+    bimg = np.concatenate([np.zeros(300), rng.integers(0, 2, 50)]).astype(np.int32)
+    x = torch.from_numpy(img).to(dev).requires_grad_(True)
+    out = ops().roi_align([x], torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
+                          (7, 7), [1.0], 0, pad_border=False, box_mode=ops().BOX_MODE_RAW)
+    g = rng.normal(size=tuple(out.shape)).astype(F32)
+    out.backward(torch.from_numpy(g).to(dev))
+    want = oracle.crop_and_resize_grad_image(g, boxes, bimg, (2, 24, 30))
+    got = x.grad.cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-3)
+    x.grad = None
+    out = ops().roi_align([x], torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
+                          (7, 7), [1.0], 0, pad_border=False, box_mode=ops().BOX_MODE_RAW)
+    out.backward(torch.from_numpy(g).to(dev))
+    assert np.array_equal(x.grad.cpu().numpy(), got)
+
+
+def test_roi_align_backward_is_deterministic(dev):
+    rng = np.random.default_rng(11)
+    strides = [4, 8, 16, 32]
+    feats = [torch.from_numpy(rng.normal(size=(2, 256 // s, 320 // s, 256)).astype(F32)).to(dev)
+             .requires_grad_(True) for s in strides]
+    boxes = torch.from_numpy(rand_boxes(rng, 512, 256, 320, 2, 300)).to(dev)
+    bimg = torch.from_numpy(rng.integers(0, 2, size=512).astype(np.int32)).to(dev)
+    g = torch.randn(512, 7, 7, 256, device=dev)
+    runs = []
+    for _ in range(2):
+        for f in feats:
+            f.grad = None
+        out = ops().roi_align(feats, boxes, bimg, (7, 7), [1.0 / s for s in strides], 0, True)
+        out.backward(g)
+        runs.append([f.grad.clone() for f in feats])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
 
 
 def test_roi_align_backward_is_adjoint_multilevel(dev):

@@ -106,7 +106,8 @@ def test_training_step_gradients_reach_every_trainable_parameter(dev):
     trainable = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
     frozen = [n for n, p in model.named_parameters() if not p.requires_grad]
     # FREEZE_AT = 2: stem + res2 frozen
-    assert frozen and all(".stem." in n or ".res2." in n for n in frozen), frozen[:5]
+    assert frozen and all(".stem." in n or ".stages.0." in n for n in frozen), frozen[:5]
+    assert any(".stages.1." in n for n, _ in trainable)
     missing = [n for n, p in trainable if p.grad is None]
     assert not missing, missing[:10]
     bad = [n for n, p in trainable if not torch.isfinite(p.grad).all()]
