@@ -54,6 +54,13 @@ _SIGS = {
     "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_int, P]),
     "d2mi_conv2d_workspace_size": (c_size_t, [c_int] * 10),
+    "d2mi_conv2d_wgrad_workspace_size": (c_size_t, [c_int] * 10),
+    "d2mi_fold_frozen_bn": (c_int, [P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P, P,
+                                    P, P]),
+    "d2mi_fold_frozen_bn_bwd_workspace_size": (c_size_t, [c_int]),
+    "d2mi_fold_frozen_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int,
+                                        P, P, P, P, P, c_size_t, P]),
+    "d2mi_conv2d_wgrad": (c_int, [P, P, P, P] + [c_int] * 10 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
 }

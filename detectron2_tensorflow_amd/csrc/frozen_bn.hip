@@ -1,0 +1,152 @@
+// FrozenBN folded into the preceding convolution, forward and backward, as two
+// fused kernels instead of the ~14 elementwise launches per conv autograd makes
+// of  scale = gamma * rsqrt(var + eps),  w_eff = w * scale,  b_eff = beta - mean*scale
+// (+ bias * scale).
+//
+// Reference: lib/layers/normalization.py:15-119 (BatchNorm with training=False:
+// moving statistics, gamma / beta trainable above FREEZE_AT — the
+// resnet_arg_scope of lib/modeling/backbone/resnet.py:22-46) applied after
+// Conv2D (lib/layers/convolutional.py:198-263).  conv(x, w) * scale + shift ==
+// conv(x, w * scale) + shift, so the frozen affine folds into the weights.
+//
+// Layout: w HWIO [rows = KH*KW*Cin][Cout] (Cout contiguous).  Forward writes
+// w_eff (HWIO) and/or the MFMA-packed copy [KH][KW][Cout][Cin] in the same
+// pass.  Backward: gw = gw_eff * scale (elementwise, same pass) and the
+// per-channel reductions  sum_rows gw_eff * w  split over row chunks into a
+// workspace and summed in a FIXED chunk order by a second kernel, which also
+// forms d gamma, d beta and d bias.
+#include "common.h"
+
+namespace d2mi {
+namespace {
+
+constexpr int kRowChunks = 32;
+
+__device__ __forceinline__ float bn_inv(const float* var, float eps, int c) {
+  return 1.f / sqrtf(var[c] + eps);
+}
+
+__global__ void fold_bn_kernel(const float* __restrict__ w, const float* __restrict__ bias,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ mean, const float* __restrict__ var,
+                               float eps, int rows, int Cout, int taps, int Cin,
+                               float* __restrict__ w_eff, float* __restrict__ w_packed,
+                               float* __restrict__ b_eff) {
+  const int co = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (co >= Cout) return;
+  const float inv = bn_inv(var, eps, co);
+  const float scale = gamma ? inv * gamma[co] : inv;
+  if (blockIdx.y == 0 && threadIdx.x < 64) {
+    float shift = -mean[co] * scale;
+    if (beta) shift = shift + beta[co];
+    b_eff[co] = bias ? bias[co] * scale + shift : shift;
+  }
+  const int rstep = gridDim.y * (blockDim.x >> 6);
+  for (int r = blockIdx.y * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += rstep) {
+    const float v = w[(size_t)r * Cout + co] * scale;
+    if (w_eff) w_eff[(size_t)r * Cout + co] = v;
+    if (w_packed) {  // [tap][co][ci]
+      const int tap = r / Cin, ci = r - tap * Cin;
+      w_packed[((size_t)tap * Cout + co) * Cin + ci] = v;
+    }
+  }
+}
+
+// partial[chunk][0][co] = sum gw_eff * w over the chunk's rows; gw = gw_eff * scale.
+__global__ void fold_bn_bwd_kernel(const float* __restrict__ gw_eff, const float* __restrict__ w,
+                                   const float* __restrict__ gamma, const float* __restrict__ var,
+                                   float eps, int rows, int Cout, float* __restrict__ gw,
+                                   float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int co = blockIdx.x * 64 + lane;
+  const bool live = co < Cout;
+  const int chunk = blockIdx.y;
+  const int per = (rows + kRowChunks - 1) / kRowChunks;
+  const int r0 = chunk * per, r1 = min(rows, r0 + per);
+  float scale = 0.f;
+  if (live) {
+    const float inv = bn_inv(var, eps, co);
+    scale = gamma ? inv * gamma[co] : inv;
+  }
+  float s = 0.f;
+  if (live) {
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const float g = gw_eff[(size_t)r * Cout + co];
+      s += g * w[(size_t)r * Cout + co];
+      if (gw) gw[(size_t)r * Cout + co] = g * scale;
+    }
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && live)
+    partial[(size_t)chunk * Cout + co] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ void fold_bn_bwd_finish_kernel(const float* __restrict__ partial,
+                                          const float* __restrict__ gb_eff,
+                                          const float* __restrict__ bias,
+                                          const float* __restrict__ gamma,
+                                          const float* __restrict__ mean,
+                                          const float* __restrict__ var, float eps, int Cout,
+                                          float* __restrict__ gbias, float* __restrict__ ggamma,
+                                          float* __restrict__ gbeta) {
+  const int co = blockIdx.x * blockDim.x + threadIdx.x;
+  if (co >= Cout) return;
+  float gs = 0.f;
+  for (int k = 0; k < kRowChunks; ++k) gs += partial[(size_t)k * Cout + co];
+  const float inv = bn_inv(var, eps, co);
+  const float scale = gamma ? inv * gamma[co] : inv;
+  const float gb = gb_eff ? gb_eff[co] : 0.f;
+  // b_eff = bias * scale + beta - mean * scale
+  gs = gs + gb * ((bias ? bias[co] : 0.f) - mean[co]);
+  if (ggamma) ggamma[co] = gs * inv;
+  if (gbeta) gbeta[co] = gb;
+  if (gbias) gbias[co] = gb * scale;
+}
+
+}  // namespace
+}  // namespace d2mi
+
+using namespace d2mi;
+
+extern "C" int d2mi_fold_frozen_bn(const float* w_hwio, const float* bias, const float* gamma,
+                                   const float* beta, const float* mean, const float* var,
+                                   float eps, int KH, int KW, int Cin, int Cout, float* w_eff,
+                                   float* w_packed, float* b_eff, void* stream) {
+  D2MI_REQUIRE(KH > 0 && KW > 0 && Cin > 0 && Cout > 0, "bad weight shape");
+  D2MI_REQUIRE(w_hwio && mean && var && b_eff, "w, mean, var and b_eff are required");
+  const int rows = KH * KW * Cin;
+  const int gy = std::min(64, std::max(1, rows / 64));
+  dim3 grid((Cout + 63) / 64, gy);
+  hipLaunchKernelGGL(fold_bn_kernel, grid, dim3(256), 0, as_stream(stream), w_hwio, bias, gamma,
+                     beta, mean, var, eps, rows, Cout, KH * KW, Cin, w_eff, w_packed, b_eff);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t d2mi_fold_frozen_bn_bwd_workspace_size(int Cout) {
+  return (size_t)kRowChunks * (size_t)(Cout > 0 ? Cout : 0) * sizeof(float);
+}
+
+extern "C" int d2mi_fold_frozen_bn_bwd(const float* gw_eff, const float* gb_eff,
+                                       const float* w_hwio, const float* bias, const float* gamma,
+                                       const float* mean, const float* var, float eps, int KH,
+                                       int KW, int Cin, int Cout, float* gw, float* gbias,
+                                       float* ggamma, float* gbeta, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(KH > 0 && KW > 0 && Cin > 0 && Cout > 0, "bad weight shape");
+  D2MI_REQUIRE(gw_eff && w_hwio && mean && var, "gw_eff, w, mean and var are required");
+  D2MI_REQUIRE(workspace_bytes >= d2mi_fold_frozen_bn_bwd_workspace_size(Cout) && workspace,
+               "fold_frozen_bn_bwd workspace too small");
+  const int rows = KH * KW * Cin;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(fold_bn_bwd_kernel, dim3((Cout + 63) / 64, kRowChunks), dim3(256), 0, st,
+                     gw_eff, w_hwio, gamma, var, eps, rows, Cout, gw, (float*)workspace);
+  D2MI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(fold_bn_bwd_finish_kernel, dim3((Cout + 255) / 256), dim3(256), 0, st,
+                     (const float*)workspace, gb_eff, bias, gamma, mean, var, eps, Cout, gbias,
+                     ggamma, gbeta);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}

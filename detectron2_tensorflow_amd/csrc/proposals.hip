@@ -181,7 +181,8 @@ __global__ void slot_map_kernel(const int32_t* roi_img, const int32_t* roi_slot,
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const int n = roi_img[r], s = roi_slot[r];
-  if (n < 0 || n >= N || s < 0 || s >= P) {
+  if (s < 0) return;  // ignored row (an invalid / padded proposal)
+  if (n < 0 || n >= N || s >= P) {
     atomicOr(err, kErrBoxInd);
     return;
   }

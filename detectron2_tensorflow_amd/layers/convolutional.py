@@ -10,7 +10,10 @@ RPN head and the mask head use it — and raises if the tensor is not on the GPU
 backbone (a caller of the hot path, outside its scope).
 ``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation,
 Cin % 4 == 0) and the input is on the GPU.
-Backward of the mfma path: dgrad/wgrad via torch.nn.grad on the GPU.
+Backward of the mfma path: dgrad on the same MFMA kernel (flipped kernel);
+wgrad on the MFMA wgrad kernel or hipBLASLt / MIOpen, whichever measured
+faster for the shape (see _wgrad); stride-2 KxK dgrad and Cout % 4 != 0 use
+torch.nn.grad.
 """
 import torch
 import torch.nn.functional as F
@@ -38,6 +41,54 @@ def same_pads(kernel_size, rate=1):
     return pb, pad_total - pb
 
 
+def _dgrad(gy, w, x_shape, stride, pb, pe):
+    """Input gradient.  Stride 1: a forward conv of gy with the spatially
+    flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
+    of the transposed conv — on the MFMA kernel, padded (KH-1-pb, KH-1-pe).
+    1x1 stride s: the MFMA GEMM gy . W^T on the strided grid, scattered into
+    zeros.  Anything else: torch.nn.grad (MIOpen)."""
+    KH, KW, Cin, Cout = w.shape
+    gy = gy.contiguous()
+    if KH == KW and Cout % 4 == 0:
+        if stride == 1 and max(pb, pe) <= KH - 1:
+            wd = w.detach().flip(0, 1).contiguous() if KH > 1 else w.detach().contiguous()
+            return ops.conv2d_nhwc(gy, wd, None, 1, (KH - 1 - pb, KH - 1 - pe))
+        if KH == 1 and pb == 0 and pe == 0:
+            g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
+            gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
+            gx[:, ::stride, ::stride] = g
+            return gx
+    xin_shape = (x_shape[0], x_shape[3], x_shape[1] + pb + pe, x_shape[2] + pb + pe)
+    gx = torch.nn.grad.conv2d_input(xin_shape, w.permute(3, 2, 0, 1), gy.permute(0, 3, 1, 2),
+                                    stride, 0)
+    gx = gx[:, :, pb:gx.shape[2] - pe, pb:gx.shape[3] - pe]
+    return gx.permute(0, 2, 3, 1)
+
+
+def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
+    """(weight gradient HWIO, bias gradient or None).
+
+    Routed by measurement (tools/bench_kernels.py --only wgrad, MI355X):
+    1x1 over >= 32k output pixels -> the MFMA wgrad kernel (d2mi_conv2d_wgrad,
+    bias gradient fused; 67 TF/s vs 45 for hipBLASLt on the p2 lateral);
+    other 1x1 -> X^T . dY as one hipBLASLt GEMM; KxK -> torch.nn.grad (MIOpen's
+    igemm wrw kernels, 121 TF/s on the FPN p2 3x3 vs 91 for ours)."""
+    KH, KW, Cin, Cout = w_shape
+    if KH == 1 and KW == 1 and pb == 0 and pe == 0:
+        P = gy.numel() // Cout
+        if P >= 32768 and Cin % 4 == 0 and Cout % 4 == 0:
+            if want_bias:
+                return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0), with_bias=True)
+            return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0)), None
+        xs = x if stride == 1 else x[:, ::stride, ::stride]
+        xs = xs.reshape(-1, Cin)
+        return torch.mm(xs.t(), gy.reshape(-1, Cout)).reshape(1, 1, Cin, Cout), None
+    xin = F.pad(x, (0, 0, pb, pe, pb, pe)) if (pb or pe) else x
+    gw = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (Cout, Cin, KH, KW),
+                                     gy.permute(0, 3, 1, 2), stride, 0)
+    return gw.permute(2, 3, 1, 0), None
+
+
 class _ConvMFMAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
@@ -56,32 +107,20 @@ class _ConvMFMAFn(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         stride, (pb, pe), relu, has_bias, has_td, has_res = ctx.conf
         if relu:  # relu is the last op whenever an add is fused (relu_after)
-            gy = gy * (y > 0).to(gy.dtype)
+            gy = torch.ops.aten.threshold_backward(gy, y, 0.0)
         gtd = None
         if has_td:
             N, OH, OW, C = gy.shape
             g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
         gres = gy if has_res else None
-        gy_nchw = gy.permute(0, 3, 1, 2)
-        w_oihw = w.permute(3, 2, 0, 1)
-        xin = x
-        if pb != pe:
-            xin = F.pad(x, (0, 0, pb, pe, pb, pe))
-            pad = 0
-        else:
-            pad = pb
-        x_nchw = xin.permute(0, 3, 1, 2)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = torch.nn.grad.conv2d_input(x_nchw.shape, w_oihw, gy_nchw, stride, pad)
-            if pb != pe:
-                gx = gx[:, :, pb:gx.shape[2] - pe, pb:gx.shape[3] - pe]
-            gx = gx.permute(0, 2, 3, 1)
+            gx = _dgrad(gy, w, x.shape, stride, pb, pe)
+        want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            gw = torch.nn.grad.conv2d_weight(x_nchw, w_oihw.shape, gy_nchw, stride, pad)
-            gw = gw.permute(2, 3, 1, 0)
-        if has_bias and ctx.needs_input_grad[2]:
+            gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
+        if want_b and gb is None:
             gb = gy.sum((0, 1, 2))
         return gx, gw, gb, None, None, None, None, gtd, gres, None
 
@@ -146,22 +185,25 @@ class Conv2D(Layer):
                     if t is not None]
         return tuple(key)
 
-    def effective_params(self):
-        """(weights HWIO, bias) with a frozen BatchNorm folded in, plus the
-        normalizer still to apply (None when folded).  Cached while autograd
-        is off (inference); recomputed (differentiably) otherwise."""
+    def effective_params(self, want_packed=False):
+        """(weights HWIO, bias, normalizer still to apply, packed-or-None) with a
+        frozen BatchNorm folded in by one fused HIP kernel (d2mi_fold_frozen_bn,
+        differentiable w.r.t. weights / bias / gamma / beta).  Cached while
+        autograd is off (inference)."""
         norm = self.normalizer_fn
         if not isinstance(norm, BatchNorm):
-            return self.weights, self.bias, norm
-        if not torch.is_grad_enabled() and getattr(self, "_fold_key", None) == self._param_key():
-            return self._fold_w, self._fold_b, None
-        scale, shift = norm.folded()
-        w = self.weights * scale
-        b = shift if self.bias is None else self.bias * scale + shift
+            return self.weights, self.bias, norm, None
+        key = self._param_key()
+        if not torch.is_grad_enabled() and getattr(self, "_fold_key", None) == key:
+            return self._fold_w, self._fold_b, None, self._fold_p
+        if not self.weights.is_cuda:
+            raise RuntimeError(f"{self.scope}: the FrozenBN fold runs on the GPU (HIP)")
+        w, b, packed = ops.fold_frozen_bn(self.weights, self.bias, norm.gamma, norm.beta,
+                                          norm.moving_mean, norm.moving_variance, norm.epsilon,
+                                          want_packed)
         if not torch.is_grad_enabled():
-            self._fold_w, self._fold_b, self._fold_key = w.contiguous(), b.contiguous(), self._param_key()
-            return self._fold_w, self._fold_b, None
-        return w, b, None
+            self._fold_w, self._fold_b, self._fold_p, self._fold_key = w, b, packed, key
+        return w, b, None, packed
 
     def packed_weights(self, w_eff=None):
         key = self._param_key()
@@ -179,7 +221,7 @@ class Conv2D(Layer):
         impl = self.impl
         if impl == "auto":
             impl = "mfma" if self._mfma_eligible(inputs) else "torch"
-        w, b, norm = self.effective_params()
+        w, b, norm, packed = self.effective_params(want_packed=(impl == "mfma"))
         if final_relu:
             if self.act_fn is not None:
                 raise ValueError("final_relu is for layers without an activation")
@@ -195,7 +237,9 @@ class Conv2D(Layer):
             relu_after_add = relu_after_add or final_relu
             if (topdown is not None or residual is not None) and fuse_relu and not relu_after_add:
                 raise ValueError("relu(conv) + add cannot be fused; use relu_after_add")
-            ret = _ConvMFMAFn.apply(inputs, w, b, self.packed_weights(w), self.stride, pads,
+            if packed is None:
+                packed = self.packed_weights(w)
+            ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add)
             if norm is not None:
                 ret = norm(ret)

@@ -284,6 +284,87 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     return y
 
 
+def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False):
+    """HWIO weight gradient of conv2d_nhwc on the MFMA wgrad kernel; with_bias
+    also returns the bias gradient (dy summed over pixels) from the same pass."""
+    x, dy = _f32c(x), _f32c(dy)
+    _C.require_device(x, dy)
+    N, H, W, Cin = x.shape
+    Cout = dy.shape[-1]
+    KH = KW = int(kernel_size)
+    pb, pe = pad
+    dw = torch.empty((KH, KW, Cin, Cout), dtype=torch.float32, device=x.device)
+    db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
+    args = (N, H, W, Cin, Cout, KH, KW, int(stride), int(pb), int(pe))
+    wsb = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
+    ws = _C.workspace(wsb, x.device) if wsb else None
+    ev = KernelTimer.start()
+    rc = _C.lib().d2mi_conv2d_wgrad(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
+                                    _C.ptr(ws), wsb, _C.stream_of(x.device))
+    KernelTimer.stop(ev, "conv2d_wgrad_mfma", 2.0 * dy.numel() * KH * KW * Cin)
+    _C.check(rc, "d2mi_conv2d_wgrad")
+    return (dw, db) if with_bias else dw
+
+
+# ---------------------------------------------------------- FrozenBN fold
+class _FoldFrozenBNFn(torch.autograd.Function):
+    """(w_eff, b_eff, packed) = conv weights with a frozen BatchNorm folded in
+    (d2mi_fold_frozen_bn); packed is the MFMA layout of w_eff (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, w, bias, gamma, beta, mean, var, eps, want_packed):
+        _C.require_device(w, mean, var)
+        KH, KW, Cin, Cout = w.shape
+        w = _f32c(w)
+        w_eff = torch.empty_like(w)
+        packed = (torch.empty((KH, KW, Cout, Cin), dtype=torch.float32, device=w.device)
+                  if want_packed else None)
+        b_eff = torch.empty((Cout,), dtype=torch.float32, device=w.device)
+        rc = _C.lib().d2mi_fold_frozen_bn(_C.ptr(w), _C.ptr(bias), _C.ptr(gamma), _C.ptr(beta),
+                                          _C.ptr(mean), _C.ptr(var), float(eps), KH, KW, Cin,
+                                          Cout, _C.ptr(w_eff), _C.ptr(packed), _C.ptr(b_eff),
+                                          _C.stream_of(w.device))
+        _C.check(rc, "d2mi_fold_frozen_bn")
+        ctx.save_for_backward(w, bias, gamma, mean, var)
+        ctx.eps = float(eps)
+        ctx.has = (bias is not None, gamma is not None, beta is not None)
+        if packed is not None:
+            ctx.mark_non_differentiable(packed)
+        return w_eff, b_eff, packed
+
+    @staticmethod
+    def backward(ctx, gw_eff, gb_eff, _gpacked):
+        w, bias, gamma, mean, var = ctx.saved_tensors
+        KH, KW, Cin, Cout = w.shape
+        has_bias, has_gamma, has_beta = ctx.has
+        need = ctx.needs_input_grad
+        dev = w.device
+        if gw_eff is None:
+            gw_eff = torch.zeros_like(w)
+        gw_eff = _f32c(gw_eff)
+        gb_eff = _f32c(gb_eff) if gb_eff is not None else None
+        mk = lambda cond, shape: torch.empty(shape, dtype=torch.float32, device=dev) if cond else None
+        gw = mk(need[0], w.shape)
+        gbias = mk(has_bias and need[1], (Cout,))
+        ggamma = mk(has_gamma and need[2], (Cout,))
+        gbeta = mk(has_beta and need[3], (Cout,))
+        wsb = _C.lib().d2mi_fold_frozen_bn_bwd_workspace_size(Cout)
+        ws = _C.workspace(wsb, dev)
+        rc = _C.lib().d2mi_fold_frozen_bn_bwd(
+            _C.ptr(gw_eff), _C.ptr(gb_eff), _C.ptr(w), _C.ptr(bias), _C.ptr(gamma), _C.ptr(mean),
+            _C.ptr(var), ctx.eps, KH, KW, Cin, Cout, _C.ptr(gw), _C.ptr(gbias), _C.ptr(ggamma),
+            _C.ptr(gbeta), _C.ptr(ws), wsb, _C.stream_of(dev))
+        _C.check(rc, "d2mi_fold_frozen_bn_bwd")
+        return gw, gbias, ggamma, gbeta, None, None, None, None
+
+
+def fold_frozen_bn(w_hwio, bias, gamma, beta, mean, var, eps, want_packed=False):
+    """Conv weights (HWIO) with a frozen BatchNorm folded in: returns
+    (w_eff, b_eff, packed-or-None), differentiable w.r.t. w, bias, gamma, beta."""
+    return _FoldFrozenBNFn.apply(w_hwio, bias, gamma, beta, mean, var, float(eps),
+                                 bool(want_packed))
+
+
 # -------------------------------------------------------------- matrix NMS
 def matrix_nms_scores(masks, classes, scores, sum_masks=None, kernel="gaussian", sigma=2.0):
     if kernel not in ("gaussian", "linear"):

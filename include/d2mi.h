@@ -233,6 +233,41 @@ int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias
                         int pad_end, int flags, void* workspace, size_t workspace_bytes,
                         void* stream);
 
+/* Weight gradient of the same convolution (the tf.gradients of Conv2D.call,
+ * lib/layers/convolutional.py:198-263, w.r.t. its HWIO kernel):
+ *   dw[kh][kw][ci][co] = sum_{n,oy,ox} x[n, oy*s-pb+kh, ox*s-pb+kw, ci] * dy[n,oy,ox,co].
+ * x [N,H,W,Cin], dy [N,OH,OW,Cout] (OH/OW as the forward), dw HWIO, written;
+ * dbias [Cout] (nullable) receives sum_p dy[p][co], the bias gradient.
+ * Cin, Cout multiples of 4.  With d2mi_conv2d_wgrad_workspace_size() bytes the
+ * pixel reduction is split over workgroups and summed in a fixed order. */
+size_t d2mi_conv2d_wgrad_workspace_size(int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                                        int stride, int pad_beg, int pad_end);
+int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio, float* dbias, int N,
+                      int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
+                      int pad_end, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------- FrozenBN fold
+ * A frozen BatchNorm (moving statistics; lib/layers/normalization.py:15-119
+ * with training=False, gamma/beta trainable above FREEZE_AT per
+ * lib/modeling/backbone/resnet.py:22-46) folded into the preceding Conv2D:
+ *   scale = gamma / sqrt(var + eps);  w_eff = w * scale;
+ *   b_eff = bias * scale + beta - mean * scale.
+ * w HWIO [KH,KW,Cin,Cout]; bias / gamma / beta nullable.  Writes w_eff (HWIO,
+ * nullable), w_packed ([KH,KW,Cout,Cin] for d2mi_conv2d_nhwc, nullable) and
+ * b_eff [Cout]. */
+int d2mi_fold_frozen_bn(const float* w_hwio, const float* bias, const float* gamma,
+                        const float* beta, const float* mean, const float* var, float eps,
+                        int KH, int KW, int Cin, int Cout, float* w_eff, float* w_packed,
+                        float* b_eff, void* stream);
+/* Backward: from gw_eff (HWIO) and gb_eff ([Cout], nullable) writes gw, gbias,
+ * ggamma, gbeta (each nullable); per-channel reductions in a fixed order. */
+size_t d2mi_fold_frozen_bn_bwd_workspace_size(int Cout);
+int d2mi_fold_frozen_bn_bwd(const float* gw_eff, const float* gb_eff, const float* w_hwio,
+                            const float* bias, const float* gamma, const float* mean,
+                            const float* var, float eps, int KH, int KW, int Cin, int Cout,
+                            float* gw, float* gbias, float* ggamma, float* gbeta,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

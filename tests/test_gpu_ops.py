@@ -122,8 +122,9 @@ def test_roi_align_backward_raw_large_crops_and_ragged_channels(dev, C, crop, sr
     g = rng.normal(size=tuple(out.shape)).astype(F32)
     out.backward(torch.from_numpy(g).to(dev))
     if sr == 0:
+        # pixels with > 64 contributions are summed as 64-long partials: not bit-exact
         want = oracle.crop_and_resize_grad_image(g, boxes, bimg, (3, 40, 52))
-        np.testing.assert_array_equal(x.grad.cpu().numpy(), want)
+        np.testing.assert_allclose(x.grad.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
     else:
         lhs = (out.double() * torch.from_numpy(g).to(dev).double()).sum().item()
         rhs = (x.double() * x.grad.double()).sum().item()
@@ -356,6 +357,39 @@ def test_fast_rcnn_inference_vs_oracle(dev):
         assert_boxes_close(gb[n].cpu().numpy(), wb)
 
 
+def test_fast_rcnn_inference_dense_layout_ignores_negative_slots(dev):
+    """The model's dense [N, P] layout: padded rows carry roi_slot = -1 and are
+    skipped without raising the error word."""
+    from detectron2_tensorflow_amd import _C
+    rng = np.random.default_rng(32)
+    N, P, K = 2, 200, 80
+    image_hw = np.array([[800, 1333], [640, 1000]], np.int32)
+    valid = np.ones((N, P), bool)
+    valid[1, 150:] = False
+    roi_img = np.repeat(np.arange(N), P).astype(np.int32)
+    roi_slot = np.where(valid.reshape(-1), np.tile(np.arange(P), N), -1).astype(np.int32)
+    props = np.concatenate([rand_boxes(rng, P, *image_hw[n]) for n in range(N)])
+    logits = rng.normal(0, 3, size=(N * P, K + 1)).astype(F32)
+    deltas = rng.normal(0, 0.5, size=(N * P, K * 4)).astype(F32)
+    w = (10.0, 10.0, 5.0, 5.0)
+    keep = valid.reshape(-1)
+    want = oracle.fast_rcnn_inference(oracle.apply_deltas(deltas[keep], props[keep], w),
+                                      oracle.softmax(logits[keep]), roi_img[keep], roi_slot[keep],
+                                      P, image_hw, 0.05, 0.5, 100)
+    _C.clear_errors()
+    t = lambda a: torch.from_numpy(a).to(dev)
+    gb, gs, gc, gv, groi = ops().fast_rcnn_inference(t(logits), t(deltas), t(props), t(roi_img),
+                                                      t(roi_slot), N, P, t(image_hw), w, 0.05,
+                                                      0.5, 100)
+    _C.raise_on_errors(dev)
+    for n in range(N):
+        wb, wsc, wc, wv, wroi = want[n]
+        np.testing.assert_array_equal(gv[n].cpu().numpy(), wv)
+        np.testing.assert_array_equal(gc[n].cpu().numpy(), wc)
+        np.testing.assert_allclose(gs[n].cpu().numpy(), wsc, rtol=2e-6, atol=1e-7)
+        assert_boxes_close(gb[n].cpu().numpy(), wb)
+
+
 # -------------------------------------------------------------- RetinaNet
 def test_retinanet_inference_vs_oracle(dev):
     rng = np.random.default_rng(41)
@@ -457,3 +491,108 @@ def test_conv2d_residual_relu_after_and_split_k(dev, shape):
                            residual=res.to(dev), relu_after_add=True)
     assert torch.equal(y1, y2)
     np.testing.assert_allclose(y1.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("conf", [
+    # N, H, W, Cin, Cout, k, stride, relu, topdown, residual
+    (2, 25, 42, 256, 256, 3, 1, True, False, False),   # FPN/RPN/mask 3x3: MFMA dgrad
+    (2, 50, 84, 512, 256, 1, 1, False, True, False),   # FPN lateral + top-down
+    (2, 50, 84, 1024, 256, 1, 1, False, False, True),  # bottleneck conv3 + residual
+    (2, 50, 84, 512, 1024, 1, 2, False, False, False), # strided shortcut: GEMM + scatter
+    (1, 13, 21, 256, 3, 1, 1, False, False, False),    # objectness 1x1: Cout=3 dgrad fallback
+    (1, 17, 9, 64, 96, 3, 2, True, False, False),      # 3x3 stride 2: MIOpen fallback
+])
+def test_conv_mfma_autograd_matches_torch(dev, conf):
+    """Gradients of the MFMA conv layer (x, w, b, top-down, residual) vs
+    autograd of the fp64 torch reference."""
+    from detectron2_tensorflow_amd.layers.convolutional import _ConvMFMAFn, same_pads
+    N, H, W, Cin, Cout, k, stride, relu, td, res = conf
+    g = torch.Generator().manual_seed(sum(conf[:7]))
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
+    b = torch.randn(Cout, generator=g)
+    pads = same_pads(k)
+    OH = (H + sum(pads) - k) // stride + 1
+    OW = (W + sum(pads) - k) // stride + 1
+    top = torch.randn(N, (OH + 1) // 2, (OW + 1) // 2, Cout, generator=g) if td else None
+    resid = torch.randn(N, OH, OW, Cout, generator=g) if res else None
+    gy = torch.randn(N, OH, OW, Cout, generator=g)
+
+    def ref_fn(x, w, b, top, resid):
+        xp = torch.nn.functional.pad(x, (0, 0, pads[0], pads[1], pads[0], pads[1]))
+        y = torch.nn.functional.conv2d(xp.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), b,
+                                       stride=stride).permute(0, 2, 3, 1)
+        if top is not None:
+            y = y + top.repeat_interleave(2, 1).repeat_interleave(2, 2)[:, :OH, :OW]
+        if resid is not None:
+            y = y + resid
+        return torch.relu(y) if relu else y
+
+    leaves = [t.double().requires_grad_(True) if t is not None else None
+              for t in (x, w, b, top, resid)]
+    ref_fn(*leaves).backward(gy.double())
+    dl = [t.to(dev).requires_grad_(True) if t is not None else None for t in (x, w, b, top, resid)]
+    wp = ops().pack_conv_weights(dl[1].detach())
+    y = _ConvMFMAFn.apply(dl[0], dl[1], dl[2], wp, stride, pads, relu, dl[3], dl[4],
+                          relu and (td or res))
+    y.backward(gy.to(dev))
+    for name, a, r in zip("x w b top res".split(), dl, leaves):
+        if a is None:
+            continue
+        np.testing.assert_allclose(a.grad.cpu().double().numpy(), r.grad.numpy(), rtol=1e-4,
+                                   atol=2e-4 * max(1.0, float(r.grad.abs().max())), err_msg=name)
+
+
+@pytest.mark.parametrize("conf", [(2, 40, 52, 256, 256, 3, 1), (2, 30, 41, 64, 96, 3, 2),
+                                  (2, 200, 168, 256, 64, 1, 1), (1, 50, 84, 512, 1024, 1, 2)])
+def test_conv2d_wgrad_kernel_with_bias(dev, conf):
+    """d2mi_conv2d_wgrad (and its fused bias gradient) vs float64 torch."""
+    N, H, W, Cin, Cout, k, s = conf
+    g = torch.Generator().manual_seed(sum(conf))
+    p = (k - 1) // 2
+    x = torch.randn(N, H, W, Cin, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, OH, OW, Cout, generator=g)
+    want = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (Cout, Cin, k, k),
+                                       dy.permute(0, 3, 1, 2).double(), s, p).permute(2, 3, 1, 0)
+    dw, db = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True)
+    scale = float(want.abs().max())
+    np.testing.assert_allclose(dw.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=2e-5 * scale)
+    np.testing.assert_allclose(db.cpu().double().numpy(), dy.double().sum((0, 1, 2)).numpy(),
+                               rtol=1e-4, atol=1e-3)
+    dw2, db2 = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_fold_frozen_bn_forward_backward(dev, with_bias):
+    g = torch.Generator().manual_seed(5)
+    KH, Cin, Cout = 3, 64, 128
+    w = torch.randn(KH, KH, Cin, Cout, generator=g)
+    bias = torch.randn(Cout, generator=g) if with_bias else None
+    gamma, beta = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g)
+    mean, var = torch.randn(Cout, generator=g), torch.rand(Cout, generator=g) + 0.1
+    gw_eff, gb_eff = torch.randn(KH, KH, Cin, Cout, generator=g), torch.randn(Cout, generator=g)
+
+    def ref(w, bias, gamma, beta):
+        scale = gamma / torch.sqrt(var.double() + 1e-5)
+        b = beta - mean.double() * scale + (bias * scale if bias is not None else 0)
+        return w * scale, b
+
+    lv = [t.double().requires_grad_(True) if t is not None else None for t in (w, bias, gamma, beta)]
+    rw, rb = ref(*lv)
+    (rw * gw_eff.double()).sum().add((rb * gb_eff.double()).sum()).backward()
+    dv = [t.to(dev).requires_grad_(True) if t is not None else None for t in (w, bias, gamma, beta)]
+    we, be, packed = ops().fold_frozen_bn(dv[0], dv[1], dv[2], dv[3], mean.to(dev), var.to(dev),
+                                          1e-5, want_packed=True)
+    np.testing.assert_allclose(we.detach().cpu().double().numpy(), rw.detach().numpy(), rtol=1e-5,
+                               atol=1e-5)
+    np.testing.assert_allclose(be.detach().cpu().double().numpy(), rb.detach().numpy(), rtol=1e-5,
+                               atol=1e-5)
+    assert torch.equal(packed, ops().pack_conv_weights(we.detach()))
+    ((we * gw_eff.to(dev)).sum() + (be * gb_eff.to(dev)).sum()).backward()
+    for name, a, r in zip(["w", "bias", "gamma", "beta"], dv, lv):
+        if a is None:
+            continue
+        np.testing.assert_allclose(a.grad.cpu().double().numpy(), r.grad.numpy(), rtol=1e-4,
+                                   atol=1e-3, err_msg=name)

@@ -68,6 +68,35 @@ def bench_conv(dev, iters):
     return out
 
 
+def bench_wgrad(dev, iters):
+    """Weight gradient: MFMA wgrad kernel vs torch.nn.grad.conv2d_weight (MIOpen)."""
+    out = []
+    for name, N, H, W, Cin, Cout, k, s in CONV_SHAPES:
+        if Cout % 4:
+            continue
+        x = torch.randn(N, H, W, Cin, device=dev)
+        p = (k - 1) // 2
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        dy = torch.randn(N, OH, OW, Cout, device=dev)
+        flops = 2.0 * N * OH * OW * Cout * k * k * Cin
+        ms = timeit(lambda: ops.conv2d_wgrad(x, dy, k, s, (p, p)), iters)
+        xc, dyc = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
+        if k == 1:
+            x2, dy2 = x.reshape(-1, Cin), dy.reshape(-1, Cout)
+            ms_t = timeit(lambda: torch.mm(x2.t(), dy2), iters)
+        else:
+            ms_t = timeit(lambda: torch.nn.grad.conv2d_weight(xc, (Cout, Cin, k, k), dyc, s, p),
+                          iters)
+        ref = torch.nn.grad.conv2d_weight(xc, (Cout, Cin, k, k), dyc, s, p).permute(2, 3, 1, 0)
+        err = float((ops.conv2d_wgrad(x, dy, k, s, (p, p)) - ref).abs().max() /
+                    ref.abs().max().clamp(min=1e-30))
+        out.append({"kernel": "wgrad", "shape": name, "mfma_us": round(ms * 1e3, 1),
+                    "mfma_tflops": round(flops / ms / 1e9, 1),
+                    "miopen_us": round(ms_t * 1e3, 1),
+                    "miopen_tflops": round(flops / ms_t / 1e9, 1), "max_rel_err": err})
+    return out
+
+
 def bench_roi(dev, iters):
     g = torch.Generator(device="cpu").manual_seed(0)
     feats = [torch.randn(2, 800 // s, 1344 // s, 256, generator=g).to(dev) for s in (4, 8, 16, 32)]
@@ -113,12 +142,13 @@ def bench_topk(dev, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="conv,roi,nms,topk")
+    ap.add_argument("--only", default="conv,wgrad,roi,nms,topk")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     _C.load()
     dev = torch.device("cuda:0")
-    fns = {"conv": bench_conv, "roi": bench_roi, "nms": bench_nms, "topk": bench_topk}
+    fns = {"conv": bench_conv, "wgrad": bench_wgrad, "roi": bench_roi, "nms": bench_nms,
+           "topk": bench_topk}
     for name in a.only.split(","):
         for row in fns[name](dev, a.iters):
             print(json.dumps(row), flush=True)

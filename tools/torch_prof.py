@@ -1,0 +1,65 @@
+#!/usr/bin/env python
+"""Attribute GPU kernel time of bench.py's step to PyTorch ops (torch.profiler).
+
+usage: python tools/torch_prof.py [--mode train|infer] [--steps 3] [--height 800 --width 1333]
+Prints the top ops by self device time and writes gpurun_out/torch_prof_<mode>.txt.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="train")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--width", type=int, default=1333)
+    ap.add_argument("--rows", type=int, default=60)
+    a = ap.parse_args()
+    import bench
+    sys.argv = [sys.argv[0], "--mode", a.mode, "--height", str(a.height), "--width", str(a.width)]
+    args = bench.parse()
+    args.gpus = 1
+    dev = torch.device("cuda", 0)
+    from detectron2_tensorflow_amd import _C
+    _C.load()
+    cfg, model = bench.build(args, dev)
+    batch = bench.synthetic_batch(args, dev, 0)
+    bench.calibrate_scores(model, batch)
+    if a.mode == "train":
+        from detectron2_tensorflow_amd.engine import Trainer
+        tr = Trainer(cfg, model)
+        step = lambda: tr.step(batch)
+        ctx = torch.enable_grad
+    else:
+        step = lambda: model.inference(batch)
+        ctx = torch.no_grad
+    with ctx():
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                     record_shapes=True) as prof:
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+    table = prof.key_averages(group_by_input_shape=False).table(
+        sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60)
+    shapes = prof.key_averages(group_by_input_shape=True).table(
+        sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=50,
+        max_shapes_column_width=90)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"torch_prof_{a.mode}.txt"), "w") as f:
+        f.write(table + "\n\n" + shapes)
+    print(table)
+
+
+if __name__ == "__main__":
+    main()
