@@ -213,14 +213,63 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
         }
         continue;
       }
+      if (a.splits > 1) {
+        float* pp = a.partial + ((size_t)split * a.M + mb) * a.Cout + co;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dm = (r & 3) + 8 * (r >> 2);
+          if (mb + dm < a.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
+        }
+        continue;
+      }
+      // residual / top-down operands: all 16 loads issued before any store
+      // (y may not alias them; without this the loads serialise behind the stores)
+      float add[16];
+      // pixel coordinates of row mb, then stepped (dm < 32): no per-element division
+      int tn = 0, toh = 0, tow = 0, last = 0;
+      if (a.topdown) {
+        const int mm = min(mb, a.M - 1);
+        tn = mm / (a.OH * a.OW);
+        const int rem = mm - tn * a.OH * a.OW;
+        toh = rem / a.OW;
+        tow = rem - toh * a.OW;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        const int m = mb + dm;
+        float v = 0.f;
+        if (a.topdown) {  // advance (n, oh, ow) from row mb + last to mb + dm
+          tow += dm - last;
+          last = dm;
+          while (tow >= a.OW) {
+            tow -= a.OW;
+            if (++toh == a.OH) { toh = 0; ++tn; }
+          }
+        }
+        if (m < a.M) {
+          if (a.residual) v = a.residual[(size_t)m * a.Cout + co];
+          if (a.topdown)
+            v = v + a.topdown[(((size_t)tn * a.tdH + (toh >> 1)) * a.tdW + (tow >> 1)) * a.Cout +
+                              co];
+        }
+        add[r] = v;
+      }
+      const bool relu_after = (a.flags & kReluAfterResidual) != 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb + (r & 3) + 8 * (r >> 2);
         if (m >= a.M) continue;
-        if (a.splits > 1)
-          a.partial[((size_t)split * a.M + m) * a.Cout + co] = acc[i][j][r];
-        else
-          a.y[(size_t)m * a.Cout + co] = epilogue(a, acc[i][j][r], m, co);
+        float v = acc[i][j][r] + bv;
+        if (relu && !relu_after) v = fmaxf(v, 0.f);
+        // epilogue() order: conv + bias, (+ top-down) (+ residual)
+        if (a.topdown && a.residual) {
+          v = epilogue(a, acc[i][j][r], m, co);
+        } else {
+          v = v + add[r];
+          if (relu && relu_after) v = fmaxf(v, 0.f);
+        }
+        a.y[(size_t)m * a.Cout + co] = v;
       }
     }
   }

@@ -22,11 +22,13 @@ class KernelTimer:
     ``work`` is the op's ALGORITHMIC flops (conv) or bytes (ROIAlign)."""
 
     enabled = False
+    detail = False   # also key records by shape (tools/conv_shapes.py)
     records = []
 
     @classmethod
-    def reset(cls, enabled=True):
+    def reset(cls, enabled=True, detail=False):
         cls.enabled = enabled
+        cls.detail = detail
         cls.records = []
 
     @classmethod
@@ -279,7 +281,10 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                       _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
                                       int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
                                       _C.stream_of(x.device))
-    KernelTimer.stop(ev, "conv2d_mfma", 2.0 * N * OH * OW * Cout * KH * KW * Cin)
+    fl = 2.0 * N * OH * OW * Cout * KH * KW * Cin
+    KernelTimer.stop(ev, "conv2d_mfma", fl)
+    if KernelTimer.detail and ev is not None:
+        KernelTimer.stop(ev, f"conv {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride} p{pb}{pe}", fl)
     _C.check(rc, "d2mi_conv2d_nhwc")
     return y
 
@@ -302,6 +307,9 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False):
     rc = _C.lib().d2mi_conv2d_wgrad(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
                                     _C.ptr(ws), wsb, _C.stream_of(x.device))
     KernelTimer.stop(ev, "conv2d_wgrad_mfma", 2.0 * dy.numel() * KH * KW * Cin)
+    if KernelTimer.detail and ev is not None:
+        KernelTimer.stop(ev, f"wgrad {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride}",
+                         2.0 * dy.numel() * KH * KW * Cin)
     _C.check(rc, "d2mi_conv2d_wgrad")
     return (dw, db) if with_bias else dw
 

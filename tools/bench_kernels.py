@@ -44,6 +44,9 @@ CONV_SHAPES = [
     ("res2_conv2 3x3", 2, 200, 336, 64, 64, 3, 1),
     ("res4_conv1 1x1", 2, 50, 84, 1024, 256, 1, 1),
     ("res3_conv2 3x3", 2, 100, 168, 128, 128, 3, 1),
+    ("res2_conv3 1x1 +res", 2, 200, 336, 64, 256, 1, 1),
+    ("res4_conv3 1x1 +res", 2, 50, 84, 256, 1024, 1, 1),
+    ("fpn_lat_p2 1x1 +td", 2, 200, 336, 256, 256, 1, 1),
 ]
 
 
@@ -57,7 +60,14 @@ def bench_conv(dev, iters):
         p = (k - 1) // 2
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         flops = 2.0 * N * OH * OW * Cout * k * k * Cin
-        ms = timeit(lambda: ops.conv2d_nhwc(x, wp, b, s, (p, p)), iters)
+        res = td = None
+        if name.endswith("+res"):
+            res = torch.randn(N, OH, OW, Cout, device=dev)
+        if name.endswith("+td"):
+            td = torch.randn(N, (OH + 1) // 2, (OW + 1) // 2, Cout, device=dev)
+        ms = timeit(lambda: ops.conv2d_nhwc(x, wp, b, s, (p, p), relu=res is not None,
+                                            residual=res, topdown=td,
+                                            relu_after_add=res is not None), iters)
         xc = x.permute(0, 3, 1, 2)
         wc = w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last)
         ms_t = timeit(lambda: F.conv2d(xc, wc, b, stride=s, padding=p), iters)
@@ -72,7 +82,7 @@ def bench_wgrad(dev, iters):
     """Weight gradient: MFMA wgrad kernel vs torch.nn.grad.conv2d_weight (MIOpen)."""
     out = []
     for name, N, H, W, Cin, Cout, k, s in CONV_SHAPES:
-        if Cout % 4:
+        if Cout % 4 or "+" in name:
             continue
         x = torch.randn(N, H, W, Cin, device=dev)
         p = (k - 1) // 2
