@@ -115,7 +115,24 @@ def synthetic_batch(args, device, rank):
     return synthetic_images(args.batch, args.height, args.width, 1000 + rank, device)
 
 
-def kernel_report(summary):
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_train_pmc.json")
+
+
+def pmc_traffic(group, mode):
+    """HBM bytes per launch of a kernel group from the committed rocprofv3 PMC
+    passes (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)
+    of this same bench command in training mode; None when not available."""
+    if mode != "train" or not os.path.exists(PMC_FILE):
+        return None
+    try:
+        with open(PMC_FILE) as f:
+            g = json.load(f)["groups"].get(group)
+        return round(g["traffic_bytes_per_launch"]) if g else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def kernel_report(summary, mode="infer"):
     """Roofline objects from the live HIP-event timings of the timed region."""
     rep = {}
     if "conv2d_mfma" in summary:
@@ -123,9 +140,19 @@ def kernel_report(summary):
         ach = flops / (ms * 1e-3) / 1e12
         rep["conv2d_mfma"] = {"bound": "mfma", "achieved": round(ach, 2),
                               "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                              "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4),
+                              "traffic": pmc_traffic("conv2d_mfma", mode),
                               "launches": n, "avg_us": round(ms * 1e3 / n, 2),
                               "algorithmic_per_launch": flops / n}
+    if "conv2d_wgrad_mfma" in summary:
+        n, ms, flops = summary["conv2d_wgrad_mfma"]
+        ach = flops / (ms * 1e-3) / 1e12
+        rep["conv2d_wgrad_mfma"] = {"bound": "mfma", "achieved": round(ach, 2),
+                                    "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4),
+                                    "traffic": pmc_traffic("conv_wgrad", mode), "launches": n,
+                                    "avg_us": round(ms * 1e3 / n, 2),
+                                    "algorithmic_per_launch": flops / n}
     for name in ("roi_align_fwd", "roi_align_bwd"):
         if name not in summary:
             continue
@@ -133,7 +160,7 @@ def kernel_report(summary):
         ach = byts / (ms * 1e-3) / 1e9
         rep[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                     "traffic": pmc_traffic(name, mode), "launches": n, "avg_us": round(ms * 1e3 / n, 2),
                      "algorithmic_per_launch": byts / n}
     return rep
 
@@ -164,10 +191,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # D2MI_REHEARSE_ONE_GPU=1: every rank on cuda:0 over gloo — exercises the DP
+    # code path (bucketed all-reduce hooks, barrier, max-time) on a 1-GPU box;
+    # never a measurement.
+    rehearse = os.environ.get("D2MI_REHEARSE_ONE_GPU") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     args.gpus = world
     device = torch.device("cuda", local)
     from detectron2_tensorflow_amd import _C
@@ -208,13 +244,22 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     _C.raise_on_errors(device)
+    in_sync = None
+    if world > 1 and args.mode == "train":
+        # every replica must hold identical weights after the DP steps
+        with torch.no_grad():
+            ck = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum()
+            ck = ck.reshape(1).to(device)
+        allck = [torch.zeros_like(ck) for _ in range(world)]
+        torch.distributed.all_gather(allck, ck)
+        in_sync = all(bool(torch.equal(allck[0], c)) for c in allck)
     if args.mode == "train":
         extra = {"losses_last_step_rank0": {k: round(float(v.detach()), 4) for k, v in out.items()}}
     else:
         extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 
     if rank == 0:
-        kernels = kernel_report(summary)
+        kernels = kernel_report(summary, args.mode)
         result = {
             "metric": "img/sec whole-node Mask R-CNN R50-FPN @1333x800"
                       if args.model.startswith("mask") else "img/sec Faster R-CNN R50-FPN @1333x800",
@@ -236,6 +281,7 @@ def main():
                             "parallelism": (f"dp{world}" if args.mode == "train" else f"replicas{world}"),
                             "mode": args.mode}, **extra),
             "roofline": kernels.get("conv2d_mfma"),
+            **({"replicas_in_sync": in_sync} if in_sync is not None else {}),
             "kernels": kernels,
         }
         if args.cpu_baseline and world == 1:

@@ -1,0 +1,70 @@
+#!/usr/bin/env python
+"""Average FETCH_SIZE / WRITE_SIZE per dispatch of the hot kernels.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch (rocprofv3).  gfx950
+correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the
+bytes of 16 B/lane coalesced reads, so it is doubled here; WRITE_SIZE is taken
+as reported (exact for 16 B/lane stores; our conv epilogue stores 4 B/lane, an
+uncalibrated width — noted in the output).
+
+usage: pmc_summarize.py <fetch dir> <write dir> <out.json>
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+GROUPS = {
+    "conv2d_mfma": re.compile(r"conv_mfma_kernel|splitk_reduce_kernel"),
+    "conv_mfma_kernel": re.compile(r"conv_mfma_kernel"),
+    "roi_align_fwd": re.compile(r"roi_align_fwd_kernel"),
+    "roi_align_bwd": re.compile(r"roi_bwd_"),
+    "conv_wgrad": re.compile(r"conv_wgrad_kernel|wgrad_reduce_kernel"),
+}
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = collections.defaultdict(lambda: [0, 0.0])
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r.get("Kernel_Name", "")
+            per[name][0] += 1
+            per[name][1] += float(r["Counter_Value"])
+    return per
+
+
+def main():
+    fd, wd, out = sys.argv[1:4]
+    fetch = load(fd, "FETCH_SIZE")
+    write = load(wd, "WRITE_SIZE")
+    res = {"units": "bytes per dispatch", "fetch_correction": 2.0,
+           "note": "FETCH_SIZE x2 (gfx950 16 B/lane reads); WRITE_SIZE as reported",
+           "groups": {}}
+    for g, rx in GROUPS.items():
+        fn = sum(v[0] for k, v in fetch.items() if rx.search(k))
+        fb = sum(v[1] for k, v in fetch.items() if rx.search(k))
+        wn = sum(v[0] for k, v in write.items() if rx.search(k))
+        wb = sum(v[1] for k, v in write.items() if rx.search(k))
+        if fn == 0 and wn == 0:
+            continue
+        main_n = sum(v[0] for k, v in fetch.items()
+                     if rx.search(k) and "reduce" not in k)
+        res["groups"][g] = {
+            "dispatches": fn, "main_kernel_dispatches": main_n,
+            "fetch_bytes_per_launch": 2.0 * fb * 1024 / max(main_n, 1),
+            "write_bytes_per_launch": wb * 1024 / max(main_n, 1),
+        }
+        res["groups"][g]["traffic_bytes_per_launch"] = (
+            res["groups"][g]["fetch_bytes_per_launch"] + res["groups"][g]["write_bytes_per_launch"])
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
