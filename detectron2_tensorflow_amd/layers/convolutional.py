@@ -248,11 +248,19 @@ class Conv2D(Layer):
             if final_relu and not fuse_relu:
                 ret = torch.relu(ret)
             return ret
-        # torch (channels_last) path: backbone 3x3 convs / the stem
-        x = fix_padding(inputs, self.kernel_size, self.padding, self.rate)
+        # torch (channels_last) path: backbone 3x3 convs / the stem.  A symmetric
+        # SAME pad is the conv's own zero padding (no padded copy of the input).
+        pad = 0
+        x = inputs
+        if self.padding == "SAME" and self.kernel_size != 1:
+            pb, pe = same_pads(self.kernel_size, self.rate)
+            if pb == pe:
+                pad = pb
+            else:
+                x = fix_padding(inputs, self.kernel_size, self.padding, self.rate)
         y = F.conv2d(x.permute(0, 3, 1, 2),
                      w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last), b,
-                     stride=self.stride, dilation=self.rate, groups=self.num_groups)
+                     stride=self.stride, padding=pad, dilation=self.rate, groups=self.num_groups)
         ret = y.permute(0, 2, 3, 1)
         if norm is not None:
             ret = norm(ret)

@@ -50,9 +50,15 @@ CONV_SHAPES = [
 ]
 
 
+SHAPE_FILTER = None
+NO_MIOPEN = False
+
+
 def bench_conv(dev, iters):
     out = []
     for name, N, H, W, Cin, Cout, k, s in CONV_SHAPES:
+        if SHAPE_FILTER and SHAPE_FILTER not in name:
+            continue
         x = torch.randn(N, H, W, Cin, device=dev)
         w = torch.randn(k, k, Cin, Cout, device=dev) / math.sqrt(k * k * Cin)
         b = torch.randn(Cout, device=dev)
@@ -70,7 +76,8 @@ def bench_conv(dev, iters):
                                             relu_after_add=res is not None), iters)
         xc = x.permute(0, 3, 1, 2)
         wc = w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last)
-        ms_t = timeit(lambda: F.conv2d(xc, wc, b, stride=s, padding=p), iters)
+        ms_t = float("nan") if NO_MIOPEN else timeit(
+            lambda: F.conv2d(xc, wc, b, stride=s, padding=p), iters)
         out.append({"kernel": "conv", "shape": name, "mfma_us": round(ms * 1e3, 1),
                     "mfma_tflops": round(flops / ms / 1e9, 1),
                     "miopen_us": round(ms_t * 1e3, 1),
@@ -154,7 +161,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="conv,wgrad,roi,nms,topk")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shape", default=None, help="substring filter on conv shape names")
+    ap.add_argument("--no-miopen", action="store_true")
     a = ap.parse_args()
+    global SHAPE_FILTER, NO_MIOPEN
+    SHAPE_FILTER = a.shape
+    NO_MIOPEN = a.no_miopen
     _C.load()
     dev = torch.device("cuda:0")
     fns = {"conv": bench_conv, "wgrad": bench_wgrad, "roi": bench_roi, "nms": bench_nms,
