@@ -82,7 +82,10 @@ def build(args, device):
 @torch.no_grad()
 def calibrate_scores(model, batch):
     """Rescale the class / objectness logit weights so the random-init model
-    emits BASELINE.md's synthetic score distributions."""
+    emits BASELINE.md's synthetic score distributions, and the RPN anchor
+    deltas to N(0, 0.1^2): the unnormalised features of a random-init ResNet
+    otherwise give deltas of O(10), which collapse most proposals onto the
+    image border (a random-init artefact, not a training distribution)."""
     stats = {}
 
     def grab(name):
@@ -106,6 +109,7 @@ def calibrate_scores(model, batch):
     cls.weights.normal_(0.0, 3.0 / math.sqrt(max(stats["box"], 1e-12)))
     obj = rpn_head.objectness_logits
     obj.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["rpn"], 1e-12)))
+    rpn_head.anchor_deltas.weights.normal_(0.0, 0.1 / math.sqrt(max(stats["rpn"], 1e-12)))
 
 
 def synthetic_batch(args, device, rank):

@@ -159,6 +159,43 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
   const int C = a.C;
   const bool pad = a.pad_border != 0;
   const int b_end = min(nbins, (int)(blockIdx.y + 1) * kBinsPerBlock);
+  if (VEC4 && S == 1 && C == 256) {
+    // Common case (C = 256, one sample per bin): U bins per wave iteration with
+    // all 4U corner loads issued before any is consumed (the taps are clamped
+    // to valid rows, so the loads are unconditional; invalid samples are zeroed
+    // after) — memory-level parallelism instead of one latency per bin.
+    constexpr int U = 4;
+    const float4* p = reinterpret_cast<const float4*>(base);
+    for (int bb = blockIdx.y * kBinsPerBlock + wave; bb < b_end; bb += 4 * U) {
+      float4 c00[U], c01[U], c10[U], c11[U];
+      float ly[U], lx[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int bin = min(bb + 4 * u, b_end - 1);
+        const int oy = bin / a.out_w, ox = bin - oy * a.out_w;
+        const Tap ty = make_tap(in_coord(g.y1, g.y2, g.hs, oy, g.ch, g.Hp), g.Hp, g.H, pad);
+        const Tap tx = make_tap(in_coord(g.x1, g.x2, g.ws, ox, g.cw, g.Wp), g.Wp, g.W, pad);
+        ok[u] = g.ok && ty.valid && tx.valid;
+        ly[u] = ty.lerp;
+        lx[u] = tx.lerp;
+        c00[u] = p[((size_t)ty.r0 * g.W + tx.r0) * 64 + lane];
+        c01[u] = p[((size_t)ty.r0 * g.W + tx.r1) * 64 + lane];
+        c10[u] = p[((size_t)ty.r1 * g.W + tx.r0) * 64 + lane];
+        c11[u] = p[((size_t)ty.r1 * g.W + tx.r1) * 64 + lane];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int bin = bb + 4 * u;
+        if (bin >= b_end) break;
+        const float4 top = lerp4(c00[u], c01[u], lx[u]);
+        const float4 bot = lerp4(c10[u], c11[u], lx[u]);
+        const float4 v = ok[u] ? lerp4(top, bot, ly[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<float4*>(a.out + ((size_t)r * nbins + bin) * C)[lane] = v;
+      }
+    }
+    return;
+  }
   for (int bin = blockIdx.y * kBinsPerBlock + wave; bin < b_end; bin += 4) {
     const int oy = bin / a.out_w, ox = bin - oy * a.out_w;
     float* dst = a.out + ((size_t)r * nbins + bin) * C;

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--height", type=int, default=800)
     ap.add_argument("--width", type=int, default=1333)
     ap.add_argument("--rows", type=int, default=60)
+    ap.add_argument("--stacks", action="store_true", help="group small ops by Python stack")
     a = ap.parse_args()
     import bench
     sys.argv = [sys.argv[0], "--mode", a.mode, "--height", str(a.height), "--width", str(a.width)]
@@ -46,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
-                     record_shapes=True) as prof:
+                     record_shapes=True, with_stack=a.stacks) as prof:
             for _ in range(a.steps):
                 step()
             torch.cuda.synchronize()
@@ -55,6 +56,9 @@ def main():
     shapes = prof.key_averages(group_by_input_shape=True).table(
         sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=50,
         max_shapes_column_width=90)
+    if a.stacks:
+        shapes = prof.key_averages(group_by_stack_n=6).table(
+            sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=40)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"torch_prof_{a.mode}.txt"), "w") as f:
         f.write(table + "\n\n" + shapes)
