@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--height", type=int, default=800)
     p.add_argument("--width", type=int, default=1333)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
-    p.add_argument("--cpu-images", type=int, default=1)
+    p.add_argument("--cpu-images", type=int, default=2, help="images per CPU iteration (<= batch)")
+    p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--mode", default="train", choices=["train", "infer"])
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
@@ -169,25 +170,41 @@ def kernel_report(summary, mode="infer"):
     return rep
 
 
-def cpu_baseline(args, model, batch):
+def cpu_baseline(args, model, batch, cfg=None):
+    """The oracle's CPU restatement timed on this host (rank 0, N=1): for
+    --mode train one training iteration (oracle/cpu_train.py: forward with
+    autograd, losses, backward, update) on ONE image of the same size — the
+    bounded sample; for --mode infer the inference forward (cpu_pipeline.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cpu_pipeline import CPUReference, cpu_cores
     cores = cpu_cores()
-    ref = CPUReference(model)
-    model.eval()
-    n = args.cpu_images
+    n = min(args.cpu_images, args.batch)
+    iters = max(1, args.cpu_iters)
     imgs = batch["image"][:n].cpu().numpy()
     shapes = batch["image_shape"][:n].cpu().numpy()
-    ref(imgs[:1, :256, :320], [[256, 320]], threads=cores)  # warm the libraries
-    t0 = time.perf_counter()
-    ref(imgs, shapes, threads=cores)
-    dt = time.perf_counter() - t0
-    what = ("inference forward only (the CPU restatement has no backward; a training step "
-            "costs more)" if args.mode == "train" else "inference")
-    return {"value": round(n / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
-            "sample": f"{n} image(s) {args.height}x{args.width}, whole {args.model} {what}, "
-                      f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU convs), "
-                      f"{dt:.1f} s"}
+    if args.mode == "train":
+        import cpu_train
+        step = cpu_train.CPUTrainStep(model, cfg)
+        inst = {k: v[:n].cpu() for k, v in batch["instances"].items()}
+        small = {k: v[:1] for k, v in inst.items()}
+        step.step(imgs[:1, :256, :320], [[256, 320]], small, threads=cores)  # warm the libraries
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            step.step(imgs, shapes, inst, threads=cores)
+        dt = time.perf_counter() - t0
+        what = "training iteration(s) (forward + losses + backward + Momentum-SGD update)"
+    else:
+        ref = CPUReference(model.eval())
+        ref(imgs[:1, :256, :320], [[256, 320]], threads=cores)  # warm the libraries
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            ref(imgs, shapes, threads=cores)
+        dt = time.perf_counter() - t0
+        what = "inference forward(s)"
+    return {"value": round(n * iters / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
+            "sample": f"{iters} x {n} image(s) {args.height}x{args.width}, {args.model} {what}, "
+                      f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU "
+                      f"convs/autograd), {dt:.1f} s on {cores} threads"}
 
 
 def main():
@@ -289,7 +306,7 @@ def main():
             "kernels": kernels,
         }
         if args.cpu_baseline and world == 1:
-            result["cpu_baseline"] = cpu_baseline(args, model, batch)
+            result["cpu_baseline"] = cpu_baseline(args, model, batch, cfg)
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

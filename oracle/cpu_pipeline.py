@@ -61,6 +61,19 @@ def _backbone(bb, x):
     return outs
 
 
+def _fpn(neck, x_feats):
+    """FPN.call (fpn.py:121-159) + LastLevelMaxPool (fpn.py:171-183)."""
+    x = [x_feats[f] for f in neck.in_features[::-1]]
+    prev = _conv(x[0], neck.lateral_convs[0])
+    results = [_conv(prev, neck.output_convs[0])]
+    for f, lat, out in zip(x[1:], neck.lateral_convs[1:], neck.output_convs[1:]):
+        top = prev.repeat_interleave(2, 1).repeat_interleave(2, 2)
+        prev = _conv(f, lat) + top
+        results.insert(0, _conv(prev, out))
+    results.append(results[-1][:, ::2, ::2, :])  # LastLevelMaxPool
+    return dict(zip(neck._out_features, results))
+
+
 class CPUReference:
     def __init__(self, model):
         self.m = copy.deepcopy(model).cpu().eval()
@@ -68,16 +81,7 @@ class CPUReference:
             p.requires_grad_(False)
 
     def fpn(self, feats):
-        neck = self.m.neck
-        x = [feats[f] for f in neck.in_features[::-1]]
-        prev = _conv(x[0], neck.lateral_convs[0])
-        results = [_conv(prev, neck.output_convs[0])]
-        for f, lat, out in zip(x[1:], neck.lateral_convs[1:], neck.output_convs[1:]):
-            top = prev.repeat_interleave(2, 1).repeat_interleave(2, 2)
-            prev = _conv(f, lat) + top
-            results.insert(0, _conv(prev, out))
-        results.append(results[-1][:, ::2, ::2, :])  # LastLevelMaxPool
-        return dict(zip(neck._out_features, results))
+        return _fpn(self.m.neck, feats)
 
     @torch.no_grad()
     def __call__(self, images, image_shapes, threads=None):
@@ -155,7 +159,21 @@ class CPUReference:
 
 
 def cpu_cores():
+    """CPUs this process may actually use: the affinity mask, capped by a
+    cgroup-v2 CPU quota and by OMP_NUM_THREADS when set (on the GPU box the
+    affinity mask shows the whole machine while the job gets a share of it)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n

@@ -292,3 +292,27 @@ def test_bucketed_allreduce_gloo_world2_matches_single_process(tmp_path):
         opt.step(0.05)
     for k, v in model.state_dict().items():
         torch.testing.assert_close(r0[k], v, rtol=1e-5, atol=1e-6)
+
+
+def test_cpu_training_step_restatement_runs_and_updates():
+    """oracle/cpu_train.py (bench.py's training cpu_baseline): one step on a tiny
+    image gives finite losses and moves the trainable weights only."""
+    import cpu_train
+    from detectron2_tensorflow_amd.config import finalize
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.utils.synthetic import synthetic_train_batch
+    cfg = _small_cfg()
+    cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = "raw"
+    finalize(cfg, True, 1, {"num_thing_classes": 80, "num_stuff_classes": 53,
+                            "stuff_ignore_value": 0})
+    torch.manual_seed(0)
+    model = build_model(cfg)
+    step = cpu_train.CPUTrainStep(model, cfg)
+    b = synthetic_train_batch(1, 128, 160, 0, torch.device("cpu"), sqrt_area=(16.0, 96.0))
+    w_tr = step.m.roi_heads.box_head.fcs[0].weights.detach().clone()
+    w_fz = step.m.backbone.stem.conv1.weights.detach().clone()
+    losses = step.step(b["image"].numpy(), b["image_shape"].numpy(), b["instances"], threads=4)
+    assert set(losses) == {"loss_rpn_cls", "loss_rpn_loc", "loss_cls", "loss_box_reg", "loss_mask"}
+    assert all(np.isfinite(v) for v in losses.values()), losses
+    assert not torch.equal(w_tr, step.m.roi_heads.box_head.fcs[0].weights.detach())
+    assert torch.equal(w_fz, step.m.backbone.stem.conv1.weights.detach())
