@@ -63,6 +63,9 @@ _SIGS = {
     "d2mi_conv2d_wgrad": (c_int, [P, P, P, P] + [c_int] * 10 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "d2mi_conv2d_nhwc_x3": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "d2mi_split_bf16x3": (c_int, [P, ctypes.c_int64, P, P]),
 }
 
 EXPORTED = tuple(_SIGS)

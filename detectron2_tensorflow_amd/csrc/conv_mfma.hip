@@ -27,6 +27,20 @@
 // (deterministic) and applies the epilogue.
 // fp32 in / fp32 accumulate: exact-f32 products; results differ from a CPU
 // conv only by summation order (the parity tests bound it).
+//
+// SPLIT variant (flags bit 2, kSplit3): the same f32 operands, multiplied on
+// the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate per clock).
+// Each f32 x is split EXACTLY into three bf16 terms by truncation,
+//   h = x & 0xffff0000,  m = (x - h) & 0xffff0000,  l = x - h - m,
+// (8 + 8 + 8 significant bits = f32's 24: h + m + l == x bit for bit), and
+// a*b is formed from the six products whose order is <= 2^-16 relative,
+//   ah*bh + ah*bm + am*bh + ah*bl + am*bm + al*bh,
+// dropping am*bl + al*bm + al*bl (<= 2^-23 * |a*b| together, below f32's own
+// rounding of the product, 2^-24 relative per accumulation step on top).
+// The 3 bf16 planes of each staged A/B tile live in LDS as [plane][row][32]
+// with XOR-swizzled 16-B chunks (swz(): conflict-free reads and writes).  Six bf16 MFMAs per 32x32x16 step = 2.67x the f32-MFMA rate at
+// f32-class error (tests: error vs float64 within a small factor of the
+// native f32 path's).
 #include "common.h"
 
 namespace d2mi {
@@ -34,9 +48,39 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32, LDSP = 36;
+constexpr int BK = 32, LDSP = 36, LDSB = 32;
 
-enum EpiFlags { kRelu = 1, kReluAfterResidual = 2 };
+// bf16 LDS images: 64-B rows (32 bf16 = one BK step) whose four 16-B chunks
+// are XOR-swizzled by (row >> 2) & 3.  ds_read_b128 phases (lanes
+// {0-3,12-15,20-27}, ... reading one chunk of 16 rows) and ds_write_b128 /
+// b64 phases (2 whole rows) then touch every bank once: conflict-free.
+__device__ __forceinline__ int swz(int row, int elem) {
+  return row * LDSB + ((((elem >> 3) ^ (row >> 2)) & 3) << 3) + (elem & 7);
+}
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+enum EpiFlags { kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4 };
+
+// Exact 3-term bf16 split of four floats (truncation; see the header).
+// Each output packs 4 bf16 (element order = float4 order).
+__device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hb[e] = __float_as_uint(x[e]) & 0xffff0000u;
+    const float r = x[e] - __uint_as_float(hb[e]);
+    mb[e] = __float_as_uint(r) & 0xffff0000u;
+    lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
+  }
+  h.x = (hb[0] >> 16) | hb[1];
+  h.y = (hb[2] >> 16) | hb[3];
+  m.x = (mb[0] >> 16) | mb[1];
+  m.y = (mb[2] >> 16) | mb[3];
+  l.x = (lb[0] >> 16) | (lb[1] & 0xffff0000u);
+  l.y = (lb[2] >> 16) | (lb[3] & 0xffff0000u);
+}
 
 struct ConvArgs {
   const float* x;
@@ -48,6 +92,11 @@ struct ConvArgs {
   float* partial;  // split-K workspace [splits][M][Cout] (nullable)
   int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW, flags;
   int M, nM, nN, ntiles, splits, kt_per_split, nk, cchunks;
+  int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
+  // pre-split operands (conv_x3_kernel): 3 bf16 planes each, plane strides in bytes
+  const uint16_t* x3;
+  const uint16_t* w3;
+  int x_plane_bytes, w_plane_bytes;
   int tdH, tdW;
 };
 
@@ -67,129 +116,12 @@ __device__ __forceinline__ float epilogue(const ConvArgs& a, float acc, int m, i
   return v;
 }
 
-// DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
-// 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
-// 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
-template <int WM, int WN, int TM, int TN, bool DB>
-__global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
-  constexpr int NB = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) float As[NB][BM * LDSP];
-  __shared__ __attribute__((aligned(16))) float Bs[NB][BN * LDSP];
-
-  // XCD-aware tile order: consecutive tiles (the Cout tiles of one pixel tile
-  // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
-  const int orig = blockIdx.x;
-  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-  const int mt = tile / a.nN, nt = tile - mt * a.nN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int split = blockIdx.y;
-  const int kt0 = split * a.kt_per_split;
-  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
-
-  const int srow = tid >> 3, schunk = (tid & 7) * 4;
-  int pn[RA], ph[RA], pw[RA];
-  bool pv[RA];
-#pragma unroll
-  for (int p = 0; p < RA; ++p) {
-    const int m = m0 + srow + 32 * p;
-    pv[p] = m < a.M;
-    const int mm = pv[p] ? m : 0;
-    pn[p] = mm / (a.OH * a.OW);
-    const int rem = mm - pn[p] * a.OH * a.OW;
-    ph[p] = rem / a.OW;
-    pw[p] = rem - ph[p] * a.OW;
-  }
-
-  float4 ra[RA], rb[RB];
-  auto load_tile = [&](int kt) {
-    const int tap = kt / a.cchunks;
-    const int c0 = (kt - tap * a.cchunks) * BK + schunk;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const bool cok = c0 < a.Cin;
-#pragma unroll
-    for (int p = 0; p < RA; ++p) {
-      const int ih = ph[p] * a.stride - a.pad + kh;
-      const int iw = pw[p] * a.stride - a.pad + kw;
-      const bool ok = cok && pv[p] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      ra[p] = ok ? ld4(a.x + (((size_t)pn[p] * a.H + ih) * a.W + iw) * a.Cin + c0)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int p = 0; p < RB; ++p) {
-      const int co = n0 + srow + 32 * p;
-      rb[p] = (cok && co < a.Cout) ? ld4(a.w + (((size_t)tap * a.Cout + co) * a.Cin + c0))
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < RA; ++p)
-      *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = ra[p];
-#pragma unroll
-    for (int p = 0; p < RB; ++p)
-      *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = rb[p];
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
+// Epilogue shared by the conv kernels: bias, ReLU, top-down / residual adds
+// (or the split-K partial slab), written straight from the MFMA accumulators.
+template <int WN, int TM, int TN>
+__device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)[TM][TN], int m0,
+                                              int n0, int wr, int wc, int lane, int split) {
   const int li = lane & 31, lh = lane >> 5;
-  if (kt0 < kt1) {
-    load_tile(kt0);
-    store_tile(0);
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
-      const float* A = As[buf];
-      const float* B = Bs[buf];
-#pragma unroll
-      for (int s0 = 0; s0 < 16; s0 += 4) {
-        float4 fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const float4*>(
-              &A[((wr * TM + i) * 32 + li) * LDSP + lh * 16 + s0]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const float4*>(
-              &B[((wc * TN + j) * 32 + li) * LDSP + lh * 16 + s0]);
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][ss], fb[j][ss], acc[i][j],
-                                                                0, 0, 0);
-      }
-      if (DB) {
-        if (more) store_tile(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-      } else {
-        __syncthreads();
-        if (more) {
-          store_tile(0);
-          __syncthreads();
-        }
-      }
-    }
-  }
-
   // C/D map for 32x32: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const bool simple = a.splits == 1 && !a.topdown && !a.residual;
   const bool relu = (a.flags & kRelu) != 0;
@@ -275,6 +207,380 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   }
 }
 
+// DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
+// 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
+// 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
+template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT>
+__global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
+  constexpr int NB = DB ? 2 : 1;
+  // f32: [row][36] floats; SPLIT: [3 planes][row][40] bf16 (as uint16)
+  constexpr int A_WORDS = SPLIT ? 3 * BM * LDSB / 2 : BM * LDSP;
+  constexpr int B_WORDS = SPLIT ? 3 * BN * LDSB / 2 : BN * LDSP;
+  __shared__ __attribute__((aligned(16))) float As[NB][A_WORDS];
+  __shared__ __attribute__((aligned(16))) float Bs[NB][B_WORDS];
+
+  // XCD-aware tile order: consecutive tiles (the Cout tiles of one pixel tile
+  // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
+  const int orig = blockIdx.x;
+  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
+  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.y;
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+
+  const int srow = tid >> 3, schunk = (tid & 7) * 4;
+  // Per staged row: top-left input pixel of its receptive field (ih0, iw0)
+  // and that pixel's element offset; invalid rows get ih0 = INT_MIN/2 so
+  // every tap fails the range test.  Loads are raw buffer loads: an invalid
+  // (row, tap) gets an out-of-range offset and the hardware range check
+  // returns zeros (no branches around the loads, 32-bit offsets; the host
+  // keeps x and w below 2 GiB per launch).
+  int ih0[RA], iw0[RA], base[RA];
+#pragma unroll
+  for (int p = 0; p < RA; ++p) {
+    const int m = m0 + srow + 32 * p;
+    const int mm = m < a.M ? m : 0;
+    const int n = mm / (a.OH * a.OW);
+    const int rem = mm - n * a.OH * a.OW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int ihv = oh * a.stride - a.pad;
+    ih0[p] = m < a.M ? ihv : -(1 << 29);
+    iw0[p] = ow * a.stride - a.pad;
+    base[p] = ((n * a.H + ihv) * a.W + iw0[p]) * a.Cin + schunk;
+  }
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+
+  float4 ra[RA], rb[RB];
+  auto load_tile = [&](int kt) {
+    // channel-chunk-major, tap-minor K order: consecutive k-steps read the
+    // same 32 channels at neighbouring pixels (the 3x3 taps), which are
+    // still in L2 (tap-major order re-fetched them Cin/32 steps later)
+    const int taps = a.KH * a.KW;
+    const int chunk = kt / taps;
+    const int tap = kt - chunk * taps;
+    const int cc = chunk * BK;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const bool cok = cc + schunk < a.Cin;
+    const int toff = (kh * a.W + kw) * a.Cin + cc;
+#pragma unroll
+    for (int p = 0; p < RA; ++p) {
+      // bitwise &: no short-circuit branches around the loads
+      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)a.H) &
+                      ((unsigned)(iw0[p] + kw) < (unsigned)a.W);
+      const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
+      ra[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+    }
+#pragma unroll
+    for (int p = 0; p < RB; ++p) {
+      const int co = n0 + srow + 32 * p;
+      const uint32_t off = (cok & (co < a.Cout))
+                               ? (uint32_t)((tap * a.Cout + co) * a.Cin + cc + schunk) * 4u
+                               : kOOB;
+      rb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+    }
+  };
+  auto store_tile = [&](int buf) {
+    if constexpr (SPLIT) {
+      uint16_t* A16 = reinterpret_cast<uint16_t*>(As[buf]);
+      uint16_t* B16 = reinterpret_cast<uint16_t*>(Bs[buf]);
+#pragma unroll
+      for (int p = 0; p < RA; ++p) {
+        uint2 h, m, l;
+        split3(ra[p], h, m, l);
+        const int o = swz(srow + 32 * p, schunk);
+        *reinterpret_cast<uint2*>(&A16[o]) = h;
+        *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&A16[2 * BM * LDSB + o]) = l;
+      }
+#pragma unroll
+      for (int p = 0; p < RB; ++p) {
+        uint2 h, m, l;
+        split3(rb[p], h, m, l);
+        const int o = swz(srow + 32 * p, schunk);
+        *reinterpret_cast<uint2*>(&B16[o]) = h;
+        *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&B16[2 * BN * LDSB + o]) = l;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < RA; ++p)
+        *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = ra[p];
+#pragma unroll
+      for (int p = 0; p < RB; ++p)
+        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = rb[p];
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      if constexpr (SPLIT) {
+        const uint16_t* A16 = reinterpret_cast<const uint16_t*>(As[buf]);
+        const uint16_t* B16 = reinterpret_cast<const uint16_t*>(Bs[buf]);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // two 16-deep bf16 MFMA steps per 32-deep stage
+          bf16x8 fa[3][TM], fb[3][TN];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              fa[pl][i] = *reinterpret_cast<const bf16x8*>(
+                  &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fb[pl][j] = *reinterpret_cast<const bf16x8*>(
+                  &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+          }
+          // small terms first, then the dominant h*h
+          constexpr int PA[6] = {1, 2, 0, 0, 1, 0};
+          constexpr int PB[6] = {1, 0, 2, 1, 0, 0};
+#pragma unroll
+          for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
+                                                                     acc[i][j], 0, 0, 0);
+        }
+      } else {
+      const float* A = As[buf];
+      const float* B = Bs[buf];
+#pragma unroll
+      for (int s0 = 0; s0 < 16; s0 += 4) {
+        float4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const float4*>(
+              &A[((wr * TM + i) * 32 + li) * LDSP + lh * 16 + s0]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const float4*>(
+              &B[((wc * TN + j) * 32 + li) * LDSP + lh * 16 + s0]);
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][ss], fb[j][ss], acc[i][j],
+                                                                0, 0, 0);
+      }
+      }
+      if (DB) {
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      } else {
+        __syncthreads();
+        if (more) {
+          store_tile(0);
+          __syncthreads();
+        }
+      }
+    }
+  }
+
+  store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+}
+
+// Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
+// exact split, d2mi_split_bf16x3 / a producer that wrote them), so staging is
+// a plain copy global -> LDS (no VALU split per tap and per Cout tile) and the
+// MFMA loop is the SPLIT one.  4 threads per staged row, 8 channels each:
+// one 16-B buffer load per (row, plane).  Requires Cin % 8 == 0.
+template <int WM, int WN, int TM, int TN, bool DB>
+__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int PA = (BM * 4 + 255) / 256, PB = (BN * 4 + 255) / 256;
+  constexpr int NB = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t As[NB][3 * BM * LDSB];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NB][3 * BN * LDSB];
+
+  const int orig = blockIdx.x;
+  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
+  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.y;
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int r4 = tid >> 2, c8 = (tid & 3) * 8;
+
+  int ih0[PA], iw0[PA], base[PA];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int m = m0 + r4 + 64 * p;
+    const int mm = m < a.M ? m : 0;
+    const int n = mm / (a.OH * a.OW);
+    const int rem = mm - n * a.OH * a.OW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int ihv = oh * a.stride - a.pad;
+    ih0[p] = m < a.M ? ihv : -(1 << 29);
+    iw0[p] = ow * a.stride - a.pad;
+    base[p] = ((n * a.H + ihv) * a.W + iw0[p]) * a.Cin + c8;
+  }
+  __amdgpu_buffer_rsrc_t xr[3], wr3[3];
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    xr[pl] = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.x3) + (size_t)pl * (a.x_plane_bytes / 2), 0, a.x_plane_bytes,
+        0x00020000);
+    wr3[pl] = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.w3) + (size_t)pl * (a.w_plane_bytes / 2), 0, a.w_plane_bytes,
+        0x00020000);
+  }
+  constexpr uint32_t kOOB = 0x80000000u;
+
+  uint4 ra[PA][3], rb[PB][3];
+  auto load_tile = [&](int kt) {
+    // channel-chunk-major, tap-minor K order: consecutive k-steps read the
+    // same 32 channels at neighbouring pixels (the 3x3 taps), which are
+    // still in L2 (tap-major order re-fetched them Cin/32 steps later)
+    const int taps = a.KH * a.KW;
+    const int chunk = kt / taps;
+    const int tap = kt - chunk * taps;
+    const int cc = chunk * BK;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const bool cok = cc + c8 < a.Cin;
+    const int toff = (kh * a.W + kw) * a.Cin + cc;
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)a.H) &
+                      ((unsigned)(iw0[p] + kw) < (unsigned)a.W);
+      const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 2u : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        ra[p][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr[pl], off, 0, 0));
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int co = n0 + r4 + 64 * p;
+      const uint32_t off = (cok & (co < a.Cout) & (r4 + 64 * p < BN))
+                               ? (uint32_t)((tap * a.Cout + co) * a.Cin + cc + c8) * 2u
+                               : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        rb[p][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr3[pl], off, 0, 0));
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        *reinterpret_cast<uint4*>(&As[buf][pl * BM * LDSB + swz(r4 + 64 * p, c8)]) = ra[p][pl];
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      if (BN % 64 == 0 || r4 + 64 * p < BN)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          *reinterpret_cast<uint4*>(&Bs[buf][pl * BN * LDSB + swz(r4 + 64 * p, c8)]) =
+              rb[p][pl];
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      const uint16_t* A16 = As[buf];
+      const uint16_t* B16 = Bs[buf];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[3][TM], fb[3][TN];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fa[pl][i] = *reinterpret_cast<const bf16x8*>(
+                &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[pl][j] = *reinterpret_cast<const bf16x8*>(
+                &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+        }
+        constexpr int PAi[6] = {1, 2, 0, 0, 1, 0};
+        constexpr int PBi[6] = {1, 0, 2, 1, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PAi[t]][i], fb[PBi[t]][j],
+                                                                   acc[i][j], 0, 0, 0);
+      }
+      if (DB) {
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      } else {
+        __syncthreads();
+        if (more) {
+          store_tile(0);
+          __syncthreads();
+        }
+      }
+    }
+  }
+  store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+}
+
+// x [n] f32 -> [3][n] bf16 planes (h, m, l of the exact truncation split).
+__global__ void split3_kernel(const float4* __restrict__ x, int64_t n4, uint2* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint2 h, m, l;
+    split3(x[i], h, m, l);
+    out[i] = h;
+    out[n4 + i] = m;
+    out[2 * n4 + i] = l;
+  }
+}
+
 // Fixed-order split-K reduction + epilogue (deterministic).
 __global__ void splitk_reduce_kernel(ConvArgs a) {
   const int64_t total = (int64_t)a.M * a.Cout;
@@ -339,6 +645,33 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
   return 0;
 }
 
+template <bool SPLIT>
+static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  if (cfg == 0) {
+    if (db)
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT>), grid, dim3(256), 0, st, a);
+  } else if (cfg == 1) {
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT>), grid, dim3(256), 0, st, a);
+  }
+}
+
+static void launch_x3(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  if (cfg == 0) {
+    if (db)
+      hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
+  } else if (cfg == 1) {
+    hipLaunchKernelGGL((conv_x3_kernel<4, 1, 1, 2, true>), grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_x3_kernel<4, 1, 1, 1, true>), grid, dim3(256), 0, st, a);
+  }
+}
+
 static int conv_dims(int H, int W, int KH, int KW, int stride, int pb, int pe, int& OH, int& OW) {
   OH = (H + pb + pe - KH) / stride + 1;
   OW = (W + pb + pe - KW) / stride + 1;
@@ -353,19 +686,21 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
   return p.splits > 1 ? (size_t)p.splits * N * OH * OW * Cout * sizeof(float) : 0;
 }
 
-extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
-                                   const float* topdown, const float* residual, float* y, int N,
-                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
-                                   int pad_beg, int pad_end, int flags, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
-               "bad conv shape");
-  D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
-  D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_packed & 15) == 0,
-               "x and w must be 16-byte aligned");
-  D2MI_REQUIRE((flags & ~3) == 0, "flags: bit0 relu, bit1 relu after the residual/top-down add");
+// Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
+static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
+                     const uint16_t* w3, const float* bias, const float* topdown,
+                     const float* residual, float* y, int N, int H, int W, int Cin, int Cout,
+                     int KH, int KW, int stride, int pad_beg, int pad_end, int flags,
+                     void* workspace, size_t workspace_bytes, void* stream) {
   ConvArgs a;
   a.x = x;
+  a.x3 = x3;
+  a.w3 = w3;
+  const int64_t xe = (int64_t)N * H * W * Cin, we = (int64_t)KH * KW * Cin * Cout;
+  a.x_bytes = x ? (int)(xe * 4) : 0;
+  a.w_bytes = w_packed ? (int)(we * 4) : 0;
+  a.x_plane_bytes = x3 ? (int)(xe * 2) : 0;
+  a.w_plane_bytes = w3 ? (int)(we * 2) : 0;
   a.w = w_packed;
   a.bias = bias;
   a.topdown = topdown;
@@ -407,14 +742,12 @@ extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const 
   static const char* force = getenv("D2MI_CONV_DB");
   bool db = (size_t)a.ntiles * a.splits < 1024;
   if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
-  if (p.cfg == 0) {
-    if (db) hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
-  } else if (p.cfg == 1) {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true>), grid, dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true>), grid, dim3(256), 0, st, a);
-  }
+  if (x3)
+    launch_x3(p.cfg, db, grid, st, a);
+  else if (flags & kSplit3)
+    launch_conv<true>(p.cfg, db, grid, st, a);
+  else
+    launch_conv<false>(p.cfg, db, grid, st, a);
   D2MI_LAUNCH_CHECK();
   if (a.splits > 1) {
     const int64_t total = (int64_t)a.M * Cout;
@@ -425,6 +758,46 @@ extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const 
   return 0;
 }
 
+
+extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
+                                   const float* topdown, const float* residual, float* y, int N,
+                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                   int pad_beg, int pad_end, int flags, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
+               "bad conv shape");
+  D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
+  D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_packed & 15) == 0,
+               "x and w must be 16-byte aligned");
+  D2MI_REQUIRE((flags & ~7) == 0,
+               "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
+               "MFMA products");
+  // 32-bit buffer offsets: batches whose input is >= 2 GiB run as image chunks
+  const int64_t img_bytes = (int64_t)H * W * Cin * sizeof(float);
+  D2MI_REQUIRE(img_bytes < (1ll << 31), "one conv input image must be < 2 GiB");
+  D2MI_REQUIRE((int64_t)KH * KW * Cin * Cout * sizeof(float) < (1ll << 31),
+               "conv weights must be < 2 GiB");
+  if ((int64_t)N * img_bytes >= (1ll << 31)) {
+    int OH0, OW0;
+    D2MI_REQUIRE(conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH0, OW0) == 0,
+                 "conv output is empty");
+    const int chunk = (int)(((1ll << 31) - 1) / img_bytes);
+    const size_t xs = (size_t)H * W * Cin, ys = (size_t)OH0 * OW0 * Cout;
+    const size_t ts = (size_t)((OH0 + 1) / 2) * ((OW0 + 1) / 2) * Cout;
+    for (int n0 = 0; n0 < N; n0 += chunk) {
+      const int nn = std::min(chunk, N - n0);
+      const int rc = d2mi_conv2d_nhwc_ex(
+          x + n0 * xs, w_packed, bias, topdown ? topdown + n0 * ts : nullptr,
+          residual ? residual + n0 * ys : nullptr, y + n0 * ys, nn, H, W, Cin, Cout, KH, KW,
+          stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, y, N, H, W, Cin, Cout,
+                   KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+}
+
 extern "C" int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const float* bias,
                                 const float* topdown, const float* residual, float* y, int N,
                                 int H, int W, int Cin, int Cout, int KH, int KW, int stride,
@@ -432,4 +805,34 @@ extern "C" int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const flo
   D2MI_REQUIRE(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
   return d2mi_conv2d_nhwc_ex(x, w_packed, bias, topdown, residual, y, N, H, W, Cin, Cout, KH, KW,
                              stride, pad_beg, pad_end, act ? kRelu : 0, nullptr, 0, stream);
+}
+
+extern "C" int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream) {
+  D2MI_REQUIRE(n >= 0 && n % 4 == 0, "split: n must be a multiple of 4 (got %lld)", (long long)n);
+  D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 7) == 0, "split: misaligned buffers");
+  if (n == 0) return 0;
+  const int64_t n4 = n / 4;
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 16384);
+  hipLaunchKernelGGL(split3_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(x), n4, reinterpret_cast<uint2*>(out));
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
+                                   const float* topdown, const float* residual, float* y, int N,
+                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                   int pad_beg, int pad_end, int flags, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
+               "bad conv shape");
+  D2MI_REQUIRE(Cin % 8 == 0, "pre-split conv: Cin must be a multiple of 8 (got %d)", Cin);
+  D2MI_REQUIRE(((uintptr_t)x3 & 15) == 0 && ((uintptr_t)w3 & 15) == 0,
+               "x3 and w3 must be 16-byte aligned");
+  D2MI_REQUIRE((flags & ~3) == 0, "flags: bit0 relu, bit1 relu after the residual/top-down add");
+  D2MI_REQUIRE(3 * 2 * (int64_t)N * H * W * Cin < (1ll << 31),
+               "pre-split conv input (3 bf16 planes) must be < 2 GiB; use d2mi_conv2d_nhwc_ex");
+  D2MI_REQUIRE(3 * 2 * (int64_t)KH * KW * Cin * Cout < (1ll << 31), "conv weights too large");
+  return conv_core(nullptr, x3, nullptr, w3, bias, topdown, residual, y, N, H, W, Cin, Cout, KH,
+                   KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
 }

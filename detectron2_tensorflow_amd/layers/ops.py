@@ -6,6 +6,7 @@ CPU/eager fallback for the hot path.  Shapes and argument meaning follow the
 reference op they replace (cited per function).
 """
 import math
+import os
 
 import torch
 
@@ -250,11 +251,42 @@ def pack_conv_weights(w_hwio):
     return out
 
 
+# Conv MFMA product form: "f32" = v_mfma_f32_32x32x2_f32 (exact f32 products);
+# "split" = the same f32 operands split exactly into three bf16 terms
+# (h + m + l == x) and multiplied with six v_mfma_f32_32x32x16_bf16 products
+# (f32-class error, see csrc/conv_mfma.hip).  With Cin % 8 == 0 the split is
+# done once per operand (d2mi_split_bf16x3) and the conv reads the planes
+# (d2mi_conv2d_nhwc_x3); otherwise the conv splits while staging.
+# Process-wide default from D2MI_CONV_MATH.
+CONV_MATH = os.environ.get("D2MI_CONV_MATH", "f32")
+
+
+def split_bf16x3(x):
+    """f32 tensor -> int16 [3, *x.shape]: bf16 bit patterns of the exact split
+    x = h + m + l (truncation; csrc/conv_mfma.hip split3)."""
+    x = _f32c(x)
+    _C.require_device(x)
+    if x.numel() % 4:
+        raise ValueError("split_bf16x3: numel must be a multiple of 4")
+    out = torch.empty((3,) + tuple(x.shape), dtype=torch.int16, device=x.device)
+    rc = _C.lib().d2mi_split_bf16x3(_C.ptr(x), x.numel(), _C.ptr(out), _C.stream_of(x.device))
+    _C.check(rc, "d2mi_split_bf16x3")
+    return out
+
+
+def _presplit_ok(x, Cin):
+    return Cin % 8 == 0 and 6 * x.numel() < 2 ** 31
+
+
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
-                residual=None, relu_after_add=False):
+                residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
-    relu(conv + bias) + residual/topdown."""
+    relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
+    CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x."""
+    math_mode = math_mode or CONV_MATH
+    if math_mode not in ("f32", "split"):
+        raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
     x = _f32c(x)
     _C.require_device(x, w_packed)
     N, H, W, Cin = x.shape
@@ -272,15 +304,27 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                              f"{(N, OH, OW, Cout)}")
     if residual is not None:
         residual = _f32c(residual)
+    presplit = math_mode == "split" and _presplit_ok(x, Cin)
     flags = (1 if relu else 0) | (2 if relu_after_add else 0)
+    if math_mode == "split" and not presplit:
+        flags |= 4
     wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
                                               int(pe))
     ws = _C.workspace(wsb, x.device) if wsb else None
+    if presplit:
+        x3 = x_split if x_split is not None else split_bf16x3(x)
+        w3 = w_split if w_split is not None else split_bf16x3(w_packed)
     ev = KernelTimer.start()
-    rc = _C.lib().d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias), _C.ptr(topdown),
-                                      _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
-                                      int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
-                                      _C.stream_of(x.device))
+    if presplit:
+        rc = _C.lib().d2mi_conv2d_nhwc_x3(_C.ptr(x3), _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
+                                          _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
+                                          int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
+                                          _C.stream_of(x.device))
+    else:
+        rc = _C.lib().d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
+                                          _C.ptr(topdown), _C.ptr(residual), _C.ptr(y), N, H, W,
+                                          Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
+                                          _C.ptr(ws), wsb, _C.stream_of(x.device))
     fl = 2.0 * N * OH * OW * Cout * KH * KW * Cin
     KernelTimer.stop(ev, "conv2d_mfma", fl)
     if KernelTimer.detail and ev is not None:

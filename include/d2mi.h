@@ -232,6 +232,21 @@ int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias
                         int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
                         int pad_end, int flags, void* workspace, size_t workspace_bytes,
                         void* stream);
+/* flags bit2 = "split" products: the same f32 operands, each split EXACTLY
+ * into three bf16 terms (x = h + m + l, truncation), multiplied with six
+ * bf16 MFMA products (v_mfma_f32_32x32x16_bf16; the dropped m*l, l*m, l*l
+ * terms are below f32's own rounding of the product) and accumulated in f32.
+ *
+ * d2mi_split_bf16x3: x [n] f32 -> out [3][n] (bf16 bit patterns of h, m, l);
+ * n % 4 == 0.  d2mi_conv2d_nhwc_x3: the same convolution (flags bits 0-1 as
+ * above) on operands already split by it: x3 = split of x [N,H,W,Cin],
+ * w3 = split of w_packed; Cin % 8 == 0; each operand's 3 planes < 2 GiB. */
+int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream);
+int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
+                        const float* topdown, const float* residual, float* y, int N, int H,
+                        int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
+                        int pad_end, int flags, void* workspace, size_t workspace_bytes,
+                        void* stream);
 
 /* Weight gradient of the same convolution (the tf.gradients of Conv2D.call,
  * lib/layers/convolutional.py:198-263, w.r.t. its HWIO kernel):

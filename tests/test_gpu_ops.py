@@ -455,6 +455,99 @@ def test_conv2d_mfma_vs_torch_fp32(dev, shape):
         np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("shape", [
+    (2, 20, 24, 256, 256, 1, 1, 0),
+    (2, 25, 42, 256, 256, 3, 1, 1),
+    (1, 17, 9, 64, 96, 3, 2, 1),
+    (3, 14, 14, 256, 80, 1, 1, 0),
+    (1, 33, 35, 2048, 256, 1, 1, 0),   # split-K
+    (2, 30, 40, 36, 64, 3, 1, 1),      # Cin % 32 != 0 (ragged k-chunk)
+    (2, 9, 13, 128, 12, 1, 1, 0),      # Cout 12 (128x32 tile)
+])
+def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
+    """math_mode="split": the f32 operands split exactly into 3 bf16 terms, 6
+    bf16 MFMA products (csrc/conv_mfma.hip).  Bar: the same 1e-4 as the native
+    f32 path vs float64, and an error no larger than 4x the native f32 MFMA
+    path's own (which differs from float64 by summation order only)."""
+    N, H, W, Cin, Cout, k, stride, pad = shape
+    g = torch.Generator().manual_seed(11 + sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
+    b = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(3, 2, 0, 1).double(),
+                                     b.double(), stride=stride, padding=pad).permute(0, 2, 3, 1)
+    res = torch.randn(ref.shape, generator=g).float()
+    wp = ops().pack_conv_weights(w.to(dev))
+    for fused in (False, True):
+        kw = dict(relu=True, residual=res.to(dev), relu_after_add=True) if fused else {}
+        want = torch.relu(ref + res.double()) if fused else ref
+        ys = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), stride, (pad, pad), math_mode="split", **kw)
+        yf = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), stride, (pad, pad), math_mode="f32", **kw)
+        ys2 = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), stride, (pad, pad), math_mode="split", **kw)
+        assert torch.equal(ys, ys2)  # deterministic
+        np.testing.assert_allclose(ys.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+        es = float((ys.cpu().double() - want).abs().max())
+        ef = float((yf.cpu().double() - want).abs().max())
+        assert es <= 4 * ef + 1e-6, (es, ef)
+
+
+def test_split_bf16x3_is_exact(dev):
+    """h + m + l == x bit for bit (evaluated in float64), each term a bf16.
+    Exact wherever the residuals stay normal f32 (|x| >= 2^-110 or so); below
+    that the GPU flushes the denormal residual, an error < 2^-126 absolute."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.cat([torch.randn(4096, generator=g) * 10.0 ** torch.randint(-20, 20, (4096,), generator=g),
+                   torch.tensor([0.0, -0.0, 1.0, -1.5, 3.4e38, 2.0 ** -100, 65504.0, 1 + 2.0 ** -23])])
+    x3 = ops().split_bf16x3(x.to(dev)).cpu()
+    parts = [(x3[i].to(torch.int32) << 16).view(torch.float32).double() for i in range(3)]
+    assert torch.equal(parts[0] + parts[1] + parts[2], x.double())
+
+
+def test_conv2d_presplit_matches_split_at_load(dev):
+    """d2mi_conv2d_nhwc_x3 (operands split once) computes exactly what the
+    split-while-staging kernel computes (same products, same order)."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(2, 21, 30, 64, generator=g).to(dev)
+    w = (torch.randn(3, 3, 64, 96, generator=g) / 24).to(dev)
+    b = torch.randn(96, generator=g).to(dev)
+    wp = ops().pack_conv_weights(w)
+    y_pre = ops().conv2d_nhwc(x, wp, b, 1, (1, 1), True, math_mode="split")
+    ops_mod = ops()
+    flags_ref = ops_mod.conv2d_nhwc(x[..., :60].contiguous(),
+                                    ops_mod.pack_conv_weights(w[:, :, :60].contiguous()), b, 1, (1, 1),
+                                    True, math_mode="split")  # Cin 60: split while staging
+    y_ref60 = ops_mod.conv2d_nhwc(x[..., :60].contiguous(),
+                                  ops_mod.pack_conv_weights(w[:, :, :60].contiguous()), b, 1, (1, 1),
+                                  True, math_mode="f32")
+    assert float((flags_ref - y_ref60).abs().max()) < 1e-4
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(3, 2, 0, 1).double(),
+                                     b.double(), padding=1).relu().permute(0, 2, 3, 1)
+    np.testing.assert_allclose(y_pre.cpu().double().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_conv2d_split_bf16_exact_on_bf16_representable_integers(dev):
+    """Small integers are exact in every term (h = x, m = l = 0) and their
+    products and sums are exact in f32: the split path must be bit-exact."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(-8, 9, (2, 12, 14, 64), generator=g).float()
+    w = torch.randint(-4, 5, (3, 3, 64, 96), generator=g).float()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(3, 2, 0, 1).double(),
+                                     padding=1).permute(0, 2, 3, 1)
+    y = ops().conv2d_nhwc(x.to(dev), ops().pack_conv_weights(w.to(dev)), None, 1, (1, 1),
+                          math_mode="split")
+    assert torch.equal(y.cpu().double(), ref)
+    # and a value with all three terms non-zero: 1 + 2^-9 + 2^-17 (exact split)
+    v = 1.0 + 2.0 ** -9 + 2.0 ** -17
+    xo = torch.full((1, 1, 1, 32), v)
+    wo = torch.zeros(1, 1, 32, 4)
+    wo[0, 0, 0, 0] = 1.0
+    wo[0, 0, 0, 1] = v
+    y = ops().conv2d_nhwc(xo.to(dev), ops().pack_conv_weights(wo.to(dev)), None, 1, (0, 0),
+                          math_mode="split").cpu()
+    assert float(y[0, 0, 0, 0]) == np.float32(v)
+    assert abs(float(y[0, 0, 0, 1]) - v * v) <= 2.0 ** -22
+
+
 def test_conv2d_fused_topdown_add(dev):
     """FPN merge prev = lateral(x) + up2(prev_top) fused in the epilogue."""
     g = torch.Generator().manual_seed(3)

@@ -71,15 +71,37 @@ def bench_conv(dev, iters):
             res = torch.randn(N, OH, OW, Cout, device=dev)
         if name.endswith("+td"):
             td = torch.randn(N, (OH + 1) // 2, (OW + 1) // 2, Cout, device=dev)
-        ms = timeit(lambda: ops.conv2d_nhwc(x, wp, b, s, (p, p), relu=res is not None,
-                                            residual=res, topdown=td,
-                                            relu_after_add=res is not None), iters)
+        w3 = ops.split_bf16x3(wp)
+        x3 = ops.split_bf16x3(x)
+        run = lambda mm, xs=None: ops.conv2d_nhwc(x, wp, b, s, (p, p), relu=res is not None,  # noqa: E731
+                                                  residual=res, topdown=td,
+                                                  relu_after_add=res is not None, math_mode=mm,
+                                                  w_split=w3, x_split=xs)
+        ms = timeit(lambda: run("f32"), iters)
+        ms_s = timeit(lambda: run("split"), iters)
+        ms_k = timeit(lambda: run("split", x3), iters)
+        err = {}
+        if N * H * W <= 140000:  # float64 reference on a slice of the batch
+            n1 = 1 if N <= 2 else 8
+            x64 = x[:n1].double().permute(0, 3, 1, 2)
+            ref = F.conv2d(x64, w.double().permute(3, 2, 0, 1), b.double(), stride=s, padding=p)
+            ref = ref.permute(0, 2, 3, 1)
+            if td is not None:
+                ref = ref + td[:n1].double().repeat_interleave(2, 1).repeat_interleave(2, 2)[:, :OH, :OW]
+            if res is not None:
+                ref = torch.relu(ref + res[:n1].double())
+            sc = ref.abs().max().item()
+            for mm in ("f32", "split"):
+                err[mm] = float((run(mm)[:n1].double() - ref).abs().max() / sc)
         xc = x.permute(0, 3, 1, 2)
         wc = w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last)
         ms_t = float("nan") if NO_MIOPEN else timeit(
             lambda: F.conv2d(xc, wc, b, stride=s, padding=p), iters)
         out.append({"kernel": "conv", "shape": name, "mfma_us": round(ms * 1e3, 1),
                     "mfma_tflops": round(flops / ms / 1e9, 1),
+                    "split_us": round(ms_s * 1e3, 1), "split_tflops": round(flops / ms_s / 1e9, 1),
+                    "x3conv_us": round(ms_k * 1e3, 1), "x3conv_tflops": round(flops / ms_k / 1e9, 1),
+                    "max_rel_err_f32": err.get("f32"), "max_rel_err_split": err.get("split"),
                     "miopen_us": round(ms_t * 1e3, 1),
                     "miopen_tflops": round(flops / ms_t / 1e9, 1)})
     return out
