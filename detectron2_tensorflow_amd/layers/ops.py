@@ -258,7 +258,7 @@ def pack_conv_weights(w_hwio):
 # done once per operand (d2mi_split_bf16x3) and the conv reads the planes
 # (d2mi_conv2d_nhwc_x3); otherwise the conv splits while staging.
 # Process-wide default from D2MI_CONV_MATH.
-CONV_MATH = os.environ.get("D2MI_CONV_MATH", "f32")
+CONV_MATH = os.environ.get("D2MI_CONV_MATH", "split")
 
 
 def split_bf16x3(x):
@@ -304,7 +304,14 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                              f"{(N, OH, OW, Cout)}")
     if residual is not None:
         residual = _f32c(residual)
-    presplit = math_mode == "split" and _presplit_ok(x, Cin)
+    # measured policy (tools/bench_kernels.py --only conv): narrow Cout (the
+    # 128x64 / 128x32 tiles) gains nothing from the split products; KxK
+    # kernels re-read each input element KH*KW times, so splitting it once
+    # beforehand beats splitting while staging; 1x1 convs split while staging.
+    if math_mode == "split" and Cout <= 64:
+        math_mode = "f32"
+    presplit = math_mode == "split" and _presplit_ok(x, Cin) and (
+        x_split is not None or KH * KW > 1)
     flags = (1 if relu else 0) | (2 if relu_after_add else 0)
     if math_mode == "split" and not presplit:
         flags |= 4

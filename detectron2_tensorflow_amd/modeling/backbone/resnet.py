@@ -1,8 +1,8 @@
 """ResNet backbone (lib/modeling/backbone/resnet.py:22-253, blocks.py:143-186).
 
-A caller of the hot path (out of scope as a rewrite target, SURVEY.md
-section 2): stock PyTorch-ROCm convolutions in channels_last through
-Conv2D(impl="torch"), FrozenBN folded into the conv at run time.
+A caller of the hot path: the bottleneck 1x1
+and 3x3 convs run on the MFMA conv kernel with FrozenBN folded into the
+weights at run time; the stem's 7x7 (Cin = 3) stays on MIOpen.
 Structure, strides (STRIDE_IN_1X1), the stem's zero pad + 3x3/2 VALID max
 pool and FREEZE_AT follow the reference.
 """
@@ -34,8 +34,9 @@ class BottleneckBlock(Layer):
     def __init__(self, in_channels, out_channels, bottleneck_channels, stride=1, num_groups=1,
                  stride_in_1x1=False, rate=1, **kwargs):
         super().__init__(in_channels=in_channels, out_channels=out_channels, **kwargs)
-        # 1x1 convs run on the MFMA implicit-GEMM kernel with FrozenBN folded
-        # and ReLU / residual fused in its epilogue; the 3x3 stays on MIOpen.
+        # every conv runs on the MFMA implicit-GEMM kernel with FrozenBN folded
+        # and ReLU / residual fused in its epilogue ("auto": a grouped or
+        # dilated 3x3 falls back to MIOpen)
         self.shortcut = None
         if in_channels != out_channels:
             self.shortcut = Conv2D(in_channels, out_channels, 1, stride=stride, activation=None,
@@ -44,7 +45,7 @@ class BottleneckBlock(Layer):
         self.conv1 = Conv2D(in_channels, bottleneck_channels, 1, stride=s1, impl="mfma",
                             scope="conv1")
         self.conv2 = Conv2D(bottleneck_channels, bottleneck_channels, 3, stride=s3,
-                            num_groups=num_groups, rate=rate, scope="conv2")
+                            num_groups=num_groups, rate=rate, impl="auto", scope="conv2")
         self.conv3 = Conv2D(bottleneck_channels, out_channels, 1, activation=None, impl="mfma",
                             scope="conv3")
 
