@@ -61,6 +61,7 @@ _SIGS = {
     "d2mi_fold_frozen_bn_bwd": (c_int, [P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int,
                                         P, P, P, P, P, c_size_t, P]),
     "d2mi_conv2d_wgrad": (c_int, [P, P, P, P] + [c_int] * 10 + [P, c_size_t, P]),
+    "d2mi_conv2d_wgrad_ex": (c_int, [P, P, P, P] + [c_int] * 11 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_nhwc_x3": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,

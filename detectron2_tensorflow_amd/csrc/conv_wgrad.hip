@@ -37,6 +37,7 @@ struct WgradArgs {
   int P;                      // N*OH*OW
   int nCi, nCo, ntiles;       // channel tiles per tap, co tiles, total tiles
   int splits, chunks_per_split, nchunks;
+  int x_bytes, dy_bytes;  // buffer ranges (split kernel; < 2 GiB)
 };
 
 template <int TM, int TN>
@@ -196,6 +197,223 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int split
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split-product variant (d2mi_conv2d_wgrad_ex flags bit 2): the same GEMM on
+// the bf16 MFMA with each f32 operand split exactly into three bf16 terms
+// (h + m + l == x, truncation) and six products per k-step, as
+// conv_mfma.hip's SPLIT path.  The MFMA operand wants 8 consecutive PIXELS of
+// one channel, so each thread loads 4 pixels x 4 channels (four float4),
+// transposes them in registers, splits, and writes 4 pixels (8 B) per plane
+// per channel into [plane][channel][32 pixels] LDS images with XOR-swizzled
+// 16-B chunks.  The bias gradient is summed from the f32 dY values before
+// the split and reduced over the pixel groups in a fixed order.
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int LDW = 32;  // bf16 per LDS row (one 32-pixel chunk)
+
+__device__ __forceinline__ int wswz(int row, int elem) {
+  return row * LDW + ((((elem >> 3) ^ (row >> 2)) & 3) << 3) + (elem & 7);
+}
+
+__device__ __forceinline__ void split3w(const float4 v, uint2& h, uint2& m, uint2& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hb[e] = __float_as_uint(x[e]) & 0xffff0000u;
+    const float r = x[e] - __uint_as_float(hb[e]);
+    mb[e] = __float_as_uint(r) & 0xffff0000u;
+    lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
+  }
+  h.x = (hb[0] >> 16) | hb[1];
+  h.y = (hb[2] >> 16) | hb[3];
+  m.x = (mb[0] >> 16) | mb[1];
+  m.y = (mb[2] >> 16) | mb[3];
+  l.x = (lb[0] >> 16) | (lb[1] & 0xffff0000u);
+  l.y = (lb[2] >> 16) | (lb[3] & 0xffff0000u);
+}
+
+// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery).
+struct FastDiv {
+  uint32_t d, m, l;
+};
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.l;
+}
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_split_kernel(WgradArgs a, FastDiv fd_hw,
+                                                                  FastDiv fd_w) {
+  constexpr int BM = 2 * TM * 32, BN = 2 * TN * 32;
+  constexpr int GA = BM / 4, GB = BN / 4;  // 4-channel groups
+  __shared__ __attribute__((aligned(16))) uint16_t As[3 * BM * LDW];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * BN * LDW];
+  __shared__ float bred[8][BN];
+
+  const int tile = blockIdx.x;
+  const int per_tap = a.nCi * a.nCo;
+  const int tap = tile / per_tap;
+  const int rem = tile - tap * per_tap;
+  const int cit = rem / a.nCo, cot = rem - cit * a.nCo;
+  const int kh = tap / a.KW, kw = tap - kh * a.KW;
+  const int ci0 = cit * BM, co0 = cot * BN;
+  const int split = blockIdx.y;
+  const int c_begin = split * a.chunks_per_split;
+  const int c_end = min(a.nchunks, c_begin + a.chunks_per_split);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // A items: (cg, pg) = (tid % GA, tid / GA) for tid < 8 * GA; B likewise
+  const bool a_on = tid < 8 * GA, b_on = tid < 8 * GB;
+  const int cga = tid % GA, pga = tid / GA;
+  const int cgb = tid % GB, pgb = tid / GB;
+  const int ci = ci0 + 4 * cga, co = co0 + 4 * cgb;
+  const bool ci_ok = a_on && ci < a.Cin, co_ok = b_on && co < a.Cout;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.dy), 0, a.dy_bytes, 0x00020000);
+  constexpr uint32_t kOOB = 0x80000000u;
+
+  float4 ra[4], rb[4];
+  auto load_chunk = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = ch * KP + 4 * pga + q;
+      const uint32_t n = fdiv((uint32_t)p, fd_hw);
+      const int r2 = p - (int)n * (a.OH * a.OW);
+      const int oy = (int)fdiv((uint32_t)r2, fd_w), ox = r2 - oy * a.OW;
+      const int iy = oy * a.stride - a.pad + kh, ix = ox * a.stride - a.pad + kw;
+      const bool ok = ci_ok & (p < a.P) & ((unsigned)iy < (unsigned)a.H) &
+                      ((unsigned)ix < (unsigned)a.W);
+      const uint32_t off = ok ? (uint32_t)(((((int)n * a.H + iy) * a.W + ix) * a.Cin + ci) * 4) : kOOB;
+      ra[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      const int pb = ch * KP + 4 * pgb + q;
+      const uint32_t offb = (co_ok & (pb < a.P)) ? (uint32_t)((pb * a.Cout + co) * 4) : kOOB;
+      rb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, offb, 0, 0));
+    }
+  };
+  const bool do_bias = a.dbias != nullptr && tap == 0 && cit == 0;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  auto store_chunk = [&]() {
+    if (a_on) {
+      const float* f = reinterpret_cast<const float*>(ra);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 h, m, l;
+        split3w(make_float4(f[j], f[4 + j], f[8 + j], f[12 + j]), h, m, l);
+        const int o = wswz(4 * cga + j, 4 * pga);
+        *reinterpret_cast<uint2*>(&As[o]) = h;
+        *reinterpret_cast<uint2*>(&As[BM * LDW + o]) = m;
+        *reinterpret_cast<uint2*>(&As[2 * BM * LDW + o]) = l;
+      }
+    }
+    if (b_on) {
+      const float* f = reinterpret_cast<const float*>(rb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = make_float4(f[j], f[4 + j], f[8 + j], f[12 + j]);
+        if (do_bias) bsum[j] += ((v.x + v.y) + v.z) + v.w;
+        uint2 h, m, l;
+        split3w(v, h, m, l);
+        const int o = wswz(4 * cgb + j, 4 * pgb);
+        *reinterpret_cast<uint2*>(&Bs[o]) = h;
+        *reinterpret_cast<uint2*>(&Bs[BN * LDW + o]) = m;
+        *reinterpret_cast<uint2*>(&Bs[2 * BN * LDW + o]) = l;
+      }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (c_begin < c_end) {
+    load_chunk(c_begin);
+    for (int ch = c_begin; ch < c_end; ++ch) {
+      store_chunk();
+      __syncthreads();
+      if (ch + 1 < c_end) load_chunk(ch + 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[3][TM], fb[3][TN];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fa[pl][i] = *reinterpret_cast<const bf16x8*>(
+                &As[pl * BM * LDW + wswz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[pl][j] = *reinterpret_cast<const bf16x8*>(
+                &Bs[pl * BN * LDW + wswz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+        }
+        constexpr int PAi[6] = {1, 2, 0, 0, 1, 0};
+        constexpr int PBi[6] = {1, 0, 2, 1, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PAi[t]][i], fb[PBi[t]][j],
+                                                                   acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+
+  if (do_bias) {  // fixed-order reduction over the 8 pixel groups
+    if (b_on) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bred[pgb][4 * cgb + j] = bsum[j];
+    }
+    __syncthreads();
+    if (tid < BN && co0 + tid < a.Cout) {
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s += bred[g][tid];
+      if (a.splits > 1) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
+      else a.dbias[co0 + tid] = s;
+    }
+  }
+
+  const size_t wsz = (size_t)a.KH * a.KW * a.Cin * a.Cout;
+  float* out = a.splits > 1 ? a.partial + (size_t)split * wsz : a.dw;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int oc = co0 + (wc * TN + j) * 32 + li;
+    if (oc >= a.Cout) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cb = ci0 + (wr * TM + i) * 32 + 4 * lh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = cb + (r & 3) + 8 * (r >> 2);
+        if (c < a.Cin) out[((size_t)tap * a.Cin + c) * a.Cout + oc] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.l = l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+
 struct WPlan {
   int TM, TN, BM, BN, ntiles, splits, chunks_per_split, nchunks;
 };
@@ -236,10 +454,11 @@ extern "C" size_t d2mi_conv2d_wgrad_workspace_size(int N, int H, int W, int Cin,
                       : 0;
 }
 
-extern "C" int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio, float* dbias,
-                                 int N, int H, int W, int Cin, int Cout, int KH, int KW,
-                                 int stride, int pad_beg, int pad_end, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_hwio,
+                                    float* dbias, int N, int H, int W, int Cin, int Cout, int KH,
+                                    int KW, int stride, int pad_beg, int pad_end, int flags,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE((flags & ~4) == 0, "wgrad flags: bit2 = split-bf16 products");
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0 && Cout % 4 == 0, "Cin and Cout must be multiples of 4 (%d, %d)",
@@ -282,7 +501,23 @@ extern "C" int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio
   a.pbias = p.splits > 1 ? (float*)workspace + (size_t)p.splits * KH * KW * Cin * Cout : nullptr;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
-  if (p.TM == 2 && p.TN == 2)
+  const bool split3 = (flags & 4) != 0;
+  if (split3) {
+    D2MI_REQUIRE((int64_t)N * H * W * Cin * 4 < (1ll << 31) &&
+                     (int64_t)a.P * Cout * 4 < (1ll << 31),
+                 "split wgrad: x and dy must each be < 2 GiB");
+    a.x_bytes = (int)((int64_t)N * H * W * Cin * 4);
+    a.dy_bytes = (int)((int64_t)a.P * Cout * 4);
+    const FastDiv fhw = make_fastdiv((uint32_t)(a.OH * a.OW)), fw = make_fastdiv((uint32_t)a.OW);
+    if (p.TM == 2 && p.TN == 2)
+      hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 2>), grid, dim3(256), 0, st, a, fhw, fw);
+    else if (p.TM == 2)
+      hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 1>), grid, dim3(256), 0, st, a, fhw, fw);
+    else if (p.TN == 2)
+      hipLaunchKernelGGL((conv_wgrad_split_kernel<1, 2>), grid, dim3(256), 0, st, a, fhw, fw);
+    else
+      hipLaunchKernelGGL((conv_wgrad_split_kernel<1, 1>), grid, dim3(256), 0, st, a, fhw, fw);
+  } else if (p.TM == 2 && p.TN == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<2, 2>), grid, dim3(256), 0, st, a);
   else if (p.TM == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<2, 1>), grid, dim3(256), 0, st, a);
@@ -299,4 +534,12 @@ extern "C" int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio
     D2MI_LAUNCH_CHECK();
   }
   return 0;
+}
+
+extern "C" int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio, float* dbias,
+                                 int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                                 int stride, int pad_beg, int pad_end, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  return d2mi_conv2d_wgrad_ex(x, dy, dw_hwio, dbias, N, H, W, Cin, Cout, KH, KW, stride,
+                              pad_beg, pad_end, 0, workspace, workspace_bytes, stream);
 }

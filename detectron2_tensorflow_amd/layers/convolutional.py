@@ -69,20 +69,27 @@ def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
     """(weight gradient HWIO, bias gradient or None).
 
     Routed by measurement (tools/bench_kernels.py --only wgrad, MI355X):
-    1x1 over >= 32k output pixels -> the MFMA wgrad kernel (d2mi_conv2d_wgrad,
-    bias gradient fused; 67 TF/s vs 45 for hipBLASLt on the p2 lateral);
-    other 1x1 -> X^T . dY as one hipBLASLt GEMM; KxK -> torch.nn.grad (MIOpen's
-    igemm wrw kernels, 121 TF/s on the FPN p2 3x3 vs 91 for ours)."""
+    with split products (the default, ops.CONV_MATH) every KxK and every 1x1
+    over >= 32k output pixels runs on the MFMA wgrad kernel (bias gradient
+    fused; FPN p2 3x3 154 TF/s vs MIOpen's 122, mask-head 3x3 147 vs 110);
+    smaller 1x1 -> X^T . dY as one hipBLASLt GEMM.  With f32 products the
+    KxK go to MIOpen's igemm wrw, which beats the f32 MFMA kernel there."""
     KH, KW, Cin, Cout = w_shape
+    split = ops.CONV_MATH == "split"
+    eligible = Cin % 4 == 0 and Cout % 4 == 0
     if KH == 1 and KW == 1 and pb == 0 and pe == 0:
         P = gy.numel() // Cout
-        if P >= 32768 and Cin % 4 == 0 and Cout % 4 == 0:
+        if P >= 32768 and eligible:
             if want_bias:
                 return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0), with_bias=True)
             return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0)), None
         xs = x if stride == 1 else x[:, ::stride, ::stride]
         xs = xs.reshape(-1, Cin)
         return torch.mm(xs.t(), gy.reshape(-1, Cout)).reshape(1, 1, Cin, Cout), None
+    if split and eligible and KH == KW and 6 * max(x.numel(), gy.numel()) < 2 ** 31:
+        if want_bias:
+            return ops.conv2d_wgrad(x, gy, KH, stride, (pb, pe), with_bias=True)
+        return ops.conv2d_wgrad(x, gy, KH, stride, (pb, pe)), None
     xin = F.pad(x, (0, 0, pb, pe, pb, pe)) if (pb or pe) else x
     gw = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (Cout, Cin, KH, KW),
                                      gy.permute(0, 3, 1, 2), stride, 0)

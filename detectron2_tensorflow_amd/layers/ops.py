@@ -340,9 +340,13 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     return y
 
 
-def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False):
+def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math_mode=None):
     """HWIO weight gradient of conv2d_nhwc on the MFMA wgrad kernel; with_bias
-    also returns the bias gradient (dy summed over pixels) from the same pass."""
+    also returns the bias gradient (dy summed over pixels) from the same pass.
+    math_mode: "f32" | "split" (None: CONV_MATH), as conv2d_nhwc."""
+    math_mode = math_mode or CONV_MATH
+    if math_mode not in ("f32", "split"):
+        raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
     x, dy = _f32c(x), _f32c(dy)
     _C.require_device(x, dy)
     N, H, W, Cin = x.shape
@@ -355,8 +359,9 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False):
     wsb = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
     ws = _C.workspace(wsb, x.device) if wsb else None
     ev = KernelTimer.start()
-    rc = _C.lib().d2mi_conv2d_wgrad(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
-                                    _C.ptr(ws), wsb, _C.stream_of(x.device))
+    flags = 4 if math_mode == "split" else 0
+    rc = _C.lib().d2mi_conv2d_wgrad_ex(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
+                                       flags, _C.ptr(ws), wsb, _C.stream_of(x.device))
     KernelTimer.stop(ev, "conv2d_wgrad_mfma", 2.0 * dy.numel() * KH * KW * Cin)
     if KernelTimer.detail and ev is not None:
         KernelTimer.stop(ev, f"wgrad {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride}",

@@ -260,6 +260,12 @@ size_t d2mi_conv2d_wgrad_workspace_size(int N, int H, int W, int Cin, int Cout, 
 int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio, float* dbias, int N,
                       int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
                       int pad_end, void* workspace, size_t workspace_bytes, void* stream);
+/* flags bit2: the split-bf16 products of d2mi_conv2d_nhwc_ex (exact 3-term
+ * split of x and dy, six bf16 MFMA products, f32 accumulation). */
+int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_hwio, float* dbias, int N,
+                         int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad_beg, int pad_end, int flags, void* workspace,
+                         size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------- FrozenBN fold
  * A frozen BatchNorm (moving statistics; lib/layers/normalization.py:15-119

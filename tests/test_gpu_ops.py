@@ -636,10 +636,13 @@ def test_conv_mfma_autograd_matches_torch(dev, conf):
                                    atol=2e-4 * max(1.0, float(r.grad.abs().max())), err_msg=name)
 
 
+@pytest.mark.parametrize("mode", ["f32", "split"])
 @pytest.mark.parametrize("conf", [(2, 40, 52, 256, 256, 3, 1), (2, 30, 41, 64, 96, 3, 2),
-                                  (2, 200, 168, 256, 64, 1, 1), (1, 50, 84, 512, 1024, 1, 2)])
-def test_conv2d_wgrad_kernel_with_bias(dev, conf):
-    """d2mi_conv2d_wgrad (and its fused bias gradient) vs float64 torch."""
+                                  (2, 200, 168, 256, 64, 1, 1), (1, 50, 84, 512, 1024, 1, 2),
+                                  (3, 14, 14, 36, 20, 3, 1)])
+def test_conv2d_wgrad_kernel_with_bias(dev, conf, mode):
+    """d2mi_conv2d_wgrad_ex (and its fused bias gradient), f32 and split
+    products, vs float64 torch."""
     N, H, W, Cin, Cout, k, s = conf
     g = torch.Generator().manual_seed(sum(conf))
     p = (k - 1) // 2
@@ -648,12 +651,14 @@ def test_conv2d_wgrad_kernel_with_bias(dev, conf):
     dy = torch.randn(N, OH, OW, Cout, generator=g)
     want = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (Cout, Cin, k, k),
                                        dy.permute(0, 3, 1, 2).double(), s, p).permute(2, 3, 1, 0)
-    dw, db = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True)
+    dw, db = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True,
+                                math_mode=mode)
     scale = float(want.abs().max())
     np.testing.assert_allclose(dw.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=2e-5 * scale)
     np.testing.assert_allclose(db.cpu().double().numpy(), dy.double().sum((0, 1, 2)).numpy(),
                                rtol=1e-4, atol=1e-3)
-    dw2, db2 = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True)
+    dw2, db2 = ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True,
+                                  math_mode=mode)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 

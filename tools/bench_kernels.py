@@ -118,7 +118,8 @@ def bench_wgrad(dev, iters):
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         dy = torch.randn(N, OH, OW, Cout, device=dev)
         flops = 2.0 * N * OH * OW * Cout * k * k * Cin
-        ms = timeit(lambda: ops.conv2d_wgrad(x, dy, k, s, (p, p)), iters)
+        ms = timeit(lambda: ops.conv2d_wgrad(x, dy, k, s, (p, p), math_mode="f32"), iters)
+        ms_s = timeit(lambda: ops.conv2d_wgrad(x, dy, k, s, (p, p), math_mode="split"), iters)
         xc, dyc = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
         if k == 1:
             x2, dy2 = x.reshape(-1, Cin), dy.reshape(-1, Cout)
@@ -127,12 +128,16 @@ def bench_wgrad(dev, iters):
             ms_t = timeit(lambda: torch.nn.grad.conv2d_weight(xc, (Cout, Cin, k, k), dyc, s, p),
                           iters)
         ref = torch.nn.grad.conv2d_weight(xc, (Cout, Cin, k, k), dyc, s, p).permute(2, 3, 1, 0)
-        err = float((ops.conv2d_wgrad(x, dy, k, s, (p, p)) - ref).abs().max() /
+        err = float((ops.conv2d_wgrad(x, dy, k, s, (p, p), math_mode="f32") - ref).abs().max() /
                     ref.abs().max().clamp(min=1e-30))
+        err_s = float((ops.conv2d_wgrad(x, dy, k, s, (p, p), math_mode="split") - ref).abs().max() /
+                      ref.abs().max().clamp(min=1e-30))
         out.append({"kernel": "wgrad", "shape": name, "mfma_us": round(ms * 1e3, 1),
                     "mfma_tflops": round(flops / ms / 1e9, 1),
                     "miopen_us": round(ms_t * 1e3, 1),
-                    "miopen_tflops": round(flops / ms_t / 1e9, 1), "max_rel_err": err})
+                    "miopen_tflops": round(flops / ms_t / 1e9, 1), "max_rel_err": err,
+                    "split_us": round(ms_s * 1e3, 1), "split_tflops": round(flops / ms_s / 1e9, 1),
+                    "max_rel_err_split": err_s})
     return out
 
 
