@@ -737,10 +737,12 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.tdW = (a.OW + 1) / 2;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
-  // workgroups per launch well above 2 per CU: single-buffered (occupancy);
-  // otherwise double-buffered.  D2MI_CONV_DB=0/1 forces one (tuning).
+  // 128x128 tiles: single-buffered LDS (two barriers per k-step, 2 workgroups
+  // per CU) measured faster than double-buffered (1 workgroup per CU) on every
+  // Mask R-CNN shape, f32 and split, large grids and small
+  // (tools/exp_conv_db.sh).  D2MI_CONV_DB=1 forces double buffering (tuning).
   static const char* force = getenv("D2MI_CONV_DB");
-  bool db = (size_t)a.ntiles * a.splits < 1024;
+  bool db = false;
   if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
   if (x3)
     launch_x3(p.cfg, db, grid, st, a);

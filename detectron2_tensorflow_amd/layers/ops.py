@@ -259,6 +259,11 @@ def pack_conv_weights(w_hwio):
 # (d2mi_conv2d_nhwc_x3); otherwise the conv splits while staging.
 # Process-wide default from D2MI_CONV_MATH.
 CONV_MATH = os.environ.get("D2MI_CONV_MATH", "split")
+# Pre-splitting a KxK conv's input (one extra pass) measured slower than
+# splitting while staging once the conv runs 2 workgroups per CU
+# (tools/exp_conv_presplit.sh); kept as a knob and for callers that already
+# hold the planes (x_split).
+PRESPLIT_KXK = os.environ.get("D2MI_CONV_PRESPLIT", "0") == "1"
 
 
 def split_bf16x3(x):
@@ -305,13 +310,11 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     if residual is not None:
         residual = _f32c(residual)
     # measured policy (tools/bench_kernels.py --only conv): narrow Cout (the
-    # 128x64 / 128x32 tiles) gains nothing from the split products; KxK
-    # kernels re-read each input element KH*KW times, so splitting it once
-    # beforehand beats splitting while staging; 1x1 convs split while staging.
+    # 128x64 / 128x32 tiles) gains nothing from the split products.
     if math_mode == "split" and Cout <= 64:
         math_mode = "f32"
     presplit = math_mode == "split" and _presplit_ok(x, Cin) and (
-        x_split is not None or KH * KW > 1)
+        x_split is not None or (KH * KW > 1 and PRESPLIT_KXK))
     flags = (1 if relu else 0) | (2 if relu_after_add else 0)
     if math_mode == "split" and not presplit:
         flags |= 4
