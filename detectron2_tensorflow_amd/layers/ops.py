@@ -336,7 +336,7 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                           Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
                                           _C.ptr(ws), wsb, _C.stream_of(x.device))
     fl = 2.0 * N * OH * OW * Cout * KH * KW * Cin
-    KernelTimer.stop(ev, "conv2d_mfma", fl)
+    KernelTimer.stop(ev, "conv2d_split" if math_mode == "split" else "conv2d_mfma", fl)
     if KernelTimer.detail and ev is not None:
         KernelTimer.stop(ev, f"conv {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride} p{pb}{pe}", fl)
     _C.check(rc, "d2mi_conv2d_nhwc")
@@ -365,7 +365,8 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math
     flags = 4 if math_mode == "split" else 0
     rc = _C.lib().d2mi_conv2d_wgrad_ex(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
                                        flags, _C.ptr(ws), wsb, _C.stream_of(x.device))
-    KernelTimer.stop(ev, "conv2d_wgrad_mfma", 2.0 * dy.numel() * KH * KW * Cin)
+    KernelTimer.stop(ev, "conv2d_wgrad_split" if flags else "conv2d_wgrad_mfma",
+                     2.0 * dy.numel() * KH * KW * Cin)
     if KernelTimer.detail and ev is not None:
         KernelTimer.stop(ev, f"wgrad {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride}",
                          2.0 * dy.numel() * KH * KW * Cin)

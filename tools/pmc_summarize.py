@@ -17,12 +17,15 @@ import os
 import re
 import sys
 
+# the split-K reduction launches are counted with the split-product group (the
+# bulk of the conv calls); per-launch figures divide by the main kernel's count
 GROUPS = {
-    "conv2d_mfma": re.compile(r"conv_mfma_kernel|splitk_reduce_kernel"),
-    "conv_mfma_kernel": re.compile(r"conv_mfma_kernel"),
+    "conv2d_split": re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce_kernel"),
+    "conv2d_mfma": re.compile(r"conv_mfma_kernel<[^>]*, false>"),
     "roi_align_fwd": re.compile(r"roi_align_fwd_kernel"),
     "roi_align_bwd": re.compile(r"roi_bwd_"),
-    "conv_wgrad": re.compile(r"conv_wgrad_kernel|wgrad_reduce_kernel"),
+    "conv_wgrad_split": re.compile(r"conv_wgrad_split_kernel|wgrad_reduce_kernel"),
+    "conv_wgrad": re.compile(r"conv_wgrad_kernel<"),
 }
 
 
