@@ -278,6 +278,11 @@ def main():
         in_sync = all(bool(torch.equal(allck[0], c)) for c in allck)
     if args.mode == "train":
         extra = {"losses_last_step_rank0": {k: round(float(v.detach()), 4) for k, v in out.items()}}
+        rh = getattr(model, "roi_heads", None)
+        if getattr(rh, "last_mask_rows", None) is not None:
+            # mask head rows of the last step: the foreground ROIs (as the
+            # reference) padded to a multiple of MASK_ROW_BUCKET
+            extra["mask_head_rows_last_step_rank0"] = rh.last_mask_rows
     else:
         extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 

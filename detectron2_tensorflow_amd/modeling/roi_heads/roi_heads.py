@@ -99,6 +99,8 @@ class ROIHeads(Layer):
 
 @ROI_HEADS_REGISTRY.register()
 class StandardROIHeads(ROIHeads):
+    MASK_ROW_BUCKET = 32
+
     def __init__(self, cfg, input_shape, **kwargs):
         super().__init__(cfg, input_shape, **kwargs)
         self._init_box_head(cfg)
@@ -123,6 +125,11 @@ class StandardROIHeads(ROIHeads):
             return
         m = cfg.MODEL.ROI_MASK_HEAD
         self.use_mini_masks = cfg.TRANSFORM.RESIZE.USE_MINI_MASKS
+        # True: mask head on the foreground rows only, like the reference (one
+        # host sync per step); False: fixed [N, S*POSITIVE_FRACTION] rows with
+        # a validity mask (no host sync, capturable).
+        self.mask_compact_rows = True
+        self.last_mask_rows = None
         scales = tuple(1.0 / self.feature_strides[k] for k in self.in_features)
         c = [self.feature_channels[f] for f in self.in_features][0]
         self.mask_pooler = ROIPooler(m.POOLER_RESOLUTION, scales, m.POOLER_SAMPLING_RATIO,
@@ -181,19 +188,34 @@ class StandardROIHeads(ROIHeads):
         int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
         foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
         F_ = int(self.batch_size_per_image * self.positive_sample_fraction)
-        boxes = sampled["boxes"][:, :F_].contiguous()
-        N = boxes.shape[0]
-        cls = sampled["gt_classes"][:, :F_]
-        fg = sampled["is_valid"][:, :F_] & (cls >= 0) & (cls < self.num_classes)
-        img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(F_)
-        x = self.mask_pooler.pool(feats, boxes.reshape(-1, 4), img)
-        _, logits = self.mask_head(x)
+        boxes = sampled["boxes"][:, :F_].reshape(-1, 4)
+        N = sampled["boxes"].shape[0]
+        dev = boxes.device
+        cls = sampled["gt_classes"][:, :F_].reshape(-1)
+        fg = (sampled["is_valid"][:, :F_] & (sampled["gt_classes"][:, :F_] >= 0)
+              & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
+        img = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(F_)
         gm = targets["gt_masks"]
         G = gm.shape[1]
-        mind = sampled["gt_index"][:, :F_] + torch.arange(N, device=boxes.device)[:, None] * G
-        return mask_rcnn_loss(logits, boxes.reshape(-1, 4), sampled["gt_boxes"][:, :F_].reshape(-1, 4),
-                              cls.reshape(-1), gm.reshape(N * G, *gm.shape[2:]), mind.reshape(-1),
-                              fg.reshape(-1), self.use_mini_masks)
+        mind = (sampled["gt_index"][:, :F_] + torch.arange(N, device=dev)[:, None] * G).reshape(-1)
+        gt_boxes = sampled["gt_boxes"][:, :F_].reshape(-1, 4)
+        if self.mask_compact_rows:
+            # The reference runs the mask head on the foreground proposals only
+            # (select_foreground_proposals, roi_heads.py:35-62 + :594-600).  One
+            # host read of the foreground count; the rows are gathered fg-first
+            # (image order kept) and padded to a multiple of MASK_ROW_BUCKET
+            # with masked-out rows, which bounds the number of distinct shapes.
+            nfg = int(fg.sum())
+            B = fg.numel()
+            R = min(B, max(self.MASK_ROW_BUCKET, -(-nfg // self.MASK_ROW_BUCKET) * self.MASK_ROW_BUCKET))
+            key = (~fg).to(torch.int64) * B + torch.arange(B, device=dev)
+            rows = key.sort().values[:R] % B
+            boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))
+            self.last_mask_rows = R
+        x = self.mask_pooler.pool(feats, boxes.contiguous(), img)
+        _, logits = self.mask_head(x)
+        return mask_rcnn_loss(logits, boxes, gt_boxes, cls, gm.reshape(N * G, *gm.shape[2:]), mind,
+                              fg, self.use_mini_masks)
 
     def forward_with_given_boxes(self, features, instances, image_shape=None):
         assert not self.training

@@ -130,3 +130,29 @@ def test_trainer_overfits_one_batch(dev):
     first = np.mean([h["total_loss"] for h in hist[:3]])
     last = np.mean([h["total_loss"] for h in hist[-3:]])
     assert last < 0.8 * first, (first, last, hist[-1])
+
+
+def test_mask_head_on_foreground_rows_matches_fixed_layout(dev):
+    """The compacted mask branch (foreground rows only, as the reference's
+    select_foreground_proposals) gives the fixed-slot layout's loss and
+    mask-head gradients: the extra rows of the fixed layout are masked out."""
+    from detectron2_tensorflow_amd.utils.synthetic import synthetic_train_batch
+    cfg, model = _train_model(dev)
+    batch = synthetic_train_batch(2, 256, 320, 2, dev)
+    rh = model.roi_heads
+    res = {}
+    for compact in (False, True):
+        model.zero_grad(set_to_none=True)
+        rh.mask_compact_rows = compact
+        torch.manual_seed(5)  # same subsampling draw
+        losses = model(batch)
+        losses["loss_mask"].backward()
+        res[compact] = (losses["loss_mask"].item(),
+                        {n: p.grad.clone() for n, p in rh.mask_head.named_parameters()
+                         if p.grad is not None})
+    assert rh.last_mask_rows is not None and rh.last_mask_rows % rh.MASK_ROW_BUCKET == 0
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-5, abs=1e-7)
+    assert res[True][1].keys() == res[False][1].keys() and res[True][1]
+    for n, g in res[False][1].items():
+        # summation order differs with the row count (split-K / wgrad partitions)
+        torch.testing.assert_close(res[True][1][n], g, rtol=1e-4, atol=1e-4 * g.abs().max().item())
