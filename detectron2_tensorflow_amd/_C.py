@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libd2mi_hip.so")
+# D2MI_LIB: an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("D2MI_LIB") or os.path.join(_HERE, "lib", "libd2mi_hip.so")
 
 _lib = None
 _load_error = None

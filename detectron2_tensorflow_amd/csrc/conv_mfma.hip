@@ -262,11 +262,16 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
   constexpr uint32_t kOOB = 0x80000000u;
 
-  float4 ra[RA], rb[RB];
-  auto load_tile = [&](int kt) {
-    // channel-chunk-major, tap-minor K order: consecutive k-steps read the
-    // same 32 channels at neighbouring pixels (the 3x3 taps), which are
-    // still in L2 (tap-major order re-fetched them Cin/32 steps later)
+  // Staging registers.  Single-buffered LDS runs a 2-deep prefetch of the
+  // activation tile (k-step kt+2 loads while kt computes and kt+1 waits in
+  // the other set) and a 1-deep prefetch of the weight tile (small and
+  // L2-resident): an activation gather has two compute phases to return, one
+  // phase (~0.6 us at 2 workgroups/CU) being below its loaded latency.
+  float4 ra[2][RA], rb[RB];
+  // channel-chunk-major, tap-minor K order: consecutive k-steps read the
+  // same 32 channels at neighbouring pixels (the 3x3 taps), which are still
+  // in L2 (tap-major order re-fetched them Cin/32 steps later)
+  auto load_a = [&](int kt, float4 (&la)[RA]) {
     const int taps = a.KH * a.KW;
     const int chunk = kt / taps;
     const int tap = kt - chunk * taps;
@@ -280,8 +285,15 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)a.H) &
                       ((unsigned)(iw0[p] + kw) < (unsigned)a.W);
       const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
-      ra[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+      la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
     }
+  };
+  auto load_b = [&](int kt) {
+    const int taps = a.KH * a.KW;
+    const int chunk = kt / taps;
+    const int tap = kt - chunk * taps;
+    const int cc = chunk * BK;
+    const bool cok = cc + schunk < a.Cin;
 #pragma unroll
     for (int p = 0; p < RB; ++p) {
       const int co = n0 + srow + 32 * p;
@@ -291,14 +303,14 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       rb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
     if constexpr (SPLIT) {
       uint16_t* A16 = reinterpret_cast<uint16_t*>(As[buf]);
       uint16_t* B16 = reinterpret_cast<uint16_t*>(Bs[buf]);
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
         uint2 h, m, l;
-        split3(ra[p], h, m, l);
+        split3(la[p], h, m, l);
         const int o = swz(srow + 32 * p, schunk);
         *reinterpret_cast<uint2*>(&A16[o]) = h;
         *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        split3(rb[p], h, m, l);
+        split3(lb[p], h, m, l);
         const int o = swz(srow + 32 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -316,10 +328,10 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
     } else {
 #pragma unroll
       for (int p = 0; p < RA; ++p)
-        *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = ra[p];
+        *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = la[p];
 #pragma unroll
       for (int p = 0; p < RB; ++p)
-        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = rb[p];
+        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = lb[p];
     }
   };
 
@@ -332,44 +344,37 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
-  if (kt0 < kt1) {
-    load_tile(kt0);
-    store_tile(0);
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
-      if constexpr (SPLIT) {
-        const uint16_t* A16 = reinterpret_cast<const uint16_t*>(As[buf]);
-        const uint16_t* B16 = reinterpret_cast<const uint16_t*>(Bs[buf]);
+  auto compute = [&](int buf) {
+    if constexpr (SPLIT) {
+      const uint16_t* A16 = reinterpret_cast<const uint16_t*>(As[buf]);
+      const uint16_t* B16 = reinterpret_cast<const uint16_t*>(Bs[buf]);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {  // two 16-deep bf16 MFMA steps per 32-deep stage
-          bf16x8 fa[3][TM], fb[3][TN];
+      for (int ks = 0; ks < 2; ++ks) {  // two 16-deep bf16 MFMA steps per 32-deep stage
+        bf16x8 fa[3][TM], fb[3][TN];
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-              fa[pl][i] = *reinterpret_cast<const bf16x8*>(
-                  &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+          for (int i = 0; i < TM; ++i)
+            fa[pl][i] = *reinterpret_cast<const bf16x8*>(
+                &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[pl][j] = *reinterpret_cast<const bf16x8*>(
+                &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+        }
+        // small terms first, then the dominant h*h
+        constexpr int PA[6] = {1, 2, 0, 0, 1, 0};
+        constexpr int PB[6] = {1, 0, 2, 1, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              fb[pl][j] = *reinterpret_cast<const bf16x8*>(
-                  &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
-          }
-          // small terms first, then the dominant h*h
-          constexpr int PA[6] = {1, 2, 0, 0, 1, 0};
-          constexpr int PB[6] = {1, 0, 2, 1, 0, 0};
-#pragma unroll
-          for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-              for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
-                                                                     acc[i][j], 0, 0, 0);
-        }
-      } else {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
+                                                                   acc[i][j], 0, 0, 0);
+      }
+    } else {
       const float* A = As[buf];
       const float* B = Bs[buf];
 #pragma unroll
@@ -392,17 +397,49 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][ss], fb[j][ss], acc[i][j],
                                                                 0, 0, 0);
       }
-      }
-      if (DB) {
-        if (more) store_tile(buf ^ 1);
+    }
+  };
+
+  if (kt0 < kt1) {
+    if constexpr (DB) {
+      load_a(kt0, ra[0]);
+      load_b(kt0);
+      store_tile(0, ra[0], rb);
+      __syncthreads();
+      int buf = 0;
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) {
+          load_a(kt + 1, ra[0]);
+          load_b(kt + 1);
+        }
+        compute(buf);
+        if (more) store_tile(buf ^ 1, ra[0], rb);
         __syncthreads();
         buf ^= 1;
-      } else {
+      }
+    } else {
+      // step(kt): activation set F is free (its k-step is in LDS), set X
+      // holds kt + 1.  B(kt+1) is issued before A(kt+2), so the store of
+      // k-step kt+1 leaves only A(kt+2) in flight.
+      auto step = [&](int kt, float4 (&F)[RA], const float4 (&X)[RA]) {
+        if (kt + 1 < kt1) load_b(kt + 1);
+        if (kt + 2 < kt1) load_a(kt + 2, F);
+        compute(0);
         __syncthreads();
-        if (more) {
-          store_tile(0);
+        if (kt + 1 < kt1) {
+          store_tile(0, X, rb);
           __syncthreads();
         }
+      };
+      load_a(kt0, ra[0]);
+      load_b(kt0);
+      if (kt0 + 1 < kt1) load_a(kt0 + 1, ra[1]);
+      store_tile(0, ra[0], rb);
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; kt += 2) {
+        step(kt, ra[0], ra[1]);
+        if (kt + 1 < kt1) step(kt + 1, ra[1], ra[0]);
       }
     }
   }

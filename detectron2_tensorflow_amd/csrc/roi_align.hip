@@ -36,6 +36,7 @@ struct RoiArgs {
   float* out;
   const float* gout;
   int32_t* err;
+  int bpb;  // forward: output bins per workgroup (16, 32 or 64)
 };
 
 struct RoiGeom {
@@ -140,7 +141,10 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float t) {
                      a.w + (b.w - a.w) * t);
 }
 
-constexpr int kBinsPerBlock = 64;
+// Forward grid: (R, ceil(bins / bpb)); bpb = 64 bins per 4-wave workgroup,
+// halved (down to 16) while the grid has fewer than 2048 workgroups, so the
+// few-ROI launches (the mask pooler's foreground ROIs) still fill 256 CUs.
+constexpr int kMaxBinsPerBlock = 64, kMinBinsPerBlock = 16, kFwdMinBlocks = 2048;
 
 template <bool VEC4>
 __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
   const float* base = a.feat[g.lvl] + (size_t)(g.ok ? g.n : 0) * g.H * g.W * a.C;
   const int C = a.C;
   const bool pad = a.pad_border != 0;
-  const int b_end = min(nbins, (int)(blockIdx.y + 1) * kBinsPerBlock);
+  const int b_end = min(nbins, (int)(blockIdx.y + 1) * a.bpb);
   if (VEC4 && S == 1 && C == 256) {
     // Common case (C = 256, one sample per bin): U bins per wave iteration with
     // all 4U corner loads issued before any is consumed (the taps are clamped
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
     // after) — memory-level parallelism instead of one latency per bin.
     constexpr int U = 4;
     const float4* p = reinterpret_cast<const float4*>(base);
-    for (int bb = blockIdx.y * kBinsPerBlock + wave; bb < b_end; bb += 4 * U) {
+    for (int bb = blockIdx.y * a.bpb + wave; bb < b_end; bb += 4 * U) {
       float4 c00[U], c01[U], c10[U], c11[U];
       float ly[U], lx[U];
       bool ok[U];
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
     }
     return;
   }
-  for (int bin = blockIdx.y * kBinsPerBlock + wave; bin < b_end; bin += 4) {
+  for (int bin = blockIdx.y * a.bpb + wave; bin < b_end; bin += 4) {
     const int oy = bin / a.out_w, ox = bin - oy * a.out_w;
     float* dst = a.out + ((size_t)r * nbins + bin) * C;
     if (VEC4) {
@@ -277,9 +281,10 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 //      segments (exclusive scan of their segment counts) summed by one wave
 //      each into a partial row — bounded work per wave however many ROIs pile
 //      onto one pixel (collapsed proposals at the image border do);
-//   6. one wave per feature-map pixel, lanes over channels (float4): sum its
-//      contributions (or its segments' partials) in order and store it —
-//      every element of every grad map is written exactly once.
+//   6. the grad maps are zero-filled (memset, full bandwidth) and the touched
+//      pixels (compact list from step 4) are summed by waves striding over
+//      that list, lanes over channels (float4): each sums its contributions
+//      (or its segments' partials) in order and stores the pixel once.
 // Summation order per pixel is (box, y, x, corner), the TF kernel's loop order
 // (partials regroup it for pixels past kSeg): deterministic run to run, and
 // bit-identical to the TF scatter for pixels with at most kSeg contributions
@@ -343,15 +348,36 @@ __global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, const RoiGeom* __restr
 }
 
 // run_start[p] = first sorted index of pixel p (-1 untouched), run_end[p] = one past its last.
-__global__ void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
+// Every touched pixel is also appended to touched[] (*n_touched entries; the
+// list order varies run to run, the per-pixel sums do not).
+__global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
                                     long long total_pixels, int32_t* __restrict__ run_start,
-                                    int32_t* __restrict__ run_end) {
+                                    int32_t* __restrict__ run_end, int32_t* __restrict__ touched,
+                                    int32_t* __restrict__ n_touched) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t p = keys[i] >> low_bits;
-  if ((long long)p >= total_pixels) return;  // invalid contributions sort last
-  if (i == 0 || (keys[i - 1] >> low_bits) != p) run_start[p] = (int32_t)i;
-  if (i == n - 1 || (keys[i + 1] >> low_bits) != p) run_end[p] = (int32_t)(i + 1);
+  const uint64_t p = i < n ? keys[i] >> low_bits : ~0ull;
+  const bool live = i < n && (long long)p < total_pixels;  // invalid contributions sort last
+  const bool first = live && (i == 0 || (keys[i - 1] >> low_bits) != p);
+  // one global counter atomic per 1024-thread workgroup: same-address device
+  // atomics serialise (one per wave still cost ~20 us per launch); the waves'
+  // offsets come from an LDS counter
+  __shared__ int wg_count, wg_base;
+  if (threadIdx.x == 0) wg_count = 0;
+  __syncthreads();
+  const uint64_t m = __ballot(first);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (m && lane == 0) base = atomicAdd(&wg_count, __popcll(m));
+  base = __shfl(base, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) wg_base = wg_count ? atomicAdd(n_touched, wg_count) : 0;
+  __syncthreads();
+  base += wg_base;
+  if (first) {
+    run_start[p] = (int32_t)i;
+    touched[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+  }
+  if (live && (i == n - 1 || (keys[i + 1] >> low_bits) != p)) run_end[p] = (int32_t)(i + 1);
 }
 
 // nseg[p] = number of kSeg segments of pixel p when it has more than kSeg
@@ -460,47 +486,55 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
   }
 }
 
-// One wave per feature-map pixel.
+// Touched pixels only (the grad maps were zero-filled at full bandwidth
+// first): waves stride over the compact touched-pixel list, one pixel per wave
+// iteration, so the dependent load chain of a pixel (run bounds -> sorted keys
+// -> records -> grad_out rows) overlaps across waves instead of a wave per
+// feature-map pixel (most of which only stored zeros) -- that launch was bound
+// by wave start-up and latency, at ~1/4 of its store bandwidth.
 template <bool VEC4>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
     RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
     int low_bits, const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
     const int32_t* __restrict__ nseg, const int32_t* __restrict__ seg_first,
-    const float* __restrict__ partial, long long total_pixels) {
-  const long long pix = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const float* __restrict__ partial, const int32_t* __restrict__ touched,
+    const int32_t* __restrict__ n_touched) {
   const int lane = threadIdx.x & 63;
-  if (pix >= total_pixels) return;
-  int l = 0;
-  while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
   const int C = a.C;
-  float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
-  const int i0 = run_start[pix];
-  const int i1 = i0 >= 0 ? run_end[pix] : i0;
-  const int ns = i0 >= 0 ? nseg[pix] : 0;
-  const int f = ns ? seg_first[pix] : 0;
   const uint64_t low_mask = (1ull << low_bits) - 1ull;
   const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
   const int step = VEC4 ? 256 : 64;
-  for (int c0 = 0; c0 < C; c0 += step) {
-    const int c = c0 + (VEC4 ? lane * 4 : lane);
-    const bool live = c < C;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ns == 0 && i0 >= 0) {
-      acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
-    } else if (ns > 0 && live) {
-      for (int j = 0; j < ns; ++j) {
-        const float* src = partial + (size_t)(f + j) * C + c;
-        if (VEC4) {
-          const float4 v = *reinterpret_cast<const float4*>(src);
-          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        } else {
-          acc.x += *src;
+  const int nt = *n_touched;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += gridDim.x * 4) {
+    const long long pix = touched[t];
+    int l = 0;
+    while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
+    float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
+    const int i0 = run_start[pix];
+    const int i1 = run_end[pix];
+    const int ns = nseg[pix];
+    const int f = ns ? seg_first[pix] : 0;
+    for (int c0 = 0; c0 < C; c0 += step) {
+      const int c = c0 + (VEC4 ? lane * 4 : lane);
+      const bool live = c < C;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ns == 0) {
+        acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
+      } else if (live) {
+        for (int j = 0; j < ns; ++j) {
+          const float* src = partial + (size_t)(f + j) * C + c;
+          if (VEC4) {
+            const float4 v = *reinterpret_cast<const float4*>(src);
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+          } else {
+            acc.x += *src;
+          }
         }
       }
-    }
-    if (live) {
-      if (VEC4) *reinterpret_cast<float4*>(dst + c) = acc;
-      else dst[c] = acc.x;
+      if (live) {
+        if (VEC4) *reinterpret_cast<float4*>(dst + c) = acc;
+        else dst[c] = acc.x;
+      }
     }
   }
 }
@@ -573,7 +607,11 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   a.out = out;
   if (R == 0) return 0;
   const int nbins = out_h * out_w;
-  dim3 grid(R, (nbins + kBinsPerBlock - 1) / kBinsPerBlock);
+  a.bpb = kMaxBinsPerBlock;
+  while (a.bpb > kMinBinsPerBlock &&
+         (long long)R * ((nbins + a.bpb - 1) / a.bpb) < kFwdMinBlocks)
+    a.bpb /= 2;
+  dim3 grid(R, (nbins + a.bpb - 1) / a.bpb);
   if (vec4)
     hipLaunchKernelGGL(roi_align_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), a);
   else
@@ -592,7 +630,7 @@ int bits_for(unsigned long long v) {  // smallest b with 2^b > v
 }
 
 struct BwdPlan {
-  long long total_pixels, n_keys, n_samples, max_segs;
+  long long total_pixels, n_keys, n_samples, max_segs, max_touched;
   int low_bits, end_bit;
   PixMap pm;
 };
@@ -611,6 +649,7 @@ int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, i
   p->total_pixels = t;
   // every split pixel has > kSeg contributions: segments <= 2 * n / kSeg
   p->max_segs = 2 * (p->n_keys / kSeg) + 1;
+  p->max_touched = std::min(p->n_keys, t);
   p->low_bits = max(1, bits_for(p->n_keys > 0 ? (unsigned long long)(p->n_keys - 1) : 0ull));
   p->end_bit = p->low_bits + bits_for((unsigned long long)t);
   D2MI_REQUIRE(p->end_bit <= 64, "ROIAlign backward key space too large (%d bits)", p->end_bit);
@@ -630,6 +669,8 @@ void bwd_layout(WS& w, int R, int C, const BwdPlan& p) {
   w.template take<int32_t>((size_t)p.total_pixels + 1);     // seg_first
   w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
+  w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
+  w.template take<int32_t>(1);                              // their count
   w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
                             exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1)));
 }
@@ -686,11 +727,18 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
   int32_t* seg_first = w.take<int32_t>((size_t)p.total_pixels + 1);
   int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
   float* partial = w.take<float>((size_t)p.max_segs * C);
+  int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
+  int32_t* n_touched = w.take<int32_t>(1);
   const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
                                exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1));
   void* tmp = w.take<char>(tmp_bytes);
   const long long TP = p.total_pixels;
   D2MI_HIP(hipMemsetAsync(run_start, 0xff, (size_t)TP * sizeof(int32_t), st));
+  D2MI_HIP(hipMemsetAsync(n_touched, 0, sizeof(int32_t), st));
+  for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero gradient
+    D2MI_HIP(hipMemsetAsync(a.gfeat[l], 0,
+                            (size_t)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C *
+                                sizeof(float), st));
   if (p.n_keys > 0) {
     hipLaunchKernelGGL(roi_bwd_geom_kernel, dim3((R + 255) / 256), dim3(256), 0, st, a, geo);
     D2MI_LAUNCH_CHECK();
@@ -699,8 +747,9 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
     D2MI_LAUNCH_CHECK();
     rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.end_bit, tmp, tmp_bytes, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256),
-                       0, st, sorted, p.n_keys, p.low_bits, TP, run_start, run_end);
+    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
+                       0, st, sorted, p.n_keys, p.low_bits, TP, run_start, run_end, touched,
+                       n_touched);
     D2MI_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(roi_bwd_nseg_kernel, dim3((unsigned)((TP + 1 + 255) / 256)), dim3(256), 0, st,
@@ -723,13 +772,17 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
                          partial);
     D2MI_LAUNCH_CHECK();
   }
-  const dim3 grid((unsigned)((TP + 3) / 4));
+  if (p.n_keys == 0) return 0;
+  // fixed grid (the touched count stays on the device): ~8 waves per SIMD
+  const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
   if (vec4)
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
-                       p.low_bits, run_start, run_end, nseg, seg_first, partial, TP);
+                       p.low_bits, run_start, run_end, nseg, seg_first, partial, touched,
+                       n_touched);
   else
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
-                       p.low_bits, run_start, run_end, nseg, seg_first, partial, TP);
+                       p.low_bits, run_start, run_end, nseg, seg_first, partial, touched,
+                       n_touched);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

@@ -95,8 +95,11 @@ class _RoIAlignFn(torch.autograd.Function):
                                          canon_s, canon_l, _C.ptr(level), _C.ptr(out),
                                          _C.stream_of(boxes.device))
         S = max(sr, 1) ** 2
-        # algorithmic bytes: 4 f32 corner reads per sample + 1 f32 write per output
-        KernelTimer.stop(ev, "roi_align_fwd", R * out_h * out_w * C * (16 * S + 4))
+        # algorithmic bytes: 4 f32 corner reads per sample + 1 f32
+        # write per output.  Feature-pyramid pooling (C >= 64, the hot path) and
+        # narrow crops (the C = 1 mask-target crop_and_resize) are timed apart.
+        KernelTimer.stop(ev, "roi_align_fwd" if C >= 64 else "crop_and_resize_fwd_narrow",
+                         R * out_h * out_w * C * (16 * S + 4))
         _C.check(rc, "d2mi_roi_align_fwd")
         ctx.params = params
         ctx.shapes = [f.shape for f in feats]
@@ -110,7 +113,7 @@ class _RoIAlignFn(torch.autograd.Function):
         boxes, box_ind = ctx.saved_tensors
         (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
          _) = ctx.params
-        # every element is written by the kernel: no zero-fill
+        # every element is written by d2mi_roi_align_bwd (zero-fill + touched pixels)
         grads = [torch.empty(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
         g = _f32c(grad_out)
         gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
@@ -124,9 +127,11 @@ class _RoIAlignFn(torch.autograd.Function):
                                          _C.ptr(box_ind), R, out_h, out_w, sr, mode, pad, assign,
                                          min_l, max_l, canon_s, canon_l, _C.ptr(g), _C.ptr(ws), wsb,
                                          _C.stream_of(boxes.device))
-        # algorithmic bytes: one read of grad_out + one write of every grad map element
-        KernelTimer.stop(ev, "roi_align_bwd",
-                         4 * (R * out_h * out_w * C + sum(math.prod(s) for s in ctx.shapes)))
+        # algorithmic bytes: R*oh*ow*C*(4 + 32*S) = the grad_out read
+        # + 4 corner read-modify-writes per sample of the reference's scatter
+        S = max(sr, 1) ** 2
+        KernelTimer.stop(ev, "roi_align_bwd" if C >= 64 else "crop_and_resize_bwd_narrow",
+                         R * out_h * out_w * C * (4 + 32 * S))
         _C.check(rc, "d2mi_roi_align_bwd")
         return (None, None, None, *grads)
 

@@ -142,18 +142,29 @@ def bench_wgrad(dev, iters):
 
 
 def bench_roi(dev, iters):
+    """Forward and backward at the inference (2000 x 7x7, 200 x 14x14) and the
+    training shapes (1024 sampled ROIs x 7x7, 64 foreground ROIs x 14x14).
+    Algorithmic bytes per SURVEY 8d D4: fwd R*oh*ow*C*20, bwd R*oh*ow*C*36."""
     g = torch.Generator(device="cpu").manual_seed(0)
     feats = [torch.randn(2, 800 // s, 1344 // s, 256, generator=g).to(dev) for s in (4, 8, 16, 32)]
     out = []
-    for R, o in ((2000, 7), (200, 14)):
+    for R, o, bwd in ((2000, 7, False), (200, 14, False), (1024, 7, True), (64, 14, True)):
         c = torch.rand(R, 2, generator=g) * torch.tensor([800.0, 1333.0])
         sz = torch.exp(torch.rand(R, generator=g) * math.log(50) + math.log(16))
         boxes = torch.stack([c[:, 0] - sz / 2, c[:, 1] - sz / 2, c[:, 0] + sz / 2, c[:, 1] + sz / 2], 1).to(dev)
         bi = torch.randint(0, 2, (R,), generator=g, dtype=torch.int32).to(dev)
         ms = timeit(lambda: ops.roi_align(feats, boxes, bi, (o, o), [0.25, 0.125, 0.0625, 0.03125]), iters)
         byts = R * o * o * 256 * 20
-        out.append({"kernel": "roi_align", "rois": R, "out": o, "us": round(ms * 1e3, 1),
+        out.append({"kernel": "roi_align_fwd", "rois": R, "out": o, "us": round(ms * 1e3, 1),
                     "alg_GBps": round(byts / ms / 1e6, 1)})
+        if bwd:
+            fg = [f.clone().requires_grad_(True) for f in feats]
+            y = ops.roi_align(fg, boxes, bi, (o, o), [0.25, 0.125, 0.0625, 0.03125])
+            gy = torch.randn_like(y)
+            ms = timeit(lambda: torch.autograd.grad(y, fg, gy, retain_graph=True), iters)
+            byts = R * o * o * 256 * 36
+            out.append({"kernel": "roi_align_bwd", "rois": R, "out": o, "us": round(ms * 1e3, 1),
+                        "alg_GBps": round(byts / ms / 1e6, 1)})
     return out
 
 
