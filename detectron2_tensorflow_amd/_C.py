@@ -68,6 +68,7 @@ _SIGS = {
     "d2mi_conv2d_nhwc_x3": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_split_bf16x3": (c_int, [P, ctypes.c_int64, P, P]),
+    "d2mi_paste_masks": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -121,7 +121,7 @@ struct Tap {
 
 __device__ __forceinline__ Tap make_tap(float in, int img_p, int img, bool pad) {
   Tap t;
-  t.valid = !(in < 0.f || in > (float)(img_p - 1));
+  t.valid = in >= 0.f && in <= (float)(img_p - 1);  // NaN -> extrapolate (TF: UB)
   const float fl = floorf(in);
   const int lo = (int)fl;
   const int hi = (int)ceilf(in);

@@ -557,3 +557,34 @@ def retinanet_inference(box_cls, box_delta, strides, cell_anchors, num_classes, 
         _C.ptr(os_), _C.ptr(oc), _C.ptr(ov), _C.ptr(ws), wsb, _C.stream_of(dev))
     _C.check(rc, "d2mi_retinanet_inference")
     return ob, os_, oc, ov.bool()
+
+
+# ------------------------------------------------------------- mask pasting
+def paste_masks(box_masks, boxes, out_shape, valid=None, yx_scale=None, threshold=0.5):
+    """reframe_box_masks_to_image_masks (lib/structures/mask_ops.py:7-56) with
+    the threshold of detector_postprocess (postprocessing.py:47-49) fused:
+    box_masks [D, mh, mw] f32 probabilities, boxes [D, 4] yxyx absolute,
+    out_shape (H, W) canvas; valid [D] bool (False rows -> zeros); yx_scale
+    [D, 2] f32 per-box (sy, sx) applied first ("fixed" format).
+    Returns [D, H, W] uint8."""
+    box_masks = _f32c(box_masks)
+    boxes = _f32c(boxes)
+    tensors = [box_masks, boxes]
+    if valid is not None:
+        valid = valid.to(torch.uint8).contiguous()
+        tensors.append(valid)
+    if yx_scale is not None:
+        yx_scale = _f32c(yx_scale)
+        tensors.append(yx_scale)
+    _C.require_device(*tensors)
+    D, mh, mw = box_masks.shape
+    H, W = int(out_shape[0]), int(out_shape[1])
+    out = torch.empty((D, H, W), dtype=torch.uint8, device=boxes.device)
+    ev = KernelTimer.start()
+    rc = _C.lib().d2mi_paste_masks(_C.ptr(box_masks), _C.ptr(boxes), _C.ptr(yx_scale),
+                                   _C.ptr(valid), D, mh, mw, H, W, float(threshold),
+                                   _C.ptr(out), _C.stream_of(boxes.device))
+    # algorithmic bytes: the u8 canvas written + the box masks read
+    KernelTimer.stop(ev, "paste_masks", D * H * W + box_masks.numel() * 4)
+    _C.check(rc, "d2mi_paste_masks")
+    return out

@@ -5,7 +5,9 @@ RGB (NHWC), "image_shape" [N, 2] int32 true (h, w).  Preprocessing
 normalises, THEN flips to BGR when INPUT_FORMAT == "BGR", then zero-pads to
 the neck's size divisibility (rcnn.py:146-157, image_list.py:89-100).
 Inference returns {"instances": {boxes, classes, scores, is_valid[, masks]}}
-as dense [N, DETECTIONS_PER_IMAGE] tensors (fields.ResultFields names).
+as dense [N, DETECTIONS_PER_IMAGE] tensors (fields.ResultFields names); masks
+are the 28x28 probabilities ("raw") or uint8 masks pasted onto the canvas
+("conventional" / "fixed", modeling/postprocessing.py).
 
 Training (rcnn.py:62-90) takes batched_inputs["instances"] as a dict of dense
 padded ground truth: gt_boxes [N, G, 4] (y1, x1, y2, x2, absolute),
@@ -20,6 +22,7 @@ from ...structures import ImageList
 from ..backbone import build_backbone
 from ..necks import build_neck
 from ..proposal_generator import build_proposal_generator
+from ..postprocessing import detector_postprocess
 from ..roi_heads import build_roi_heads
 from .build import META_ARCH_REGISTRY
 
@@ -39,14 +42,6 @@ class _Preprocess:
             images = images.flip(-1)
         shapes = batched_inputs["image_shape"].to(device=images.device, dtype=torch.int32)
         return ImageList.from_tensors(images.contiguous(), shapes, self.neck.size_divisibility)
-
-
-def _check_output_format(fmt):
-    if fmt != "raw":
-        raise NotImplementedError(
-            f"MODEL.SEGMENTATION_OUTPUT.FORMAT={fmt!r}: pasting masks into the image "
-            "(detector_postprocess, lib/modeling/postprocessing.py:9-59) is the next row of "
-            "SURVEY.md section 8f (F1); use 'raw' (28x28 per-box masks)")
 
 
 @META_ARCH_REGISTRY.register()
@@ -80,7 +75,6 @@ class GeneralizedRCNN(_Preprocess, Layer):
 
     def inference(self, batched_inputs, detected_instances=None):
         assert not self.training
-        _check_output_format(self.segmentation_output_format)
         images = self.preprocess_image(batched_inputs)
         features = self.neck(self.backbone(images.tensor))
         if detected_instances is None:
@@ -95,6 +89,13 @@ class GeneralizedRCNN(_Preprocess, Layer):
                "scores": results.get_field("scores"), "is_valid": results.get_field("is_valid")}
         if results.has_field("pred_masks"):
             out["masks"] = results.get_field("pred_masks")
+            fmt = self.segmentation_output_format
+            if fmt != "raw":  # rcnn.py:124-133
+                if fmt == "fixed":
+                    shape = (self.segmentation_output_resolution,) * 2
+                else:  # "conventional": the padded input canvas
+                    shape = tuple(images.tensor.shape[1:3])
+                out = detector_postprocess(out, shape, fmt, images.image_shapes)
         return {"instances": out}
 
 

@@ -289,6 +289,23 @@ int d2mi_fold_frozen_bn_bwd(const float* gw_eff, const float* gb_eff, const floa
                             float* gw, float* gbias, float* ggamma, float* gbeta,
                             void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------- mask pasting
+ * Replaces detector_postprocess (lib/modeling/postprocessing.py:9-59) for the
+ * "conventional" / "fixed" SEGMENTATION_OUTPUT formats, i.e.
+ * reframe_box_masks_to_image_masks (lib/structures/mask_ops.py:7-56):
+ * normalise each box by the canvas (out_h, out_w), take the reverse box of the
+ * unit square, tf.image.crop_and_resize the box mask onto the canvas
+ * (bilinear, extrapolation 0) and threshold with tf.greater -> uint8.  Same
+ * float32 sequence as the TF CPU kernels; the f32 canvas is never stored.
+ * box_masks [D, mask_h, mask_w] f32 (probabilities); boxes [D, 4] f32 yxyx
+ * absolute; yx_scale [D, 2] f32 (nullable): per-box (sy, sx) applied first
+ * ("fixed": output_shape / image_shape, box_list_ops.scale); valid [D] u8
+ * (nullable): rows with 0 are written as zeros (SparseBoxList.to_dense);
+ * out [D, out_h, out_w] u8, 4-byte aligned. */
+int d2mi_paste_masks(const float* box_masks, const float* boxes, const float* yx_scale,
+                     const uint8_t* valid, int D, int mask_h, int mask_w, int out_h, int out_w,
+                     float threshold, uint8_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

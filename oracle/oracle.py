@@ -388,3 +388,38 @@ def matrix_nms(masks, classes, scores, sum_masks=None, kernel="gaussian", sigma=
     else:
         raise NotImplementedError(kernel)
     return (_f32(scores) * decay.min(axis=0)).astype(F32)
+
+
+def paste_masks(box_masks, boxes, out_shape, valid=None, yx_scale=None, threshold=0.5):
+    """detector_postprocess -> reframe_box_masks_to_image_masks
+    (lib/modeling/postprocessing.py:33-50, lib/structures/mask_ops.py:7-56),
+    float32 numpy glue around the C CropAndResize:
+      box_list_ops.scale (fixed format, :86-108) -> to_normalized_coordinates
+      (:806-839, scale by 1/H, 1/W) -> reverse box of the unit square
+      (mask_ops.py:37-49) -> tf.image.crop_and_resize(crop = canvas) -> tf.greater.
+    box_masks [D, mh, mw], boxes [D, 4] yxyx absolute; returns [D, H, W] uint8
+    (rows with valid False are zeros, SparseBoxList.to_dense)."""
+    m = _f32(box_masks)
+    b = _f32(boxes).reshape(-1, 4).copy()
+    D = b.shape[0]
+    H, W = int(out_shape[0]), int(out_shape[1])
+    if yx_scale is not None:
+        s = _f32(yx_scale).reshape(-1, 2)
+        b[:, 0] = s[:, 0] * b[:, 0]
+        b[:, 2] = s[:, 0] * b[:, 2]
+        b[:, 1] = s[:, 1] * b[:, 1]
+        b[:, 3] = s[:, 1] * b[:, 3]
+    ih, iw = F32(1) / F32(H), F32(1) / F32(W)
+    b[:, 0] = ih * b[:, 0]
+    b[:, 2] = ih * b[:, 2]
+    b[:, 1] = iw * b[:, 1]
+    b[:, 3] = iw * b[:, 3]
+    lo, hi = b[:, 0:2], b[:, 2:4]
+    unit = np.array([[0, 0], [1, 1]], F32)
+    rev = ((unit[None] - lo[:, None, :]) / (hi - lo)[:, None, :]).reshape(-1, 4).astype(F32)
+    out = np.zeros((D, H, W), np.uint8)
+    keep = np.arange(D) if valid is None else np.flatnonzero(np.asarray(valid))
+    if keep.size:
+        crops = crop_and_resize_tf(m[keep][..., None], rev[keep], np.arange(keep.size), (H, W))
+        out[keep] = (crops[..., 0] > F32(threshold)).astype(np.uint8)
+    return out

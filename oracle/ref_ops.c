@@ -45,7 +45,9 @@ int oracle_crop_and_resize(const float* image, int N, int H, int W, int C, const
     for (int y = 0; y < ch; ++y) {
       const float in_y = (ch > 1) ? y1 * (H - 1) + y * height_scale : 0.5 * (y1 + y2) * (H - 1);
       float* orow = out + ((size_t)b * ch + y) * cw * C;
-      if (in_y < 0 || in_y > H - 1) {
+      /* written as !(in range) so that a NaN coordinate (a degenerate box;
+       * UB in TF: (int)floorf(NaN) indexes out of bounds) extrapolates */
+      if (!(in_y >= 0 && in_y <= H - 1)) {
         memset(orow, 0, sizeof(float) * (size_t)cw * C);
         continue;
       }
@@ -55,7 +57,7 @@ int oracle_crop_and_resize(const float* image, int N, int H, int W, int C, const
       for (int x = 0; x < cw; ++x) {
         const float in_x = (cw > 1) ? x1 * (W - 1) + x * width_scale : 0.5 * (x1 + x2) * (W - 1);
         float* o = orow + (size_t)x * C;
-        if (in_x < 0 || in_x > W - 1) {
+        if (!(in_x >= 0 && in_x <= W - 1)) {
           memset(o, 0, sizeof(float) * C);
           continue;
         }
@@ -92,13 +94,13 @@ int oracle_crop_and_resize_grad_image(const float* grads, const float* boxes,
     const float width_scale = (cw > 1) ? (x2 - x1) * (W - 1) / (cw - 1) : 0;
     for (int y = 0; y < ch; ++y) {
       const float in_y = (ch > 1) ? y1 * (H - 1) + y * height_scale : 0.5 * (y1 + y2) * (H - 1);
-      if (in_y < 0 || in_y > H - 1) continue;
+      if (!(in_y >= 0 && in_y <= H - 1)) continue;
       const int top_y_index = (int)floorf(in_y);
       const int bottom_y_index = (int)ceilf(in_y);
       const float y_lerp = in_y - top_y_index;
       for (int x = 0; x < cw; ++x) {
         const float in_x = (cw > 1) ? x1 * (W - 1) + x * width_scale : 0.5 * (x1 + x2) * (W - 1);
-        if (in_x < 0 || in_x > W - 1) continue;
+        if (!(in_x >= 0 && in_x <= W - 1)) continue;
         const int left_x_index = (int)floorf(in_x);
         const int right_x_index = (int)ceilf(in_x);
         const float x_lerp = in_x - left_x_index;

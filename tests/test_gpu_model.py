@@ -145,3 +145,49 @@ def test_faster_rcnn_batch_shapes_and_determinism(dev):
     assert torch.all(a["boxes"][~v] == 0) and torch.all(a["scores"][~v] == 0)
     # boxes clipped to each image's true shape (fast_rcnn.py:111-116)
     assert torch.all(a["boxes"][0][..., 2] <= 320) and torch.all(a["boxes"][1][..., 3] <= 470)
+
+
+@pytest.mark.parametrize("fmt", ["conventional", "fixed"])
+def test_mask_rcnn_pasted_masks_match_oracle_paste(dev, fmt):
+    """SEGMENTATION_OUTPUT.FORMAT conventional / fixed (rcnn.py:124-133 ->
+    detector_postprocess): the model's uint8 canvas masks equal the oracle's
+    paste (crop_and_resize of the reverse box + tf.greater) of the same run's
+    raw 28x28 masks, boxes and validity, bit for bit."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    model = _model(dev)
+    rng = np.random.default_rng(11)
+    img = rng.uniform(0, 255, size=(2, 256, 320, 3)).astype(np.float32)
+    shapes = np.array([[256, 320], [224, 300]], np.int32)
+    batch = {"image": torch.from_numpy(img).to(dev), "image_shape": torch.from_numpy(shapes).to(dev)}
+    # given detections (inference(detected_instances=...), rcnn.py:118-122):
+    # a random-init box regressor sends its own detections to degenerate
+    # border boxes, which paste as empty masks
+    from detectron2_tensorflow_amd.structures import BoxList
+    N, D = 2, 40
+    cy, cx = rng.uniform(0, 224, (N, D)), rng.uniform(0, 300, (N, D))
+    h, w = rng.uniform(4, 150, (N, D)), rng.uniform(4, 150, (N, D))
+    bx = np.stack([cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2], -1).astype(np.float32)
+    det = BoxList(torch.from_numpy(bx).to(dev))
+    det.add_field("pred_classes", torch.from_numpy(rng.integers(0, 80, (N, D))).to(dev))
+    det.add_field("scores", torch.rand(N, D, device=dev))
+    det.add_field("is_valid", torch.from_numpy(rng.random((N, D)) < 0.9).to(dev))
+    with torch.no_grad():
+        raw = model.inference(batch, detected_instances=det)["instances"]
+        model.segmentation_output_format = fmt
+        pasted = model.inference(batch, detected_instances=det)["instances"]
+    model.segmentation_output_format = "raw"
+    R = model.segmentation_output_resolution
+    H, W = (R, R) if fmt == "fixed" else (256, 320)
+    masks = pasted["masks"].cpu().numpy()
+    assert masks.shape == (N, D, H, W) and masks.dtype == np.uint8
+    for n in range(N):
+        yx = None
+        if fmt == "fixed":
+            yx = (np.array([R, R], np.float64) / shapes[n].astype(np.float64)).astype(np.float32)
+            yx = np.repeat(yx[None], D, 0)
+        want = oracle.paste_masks(raw["masks"][n].cpu().numpy(), raw["boxes"][n].cpu().numpy(),
+                                  (H, W), valid=raw["is_valid"][n].cpu().numpy(), yx_scale=yx)
+        np.testing.assert_array_equal(masks[n], want)
+    assert masks.sum() > 0

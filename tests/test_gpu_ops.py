@@ -694,3 +694,25 @@ def test_fold_frozen_bn_forward_backward(dev, with_bias):
             continue
         np.testing.assert_allclose(a.grad.cpu().double().numpy(), r.grad.numpy(), rtol=1e-4,
                                    atol=1e-3, err_msg=name)
+
+
+@pytest.mark.parametrize("H,W,fixed", [(96, 128, False), (75, 101, False), (64, 64, True)])
+def test_paste_masks_bit_exact(dev, H, W, fixed):
+    """d2mi_paste_masks vs the oracle (crop_and_resize of the reverse box +
+    tf.greater): uint8 masks bit-exact, including boxes hanging off the canvas,
+    sub-pixel boxes, invalid slots and the 'fixed' per-box scale."""
+    rng = np.random.default_rng(H * W)
+    D = 37
+    m = rng.random((D, 28, 28)).astype(F32)
+    y1 = rng.uniform(-20, H, D)
+    x1 = rng.uniform(-20, W, D)
+    b = np.stack([y1, x1, y1 + rng.uniform(0.3, H, D), x1 + rng.uniform(0.3, W, D)], 1).astype(F32)
+    valid = rng.random(D) < 0.8
+    yx = rng.uniform(0.5, 2.0, (D, 2)).astype(F32) if fixed else None
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    got = ops().paste_masks(t(m), t(b), (H, W), valid=t(valid), yx_scale=t(yx))
+    want = oracle.paste_masks(m, b, (H, W), valid=valid, yx_scale=yx)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    assert want.sum() > 0
+    empty = ops().paste_masks(t(m[:0]), t(b[:0]), (H, W))
+    assert tuple(empty.shape) == (0, H, W)

@@ -139,3 +139,27 @@ def test_matrix_nms_kat():
     out = oracle.matrix_nms(m, np.array([0, 0, 0]), np.array([0.9, 0.8, 0.7], F32))
     iou = 4 / 6
     np.testing.assert_allclose(out, [0.9, 0.8 * math.exp(-2 * iou ** 2), 0.7], rtol=1e-6)
+
+
+def test_paste_masks_kat_in_range_region():
+    """reframe_box_masks_to_image_masks (mask_ops.py:35-56): with a constant box
+    mask above the threshold, a canvas pixel is set iff crop_and_resize samples
+    inside the mask, i.e. 0 <= (mh-1) * (y/(H-1) - y1/H) / ((y2-y1)/H) <= mh-1
+    (note the canvas is normalised by H but sampled on H-1 steps), same for x."""
+    H, W, mh = 60, 80, 28
+    box = np.array([[12.0, 20.0, 40.0, 61.0]], np.float32)
+    out = oracle.paste_masks(np.full((1, mh, mh), 0.9, np.float32), box, (H, W))[0]
+
+    def inside(n, c1, c2):
+        t = (mh - 1) * (np.arange(n) / (n - 1) - c1 / n) / ((c2 - c1) / n)
+        return (t >= 0) & (t <= mh - 1), np.minimum(np.abs(t), np.abs(t - (mh - 1)))
+
+    iy, dy = inside(H, 12.0, 40.0)
+    ix, dx = inside(W, 20.0, 61.0)
+    want = (iy[:, None] & ix[None, :]).astype(np.uint8)
+    safe = (dy[:, None] > 1e-3) & (dx[None, :] > 1e-3)
+    np.testing.assert_array_equal(out[safe], want[safe])
+    # invalid rows are zero; threshold is strict
+    z = oracle.paste_masks(np.full((2, mh, mh), 0.5, np.float32), np.repeat(box, 2, 0), (H, W),
+                           valid=np.array([True, False]))
+    assert z.sum() == 0

@@ -168,6 +168,22 @@ def bench_roi(dev, iters):
     return out
 
 
+def bench_paste(dev, iters):
+    """Mask pasting at Mask R-CNN inference size: 2 images x 100 detections,
+    28x28 masks onto the 800x1344 padded canvas ("conventional").  HBM-write
+    bound: algorithmic bytes = the uint8 canvas + the f32 box masks read."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    D, H, W = 200, 800, 1344
+    m = torch.rand(D, 28, 28, generator=g).to(dev)
+    c = torch.rand(D, 2, generator=g) * torch.tensor([800.0, 1333.0])
+    sz = torch.exp(torch.rand(D, 2, generator=g) * math.log(25) + math.log(16))
+    boxes = torch.cat([c - sz / 2, c + sz / 2], 1)[:, [0, 1, 2, 3]].to(dev)
+    ms = timeit(lambda: ops.paste_masks(m, boxes, (H, W)), iters)
+    byts = D * H * W + m.numel() * 4
+    return [{"kernel": "paste_masks", "detections": D, "canvas": [H, W], "us": round(ms * 1e3, 1),
+             "alg_GBps": round(byts / ms / 1e6, 1)}]
+
+
 def bench_nms(dev, iters):
     g = torch.Generator(device="cpu").manual_seed(1)
     out = []
@@ -197,7 +213,7 @@ def bench_topk(dev, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="conv,wgrad,roi,nms,topk")
+    ap.add_argument("--only", default="conv,wgrad,roi,paste,nms,topk")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shape", default=None, help="substring filter on conv shape names")
     ap.add_argument("--no-miopen", action="store_true")
@@ -207,7 +223,8 @@ def main():
     NO_MIOPEN = a.no_miopen
     _C.load()
     dev = torch.device("cuda:0")
-    fns = {"conv": bench_conv, "wgrad": bench_wgrad, "roi": bench_roi, "nms": bench_nms,
+    fns = {"conv": bench_conv, "wgrad": bench_wgrad, "roi": bench_roi, "paste": bench_paste,
+           "nms": bench_nms,
            "topk": bench_topk}
     for name in a.only.split(","):
         for row in fns[name](dev, a.iters):
