@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--cpu-images", type=int, default=2, help="images per CPU iteration (<= batch)")
     p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations")
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--timed-step-sample", type=int, default=-1,
+                   help="timed step whose kernel launches carry HIP events (-1: the last)")
     p.add_argument("--mode", default="train", choices=["train", "infer"])
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
     return p.parse_args()
@@ -250,10 +252,17 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
-        KernelTimer.reset(enabled=not args.no_kernel_timing)
+        # Per-launch HIP events (the live roofline) are recorded during ONE of
+        # the timed steps (--timed-step-sample, default the last): every step
+        # launches the same kernels, and events around all ~300 hot launches
+        # of every step would add ~2 ms of host time per step to the clock.
+        KernelTimer.reset(enabled=False)
+        sample = args.steps - 1 if args.timed_step_sample < 0 else min(args.timed_step_sample,
+                                                                        args.steps - 1)
         torch.cuda.nvtx.range_push("timed_region")  # roctx: tools/prof_window.py
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for i in range(args.steps):
+            KernelTimer.enabled = (i == sample) and not args.no_kernel_timing
             out = step()
         torch.cuda.synchronize()
         if world > 1:
@@ -307,7 +316,9 @@ def main():
                                         f"{args.width}x{args.height}",
                             "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                             "parallelism": (f"dp{world}" if args.mode == "train" else f"replicas{world}"),
-                            "mode": args.mode}, **extra),
+                            "mode": args.mode,
+                            "kernel_events_on_timed_step": None if args.no_kernel_timing
+                            else f"{sample + 1}/{args.steps}"}, **extra),
             # the dominant hot-path kernel: the split-product conv (else f32)
             "roofline": kernels.get("conv2d_split", kernels.get("conv2d_mfma")),
             **({"replicas_in_sync": in_sync} if in_sync is not None else {}),

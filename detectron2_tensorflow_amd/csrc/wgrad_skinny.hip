@@ -1,0 +1,127 @@
+// Weight + bias gradient of a 1x1 conv with few output channels (the RPN
+// head's fused objectness + anchor-delta 1x1, rpn.py:31-96: Cout = A + 4A =
+// 15 -> 16 with a zero pad column) over every pixel of a pyramid level:
+//   gw[ci][co] = sum_p x[p][ci] * g[p][co],   gb[co] = sum_p g[p][co]
+// i.e. X^T G with a short output (Cin x Cout <= 256 x 16) and a reduction
+// over up to ~135k pixels.  A GEMM tiling leaves 5/6 of every MFMA tile
+// empty here (hipBLASLt took 0.5 ms for Cout = 3 on p2); this is an HBM-bound
+// streaming pass instead: each 256-thread workgroup takes a chunk of kChunk
+// pixels, one input channel per thread (one coalesced 1 KiB row read per
+// pixel for Cin = 256), the chunk's G rows staged in LDS and broadcast, 16
+// f32 accumulators per thread; per-chunk partials then reduced in chunk
+// order by a second kernel (deterministic, no atomics).
+#include "common.h"
+#include "internal.h"
+
+namespace d2mi {
+namespace {
+
+constexpr int kChunk = 128;    // pixels per workgroup
+constexpr int kMaxCout = 16;
+
+__global__ __launch_bounds__(256) void wgrad_skinny_partial_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, int P, int Cin, int Cout,
+    float* __restrict__ partial /* [chunks][Cin + 1][Cout] */) {
+  __shared__ float gs[kChunk * kMaxCout];
+  const int chunk = blockIdx.x;
+  const int p0 = chunk * kChunk;
+  const int np = min(kChunk, P - p0);
+  // LDS rows padded to kMaxCout (zeros): compile-time strides, so the
+  // broadcast reads below are 16-B LDS loads
+  for (int i = threadIdx.x; i < kChunk * kMaxCout; i += blockDim.x) {
+    const int p = i / kMaxCout, j = i - p * kMaxCout;
+    gs[i] = (p < np && j < Cout) ? g[(size_t)(p0 + p) * Cout + j] : 0.f;
+  }
+  __syncthreads();
+  float* out = partial + (size_t)chunk * (Cin + 1) * Cout;
+  for (int c = threadIdx.x; c < Cin; c += blockDim.x) {
+    float acc[kMaxCout];
+#pragma unroll
+    for (int j = 0; j < kMaxCout; ++j) acc[j] = 0.f;
+    const float* xp = x + (size_t)p0 * Cin + c;
+    int p = 0;
+    for (; p + 4 <= np; p += 4) {  // 4 row loads in flight
+      float xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = xp[(size_t)(p + u) * Cin];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < kMaxCout; ++j) acc[j] = fmaf(xv[u], gs[(p + u) * kMaxCout + j], acc[j]);
+    }
+    for (; p < np; ++p) {
+      const float xv = xp[(size_t)p * Cin];
+#pragma unroll
+      for (int j = 0; j < kMaxCout; ++j) acc[j] = fmaf(xv, gs[p * kMaxCout + j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxCout; ++j)
+      if (j < Cout) out[(size_t)c * Cout + j] = acc[j];
+  }
+  if (threadIdx.x < Cout) {  // bias row: column sums of the chunk's G
+    float s = 0.f;
+    for (int p = 0; p < np; ++p) s += gs[p * kMaxCout + threadIdx.x];
+    out[(size_t)Cin * Cout + threadIdx.x] = s;
+  }
+}
+
+// Sum the chunk partials (gw rows, then the gb row) in a fixed order: 16
+// outputs per workgroup, 16 chunk segments per output summed in chunk order
+// by 16 threads, then the 16 segment sums in segment order (one thread per
+// chunk range left the p2 reduction latency-bound at ~0.3 ms).
+constexpr int kRedOut = 16, kRedSeg = 16;
+
+__global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
+    const float* __restrict__ partial, int chunks, int Cin, int Cout, float* __restrict__ gw,
+    float* __restrict__ gb) {
+  __shared__ float red[kRedSeg][kRedOut];
+  const int n = (Cin + 1) * Cout;
+  const int ol = threadIdx.x % kRedOut, sg = threadIdx.x / kRedOut;
+  const int o = blockIdx.x * kRedOut + ol;
+  const int per = (chunks + kRedSeg - 1) / kRedSeg;
+  const int k0 = sg * per, k1 = min(chunks, k0 + per);
+  float s = 0.f;
+  if (o < n)
+    for (int k = k0; k < k1; ++k) s += partial[(size_t)k * n + o];
+  red[sg][ol] = s;
+  __syncthreads();
+  if (sg == 0 && o < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < kRedSeg; ++j) t += red[j][ol];
+    if (o < Cin * Cout) gw[o] = t;
+    else if (gb) gb[o - Cin * Cout] = t;
+  }
+}
+
+}  // namespace
+}  // namespace d2mi
+
+using namespace d2mi;
+
+extern "C" size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout) {
+  if (P <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  const size_t chunks = ((size_t)P + kChunk - 1) / kChunk;
+  return chunks * (size_t)(Cin + 1) * Cout * sizeof(float);
+}
+
+extern "C" int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout,
+                                 float* gw, float* gb, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  D2MI_REQUIRE(P > 0 && Cin > 0 && Cout > 0 && Cout <= kMaxCout,
+               "wgrad_skinny: P=%d Cin=%d Cout=%d (Cout must be 1..%d)", P, Cin, Cout, kMaxCout);
+  const size_t need = d2mi_wgrad_skinny_workspace_size(P, Cin, Cout);
+  D2MI_REQUIRE(workspace && workspace_bytes >= need, "wgrad_skinny workspace too small: %zu < %zu",
+               workspace_bytes, need);
+  const int chunks = (P + kChunk - 1) / kChunk;
+  hipStream_t st = as_stream(stream);
+  float* partial = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(wgrad_skinny_partial_kernel, dim3(chunks), dim3(256), 0, st, x, g, P, Cin,
+                     Cout, partial);
+  D2MI_LAUNCH_CHECK();
+  const int n = (Cin + 1) * Cout;
+  hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((n + kRedOut - 1) / kRedOut), dim3(256), 0,
+                     st, partial, chunks, Cin, Cout, gw, gb);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}

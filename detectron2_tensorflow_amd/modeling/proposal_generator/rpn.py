@@ -47,30 +47,74 @@ class StandardRPNHead(Layer):
         self._fused_key = None
 
     def _fused_1x1(self):
+        """The objectness (A) and anchor-delta (4A) 1x1 convs as ONE conv of
+        A + 4A outputs, zero-padded to a multiple of 4 (15 -> 16): weights
+        HWIO [1, 1, C, 16], their MFMA packing, and the bias [16]."""
         wo, wd = self.objectness_logits.weights, self.anchor_deltas.weights
-        key = (wo._version, wd._version, wo.data_ptr(), wd.data_ptr())
+        bo, bd = self.objectness_logits.bias, self.anchor_deltas.bias
+        key = (wo._version, wd._version, bo._version, bd._version, wo.data_ptr(), wd.data_ptr())
         if self._fused is None or self._fused_key != key:
-            w = torch.cat([wo.detach(), wd.detach()], dim=3)
-            b = torch.cat([self.objectness_logits.bias.detach(), self.anchor_deltas.bias.detach()])
-            self._fused = (ops.pack_conv_weights(w), b.contiguous())
+            n = wo.shape[3] + wd.shape[3]
+            pad = (-n) % 4
+            w = torch.cat([wo.detach(), wd.detach(), wo.new_zeros(*wo.shape[:3], pad)], dim=3)
+            b = torch.cat([bo.detach(), bd.detach(), bo.new_zeros(pad)])
+            self._fused = (w.contiguous(), ops.pack_conv_weights(w), b.contiguous())
             self._fused_key = key
         return self._fused
 
     def call(self, features):
         rpn_features, logits, deltas = [], [], []
-        fuse = (not torch.is_grad_enabled()) and features[0].is_cuda
+        fuse = features[0].is_cuda
         for x in features:
             share = self.conv(x)
             rpn_features.append(share)
             if fuse:
-                wp, b = self._fused_1x1()
-                y = ops.conv2d_nhwc(share, wp, b)
-                logits.append(y[..., : self.A].contiguous())
-                deltas.append(y[..., self.A:].contiguous())
+                w16, wp, b16 = self._fused_1x1()
+                lg, dl = _RPNHead1x1Fn.apply(share, self.objectness_logits.weights,
+                                             self.objectness_logits.bias,
+                                             self.anchor_deltas.weights, self.anchor_deltas.bias,
+                                             w16, wp, b16)
+                logits.append(lg)
+                deltas.append(dl)
             else:
                 logits.append(self.objectness_logits(share))
                 deltas.append(self.anchor_deltas(share))
         return rpn_features, logits, deltas
+
+
+class _RPNHead1x1Fn(torch.autograd.Function):
+    """Both RPN-head 1x1 convs (rpn.py:83-96) as one 16-wide conv on the MFMA
+    kernel.  Backward: the two output gradients are concatenated (+ the zero
+    pad column) into one [.., 16] gradient; the input gradient is ONE dgrad
+    conv (instead of a dgrad per head + their sum), the weight and bias
+    gradients one skinny X^T G pass (d2mi_wgrad_skinny) sliced per head."""
+
+    @staticmethod
+    def forward(ctx, share, wo, bo, wd, bd, w16, wp, b16):
+        y = ops.conv2d_nhwc(share, wp, b16)
+        A, D = wo.shape[3], wd.shape[3]
+        ctx.save_for_backward(share, w16)
+        ctx.dims = (A, D, y.shape[-1])
+        return y[..., :A].contiguous(), y[..., A:A + D].contiguous()
+
+    @staticmethod
+    def backward(ctx, g_logits, g_deltas):
+        share, w16 = ctx.saved_tensors
+        A, D, C16 = ctx.dims
+        lead = share.shape[:-1]
+        parts = [g_logits if g_logits is not None else share.new_zeros(*lead, A),
+                 g_deltas if g_deltas is not None else share.new_zeros(*lead, D)]
+        if C16 > A + D:
+            parts.append(share.new_zeros(*lead, C16 - A - D))
+        g16 = torch.cat(parts, dim=-1)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            # 1x1 stride-1 dgrad: the forward weights' HWIO [1, 1, C, 16] is
+            # the packed layout of the transposed conv
+            gx = ops.conv2d_nhwc(g16, w16, None, 1, (0, 0))
+        gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)
+        return (gx, gw[..., :A].contiguous(), gb[:A], gw[..., A:A + D].contiguous(), gb[A:A + D],
+                None, None, None)
 
 
 @PROPOSAL_GENERATOR_REGISTRY.register()

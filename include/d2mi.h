@@ -306,6 +306,17 @@ int d2mi_paste_masks(const float* box_masks, const float* boxes, const float* yx
                      const uint8_t* valid, int D, int mask_h, int mask_w, int out_h, int out_w,
                      float threshold, uint8_t* out, void* stream);
 
+/* ------------------------------------------------ skinny 1x1 weight gradient
+ * gw[Cin][Cout] = X^T G and gb[Cout] = column sums of G over P pixels, for
+ * Cout <= 16 (the RPN head's objectness + anchor-delta 1x1 convs, fused:
+ * lib/modeling/proposal_generator/rpn.py:83-96, whose TF gradient is
+ * Conv2DBackpropFilter + BiasAddGrad).  x [P, Cin], g [P, Cout] f32
+ * contiguous; gb nullable.  Fixed-order reduction (deterministic); workspace
+ * from d2mi_wgrad_skinny_workspace_size. */
+size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout);
+int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
+                      float* gb, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -156,3 +156,46 @@ def test_mask_head_on_foreground_rows_matches_fixed_layout(dev):
     for n, g in res[False][1].items():
         # summation order differs with the row count (split-K / wgrad partitions)
         torch.testing.assert_close(res[True][1][n], g, rtol=1e-4, atol=1e-4 * g.abs().max().item())
+
+
+def test_rpn_head_fused_1x1_matches_separate_convs(dev):
+    """The fused 16-wide RPN-head 1x1 (one MFMA conv forward, one dgrad conv +
+    one skinny X^T G pass backward) gives the separate objectness / delta
+    convs' outputs and gradients (f64 reference of the same math)."""
+    from detectron2_tensorflow_amd.layers import ShapeSpec
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
+    cfg = _cfg(True)
+    torch.manual_seed(0)
+    head = StandardRPNHead(cfg, [ShapeSpec(channels=256, stride=s) for s in (4, 8, 16, 32, 64)]).to(dev)
+    with torch.no_grad():  # non-trivial biases / weights
+        for c in (head.objectness_logits, head.anchor_deltas):
+            c.weights.normal_(0, 0.05)
+            c.bias.normal_(0, 0.1)
+    xs = [torch.randn(2, h, w, 256, device=dev) for h, w in ((40, 52), (20, 26))]
+    for x in xs:
+        x.requires_grad_(True)
+    _, logits, deltas = head(xs)
+    gl = [torch.randn_like(t) for t in logits]
+    gd = [torch.randn_like(t) for t in deltas]
+    torch.autograd.backward(logits + deltas, gl + gd)
+    wo, bo = head.objectness_logits.weights, head.objectness_logits.bias
+    wd, bd = head.anchor_deltas.weights, head.anchor_deltas.bias
+    # float64 reference of the same graph
+    share = [torch.relu(torch.nn.functional.conv2d(
+        x.detach().double().permute(0, 3, 1, 2), head.conv.weights.detach().double().permute(3, 2, 0, 1),
+        head.conv.bias.detach().double(), padding=1)).permute(0, 2, 3, 1) for x in xs]
+    gwo = sum(s.reshape(-1, 256).t() @ g.double().reshape(-1, g.shape[-1]) for s, g in zip(share, gl))
+    gwd = sum(s.reshape(-1, 256).t() @ g.double().reshape(-1, g.shape[-1]) for s, g in zip(share, gd))
+    for s, lg, dl in zip(share, logits, deltas):
+        torch.testing.assert_close(lg.double(), s @ wo.detach().double()[0, 0] + bo.detach().double(),
+                                   rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(dl.double(), s @ wd.detach().double()[0, 0] + bd.detach().double(),
+                                   rtol=1e-4, atol=1e-4)
+    tol = lambda r: dict(rtol=1e-4, atol=1e-5 * r.abs().max().item())
+    torch.testing.assert_close(wo.grad[0, 0].double(), gwo, **tol(gwo))
+    torch.testing.assert_close(wd.grad[0, 0].double(), gwd, **tol(gwd))
+    gbo = sum(g.double().reshape(-1, g.shape[-1]).sum(0) for g in gl)
+    gbd = sum(g.double().reshape(-1, g.shape[-1]).sum(0) for g in gd)
+    torch.testing.assert_close(bo.grad.double(), gbo, **tol(gbo))
+    torch.testing.assert_close(bd.grad.double(), gbd, **tol(gbd))
+    assert all(torch.isfinite(x.grad).all() for x in xs)
