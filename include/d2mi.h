@@ -317,6 +317,22 @@ size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout);
 int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
                       float* gb, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------ Momentum-SGD step
+ * Replaces the update of lib/engine/trainer.py:116-139 for every trainable
+ * tensor in two launches: g' = g + wd * w (slim.l2_regularizer gradient,
+ * lib/solver/regularizer.py:6-24), per-tensor tf.clip_by_norm(g', clip_norm)
+ * (slim.learning.clip_gradient_norms; clip_norm <= 0 disables it), then
+ * ApplyMomentum: accum = accum * momentum + g''; w -= lr * accum.
+ * tensor_table / chunk_table: device arrays of the records whose sizes
+ * d2mi_sgd_table_sizes reports (tensor: {float* w; const float* g (nullable:
+ * zero gradient); float* accum; int64 numel; float wd; int32 first_chunk,
+ * num_chunks, pad}; chunk: {int32 tensor, pad; int64 begin, end}, chunks of at
+ * most chunk_elems elements, a tensor's chunks consecutive).  partial: device
+ * float [num_chunks] scratch.  Per-tensor norms are fixed-order sums. */
+int d2mi_sgd_table_sizes(int* tensor_bytes, int* chunk_bytes, int* chunk_elems);
+int d2mi_momentum_sgd(const void* tensor_table, const void* chunk_table, int num_chunks,
+                      float* partial, float clip_norm, float momentum, float lr, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
