@@ -643,6 +643,21 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int taps, int C
   }
 }
 
+// Tiled HWIO -> [tap][co][ci] (Cin % 64 == 0): 64 x 64 tiles through LDS, reads
+// along co and writes along ci both coalesced.
+__global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __restrict__ w,
+                                                                 int Cin, int Cout,
+                                                                 float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = wv; i < 64; i += 4)
+    tile[i][lane] = co0 + lane < Cout ? w[((size_t)tap * Cin + ci0 + i) * Cout + co0 + lane] : 0.f;
+  __syncthreads();
+  for (int j = wv; j < 64; j += 4)
+    if (co0 + j < Cout) out[((size_t)tap * Cout + co0 + j) * Cin + ci0 + lane] = tile[lane][j];
+}
+
 struct Plan {
   int cfg;  // 0: 128x128, 1: 128x64, 2: 128x32
   int BM, BN, splits, kt_per_split, nk, ntiles;
@@ -674,6 +689,12 @@ using namespace d2mi;
 extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout,
                                       float* w_packed, void* stream) {
   D2MI_REQUIRE(KH > 0 && KW > 0 && Cin > 0 && Cout > 0, "bad conv weight shape");
+  if (Cin % 64 == 0) {
+    hipLaunchKernelGGL(pack_weights_tiled_kernel, dim3((Cout + 63) / 64, Cin / 64, KH * KW),
+                       dim3(256), 0, as_stream(stream), w_hwio, Cin, Cout, w_packed);
+    D2MI_LAUNCH_CHECK();
+    return 0;
+  }
   const int64_t total = (int64_t)KH * KW * Cin * Cout;
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(grid), dim3(256), 0, as_stream(stream), w_hwio,

@@ -52,6 +52,45 @@ __global__ void fold_bn_kernel(const float* __restrict__ w, const float* __restr
   }
 }
 
+// Tiled variant (Cin % 64 == 0, i.e. every ResNet conv): a 64 (ci) x 64 (co)
+// tile of one tap per workgroup; w / w_eff rows are read and written along
+// co, the packed [tap][co][ci] copy is written along ci from an LDS transpose
+// -- both coalesced (the per-element version above writes the packed copy
+// with a stride of Cin between lanes).
+__global__ __launch_bounds__(256) void fold_bn_tiled_kernel(
+    const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ var,
+    float eps, int Cout, int Cin, float* __restrict__ w_eff, float* __restrict__ w_packed,
+    float* __restrict__ b_eff) {
+  __shared__ float tile[64][65];
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int co = co0 + lane;
+  const bool live = co < Cout;
+  float scale = 0.f;
+  if (live) {
+    const float inv = bn_inv(var, eps, co);
+    scale = gamma ? inv * gamma[co] : inv;
+    if (blockIdx.y == 0 && tap == 0 && wv == 0) {
+      float shift = -mean[co] * scale;
+      if (beta) shift = shift + beta[co];
+      b_eff[co] = bias ? bias[co] * scale + shift : shift;
+    }
+  }
+  for (int i = wv; i < 64; i += 4) {  // rows ci0 + i of this tap, lanes over co
+    const size_t r = (size_t)tap * Cin + ci0 + i;
+    const float v = live ? w[r * Cout + co] * scale : 0.f;
+    if (w_eff && live) w_eff[r * Cout + co] = v;
+    tile[i][lane] = v;
+  }
+  if (!w_packed) return;
+  __syncthreads();
+  for (int j = wv; j < 64; j += 4) {  // packed rows co0 + j, lanes over ci
+    if (co0 + j < Cout)
+      w_packed[((size_t)tap * Cout + co0 + j) * Cin + ci0 + lane] = tile[lane][j];
+  }
+}
+
 // partial[chunk][0][co] = sum gw_eff * w over the chunk's rows; gw = gw_eff * scale.
 __global__ void fold_bn_bwd_kernel(const float* __restrict__ gw_eff, const float* __restrict__ w,
                                    const float* __restrict__ gamma, const float* __restrict__ var,
@@ -117,6 +156,13 @@ extern "C" int d2mi_fold_frozen_bn(const float* w_hwio, const float* bias, const
   D2MI_REQUIRE(KH > 0 && KW > 0 && Cin > 0 && Cout > 0, "bad weight shape");
   D2MI_REQUIRE(w_hwio && mean && var && b_eff, "w, mean, var and b_eff are required");
   const int rows = KH * KW * Cin;
+  if (Cin % 64 == 0) {
+    dim3 grid((Cout + 63) / 64, Cin / 64, KH * KW);
+    hipLaunchKernelGGL(fold_bn_tiled_kernel, grid, dim3(256), 0, as_stream(stream), w_hwio, bias,
+                       gamma, beta, mean, var, eps, Cout, Cin, w_eff, w_packed, b_eff);
+    D2MI_LAUNCH_CHECK();
+    return 0;
+  }
   const int gy = std::min(64, std::max(1, rows / 64));
   dim3 grid((Cout + 63) / 64, gy);
   hipLaunchKernelGGL(fold_bn_kernel, grid, dim3(256), 0, as_stream(stream), w_hwio, bias, gamma,

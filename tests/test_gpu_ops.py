@@ -716,3 +716,26 @@ def test_paste_masks_bit_exact(dev, H, W, fixed):
     assert want.sum() > 0
     empty = ops().paste_masks(t(m[:0]), t(b[:0]), (H, W))
     assert tuple(empty.shape) == (0, H, W)
+
+
+@pytest.mark.parametrize("shape", [(3, 3, 64, 64), (1, 1, 256, 16), (1, 1, 1024, 80),
+                                   (3, 3, 60, 36), (1, 1, 2048, 512), (7, 7, 3, 64)])
+def test_weight_pack_and_frozen_bn_fold_layouts(dev, shape):
+    """pack_conv_weights: HWIO -> [KH, KW, Cout, Cin] bit-exact (tiled path for
+    Cin % 64 == 0, element path otherwise); the FrozenBN fold writes
+    w_eff = w * gamma / sqrt(var + eps) and its packed copy consistently."""
+    g = torch.Generator().manual_seed(sum(shape))
+    w = torch.randn(shape, generator=g).to(dev)
+    np.testing.assert_array_equal(ops().pack_conv_weights(w).cpu().numpy(),
+                                  w.permute(0, 1, 3, 2).cpu().numpy())
+    Cout = shape[3]
+    gamma, beta = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g)
+    mean, var = torch.randn(Cout, generator=g), torch.rand(Cout, generator=g) + 0.1
+    t = lambda a: a.to(dev)
+    with torch.no_grad():
+        w_eff, b_eff, packed = ops().fold_frozen_bn(w, None, t(gamma), t(beta), t(mean), t(var),
+                                                    1e-5, True)
+    scale = gamma / torch.sqrt(var + 1e-5)
+    torch.testing.assert_close(w_eff.cpu(), w.cpu() * scale, rtol=1e-6, atol=0)
+    torch.testing.assert_close(b_eff.cpu(), beta - mean * scale, rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(packed.cpu().numpy(), w_eff.permute(0, 1, 3, 2).cpu().numpy())
