@@ -94,10 +94,60 @@ __global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
   }
 }
 
+// Column sums of a row-major [rows, cols] matrix (the bias gradient of a conv
+// whose weight gradient ran as a library GEMM): workgroup (col chunk of 256,
+// row chunk of kColRows) sums its rows in order -> partial[row chunk][col];
+// then the row chunks are summed in order (wgrad_skinny_reduce_kernel's
+// two-level scheme with Cin = 0).
+constexpr int kColRows = 32;
+
+__global__ __launch_bounds__(256) void column_sum_partial_kernel(const float* __restrict__ x,
+                                                                 long long rows, int cols,
+                                                                 float* __restrict__ partial) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const long long r0 = (long long)blockIdx.y * kColRows;
+  const long long r1 = r0 + kColRows < rows ? r0 + kColRows : rows;
+  if (c >= cols) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains, fixed order
+  long long r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    s0 += x[(size_t)r * cols + c];
+    s1 += x[(size_t)(r + 1) * cols + c];
+    s2 += x[(size_t)(r + 2) * cols + c];
+    s3 += x[(size_t)(r + 3) * cols + c];
+  }
+  for (; r < r1; ++r) s0 += x[(size_t)r * cols + c];
+  partial[(size_t)blockIdx.y * cols + c] = (s0 + s1) + (s2 + s3);
+}
+
 }  // namespace
 }  // namespace d2mi
 
 using namespace d2mi;
+
+extern "C" size_t d2mi_column_sum_workspace_size(long long rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)((rows + kColRows - 1) / kColRows) * cols * sizeof(float);
+}
+
+extern "C" int d2mi_column_sum(const float* x, long long rows, int cols, float* out,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(rows > 0 && cols > 0, "column_sum: rows=%lld cols=%d", rows, cols);
+  const size_t need = d2mi_column_sum_workspace_size(rows, cols);
+  D2MI_REQUIRE(workspace && workspace_bytes >= need, "column_sum workspace too small");
+  const long long chunks = (rows + kColRows - 1) / kColRows;
+  D2MI_REQUIRE(chunks < 65536, "column_sum: too many rows");
+  hipStream_t st = as_stream(stream);
+  float* partial = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(column_sum_partial_kernel, dim3((cols + 255) / 256, (unsigned)chunks),
+                     dim3(256), 0, st, x, rows, cols, partial);
+  D2MI_LAUNCH_CHECK();
+  // reduce: rows of the partial = chunks, "Cin" = 0, Cout = cols -> gb = out
+  hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((cols + kRedOut - 1) / kRedOut), dim3(256),
+                     0, st, partial, (int)chunks, 0, cols, nullptr, out);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout) {
   if (P <= 0 || Cin <= 0 || Cout <= 0) return 0;

@@ -128,7 +128,7 @@ class _ConvMFMAFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
-            gb = gy.sum((0, 1, 2))
+            gb = ops.column_sum(gy)
         return gx, gw, gb, None, None, None, None, gtd, gres, None
 
 

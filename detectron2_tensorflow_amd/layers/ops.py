@@ -610,3 +610,18 @@ def wgrad_skinny(x, g, with_bias=True):
     KernelTimer.stop(ev, "wgrad_skinny", 4 * P * (Cin + Cout))
     _C.check(rc, "d2mi_wgrad_skinny")
     return gw, gb
+
+
+def column_sum(x):
+    """Sum over every leading dim of x [..., C] -> [C] (fixed order)."""
+    x = _f32c(x)
+    _C.require_device(x)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    out = torch.empty((C,), dtype=torch.float32, device=x.device)
+    wsb = _C.lib().d2mi_column_sum_workspace_size(rows, C)
+    ws = _C.workspace(wsb, x.device)
+    rc = _C.lib().d2mi_column_sum(_C.ptr(x), rows, C, _C.ptr(out), _C.ptr(ws), wsb,
+                                  _C.stream_of(x.device))
+    _C.check(rc, "d2mi_column_sum")
+    return out

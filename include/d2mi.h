@@ -316,6 +316,13 @@ int d2mi_paste_masks(const float* box_masks, const float* boxes, const float* yx
 size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout);
 int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
                       float* gb, void* workspace, size_t workspace_bytes, void* stream);
+/* Column sums of a row-major [rows, cols] f32 matrix (a conv's bias gradient,
+ * TF BiasAddGrad, when its weight gradient runs as a library GEMM): out[cols],
+ * fixed-order two-level reduction; workspace from
+ * d2mi_column_sum_workspace_size. */
+size_t d2mi_column_sum_workspace_size(long long rows, int cols);
+int d2mi_column_sum(const float* x, long long rows, int cols, float* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------ Momentum-SGD step
  * Replaces the update of lib/engine/trainer.py:116-139 for every trainable

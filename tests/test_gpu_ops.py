@@ -739,3 +739,25 @@ def test_weight_pack_and_frozen_bn_fold_layouts(dev, shape):
     torch.testing.assert_close(w_eff.cpu(), w.cpu() * scale, rtol=1e-6, atol=0)
     torch.testing.assert_close(b_eff.cpu(), beta - mean * scale, rtol=1e-6, atol=1e-6)
     np.testing.assert_array_equal(packed.cpu().numpy(), w_eff.permute(0, 1, 3, 2).cpu().numpy())
+
+
+def test_column_sum_and_linear_mfma_match_float64(dev):
+    """Bias-gradient column sums (d2mi_column_sum) and the long-K Linear on the
+    split-product MFMA kernels (fwd, dgrad, wgrad + bias grad) vs float64."""
+    from detectron2_tensorflow_amd.layers import Linear
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 50, 84, 1024, generator=g)
+    got = ops().column_sum(x.to(dev)).cpu().double()
+    torch.testing.assert_close(got, x.double().sum((0, 1, 2)), rtol=1e-5, atol=1e-4)
+    lin = Linear(4352, 132).to(dev)
+    with torch.no_grad():
+        lin.bias.normal_()
+    xi = torch.randn(300, 4352, generator=g).to(dev).requires_grad_(True)
+    y = lin(xi)
+    gy = torch.randn(y.shape, generator=g).to(dev)
+    y.backward(gy)
+    xd, wd, gd = xi.detach().double(), lin.weights.detach().double(), gy.double()
+    torch.testing.assert_close(y.double(), xd @ wd + lin.bias.detach().double(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(xi.grad.double(), gd @ wd.t(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(lin.weights.grad.double(), xd.t() @ gd, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(lin.bias.grad.double(), gd.sum(0), rtol=1e-5, atol=1e-4)
