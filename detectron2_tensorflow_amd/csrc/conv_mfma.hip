@@ -60,7 +60,9 @@ __device__ __forceinline__ int swz(int row, int elem) {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
-enum EpiFlags { kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4 };
+// kFlipTaps: read weight tap (KH*KW - 1 - tap) -- the spatially flipped kernel
+// of a stride-1 dgrad, without materialising the flipped copy.
+enum EpiFlags { kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4, kFlipTaps = 8 };
 
 // Exact 3-term bf16 split of four floats (truncation; see the header).
 // Each output packs 4 bf16 (element order = float4 order).
@@ -291,7 +293,8 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   auto load_b = [&](int kt) {
     const int taps = a.KH * a.KW;
     const int chunk = kt / taps;
-    const int tap = kt - chunk * taps;
+    const int tap0 = kt - chunk * taps;
+    const int tap = (a.flags & kFlipTaps) ? taps - 1 - tap0 : tap0;
     const int cc = chunk * BK;
     const bool cok = cc + schunk < a.Cin;
 #pragma unroll
@@ -523,8 +526,9 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int co = n0 + r4 + 64 * p;
+      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
       const uint32_t off = (cok & (co < a.Cout) & (r4 + 64 * p < BN))
-                               ? (uint32_t)((tap * a.Cout + co) * a.Cin + cc + c8) * 2u
+                               ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + c8) * 2u
                                : kOOB;
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
@@ -829,9 +833,9 @@ extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const 
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
   D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_packed & 15) == 0,
                "x and w must be 16-byte aligned");
-  D2MI_REQUIRE((flags & ~7) == 0,
+  D2MI_REQUIRE((flags & ~15) == 0,
                "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
-               "MFMA products");
+               "MFMA products, bit3 flipped weight taps");
   // 32-bit buffer offsets: batches whose input is >= 2 GiB run as image chunks
   const int64_t img_bytes = (int64_t)H * W * Cin * sizeof(float);
   D2MI_REQUIRE(img_bytes < (1ll << 31), "one conv input image must be < 2 GiB");

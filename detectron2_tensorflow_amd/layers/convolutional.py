@@ -44,15 +44,17 @@ def same_pads(kernel_size, rate=1):
 def _dgrad(gy, w, x_shape, stride, pb, pe):
     """Input gradient.  Stride 1: a forward conv of gy with the spatially
     flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
-    of the transposed conv — on the MFMA kernel, padded (KH-1-pb, KH-1-pe).
+    of the transposed conv, flipped by the kernel's tap indexing (kFlipTaps) —
+    on the MFMA kernel, padded (KH-1-pb, KH-1-pe).
     1x1 stride s: the MFMA GEMM gy . W^T on the strided grid, scattered into
     zeros.  Anything else: torch.nn.grad (MIOpen)."""
     KH, KW, Cin, Cout = w.shape
     gy = gy.contiguous()
     if KH == KW and Cout % 4 == 0:
         if stride == 1 and max(pb, pe) <= KH - 1:
-            wd = w.detach().flip(0, 1).contiguous() if KH > 1 else w.detach().contiguous()
-            return ops.conv2d_nhwc(gy, wd, None, 1, (KH - 1 - pb, KH - 1 - pe))
+            # the flip is an index flip inside the kernel (no flipped copy)
+            return ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1,
+                                   (KH - 1 - pb, KH - 1 - pe), flip_taps=KH > 1)
         if KH == 1 and pb == 0 and pe == 0:
             g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)

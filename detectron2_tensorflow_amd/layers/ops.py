@@ -104,12 +104,15 @@ class _RoIAlignFn(torch.autograd.Function):
         ctx.params = params
         ctx.shapes = [f.shape for f in feats]
         ctx.save_for_backward(boxes, box_ind)
+        ctx.set_materialize_grads(False)  # level (non-differentiable): no zero grad
         if level is not None:
             ctx.mark_non_differentiable(level)
         return out, level
 
     @staticmethod
     def backward(ctx, grad_out, _grad_level):
+        if grad_out is None:
+            return (None,) * (3 + len(ctx.shapes))
         boxes, box_ind = ctx.saved_tensors
         (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
          _) = ctx.params
@@ -289,11 +292,13 @@ def _presplit_ok(x, Cin):
 
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
-                residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None):
+                residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None,
+                flip_taps=False):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
-    CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x."""
+    CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x.
+    flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j])."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -318,9 +323,9 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     # 128x64 / 128x32 tiles) gains nothing from the split products.
     if math_mode == "split" and Cout <= 64:
         math_mode = "f32"
-    presplit = math_mode == "split" and _presplit_ok(x, Cin) and (
+    presplit = math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps and (
         x_split is not None or (KH * KW > 1 and PRESPLIT_KXK))
-    flags = (1 if relu else 0) | (2 if relu_after_add else 0)
+    flags = (1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
     if math_mode == "split" and not presplit:
         flags |= 4
     wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
@@ -399,6 +404,8 @@ class _FoldFrozenBNFn(torch.autograd.Function):
                                           _C.stream_of(w.device))
         _C.check(rc, "d2mi_fold_frozen_bn")
         ctx.save_for_backward(w, bias, gamma, mean, var)
+        # packed never gets a gradient: no zero tensor materialised for it
+        ctx.set_materialize_grads(False)
         ctx.eps = float(eps)
         ctx.has = (bias is not None, gamma is not None, beta is not None)
         if packed is not None:

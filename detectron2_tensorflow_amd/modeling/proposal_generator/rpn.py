@@ -94,6 +94,7 @@ class _RPNHead1x1Fn(torch.autograd.Function):
         y = ops.conv2d_nhwc(share, wp, b16)
         A, D = wo.shape[3], wd.shape[3]
         ctx.save_for_backward(share, w16)
+        ctx.set_materialize_grads(False)  # a missing head gradient is zero-filled below
         ctx.dims = (A, D, y.shape[-1])
         return y[..., :A].contiguous(), y[..., A:A + D].contiguous()
 
