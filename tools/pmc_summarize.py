@@ -17,15 +17,20 @@ import os
 import re
 import sys
 
-# the split-K reduction launches are counted with the split-product group (the
-# bulk of the conv calls); per-launch figures divide by the main kernel's count
+# (kernels of the group, the group's one-per-op kernel).  The split-K /
+# partial reductions are counted with their group; per-launch figures divide
+# by the op's main kernel count.  ROIAlign backward: its own kernels (the
+# memsets and the rocPRIM radix sort it also launches are not attributable by
+# name and are left out).
 GROUPS = {
-    "conv2d_split": re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce_kernel"),
-    "conv2d_mfma": re.compile(r"conv_mfma_kernel<[^>]*, false>"),
-    "roi_align_fwd": re.compile(r"roi_align_fwd_kernel"),
-    "roi_align_bwd": re.compile(r"roi_bwd_"),
-    "conv_wgrad_split": re.compile(r"conv_wgrad_split_kernel|wgrad_reduce_kernel"),
-    "conv_wgrad": re.compile(r"conv_wgrad_kernel<"),
+    "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce_kernel"),
+                     re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel")),
+    "conv2d_mfma": (re.compile(r"conv_mfma_kernel<[^>]*, false>"), None),
+    "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),
+    "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_pixel_kernel")),
+    "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce_kernel"),
+                         re.compile(r"conv_wgrad_split_kernel")),
+    "conv_wgrad": (re.compile(r"conv_wgrad_kernel<"), None),
 }
 
 
@@ -49,15 +54,15 @@ def main():
     res = {"units": "bytes per dispatch", "fetch_correction": 2.0,
            "note": "FETCH_SIZE x2 (gfx950 16 B/lane reads); WRITE_SIZE as reported",
            "groups": {}}
-    for g, rx in GROUPS.items():
+    for g, (rx, main_rx) in GROUPS.items():
+        main_rx = main_rx or rx
         fn = sum(v[0] for k, v in fetch.items() if rx.search(k))
         fb = sum(v[1] for k, v in fetch.items() if rx.search(k))
         wn = sum(v[0] for k, v in write.items() if rx.search(k))
         wb = sum(v[1] for k, v in write.items() if rx.search(k))
         if fn == 0 and wn == 0:
             continue
-        main_n = sum(v[0] for k, v in fetch.items()
-                     if rx.search(k) and "reduce" not in k)
+        main_n = sum(v[0] for k, v in fetch.items() if main_rx.search(k))
         res["groups"][g] = {
             "dispatches": fn, "main_kernel_dispatches": main_n,
             "fetch_bytes_per_launch": 2.0 * fb * 1024 / max(main_n, 1),
