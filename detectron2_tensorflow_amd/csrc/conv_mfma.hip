@@ -62,7 +62,12 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 // kFlipTaps: read weight tap (KH*KW - 1 - tap) -- the spatially flipped kernel
 // of a stride-1 dgrad, without materialising the flipped copy.
-enum EpiFlags { kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4, kFlipTaps = 8 };
+// kMaskByResidual: the residual operand is a ReLU output whose mask gates the
+// result, out = residual > 0 ? conv + bias : 0 (a dgrad with the producer's
+// ReLU backward fused; no add).
+enum EpiFlags {
+  kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4, kFlipTaps = 8, kMaskByResidual = 16
+};
 
 // Exact 3-term bf16 split of four floats (truncation; see the header).
 // Each output packs 4 bf16 (element order = float4 order).
@@ -113,7 +118,10 @@ __device__ __forceinline__ float epilogue(const ConvArgs& a, float acc, int m, i
     const int oh = rem / a.OW, ow = rem - oh * a.OW;
     v = v + a.topdown[(((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout + co];
   }
-  if (a.residual) v = v + a.residual[(size_t)m * a.Cout + co];
+  if (a.residual) {
+    const float r = a.residual[(size_t)m * a.Cout + co];
+    v = (a.flags & kMaskByResidual) ? (r > 0.f ? v : 0.f) : v + r;
+  }
   if ((a.flags & kRelu) && (a.flags & kReluAfterResidual)) v = fmaxf(v, 0.f);
   return v;
 }
@@ -190,6 +198,7 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         add[r] = v;
       }
       const bool relu_after = (a.flags & kReluAfterResidual) != 0;
+      const bool gate = (a.flags & kMaskByResidual) != 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb + (r & 3) + 8 * (r >> 2);
@@ -197,7 +206,9 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         float v = acc[i][j][r] + bv;
         if (relu && !relu_after) v = fmaxf(v, 0.f);
         // epilogue() order: conv + bias, (+ top-down) (+ residual)
-        if (a.topdown && a.residual) {
+        if (gate) {
+          v = add[r] > 0.f ? v : 0.f;
+        } else if (a.topdown && a.residual) {
           v = epilogue(a, acc[i][j][r], m, co);
         } else {
           v = v + add[r];
@@ -833,9 +844,11 @@ extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const 
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
   D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_packed & 15) == 0,
                "x and w must be 16-byte aligned");
-  D2MI_REQUIRE((flags & ~15) == 0,
+  D2MI_REQUIRE((flags & ~31) == 0,
                "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
-               "MFMA products, bit3 flipped weight taps");
+               "MFMA products, bit3 flipped weight taps, bit4 residual is a ReLU gate");
+  D2MI_REQUIRE(!(flags & kMaskByResidual) || (residual && !topdown && !(flags & 3)),
+               "the ReLU gate (bit4) needs the residual operand and no relu / top-down");
   // 32-bit buffer offsets: batches whose input is >= 2 GiB run as image chunks
   const int64_t img_bytes = (int64_t)H * W * Cin * sizeof(float);
   D2MI_REQUIRE(img_bytes < (1ll << 31), "one conv input image must be < 2 GiB");

@@ -41,7 +41,7 @@ def same_pads(kernel_size, rate=1):
     return pb, pad_total - pb
 
 
-def _dgrad(gy, w, x_shape, stride, pb, pe):
+def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None):
     """Input gradient.  Stride 1: a forward conv of gy with the spatially
     flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
     of the transposed conv, flipped by the kernel's tap indexing (kFlipTaps) —
@@ -54,7 +54,10 @@ def _dgrad(gy, w, x_shape, stride, pb, pe):
         if stride == 1 and max(pb, pe) <= KH - 1:
             # the flip is an index flip inside the kernel (no flipped copy)
             return ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1,
-                                   (KH - 1 - pb, KH - 1 - pe), flip_taps=KH > 1)
+                                   (KH - 1 - pb, KH - 1 - pe), flip_taps=KH > 1,
+                                   relu_gate=relu_gate)
+    if relu_gate is not None:
+        raise ValueError("relu_gate is fused into the stride-1 MFMA dgrad only")
         if KH == 1 and pb == 0 and pe == 0:
             g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
@@ -98,10 +101,22 @@ def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
     return gw.permute(2, 3, 1, 0), None
 
 
+def _gate_eligible(w_shape, stride, pb, pe):
+    KH, KW, _, Cout = w_shape
+    return KH == KW and Cout % 4 == 0 and stride == 1 and max(pb, pe) <= KH - 1
+
+
 class _ConvMFMAFn(torch.autograd.Function):
+    """Fused-ReLU chains: a conv with a fused ReLU tags its output.  A consumer
+    conv called with gate_input=True (the caller's declaration that it is the
+    SOLE consumer of that ReLU output: the bottleneck's conv2 / conv3, the mask
+    head's conv chain and deconv) applies the producer's ReLU mask in its own
+    dgrad epilogue (kMaskByResidual) and flags it; the producer then skips its
+    threshold_backward.  Without the declaration nothing is fused."""
+
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
-                relu_after=False):
+                relu_after=False, gate_input=False):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
@@ -109,13 +124,19 @@ class _ConvMFMAFn(torch.autograd.Function):
                             relu_after_add=relu_after)
         ctx.save_for_backward(x, w_hwio, y if relu else None)
         ctx.conf = (stride, pads, relu, bias is not None, topdown is not None, residual is not None)
+        ctx.in_info = getattr(x, "_d2mi_relu_info", None) if gate_input else None
+        ctx.out_info = None
+        if relu:  # (forward runs with grad mode off: tag unconditionally)
+            ctx.out_info = {"masked": False}
+            y._d2mi_relu_info = ctx.out_info
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
         stride, (pb, pe), relu, has_bias, has_td, has_res = ctx.conf
-        if relu:  # relu is the last op whenever an add is fused (relu_after)
+        if relu and not (ctx.out_info is not None and ctx.out_info["masked"]):
+            # relu is the last op whenever an add is fused (relu_after)
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)
         gtd = None
         if has_td:
@@ -125,13 +146,18 @@ class _ConvMFMAFn(torch.autograd.Function):
         gres = gy if has_res else None
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = _dgrad(gy, w, x.shape, stride, pb, pe)
+            info = ctx.in_info
+            if info is not None and _gate_eligible(w.shape, stride, pb, pe):
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x)
+                info["masked"] = True
+            else:
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe)
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
             gb = ops.column_sum(gy)
-        return gx, gw, gb, None, None, None, None, gtd, gres, None
+        return gx, gw, gb, None, None, None, None, gtd, gres, None, None
 
 
 @add_arg_scope
@@ -222,7 +248,8 @@ class Conv2D(Layer):
             self._packed_key = key
         return self._packed
 
-    def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False):
+    def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
+             relu_input_sole_consumer=False):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -249,7 +276,8 @@ class Conv2D(Layer):
             if packed is None:
                 packed = self.packed_weights(w)
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
-                                    fuse_relu, topdown, residual, relu_after_add)
+                                    fuse_relu, topdown, residual, relu_after_add,
+                                    bool(relu_input_sole_consumer))
             if norm is not None:
                 ret = norm(ret)
             if self.act_fn is not None and not fuse_relu:
@@ -319,7 +347,7 @@ class ConvTranspose2D(Layer):
             self.normalizer_fn = normalizer(**p)
         self.act_fn = get_activation(activation)
 
-    def call(self, inputs):
+    def call(self, inputs, relu_input_sole_consumer=False):
         k, s = self.kernel_size, self.stride
         N, H, W, C = inputs.shape
         if k == s:  # the mask-head case: MFMA GEMM (raises off-GPU, no CPU fallback)
@@ -327,7 +355,7 @@ class ConvTranspose2D(Layer):
             b = self.bias.repeat(k * k) if self.bias is not None else None
             fuse = self.normalizer_fn is None and is_relu(self.act_fn)
             y = _ConvMFMAFn.apply(inputs, wp.permute(0, 1, 3, 2), b, wp.detach().contiguous(), 1,
-                                  (0, 0), fuse, None, None, False)
+                                  (0, 0), fuse, None, None, False, bool(relu_input_sole_consumer))
             y = y.reshape(N, H, W, k, k, self.out_channels).permute(0, 1, 3, 2, 4, 5)
             ret = y.reshape(N, H * k, W * k, self.out_channels)
             if self.normalizer_fn is not None:

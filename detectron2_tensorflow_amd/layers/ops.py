@@ -293,12 +293,14 @@ def _presplit_ok(x, Cin):
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
                 residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None,
-                flip_taps=False):
+                flip_taps=False, relu_gate=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
     CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x.
-    flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j])."""
+    flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
+    relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv : 0
+    (a dgrad with its producer's ReLU backward fused)."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -319,13 +321,21 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                              f"{(N, OH, OW, Cout)}")
     if residual is not None:
         residual = _f32c(residual)
+    if relu_gate is not None:
+        if residual is not None or topdown is not None or relu:
+            raise ValueError("relu_gate excludes residual / topdown / relu")
+        residual = _f32c(relu_gate)
+        if residual.shape != y.shape:
+            raise ValueError(f"relu_gate {tuple(residual.shape)} != output {tuple(y.shape)}")
     # measured policy (tools/bench_kernels.py --only conv): narrow Cout (the
     # 128x64 / 128x32 tiles) gains nothing from the split products.
     if math_mode == "split" and Cout <= 64:
         math_mode = "f32"
-    presplit = math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps and (
+    presplit = (math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps
+                and relu_gate is None) and (
         x_split is not None or (KH * KW > 1 and PRESPLIT_KXK))
-    flags = (1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
+    flags = ((1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
+             | (16 if relu_gate is not None else 0))
     if math_mode == "split" and not presplit:
         flags |= 4
     wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),

@@ -51,8 +51,12 @@ class BottleneckBlock(Layer):
 
     def call(self, x):
         sc = self.shortcut(x) if self.shortcut is not None else x
-        # relu(conv3(...) + shortcut) in one kernel
-        return self.conv3(self.conv2(self.conv1(x)), residual=sc.contiguous(), final_relu=True)
+        # relu(conv3(...) + shortcut) in one kernel.  conv1 -> conv2 -> conv3 is
+        # a chain of sole consumers: each one's dgrad applies the previous
+        # ReLU's mask (no separate ReLU-backward pass).
+        h = self.conv2(self.conv1(x), relu_input_sole_consumer=True)
+        return self.conv3(h, residual=sc.contiguous(), final_relu=True,
+                          relu_input_sole_consumer=True)
 
 
 @add_arg_scope

@@ -82,9 +82,11 @@ class MaskRCNNConvUpsampleHead(Layer):
                                     weights_initializer=init.random_normal(0.001), scope="predictor")
 
     def call(self, x):
-        for layer in self.convs:
-            x = layer(x)
-        deconv = self.deconv(x)
+        # each conv (and the deconv) is the sole consumer of the previous ReLU
+        # output: its dgrad applies that ReLU's mask
+        for i, layer in enumerate(self.convs):
+            x = layer(x, relu_input_sole_consumer=i > 0)
+        deconv = self.deconv(x, relu_input_sole_consumer=len(self.convs) > 0)
         return deconv, self.predictor(deconv)
 
 

@@ -761,3 +761,42 @@ def test_column_sum_and_linear_mfma_match_float64(dev):
     torch.testing.assert_close(xi.grad.double(), gd @ wd.t(), rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(lin.weights.grad.double(), xd.t() @ gd, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(lin.bias.grad.double(), gd.sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("declared", [True, False])
+def test_relu_gate_fused_into_consumer_dgrad(dev, declared):
+    """conv(relu) -> conv(relu) -> conv chains: a consumer declared as the sole
+    consumer of a fused-ReLU output applies that ReLU's backward in its own
+    dgrad epilogue (kMaskByResidual) and the producer skips its own; without
+    the declaration nothing is fused.  Gradients match float64 autograd."""
+    from detectron2_tensorflow_amd.layers.convolutional import _ConvMFMAFn
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 12, 15, 64, generator=g)
+    ws = [torch.randn(3, 3, 64, 64, generator=g) / 24 for _ in range(3)]
+    bs = [torch.randn(64, generator=g) * 0.1 for _ in range(3)]
+    gy = torch.randn(2, 12, 15, 64, generator=g)
+
+    def ref(h, ws, bs):
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            h = torch.nn.functional.conv2d(h.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), b,
+                                           padding=1).permute(0, 2, 3, 1)
+            if i < 2:
+                h = torch.relu(h)
+        return h
+
+    lx = [t.double().requires_grad_(True) for t in [x] + ws + bs]
+    ref(lx[0], lx[1:4], lx[4:7]).backward(gy.double())
+    dx = [t.to(dev).requires_grad_(True) for t in [x] + ws + bs]
+    h = dx[0]
+    outs = []
+    for i in range(3):
+        w, b = dx[1 + i], dx[4 + i]
+        h = _ConvMFMAFn.apply(h, w, b, ops().pack_conv_weights(w.detach()), 1, (1, 1), i < 2,
+                              None, None, False, declared and i > 0)
+        outs.append(h)
+    h.backward(gy.to(dev))
+    assert outs[0]._d2mi_relu_info["masked"] is declared
+    assert outs[1]._d2mi_relu_info["masked"] is declared
+    for name, a, r in zip(["x", "w0", "w1", "w2", "b0", "b1", "b2"], dx, lx):
+        np.testing.assert_allclose(a.grad.cpu().double().numpy(), r.grad.numpy(), rtol=1e-4,
+                                   atol=2e-4 * max(1.0, float(r.grad.abs().max())), err_msg=name)
