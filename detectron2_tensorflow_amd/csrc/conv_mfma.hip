@@ -99,6 +99,10 @@ struct ConvArgs {
   float* partial;  // split-K workspace [splits][M][Cout] (nullable)
   int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW, flags;
   int M, nM, nN, ntiles, splits, kt_per_split, nk, cchunks;
+  // this launch covers tiles [tile_base, tile_base + ntiles); split-K
+  // partials cover output rows [m_base, M) (the tail launch of a grid whose
+  // last round would run mostly empty, see conv_core)
+  int tile_base, m_base;
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
   // pre-split operands (conv_x3_kernel): 3 bf16 planes each, plane strides in bytes
   const uint16_t* x3;
@@ -156,7 +160,7 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         continue;
       }
       if (a.splits > 1) {
-        float* pp = a.partial + ((size_t)split * a.M + mb) * a.Cout + co;
+        float* pp = a.partial + ((size_t)split * (a.M - a.m_base) + (mb - a.m_base)) * a.Cout + co;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int dm = (r & 3) + 8 * (r >> 2);
@@ -238,7 +242,8 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
   const int orig = blockIdx.x;
   const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int tile =
+      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
   const int mt = tile / a.nN, nt = tile - mt * a.nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int split = blockIdx.y;
@@ -476,7 +481,8 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
 
   const int orig = blockIdx.x;
   const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int tile =
+      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
   const int mt = tile / a.nN, nt = tile - mt * a.nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int split = blockIdx.y;
@@ -635,13 +641,14 @@ __global__ void split3_kernel(const float4* __restrict__ x, int64_t n4, uint2* _
 
 // Fixed-order split-K reduction + epilogue (deterministic).
 __global__ void splitk_reduce_kernel(ConvArgs a) {
-  const int64_t total = (int64_t)a.M * a.Cout;
+  const int64_t total = (int64_t)(a.M - a.m_base) * a.Cout;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
     for (int s = 0; s < a.splits; ++s) acc += a.partial[(size_t)s * total + i];
-    const int m = (int)(i / a.Cout), co = (int)(i - (int64_t)m * a.Cout);
-    a.y[i] = epilogue(a, acc, m, co);
+    const int ml = (int)(i / a.Cout), co = (int)(i - (int64_t)ml * a.Cout);
+    const int m = a.m_base + ml;
+    a.y[(size_t)m * a.Cout + co] = epilogue(a, acc, m, co);
   }
 }
 
@@ -676,7 +683,25 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
 struct Plan {
   int cfg;  // 0: 128x128, 1: 128x64, 2: 128x32
   int BM, BN, splits, kt_per_split, nk, ntiles;
+  // tail split: the first full_tiles run as whole tiles, the remaining
+  // tail_tiles (whole pixel-row blocks) split K tail_splits ways
+  int full_tiles, tail_tiles, tail_splits, tail_kt_per_split;
+  size_t ws_bytes;
 };
+
+// Resident workgroups of the 128-wide conv tiles: 2 per CU.
+static int wg_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;  // MI355X
+    slots = 2 * cus;
+  }
+  return slots;
+}
 
 Plan make_plan(int M, int Cout, int KH, int KW, int Cin) {
   Plan p;
@@ -693,6 +718,34 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin) {
   }
   p.kt_per_split = (p.nk + p.splits - 1) / p.splits;
   p.splits = (p.nk + p.kt_per_split - 1) / p.kt_per_split;
+  p.ws_bytes = p.splits > 1 ? (size_t)p.splits * M * Cout * sizeof(float) : 0;
+  // Tail split: with more tiles than resident workgroups, a last round that
+  // is mostly empty (1050 tiles = 2 rounds of 512 + 26 on the FPN p2 3x3,
+  // 525 = 512 + 13 on p3) costs about a whole round for a few tiles.  Those
+  // tiles (whole pixel-row blocks) are split along K over the idle slots
+  // instead and reduced in a fixed order.
+  p.full_tiles = p.ntiles;
+  p.tail_tiles = 0;
+  p.tail_splits = 1;
+  p.tail_kt_per_split = p.nk;
+  const int G = wg_slots();
+  if (p.splits == 1 && p.ntiles > G && p.nk >= 8) {
+    const int full = (p.ntiles / G) * G / nN * nN;
+    const int tail = p.ntiles - full;
+    if (tail > 0 && 2 * tail <= G) {
+      int S = std::min(std::min(G / tail, p.nk / 4), 32);
+      if (S >= 2) {
+        const int kps = (p.nk + S - 1) / S;
+        S = (p.nk + kps - 1) / kps;
+        p.full_tiles = full;
+        p.tail_tiles = tail;
+        p.tail_splits = S;
+        p.tail_kt_per_split = kps;
+        const int m_base = full / nN * p.BM;
+        p.ws_bytes = (size_t)S * (M - m_base) * Cout * sizeof(float);
+      }
+    }
+  }
   return p;
 }
 
@@ -756,7 +809,7 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
   int OH, OW;
   if (conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH, OW)) return 0;
   const Plan p = make_plan(N * OH * OW, Cout, KH, KW, Cin);
-  return p.splits > 1 ? (size_t)p.splits * N * OH * OW * Cout * sizeof(float) : 0;
+  return p.ws_bytes;
 }
 
 // Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
@@ -793,14 +846,17 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.flags = flags;
   a.M = N * a.OH * a.OW;
   Plan p = make_plan(a.M, Cout, KH, KW, Cin);
-  const size_t need = p.splits > 1 ? (size_t)p.splits * a.M * Cout * sizeof(float) : 0;
-  if (need > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
+  if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
     p.splits = 1;
     p.kt_per_split = p.nk;
+    p.full_tiles = p.ntiles;
+    p.tail_tiles = 0;
   }
   a.nM = (a.M + p.BM - 1) / p.BM;
   a.nN = (Cout + p.BN - 1) / p.BN;
-  a.ntiles = p.ntiles;
+  a.ntiles = p.full_tiles;
+  a.tile_base = 0;
+  a.m_base = 0;
   a.splits = p.splits;
   a.kt_per_split = p.kt_per_split;
   a.nk = p.nk;
@@ -810,6 +866,15 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.tdW = (a.OW + 1) / 2;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
+  ConvArgs t = a;  // the tail launch (when planned)
+  if (p.tail_tiles > 0) {
+    t.tile_base = p.full_tiles;
+    t.ntiles = p.tail_tiles;
+    t.m_base = p.full_tiles / a.nN * p.BM;
+    t.splits = p.tail_splits;
+    t.kt_per_split = p.tail_kt_per_split;
+    t.partial = (float*)workspace;
+  }
   // 128x128 tiles: single-buffered LDS (two barriers per k-step, 2 workgroups
   // per CU) measured faster than double-buffered (1 workgroup per CU) on every
   // Mask R-CNN shape, f32 and split, large grids and small
@@ -817,19 +882,29 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   static const char* force = getenv("D2MI_CONV_DB");
   bool db = false;
   if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
-  if (x3)
-    launch_x3(p.cfg, db, grid, st, a);
-  else if (flags & kSplit3)
-    launch_conv<true>(p.cfg, db, grid, st, a);
-  else
-    launch_conv<false>(p.cfg, db, grid, st, a);
-  D2MI_LAUNCH_CHECK();
-  if (a.splits > 1) {
-    const int64_t total = (int64_t)a.M * Cout;
-    const int g = (int)std::min<int64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, a);
+  auto launch = [&](const ConvArgs& c) {
+    const dim3 g(c.ntiles, c.splits);
+    if (x3)
+      launch_x3(p.cfg, db, g, st, c);
+    else if (flags & kSplit3)
+      launch_conv<true>(p.cfg, db, g, st, c);
+    else
+      launch_conv<false>(p.cfg, db, g, st, c);
     D2MI_LAUNCH_CHECK();
+    if (c.splits > 1) {
+      const int64_t total = (int64_t)(c.M - c.m_base) * Cout;
+      const int gr = (int)std::min<int64_t>((total + 255) / 256, 4096);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gr), dim3(256), 0, st, c);
+      D2MI_LAUNCH_CHECK();
+    }
+    return 0;
+  };
+  (void)grid;
+  if (a.ntiles > 0) {
+    const int rc = launch(a);
+    if (rc) return rc;
   }
+  if (p.tail_tiles > 0) return launch(t);
   return 0;
 }
 

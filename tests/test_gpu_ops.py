@@ -800,3 +800,33 @@ def test_relu_gate_fused_into_consumer_dgrad(dev, declared):
     for name, a, r in zip(["x", "w0", "w1", "w2", "b0", "b1", "b2"], dx, lx):
         np.testing.assert_allclose(a.grad.cpu().double().numpy(), r.grad.numpy(), rtol=1e-4,
                                    atol=2e-4 * max(1.0, float(r.grad.abs().max())), err_msg=name)
+
+
+@pytest.mark.parametrize("epi", ["relu", "residual", "topdown"])
+def test_conv2d_tail_split_matches_float64(dev, epi):
+    """Grids a little over one round of resident workgroups (here 2x100x168 ->
+    263 x 2 = 526 tiles of 128x128) run their last pixel-row blocks as a
+    split-K tail launch with a fixed-order reduce; every epilogue form stays
+    within the f32-class bound of float64."""
+    g = torch.Generator().manual_seed(3)
+    N, H, W, C = 2, 100, 168, 256
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(3, 3, C, C, generator=g) / math.sqrt(9 * C)
+    b = torch.randn(C, generator=g)
+    res = torch.randn(N, H, W, C, generator=g) if epi == "residual" else None
+    top = torch.randn(N, H // 2, W // 2, C, generator=g) if epi == "topdown" else None
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2),
+                                     w.double().permute(3, 2, 0, 1), b.double(),
+                                     padding=1).permute(0, 2, 3, 1)
+    if res is not None:
+        ref = ref + res.double()
+    if top is not None:
+        ref = ref + top.double().repeat_interleave(2, 1).repeat_interleave(2, 2)
+    if epi == "relu":
+        ref = ref.clamp(min=0)
+    t = lambda a: None if a is None else a.to(dev)
+    y = ops().conv2d_nhwc(t(x), ops().pack_conv_weights(t(w)), t(b), 1, (1, 1),
+                          relu=epi == "relu", residual=t(res), topdown=t(top))
+    np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    # the tail rows (the last 14 tiles) are really there
+    assert torch.isfinite(y[-1, -1]).all() and float(y[-1, -1].abs().sum()) > 0
