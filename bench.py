@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--timed-step-sample", type=int, default=-1,
                    help="timed step whose kernel launches carry HIP events (-1: the last)")
     p.add_argument("--mode", default="train", choices=["train", "infer"])
+    p.add_argument("--mask-format", default="conventional", choices=["conventional", "raw", "fixed"],
+                   help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
     return p.parse_args()
 
@@ -75,7 +77,9 @@ def build(args, device):
     from detectron2_tensorflow_amd.modeling import build_model
     cfg = get_cfg()
     cfg.merge_from_file(os.path.join(ROOT, CONFIGS[args.model]))
-    cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = "raw"
+    # inference: the reference's default output format (masks pasted onto the
+    # padded canvas as uint8, detector_postprocess); training never pastes
+    cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = args.mask_format if args.mode == "infer" else "raw"
     cfg.SOLVER.IMS_PER_GPU = args.batch
     finalize(cfg, training=args.mode == "train", world_size=args.gpus,
              category_map={"num_thing_classes": 80, "num_stuff_classes": 53,
@@ -200,11 +204,17 @@ def cpu_baseline(args, model, batch, cfg=None):
     else:
         ref = CPUReference(model.eval())
         ref(imgs[:1, :256, :320], [[256, 320]], threads=cores)  # warm the libraries
+        # the same output format as the timed GPU step: "conventional" pastes
+        # onto the padded canvas (size divisibility 32)
+        canvas = None
+        if args.mask_format == "conventional":
+            d = model.neck.size_divisibility or 1
+            canvas = tuple(-(-int(v) // d) * d for v in imgs.shape[1:3])
         t0 = time.perf_counter()
         for _ in range(iters):
-            ref(imgs, shapes, threads=cores)
+            ref(imgs, shapes, threads=cores, paste_to=canvas)
         dt = time.perf_counter() - t0
-        what = "inference forward(s)"
+        what = "inference forward(s)" + (" + mask pasting" if canvas else "")
     return {"value": round(n * iters / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
             "sample": f"{iters} x {n} image(s) {args.height}x{args.width}, {args.model} {what}, "
                       f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU "
@@ -318,7 +328,9 @@ def main():
                             "parallelism": (f"dp{world}" if args.mode == "train" else f"replicas{world}"),
                             "mode": args.mode,
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
-                            else f"{sample + 1}/{args.steps}"}, **extra),
+                            else f"{sample + 1}/{args.steps}",
+                            **({"mask_format": args.mask_format} if args.mode == "infer" else {})},
+                       **extra),
             # the dominant hot-path kernel: the split-product conv (else f32)
             "roofline": kernels.get("conv2d_split", kernels.get("conv2d_mfma")),
             **({"replicas_in_sync": in_sync} if in_sync is not None else {}),

@@ -84,7 +84,7 @@ class CPUReference:
         return _fpn(self.m.neck, feats)
 
     @torch.no_grad()
-    def __call__(self, images, image_shapes, threads=None):
+    def __call__(self, images, image_shapes, threads=None, paste_to=None):
         if threads:
             torch.set_num_threads(threads)
         m = self.m
@@ -155,6 +155,10 @@ class CPUReference:
             masks = np.zeros((N, D) + logit.shape[1:], F32)
             masks[di, ds] = oracle.sigmoid(logit)
             out["masks"] = masks
+            if paste_to is not None:  # detector_postprocess "conventional"
+                out["masks"] = np.stack([
+                    oracle.paste_masks(masks[n], out["boxes"][n], paste_to, valid=out["is_valid"][n])
+                    for n in range(N)])
         return out
 
 
