@@ -42,17 +42,29 @@ class Layer(torch.nn.Module):
         self.add_module(name or layer.scope, layer)
         return layer
 
-    def reference_variables(self, prefix=""):
-        """(reference variable path, tensor) pairs, e.g. ("neck/fpn_output2/weights", w)."""
-        base = prefix + (self.scope + "/" if prefix or self.scope else "")
-        for name, p in list(self.named_parameters(recurse=False)) + list(self.named_buffers(recurse=False)):
+    def reference_variables(self, prefix="", include_scope=True):
+        """(reference variable path, tensor) pairs, e.g. ("neck/fpn_output2/weights", w).
+        Layers inside ModuleLists are named by their own scopes (res2/block_1,
+        mask_fcn1, fpn_lateral2 ...), as the reference's variable scopes;
+        include_scope=False leaves out this layer's own scope (the meta-arch
+        root: the reference's variables start at backbone/, neck/, ...)."""
+        base = prefix + (self.scope + "/" if include_scope and self.scope else "")
+        transient = getattr(self, "_non_persistent_buffers_set", set())
+        bufs = [(n, b) for n, b in self.named_buffers(recurse=False) if n not in transient]
+        for name, p in list(self.named_parameters(recurse=False)) + bufs:
             yield base + name, p
-        for child in self.children():
-            if isinstance(child, Layer):
-                yield from child.reference_variables(base)
-            else:
-                for name, p in child.named_parameters():
-                    yield base + name.replace(".", "/"), p
+
+        def walk(mod, path):
+            for name, child in mod.named_children():
+                if isinstance(child, Layer):
+                    yield from child.reference_variables(path)
+                elif isinstance(child, (torch.nn.ModuleList, torch.nn.Sequential)):
+                    yield from walk(child, path)
+                else:
+                    for pn, p in child.named_parameters():
+                        yield path + name + "/" + pn.replace(".", "/"), p
+
+        yield from walk(self, base)
 
 
 class Sequential:
