@@ -75,6 +75,9 @@ _SIGS = {
     "d2mi_column_sum": (c_int, [P, ctypes.c_longlong, c_int, P, P, c_size_t, P]),
     "d2mi_sgd_table_sizes": (c_int, [P, P, P]),
     "d2mi_momentum_sgd": (c_int, [P, P, c_int, P, c_float, c_float, c_float, P]),
+    "d2mi_fold_many_sizes": (c_int, [P, P]),
+    "d2mi_fold_frozen_bn_many": (c_int, [P, c_int, c_int, P]),
+    "d2mi_fold_frozen_bn_bwd_many": (c_int, [P, c_int, c_int, c_int, P, P]),
 }
 
 EXPORTED = tuple(_SIGS)

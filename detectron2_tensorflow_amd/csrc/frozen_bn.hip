@@ -196,3 +196,149 @@ extern "C" int d2mi_fold_frozen_bn_bwd(const float* gw_eff, const float* gb_eff,
   D2MI_LAUNCH_CHECK();
   return 0;
 }
+
+// ------------------------------------------------------------ batched fold
+// Every BN-conv of the backbone folded by ONE forward launch and ONE backward
+// pair, driven by a table of d2mi_fold_entry (include/d2mi.h) instead of ~50
+// launches of each kernel above per step.  Each workgroup finds its entry by
+// binary search over the entries' first-block indices (the table is small and
+// sits in L2 after the first wave), then does the same work as
+// fold_bn_tiled_kernel / fold_bn_bwd_kernel / fold_bn_bwd_finish_kernel with
+// ci / co tails guarded, so any Cin works.  Sums keep the fixed row-chunk order
+// of the per-conv kernels: results are bit-identical to them.
+namespace d2mi {
+namespace {
+
+__device__ __forceinline__ int find_entry(const d2mi_fold_entry* __restrict__ t, int n, int b,
+                                          int which) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last entry whose begin <= b
+    const int mid = (lo + hi + 1) >> 1;
+    const int beg = which == 0 ? t[mid].fwd_begin : which == 1 ? t[mid].bwd_begin : t[mid].co_begin;
+    if (beg <= b) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void fold_bn_many_kernel(const d2mi_fold_entry* __restrict__ tab,
+                                                           int n) {
+  __shared__ float tile[64][65];
+  const d2mi_fold_entry& e = tab[find_entry(tab, n, blockIdx.x, 0)];
+  const int Cout = e.Cout, Cin = e.Cin;
+  const int nco = (Cout + 63) / 64, nci = (Cin + 63) / 64;
+  int local = blockIdx.x - e.fwd_begin;
+  const int cot = local % nco; local /= nco;
+  const int cit = local % nci;
+  const int tap = local / nci;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int co = co0 + lane;
+  const bool live = co < Cout;
+  float scale = 0.f;
+  if (live) {
+    const float inv = bn_inv(e.var, e.eps, co);
+    scale = e.gamma ? inv * e.gamma[co] : inv;
+    if (cit == 0 && tap == 0 && wv == 0) {
+      float shift = -e.mean[co] * scale;
+      if (e.beta) shift = shift + e.beta[co];
+      e.b_eff[co] = e.bias ? e.bias[co] * scale + shift : shift;
+    }
+  }
+  for (int i = wv; i < 64; i += 4) {
+    const bool row = ci0 + i < Cin;
+    const size_t r = (size_t)tap * Cin + ci0 + i;
+    const float v = live && row ? e.w[r * Cout + co] * scale : 0.f;
+    if (e.w_eff && live && row) e.w_eff[r * Cout + co] = v;
+    tile[i][lane] = v;
+  }
+  if (!e.w_packed) return;
+  __syncthreads();
+  for (int j = wv; j < 64; j += 4) {
+    if (co0 + j < Cout && ci0 + lane < Cin)
+      e.w_packed[((size_t)tap * Cout + co0 + j) * Cin + ci0 + lane] = tile[lane][j];
+  }
+}
+
+__global__ __launch_bounds__(256) void fold_bn_bwd_many_kernel(
+    const d2mi_fold_entry* __restrict__ tab, int n, float* __restrict__ ws) {
+  __shared__ float red[4][64];
+  const d2mi_fold_entry& e = tab[find_entry(tab, n, blockIdx.x, 1)];
+  const int Cout = e.Cout, rows = e.taps * e.Cin;
+  const int nco = (Cout + 63) / 64;
+  const int local = blockIdx.x - e.bwd_begin;
+  const int cot = local % nco, chunk = local / nco;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int co = cot * 64 + lane;
+  const bool live = co < Cout;
+  const int per = (rows + kRowChunks - 1) / kRowChunks;
+  const int r0 = chunk * per, r1 = min(rows, r0 + per);
+  float scale = 0.f;
+  if (live) {
+    const float inv = bn_inv(e.var, e.eps, co);
+    scale = e.gamma ? inv * e.gamma[co] : inv;
+  }
+  float s = 0.f;
+  if (live) {
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const float g = e.gw_eff ? e.gw_eff[(size_t)r * Cout + co] : 0.f;
+      s += g * e.w[(size_t)r * Cout + co];
+      if (e.gw) e.gw[(size_t)r * Cout + co] = g * scale;
+    }
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && live)
+    ws[e.partial_offset + (size_t)chunk * Cout + co] =
+        ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ void fold_bn_bwd_many_finish_kernel(const d2mi_fold_entry* __restrict__ tab, int n,
+                                               int total_cout, const float* __restrict__ ws) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total_cout) return;
+  const d2mi_fold_entry& e = tab[find_entry(tab, n, g, 2)];
+  const int Cout = e.Cout, co = g - e.co_begin;
+  const float* partial = ws + e.partial_offset;
+  float gs = 0.f;
+  for (int k = 0; k < kRowChunks; ++k) gs += partial[(size_t)k * Cout + co];
+  const float inv = bn_inv(e.var, e.eps, co);
+  const float scale = e.gamma ? inv * e.gamma[co] : inv;
+  const float gb = e.gb_eff ? e.gb_eff[co] : 0.f;
+  gs = gs + gb * ((e.bias ? e.bias[co] : 0.f) - e.mean[co]);
+  if (e.ggamma) e.ggamma[co] = gs * inv;
+  if (e.gbeta) e.gbeta[co] = gb;
+  if (e.gbias) e.gbias[co] = gb * scale;
+}
+
+}  // namespace
+}  // namespace d2mi
+
+extern "C" int d2mi_fold_many_sizes(int* entry_bytes, int* row_chunks) {
+  if (entry_bytes) *entry_bytes = (int)sizeof(d2mi_fold_entry);
+  if (row_chunks) *row_chunks = kRowChunks;
+  return 0;
+}
+
+extern "C" int d2mi_fold_frozen_bn_many(const d2mi_fold_entry* table, int num_entries,
+                                        int fwd_blocks, void* stream) {
+  D2MI_REQUIRE(table && num_entries > 0 && fwd_blocks > 0, "empty fold table");
+  hipLaunchKernelGGL(fold_bn_many_kernel, dim3(fwd_blocks), dim3(256), 0, as_stream(stream), table,
+                     num_entries);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int d2mi_fold_frozen_bn_bwd_many(const d2mi_fold_entry* table, int num_entries,
+                                            int bwd_blocks, int total_cout, float* workspace,
+                                            void* stream) {
+  D2MI_REQUIRE(table && num_entries > 0 && bwd_blocks > 0 && total_cout > 0, "empty fold table");
+  D2MI_REQUIRE(workspace, "fold_frozen_bn_bwd_many needs its workspace");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(fold_bn_bwd_many_kernel, dim3(bwd_blocks), dim3(256), 0, st, table,
+                     num_entries, workspace);
+  D2MI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(fold_bn_bwd_many_finish_kernel, dim3((total_cout + 255) / 256), dim3(256), 0,
+                     st, table, num_entries, total_cout, (const float*)workspace);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}

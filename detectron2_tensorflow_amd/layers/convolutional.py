@@ -160,6 +160,50 @@ class _ConvMFMAFn(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None, gtd, gres, None, None
 
 
+class FoldGroup:
+    """The trainable Conv2D + FrozenBN layers of one network folded together:
+    the first of them to run in a training forward folds all of them with
+    ops.fold_frozen_bn_many (one launch, and one backward pair once every
+    gradient has arrived, instead of three launches per layer); each layer
+    then takes its own result once.  A layer whose parameters changed since
+    (new version) or whose result was already taken (a second forward) makes
+    the next fetch refold the group."""
+    ENABLED = True
+
+    def __init__(self, layers):
+        self.layers = list(layers)
+        self.slots = {}
+        for layer in self.layers:
+            layer._fold_group = self
+
+    @classmethod
+    def attach(cls, module):
+        layers = [m for m in module.modules()
+                  if isinstance(m, Conv2D) and isinstance(m.normalizer_fn, BatchNorm)]
+        return cls(layers) if layers else None
+
+    def fetch(self, layer):
+        s = self.slots.get(id(layer))
+        if s is None or s[3] or s[4] != layer._param_key():
+            self._fold()
+            s = self.slots.get(id(layer))
+            if s is None:
+                return None
+        out = (s[0], s[1], s[2])
+        self.slots[id(layer)] = [None, None, None, True, s[4]]
+        return out
+
+    def _fold(self):
+        members = [m for m in self.layers if m.weights.is_cuda and m.fold_trainable()]
+        entries = []
+        for m in members:
+            n = m.normalizer_fn
+            entries.append((m.weights, m.bias, n.gamma, n.beta, n.moving_mean, n.moving_variance,
+                            n.epsilon, m.wants_packed()))
+        outs = ops.fold_frozen_bn_many(entries)
+        self.slots = {id(m): [w, b, p, False, m._param_key()] for m, (w, b, p) in zip(members, outs)}
+
+
 @add_arg_scope
 class Conv2D(Layer):
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding="SAME", rate=1,
@@ -228,17 +272,35 @@ class Conv2D(Layer):
         norm = self.normalizer_fn
         if not isinstance(norm, BatchNorm):
             return self.weights, self.bias, norm, None
-        key = self._param_key()
-        if not torch.is_grad_enabled() and getattr(self, "_fold_key", None) == key:
-            return self._fold_w, self._fold_b, None, self._fold_p
         if not self.weights.is_cuda:
             raise RuntimeError(f"{self.scope}: the FrozenBN fold runs on the GPU (HIP)")
+        # constant while autograd is off or nothing in the fold trains (the
+        # layers below FREEZE_AT): cached per parameter version
+        cacheable = not (torch.is_grad_enabled() and self.fold_trainable())
+        key = self._param_key()
+        if cacheable and getattr(self, "_fold_key", None) == key:
+            return self._fold_w, self._fold_b, None, self._fold_p
+        group = getattr(self, "_fold_group", None)
+        if not cacheable and group is not None:
+            got = group.fetch(self)
+            if got is not None:
+                return got[0], got[1], None, got[2]
         w, b, packed = ops.fold_frozen_bn(self.weights, self.bias, norm.gamma, norm.beta,
                                           norm.moving_mean, norm.moving_variance, norm.epsilon,
                                           want_packed)
-        if not torch.is_grad_enabled():
+        if cacheable:
             self._fold_w, self._fold_b, self._fold_p, self._fold_key = w, b, packed, key
         return w, b, None, packed
+
+    def fold_trainable(self):
+        norm = self.normalizer_fn
+        ts = [self.weights, self.bias] + ([norm.gamma, norm.beta] if isinstance(norm, BatchNorm)
+                                          else [])
+        return any(t is not None and t.requires_grad for t in ts)
+
+    def wants_packed(self):
+        return (self.impl in ("mfma", "auto") and self.num_groups == 1 and self.rate == 1
+                and self.in_channels % 4 == 0)
 
     def packed_weights(self, w_eff=None):
         key = self._param_key()

@@ -8,6 +8,7 @@ reference op they replace (cited per function).
 import math
 import os
 
+import numpy as np
 import torch
 
 from .. import _C
@@ -453,6 +454,150 @@ def fold_frozen_bn(w_hwio, bias, gamma, beta, mean, var, eps, want_packed=False)
     (w_eff, b_eff, packed-or-None), differentiable w.r.t. w, bias, gamma, beta."""
     return _FoldFrozenBNFn.apply(w_hwio, bias, gamma, beta, mean, var, float(eps),
                                  bool(want_packed))
+
+
+_FOLD_DT = np.dtype([(n, np.uint64) for n in (
+    "w", "bias", "gamma", "beta", "mean", "var", "w_eff", "w_packed", "b_eff", "gw_eff", "gb_eff",
+    "gw", "gbias", "ggamma", "gbeta")] + [("eps", np.float32)] + [(n, np.int32) for n in (
+        "taps", "Cin", "Cout", "fwd_begin", "bwd_begin", "co_begin", "pad")] + [
+    ("partial_offset", np.int64)])
+
+
+class _HostTable:
+    """A device copy of a host table uploaded through a small ring of pinned
+    buffers (each slot reused once its previous copy has left, by event)."""
+    RING = 4
+
+    def __init__(self, nbytes, device):
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.ring = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(self.RING)]
+        self.events = [None] * self.RING
+        self.i = 0
+
+    def upload(self, arr):
+        k = self.i
+        self.i = (k + 1) % self.RING
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        self.ring[k].numpy()[:] = arr.view(np.uint8)
+        self.dev.copy_(self.ring[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev.device))
+        self.events[k] = ev
+        return self.dev
+
+
+_fold_tables = {}
+
+
+def _fold_table(kind, n, device):
+    key = (kind, n, device)
+    t = _fold_tables.get(key)
+    if t is None:
+        sz, chunks = _C.ctypes.c_int(), _C.ctypes.c_int()
+        _C.lib().d2mi_fold_many_sizes(_C.ctypes.byref(sz), _C.ctypes.byref(chunks))
+        if sz.value != _FOLD_DT.itemsize:
+            raise RuntimeError("d2mi_fold_entry layout mismatch")
+        t = _fold_tables[key] = (_HostTable(n * _FOLD_DT.itemsize, device), chunks.value)
+    return t
+
+
+def _addr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+class _FoldManyFn(torch.autograd.Function):
+    """Every BN-conv of the network folded at once: d2mi_fold_frozen_bn_many
+    (one launch) forward, d2mi_fold_frozen_bn_bwd_many (two launches)
+    backward.  inputs: per entry (w, bias, gamma, beta, mean, var); outputs:
+    per entry (w_eff, b_eff, packed-or-None)."""
+
+    @staticmethod
+    def forward(ctx, spec, *ts):
+        n = len(spec)
+        dev = ts[0].device
+        tab = np.zeros(n, _FOLD_DT)
+        outs, saved = [], []
+        fwd = bwd = cob = part = 0
+        table, chunks = _fold_table("fwd", n, dev)
+        for i, (eps, want_packed) in enumerate(spec):
+            w, bias, gamma, beta, mean, var = ts[6 * i:6 * i + 6]
+            KH, KW, Cin, Cout = w.shape
+            if not (w.is_contiguous() and w.dtype == torch.float32 and w.device == dev):
+                raise ValueError("fold_frozen_bn_many: contiguous f32 weights on one device")
+            w_eff = torch.empty_like(w)
+            b_eff = torch.empty((Cout,), dtype=torch.float32, device=dev)
+            packed = (torch.empty((KH, KW, Cout, Cin), dtype=torch.float32, device=dev)
+                      if want_packed else None)
+            nco, taps = -(-Cout // 64), KH * KW
+            tab[i] = (_addr(w), _addr(bias), _addr(gamma), _addr(beta),
+                      _addr(mean), _addr(var), _addr(w_eff), _addr(packed), _addr(b_eff),
+                      0, 0, 0, 0, 0, 0, eps, taps, Cin, Cout, fwd, bwd, cob, 0, part)
+            fwd += nco * -(-Cin // 64) * taps
+            bwd += nco * chunks
+            cob += Cout
+            part += chunks * Cout
+            outs += [w_eff, b_eff, packed]
+            if packed is not None:
+                ctx.mark_non_differentiable(packed)
+        rc = _C.lib().d2mi_fold_frozen_bn_many(_C.ptr(table.upload(tab)), n, fwd,
+                                               _C.stream_of(dev))
+        _C.check(rc, "d2mi_fold_frozen_bn_many")
+        ctx.save_for_backward(*ts)
+        ctx.tab, ctx.sizes = tab, (bwd, cob, part)
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ts = ctx.saved_tensors
+        tab = ctx.tab
+        n = len(tab)
+        need = ctx.needs_input_grad[1:]
+        dev = ts[0].device
+        bwd, cob, part = ctx.sizes
+        ret = [None]
+        keep = []
+        for i in range(n):
+            w, bias, gamma, beta = ts[6 * i:6 * i + 4]
+            gw_eff, gb_eff = grads[3 * i], grads[3 * i + 1]
+            if gw_eff is not None:
+                gw_eff = _f32c(gw_eff)
+            if gb_eff is not None:
+                gb_eff = _f32c(gb_eff)
+            keep += [gw_eff, gb_eff]
+            Cout = w.shape[-1]
+            mk = lambda cond, t: torch.empty_like(t) if cond and t is not None else None
+            gw, gbias = mk(need[6 * i], w), mk(need[6 * i + 1], bias)
+            ggamma, gbeta = mk(need[6 * i + 2], gamma), mk(need[6 * i + 3], beta)
+            e = tab[i]
+            e["gw_eff"], e["gb_eff"] = _addr(gw_eff), _addr(gb_eff)
+            e["gw"], e["gbias"] = _addr(gw), _addr(gbias)
+            e["ggamma"], e["gbeta"] = _addr(ggamma), _addr(gbeta)
+            ret += [gw, gbias, ggamma, gbeta, None, None]
+        table, _ = _fold_table("bwd", n, dev)
+        ws = _C.workspace(part * 4, dev)
+        rc = _C.lib().d2mi_fold_frozen_bn_bwd_many(_C.ptr(table.upload(tab)), n, bwd, cob,
+                                                   _C.ptr(ws), _C.stream_of(dev))
+        _C.check(rc, "d2mi_fold_frozen_bn_bwd_many")
+        del keep
+        return tuple(ret)
+
+
+def fold_frozen_bn_many(entries):
+    """entries: [(w_hwio, bias, gamma, beta, mean, var, eps, want_packed)] ->
+    [(w_eff, b_eff, packed-or-None)], the batched fold_frozen_bn (bit-identical
+    results, differentiable w.r.t. each w, bias, gamma, beta)."""
+    if not entries:
+        return []
+    spec = tuple((float(e[6]), bool(e[7])) for e in entries)
+    ts = []
+    for e in entries:
+        _C.require_device(e[0], e[4], e[5])
+        ts += [_f32c(e[0])] + [None if t is None else _f32c(t) for t in e[1:4]] + [
+            _f32c(e[4]), _f32c(e[5])]
+    outs = _FoldManyFn.apply(spec, *ts)
+    return [tuple(outs[3 * i:3 * i + 3]) for i in range(len(entries))]
 
 
 # -------------------------------------------------------------- matrix NMS

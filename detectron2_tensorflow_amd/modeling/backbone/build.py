@@ -1,5 +1,6 @@
 """BACKBONE_REGISTRY / build_backbone (lib/modeling/backbone/build.py)."""
 from ...layers import Layer, ShapeSpec
+from ...layers.convolutional import FoldGroup
 from ...utils.registry import Registry
 
 BACKBONE_REGISTRY = Registry("BACKBONE")
@@ -21,4 +22,7 @@ class Backbone(Layer):
 def build_backbone(cfg, input_shape=None, **kwargs):
     if input_shape is None:
         input_shape = ShapeSpec(channels=len(cfg.MODEL.PIXEL_MEAN))
-    return BACKBONE_REGISTRY.get(cfg.MODEL.BACKBONE.NAME)(cfg, input_shape, **kwargs)
+    backbone = BACKBONE_REGISTRY.get(cfg.MODEL.BACKBONE.NAME)(cfg, input_shape, **kwargs)
+    if FoldGroup.ENABLED:
+        FoldGroup.attach(backbone)  # its BN-convs fold in one batch per training step
+    return backbone

@@ -288,6 +288,47 @@ int d2mi_fold_frozen_bn_bwd(const float* gw_eff, const float* gb_eff, const floa
                             const float* var, float eps, int KH, int KW, int Cin, int Cout,
                             float* gw, float* gbias, float* ggamma, float* gbeta,
                             void* workspace, size_t workspace_bytes, void* stream);
+/* Batched fold: every BN-conv of a network in one forward launch and one
+ * backward pair (same arithmetic and summation order as the per-conv calls
+ * above, so bit-identical results).  Replaces the per-layer
+ * Conv2D -> BatchNorm(training=False) pairs of lib/modeling/backbone/resnet.py
+ * (resnet_arg_scope, :22-46) for one training step.  table: DEVICE array of
+ * entries sorted by fwd_begin / bwd_begin / co_begin (each ascending):
+ *   fwd_begin  first forward workgroup: ceil(Cout/64)*ceil(Cin/64)*taps each;
+ *   bwd_begin  first backward workgroup: ceil(Cout/64)*row_chunks each;
+ *   co_begin   prefix sum of Cout;  partial_offset  floats into the backward
+ *   workspace (row_chunks*Cout each).
+ * Forward reads w/bias/gamma/beta/mean/var and writes w_eff/w_packed/b_eff
+ * (w_eff, w_packed nullable); backward reads gw_eff/gb_eff (nullable = zero)
+ * and writes gw/gbias/ggamma/gbeta (each nullable).  d2mi_fold_many_sizes
+ * reports sizeof(entry) and the row-chunk count so a host can check its
+ * layout. */
+typedef struct d2mi_fold_entry {
+  const float* w;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  const float* mean;
+  const float* var;
+  float* w_eff;
+  float* w_packed;
+  float* b_eff;
+  const float* gw_eff;
+  const float* gb_eff;
+  float* gw;
+  float* gbias;
+  float* ggamma;
+  float* gbeta;
+  float eps;
+  int taps, Cin, Cout;
+  int fwd_begin, bwd_begin, co_begin, pad;
+  long long partial_offset;
+} d2mi_fold_entry;
+int d2mi_fold_many_sizes(int* entry_bytes, int* row_chunks);
+int d2mi_fold_frozen_bn_many(const d2mi_fold_entry* table, int num_entries, int fwd_blocks,
+                             void* stream);
+int d2mi_fold_frozen_bn_bwd_many(const d2mi_fold_entry* table, int num_entries, int bwd_blocks,
+                                 int total_cout, float* workspace, void* stream);
 
 /* ------------------------------------------------------- mask pasting
  * Replaces detector_postprocess (lib/modeling/postprocessing.py:9-59) for the

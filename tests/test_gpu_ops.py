@@ -696,6 +696,51 @@ def test_fold_frozen_bn_forward_backward(dev, with_bias):
                                    atol=1e-3, err_msg=name)
 
 
+def test_fold_frozen_bn_many_bit_identical_to_per_conv(dev):
+    """d2mi_fold_frozen_bn_many / _bwd_many (one table-driven launch for every
+    conv) give the per-conv fold's w_eff, b_eff, packed and all four
+    gradients bit for bit -- mixed shapes (ci / co tails, 7x7 stem, Cout 2048),
+    entries with and without bias / packed / a gradient."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [(7, 7, 3, 64), (1, 1, 64, 256), (3, 3, 60, 36), (1, 1, 1024, 2048), (3, 3, 128, 128),
+              (1, 1, 256, 16)]
+    entries, grads = [], []
+    for i, (kh, kw, ci, co) in enumerate(shapes):
+        r = lambda *s: torch.randn(*s, generator=g)
+        ts = [r(kh, kw, ci, co), r(co) if i % 2 else None, torch.rand(co, generator=g) + 0.5,
+              r(co), r(co), torch.rand(co, generator=g) + 0.1]
+        entries.append((ts, 1e-5 if i % 3 else 1e-3, i != 3))
+        grads.append((r(kh, kw, ci, co), r(co) if i != 4 else None))
+
+    def run(batched):
+        leaves = [[t.to(dev).requires_grad_(k < 4) if t is not None else None
+                   for k, t in enumerate(ts)] for ts, _, _ in entries]
+        if batched:
+            outs = ops().fold_frozen_bn_many([(*lv, eps, pk) for lv, (_, eps, pk)
+                                              in zip(leaves, entries)])
+        else:
+            outs = [ops().fold_frozen_bn(*lv, eps, pk) for lv, (_, eps, pk) in zip(leaves, entries)]
+        ys, gs = [], []
+        for (we, be, _), (gw, gb) in zip(outs, grads):
+            ys.append(we)
+            gs.append(gw.to(dev))
+            if gb is not None:  # else b_eff gets no gradient at all
+                ys.append(be)
+                gs.append(gb.to(dev))
+        torch.autograd.backward(ys, gs)
+        return outs, leaves
+
+    a, la = run(True)
+    b, lb = run(False)
+    for (wa, ba, pa), (wb, bb, pb) in zip(a, b):
+        assert torch.equal(wa, wb) and torch.equal(ba, bb)
+        assert (pa is None) == (pb is None) and (pa is None or torch.equal(pa, pb))
+    for xa, xb in zip(la, lb):
+        for ta, tb in zip(xa[:4], xb[:4]):
+            if ta is not None:
+                assert torch.equal(ta.grad, tb.grad)
+
+
 @pytest.mark.parametrize("H,W,fixed", [(96, 128, False), (75, 101, False), (64, 64, True)])
 def test_paste_masks_bit_exact(dev, H, W, fixed):
     """d2mi_paste_masks vs the oracle (crop_and_resize of the reverse box +

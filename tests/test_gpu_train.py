@@ -239,3 +239,33 @@ def test_fused_momentum_sgd_bumps_parameter_versions(dev):
     v = p._version
     MomentumSGD([{"params": [p], "weight_decay": 0.0}]).step(0.1)
     assert p._version > v
+
+
+def test_batched_frozen_bn_fold_matches_per_layer_fold(dev):
+    """The backbone's FoldGroup (every trainable Conv2D + FrozenBN folded by
+    one launch, one backward pair) gives the per-layer fold's losses and
+    gradients exactly; a second forward with unchanged weights refolds (the
+    first graph's results are taken once)."""
+    from detectron2_tensorflow_amd.utils.synthetic import synthetic_train_batch
+    cfg, model = _train_model(dev)
+    batch = synthetic_train_batch(2, 256, 320, 2, dev)
+    convs = [m for m in model.backbone.modules() if getattr(m, "_fold_group", None) is not None]
+    group = convs[0]._fold_group
+    assert sum(m.fold_trainable() for m in convs) > 20
+    res = {}
+    for batched in (True, False, True):
+        for m in convs:
+            m._fold_group = group if batched else None
+        model.zero_grad(set_to_none=True)
+        torch.manual_seed(5)
+        losses = model(batch)
+        sum(losses.values()).backward()
+        res.setdefault(batched, []).append(
+            ({k: v.item() for k, v in losses.items()},
+             {n: p.grad.clone() for n, p in model.backbone.named_parameters() if p.grad is not None}))
+    assert any(s[3] for s in group.slots.values())
+    (la, ga), (la2, ga2) = res[True]
+    lb, gb = res[False][0]
+    assert la == lb == la2 and ga.keys() == gb.keys() == ga2.keys() and ga
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]) and torch.equal(ga[n], ga2[n]), n
