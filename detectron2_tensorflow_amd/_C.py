@@ -65,6 +65,8 @@ _SIGS = {
     "d2mi_conv2d_wgrad_ex": (c_int, [P, P, P, P] + [c_int] * 11 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "d2mi_conv2d_nhwc_gated": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_nhwc_x3": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_split_bf16x3": (c_int, [P, ctypes.c_int64, P, P]),

@@ -64,7 +64,10 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 // of a stride-1 dgrad, without materialising the flipped copy.
 // kMaskByResidual: the residual operand is a ReLU output whose mask gates the
 // result, out = residual > 0 ? conv + bias : 0 (a dgrad with the producer's
-// ReLU backward fused; no add).
+// ReLU backward fused; no add).  The host turns it into ConvArgs::gate; the
+// gated entry point (d2mi_conv2d_nhwc_gated) passes a gate AND a residual:
+// out = gate > 0 ? conv + bias + residual : 0 (a dgrad that also takes the
+// other consumer's gradient of the same ReLU output).
 enum EpiFlags {
   kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4, kFlipTaps = 8, kMaskByResidual = 16
 };
@@ -95,6 +98,7 @@ struct ConvArgs {
   const float* bias;
   const float* topdown;
   const float* residual;
+  const float* gate;  // nullable: out = gate > 0 ? out : 0 (applied last)
   float* y;
   float* partial;  // split-K workspace [splits][M][Cout] (nullable)
   int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW, flags;
@@ -103,6 +107,7 @@ struct ConvArgs {
   // partials cover output rows [m_base, M) (the tail launch of a grid whose
   // last round would run mostly empty, see conv_core)
   int tile_base, m_base;
+  int lds_epi;  // store_outputs_lds usable (Cout % 4 == 0, 16-B aligned operands)
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
   // pre-split operands (conv_x3_kernel): 3 bf16 planes each, plane strides in bytes
   const uint16_t* x3;
@@ -122,11 +127,9 @@ __device__ __forceinline__ float epilogue(const ConvArgs& a, float acc, int m, i
     const int oh = rem / a.OW, ow = rem - oh * a.OW;
     v = v + a.topdown[(((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout + co];
   }
-  if (a.residual) {
-    const float r = a.residual[(size_t)m * a.Cout + co];
-    v = (a.flags & kMaskByResidual) ? (r > 0.f ? v : 0.f) : v + r;
-  }
+  if (a.residual) v = v + a.residual[(size_t)m * a.Cout + co];
   if ((a.flags & kRelu) && (a.flags & kReluAfterResidual)) v = fmaxf(v, 0.f);
+  if (a.gate && !(a.gate[(size_t)m * a.Cout + co] > 0.f)) v = 0.f;
   return v;
 }
 
@@ -137,7 +140,7 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
                                               int n0, int wr, int wc, int lane, int split) {
   const int li = lane & 31, lh = lane >> 5;
   // C/D map for 32x32: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const bool simple = a.splits == 1 && !a.topdown && !a.residual;
+  const bool simple = a.splits == 1 && !a.topdown && !a.residual && !a.gate;
   const bool relu = (a.flags & kRelu) != 0;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -202,17 +205,15 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         add[r] = v;
       }
       const bool relu_after = (a.flags & kReluAfterResidual) != 0;
-      const bool gate = (a.flags & kMaskByResidual) != 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb + (r & 3) + 8 * (r >> 2);
         if (m >= a.M) continue;
         float v = acc[i][j][r] + bv;
         if (relu && !relu_after) v = fmaxf(v, 0.f);
-        // epilogue() order: conv + bias, (+ top-down) (+ residual)
-        if (gate) {
-          v = add[r] > 0.f ? v : 0.f;
-        } else if (a.topdown && a.residual) {
+        // epilogue() order: conv + bias, (+ top-down) (+ residual), gate last
+        // (the gate comes with Cout % 4 == 0 dgrads: normally the LDS epilogue)
+        if ((a.topdown && a.residual) || a.gate) {
           v = epilogue(a, acc[i][j][r], m, co);
         } else {
           v = v + add[r];
@@ -221,6 +222,87 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         a.y[(size_t)m * a.Cout + co] = v;
       }
     }
+  }
+}
+
+// LDS-staged epilogue (ConvArgs::lds_epi): the accumulators leave through
+// LDS one 32-row slab at a time as row-major float4s, so every store
+// instruction writes whole rows of the tile (BN * 4 bytes) instead of 32-float
+// column pieces, and the slab's residual / gate / top-down operands are
+// loaded as float4s BEFORE its LDS barrier (their latency overlaps the
+// transpose).  Same arithmetic order as epilogue(); split-K partials are
+// written raw.  smem: >= 32 * (BN + 4) floats of the kernel's LDS.
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&acc)[TM][TN],
+                                                  int m0, int n0, int wr, int wc, int lane,
+                                                  int split, float* smem) {
+  constexpr int BN = WN * TN * 32;
+  constexpr int LS = BN + 4;        // slab row stride (floats)
+  constexpr int F4 = BN / 4;        // float4 per tile row
+  constexpr int Q = 32 * F4 / 256;  // float4 per thread per slab
+  const int tid = threadIdx.x;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool part = a.splits > 1;
+  float* const dst = part ? a.partial + (size_t)split * (a.M - a.m_base) * a.Cout : a.y;
+  const int mrow0 = part ? a.m_base : 0;
+  const bool relu = (a.flags & kRelu) != 0, relu_after = (a.flags & kReluAfterResidual) != 0;
+  __syncthreads();  // the main loop's last LDS reads are complete
+#pragma unroll
+  for (int s = 0; s < WM * TM; ++s) {
+    float4 res[Q], gt[Q], td[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = idx / F4, c4 = idx - row * F4;
+      const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
+      res[q] = gt[q] = td[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!part && m < a.M && co < a.Cout) {
+        const size_t o = (size_t)m * a.Cout + co;
+        if (a.residual) res[q] = ld4(a.residual + o);
+        if (a.gate) gt[q] = ld4(a.gate + o);
+        if (a.topdown) {
+          const int n = m / (a.OH * a.OW);
+          const int rem = m - n * a.OH * a.OW;
+          const int oh = rem / a.OW, ow = rem - oh * a.OW;
+          td[q] = ld4(a.topdown + (((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout +
+                      co);
+        }
+      }
+    }
+    if (wr == s / TM) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          smem[((r & 3) + 8 * (r >> 2) + 4 * lh) * LS + (wc * TN + j) * 32 + li] = acc[s % TM][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = idx / F4, c4 = idx - row * F4;
+      const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
+      if (m >= a.M || co >= a.Cout) continue;
+      float4 v = *reinterpret_cast<const float4*>(&smem[row * LS + c4 * 4]);
+      if (!part) {
+        float* vv = reinterpret_cast<float*>(&v);
+        const float* rr = reinterpret_cast<const float*>(&res[q]);
+        const float* gg = reinterpret_cast<const float*>(&gt[q]);
+        const float* tt = reinterpret_cast<const float*>(&td[q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = vv[e] + (a.bias ? a.bias[co + e] : 0.f);
+          if (relu && !relu_after) x = fmaxf(x, 0.f);
+          if (a.topdown) x = x + tt[e];
+          if (a.residual) x = x + rr[e];
+          if (relu && relu_after) x = fmaxf(x, 0.f);
+          if (a.gate && !(gg[e] > 0.f)) x = 0.f;
+          vv[e] = x;
+        }
+      }
+      *reinterpret_cast<float4*>(dst + (size_t)(m - mrow0) * a.Cout + co) = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -237,6 +319,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   constexpr int B_WORDS = SPLIT ? 3 * BN * LDSB / 2 : BN * LDSP;
   __shared__ __attribute__((aligned(16))) float As[NB][A_WORDS];
   __shared__ __attribute__((aligned(16))) float Bs[NB][B_WORDS];
+  static_assert(NB * A_WORDS >= 32 * (BN + 4), "LDS epilogue slab does not fit in As");
 
   // XCD-aware tile order: consecutive tiles (the Cout tiles of one pixel tile
   // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
@@ -463,7 +546,10 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
-  store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+  if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
+    store_outputs_lds<WM, WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split, &As[0][0]);
+  else
+    store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
 }
 
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
@@ -478,6 +564,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
   constexpr int NB = DB ? 2 : 1;
   __shared__ __attribute__((aligned(16))) uint16_t As[NB][3 * BM * LDSB];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[NB][3 * BN * LDSB];
+  static_assert(NB * 3 * BM * LDSB / 2 >= 32 * (BN + 4), "LDS epilogue slab does not fit in As");
 
   const int orig = blockIdx.x;
   const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
@@ -624,7 +711,11 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
       }
     }
   }
-  store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+  if (WN * TN * 32 == 128 || a.lds_epi)
+    store_outputs_lds<WM, WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split,
+                                      reinterpret_cast<float*>(&As[0][0]));
+  else
+    store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
 }
 
 // x [n] f32 -> [3][n] bf16 planes (h, m, l of the exact truncation split).
@@ -703,9 +794,11 @@ static int wg_slots() {
   return slots;
 }
 
-Plan make_plan(int M, int Cout, int KH, int KW, int Cin) {
+// wide_ok: the 128x128 tile may be used -- its kernels only carry the LDS
+// epilogue (Cout % 4 == 0 and 16-B aligned operands); otherwise 128x64.
+Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   Plan p;
-  p.cfg = Cout <= 32 ? 2 : (Cout <= 64 ? 1 : 0);
+  p.cfg = Cout <= 32 ? 2 : (Cout <= 64 || !wide_ok ? 1 : 0);
   p.BM = 128;
   p.BN = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
   const int nM = (M + p.BM - 1) / p.BM, nN = (Cout + p.BN - 1) / p.BN;
@@ -808,16 +901,16 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
                                              int KW, int stride, int pad_beg, int pad_end) {
   int OH, OW;
   if (conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH, OW)) return 0;
-  const Plan p = make_plan(N * OH * OW, Cout, KH, KW, Cin);
+  const Plan p = make_plan(N * OH * OW, Cout, KH, KW, Cin, Cout % 4 == 0);
   return p.ws_bytes;
 }
 
 // Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
 static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
                      const uint16_t* w3, const float* bias, const float* topdown,
-                     const float* residual, float* y, int N, int H, int W, int Cin, int Cout,
-                     int KH, int KW, int stride, int pad_beg, int pad_end, int flags,
-                     void* workspace, size_t workspace_bytes, void* stream) {
+                     const float* residual, const float* gate, float* y, int N, int H, int W,
+                     int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
+                     int flags, void* workspace, size_t workspace_bytes, void* stream) {
   ConvArgs a;
   a.x = x;
   a.x3 = x3;
@@ -831,6 +924,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.bias = bias;
   a.topdown = topdown;
   a.residual = residual;
+  a.gate = gate;
   a.y = y;
   a.N = N;
   a.H = H;
@@ -845,7 +939,13 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
                "conv output is empty");
   a.flags = flags;
   a.M = N * a.OH * a.OW;
-  Plan p = make_plan(a.M, Cout, KH, KW, Cin);
+  {
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    static const char* off = getenv("D2MI_CONV_LDS_EPI");  // "0": register epilogue (A/B)
+    a.lds_epi = Cout % 4 == 0 && al16(y) && al16(residual) && al16(gate) && al16(topdown) &&
+                al16(workspace) && !(off && off[0] == '0');
+  }
+  Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
     p.splits = 1;
     p.kt_per_split = p.nk;
@@ -909,22 +1009,17 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
 }
 
 
-extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
-                                   const float* topdown, const float* residual, float* y, int N,
-                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
-                                   int pad_beg, int pad_end, int flags, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+// f32-operand conv with the >= 2 GiB-batch image chunking (32-bit buffer offsets).
+static int conv_f32(const float* x, const float* w_packed, const float* bias,
+                    const float* topdown, const float* residual, const float* gate, float* y,
+                    int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                    int pad_beg, int pad_end, int flags, void* workspace, size_t workspace_bytes,
+                    void* stream) {
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
   D2MI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_packed & 15) == 0,
                "x and w must be 16-byte aligned");
-  D2MI_REQUIRE((flags & ~31) == 0,
-               "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
-               "MFMA products, bit3 flipped weight taps, bit4 residual is a ReLU gate");
-  D2MI_REQUIRE(!(flags & kMaskByResidual) || (residual && !topdown && !(flags & 3)),
-               "the ReLU gate (bit4) needs the residual operand and no relu / top-down");
-  // 32-bit buffer offsets: batches whose input is >= 2 GiB run as image chunks
   const int64_t img_bytes = (int64_t)H * W * Cin * sizeof(float);
   D2MI_REQUIRE(img_bytes < (1ll << 31), "one conv input image must be < 2 GiB");
   D2MI_REQUIRE((int64_t)KH * KW * Cin * Cout * sizeof(float) < (1ll << 31),
@@ -938,16 +1033,48 @@ extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const 
     const size_t ts = (size_t)((OH0 + 1) / 2) * ((OW0 + 1) / 2) * Cout;
     for (int n0 = 0; n0 < N; n0 += chunk) {
       const int nn = std::min(chunk, N - n0);
-      const int rc = d2mi_conv2d_nhwc_ex(
+      const int rc = conv_f32(
           x + n0 * xs, w_packed, bias, topdown ? topdown + n0 * ts : nullptr,
-          residual ? residual + n0 * ys : nullptr, y + n0 * ys, nn, H, W, Cin, Cout, KH, KW,
-          stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+          residual ? residual + n0 * ys : nullptr, gate ? gate + n0 * ys : nullptr, y + n0 * ys,
+          nn, H, W, Cin, Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace,
+          workspace_bytes, stream);
       if (rc) return rc;
     }
     return 0;
   }
-  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, y, N, H, W, Cin, Cout,
-                   KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, gate, y, N, H, W, Cin,
+                   Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
+                   stream);
+}
+
+extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
+                                   const float* topdown, const float* residual, float* y, int N,
+                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                   int pad_beg, int pad_end, int flags, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE((flags & ~31) == 0,
+               "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
+               "MFMA products, bit3 flipped weight taps, bit4 residual is a ReLU gate");
+  D2MI_REQUIRE(!(flags & kMaskByResidual) || (residual && !topdown && !(flags & 3)),
+               "the ReLU gate (bit4) needs the residual operand and no relu / top-down");
+  if (flags & kMaskByResidual)
+    return conv_f32(x, w_packed, bias, nullptr, nullptr, residual, y, N, H, W, Cin, Cout, KH, KW,
+                    stride, pad_beg, pad_end, flags & ~kMaskByResidual, workspace,
+                    workspace_bytes, stream);
+  return conv_f32(x, w_packed, bias, topdown, residual, nullptr, y, N, H, W, Cin, Cout, KH, KW,
+                  stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+}
+
+extern "C" int d2mi_conv2d_nhwc_gated(const float* x, const float* w_packed, const float* bias,
+                                      const float* residual, const float* gate, float* y, int N,
+                                      int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                      int pad_beg, int pad_end, int flags, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE((flags & ~(kSplit3 | kFlipTaps)) == 0,
+               "gated conv flags: bit2 split-bf16 MFMA products, bit3 flipped weight taps");
+  D2MI_REQUIRE(gate != nullptr, "gated conv needs its gate");
+  return conv_f32(x, w_packed, bias, nullptr, residual, gate, y, N, H, W, Cin, Cout, KH, KW,
+                  stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
 }
 
 extern "C" int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const float* bias,
@@ -985,6 +1112,7 @@ extern "C" int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const
   D2MI_REQUIRE(3 * 2 * (int64_t)N * H * W * Cin < (1ll << 31),
                "pre-split conv input (3 bf16 planes) must be < 2 GiB; use d2mi_conv2d_nhwc_ex");
   D2MI_REQUIRE(3 * 2 * (int64_t)KH * KW * Cin * Cout < (1ll << 31), "conv weights too large");
-  return conv_core(nullptr, x3, nullptr, w3, bias, topdown, residual, y, N, H, W, Cin, Cout, KH,
-                   KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
+  return conv_core(nullptr, x3, nullptr, w3, bias, topdown, residual, nullptr, y, N, H, W, Cin,
+                   Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
+                   stream);
 }

@@ -41,9 +41,9 @@ def same_pads(kernel_size, rate=1):
     return pb, pad_total - pb
 
 
-def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None):
-    """Input gradient.  Stride 1: a forward conv of gy with the spatially
-    flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
+def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
+    """Input gradient (+ add, then the relu_gate mask, when given).  Stride 1:
+    a forward conv of gy with the spatially flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
     of the transposed conv, flipped by the kernel's tap indexing (kFlipTaps) —
     on the MFMA kernel, padded (KH-1-pb, KH-1-pe).
     1x1 stride s: the MFMA GEMM gy . W^T on the strided grid, scattered into
@@ -55,19 +55,19 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None):
             # the flip is an index flip inside the kernel (no flipped copy)
             return ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1,
                                    (KH - 1 - pb, KH - 1 - pe), flip_taps=KH > 1,
-                                   relu_gate=relu_gate)
-    if relu_gate is not None:
-        raise ValueError("relu_gate is fused into the stride-1 MFMA dgrad only")
+                                   residual=add, relu_gate=relu_gate)
         if KH == 1 and pb == 0 and pe == 0:
             g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
             gx[:, ::stride, ::stride] = g
-            return gx
+            return gx if add is None else gx.add_(add)
+    if relu_gate is not None:
+        raise ValueError("relu_gate is fused into the stride-1 MFMA dgrad only")
     xin_shape = (x_shape[0], x_shape[3], x_shape[1] + pb + pe, x_shape[2] + pb + pe)
     gx = torch.nn.grad.conv2d_input(xin_shape, w.permute(3, 2, 0, 1), gy.permute(0, 3, 1, 2),
                                     stride, 0)
-    gx = gx[:, :, pb:gx.shape[2] - pe, pb:gx.shape[3] - pe]
-    return gx.permute(0, 2, 3, 1)
+    gx = gx[:, :, pb:gx.shape[2] - pe, pb:gx.shape[3] - pe].permute(0, 2, 3, 1)
+    return gx if add is None else gx + add
 
 
 def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
@@ -112,11 +112,20 @@ class _ConvMFMAFn(torch.autograd.Function):
     SOLE consumer of that ReLU output: the bottleneck's conv2 / conv3, the mask
     head's conv chain and deconv) applies the producer's ReLU mask in its own
     dgrad epilogue (kMaskByResidual) and flags it; the producer then skips its
-    threshold_backward.  Without the declaration nothing is fused."""
+    threshold_backward.  Without the declaration nothing is fused.
+
+    Residual-gradient hand-off (the bottleneck's identity shortcut): the conv
+    that adds ``residual`` is given a dict ``res_grad_to`` and the conv that
+    reads the same tensor as its input the same dict as ``grad_from``.  The
+    adder's backward (always first: the reader's backward waits for the chain
+    in between) leaves the residual's gradient there instead of returning
+    it, and the reader adds it inside its dgrad epilogue -- before the ReLU
+    gate, so  gx = (dgrad + g_res) * (x > 0)  is one pass and autograd never
+    materialises the sum."""
 
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
-                relu_after=False, gate_input=False):
+                relu_after=False, gate_input=False, res_grad_to=None, grad_from=None):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
@@ -125,6 +134,8 @@ class _ConvMFMAFn(torch.autograd.Function):
         ctx.save_for_backward(x, w_hwio, y if relu else None)
         ctx.conf = (stride, pads, relu, bias is not None, topdown is not None, residual is not None)
         ctx.in_info = getattr(x, "_d2mi_relu_info", None) if gate_input else None
+        ctx.res_grad_to = res_grad_to if residual is not None else None
+        ctx.grad_from = grad_from
         ctx.out_info = None
         if relu:  # (forward runs with grad mode off: tag unconditionally)
             ctx.out_info = {"masked": False}
@@ -143,21 +154,25 @@ class _ConvMFMAFn(torch.autograd.Function):
             N, OH, OW, C = gy.shape
             g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
-        gres = gy if has_res else None
+        gres = gy if has_res and ctx.needs_input_grad[8] else None
+        if gres is not None and ctx.res_grad_to is not None:
+            ctx.res_grad_to["g"] = gres  # taken by the conv reading the same tensor
+            gres = None
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
+            add = ctx.grad_from.pop("g", None) if ctx.grad_from is not None else None
             info = ctx.in_info
             if info is not None and _gate_eligible(w.shape, stride, pb, pe):
-                gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x)
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=add)
                 info["masked"] = True
             else:
-                gx = _dgrad(gy, w, x.shape, stride, pb, pe)
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add)
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
             gb = ops.column_sum(gy)
-        return gx, gw, gb, None, None, None, None, gtd, gres, None, None
+        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None
 
 
 class FoldGroup:
@@ -311,7 +326,7 @@ class Conv2D(Layer):
         return self._packed
 
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
-             relu_input_sole_consumer=False):
+             relu_input_sole_consumer=False, res_grad_to=None, grad_from=None):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -339,7 +354,7 @@ class Conv2D(Layer):
                 packed = self.packed_weights(w)
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add,
-                                    bool(relu_input_sole_consumer))
+                                    bool(relu_input_sole_consumer), res_grad_to, grad_from)
             if norm is not None:
                 ret = norm(ret)
             if self.act_fn is not None and not fuse_relu:

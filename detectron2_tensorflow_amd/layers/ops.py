@@ -300,8 +300,9 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
     CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x.
     flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
-    relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv : 0
-    (a dgrad with its producer's ReLU backward fused)."""
+    relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv
+    (+ residual) : 0 (a dgrad with its producer's ReLU backward fused, and the
+    gradient of the producer's other consumer added first)."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -323,11 +324,13 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     if residual is not None:
         residual = _f32c(residual)
     if relu_gate is not None:
-        if residual is not None or topdown is not None or relu:
-            raise ValueError("relu_gate excludes residual / topdown / relu")
-        residual = _f32c(relu_gate)
-        if residual.shape != y.shape:
-            raise ValueError(f"relu_gate {tuple(residual.shape)} != output {tuple(y.shape)}")
+        if topdown is not None or relu:
+            raise ValueError("relu_gate excludes topdown / relu")
+        relu_gate = _f32c(relu_gate)
+        if relu_gate.shape != y.shape:
+            raise ValueError(f"relu_gate {tuple(relu_gate.shape)} != output {tuple(y.shape)}")
+    if residual is not None and residual.shape != y.shape:
+        raise ValueError(f"residual {tuple(residual.shape)} != output {tuple(y.shape)}")
     # measured policy (tools/bench_kernels.py --only conv): narrow Cout (the
     # 128x64 / 128x32 tiles) gains nothing from the split products.
     if math_mode == "split" and Cout <= 64:
@@ -335,8 +338,7 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     presplit = (math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps
                 and relu_gate is None) and (
         x_split is not None or (KH * KW > 1 and PRESPLIT_KXK))
-    flags = ((1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
-             | (16 if relu_gate is not None else 0))
+    flags = (1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
     if math_mode == "split" and not presplit:
         flags |= 4
     wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
@@ -351,6 +353,12 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                           _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
                                           int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
                                           _C.stream_of(x.device))
+    elif relu_gate is not None:
+        rc = _C.lib().d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
+                                             _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,
+                                             H, W, Cin, Cout, KH, KW, int(stride), int(pb),
+                                             int(pe), flags, _C.ptr(ws), wsb,
+                                             _C.stream_of(x.device))
     else:
         rc = _C.lib().d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                           _C.ptr(topdown), _C.ptr(residual), _C.ptr(y), N, H, W,
@@ -359,7 +367,9 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     fl = 2.0 * N * OH * OW * Cout * KH * KW * Cin
     KernelTimer.stop(ev, "conv2d_split" if math_mode == "split" else "conv2d_mfma", fl)
     if KernelTimer.detail and ev is not None:
-        KernelTimer.stop(ev, f"conv {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride} p{pb}{pe}", fl)
+        tag = ("g" if relu_gate is not None else "") + ("r" if residual is not None else "") + (
+            "f" if flip_taps else "")
+        KernelTimer.stop(ev, f"conv {N}x{H}x{W}x{Cin}->{Cout} k{KH} s{stride} p{pb}{pe} {tag}", fl)
     _C.check(rc, "d2mi_conv2d_nhwc")
     return y
 

@@ -37,6 +37,9 @@ class BottleneckBlock(Layer):
         # every conv runs on the MFMA implicit-GEMM kernel with FrozenBN folded
         # and ReLU / residual fused in its epilogue ("auto": a grouped or
         # dilated 3x3 falls back to MIOpen)
+        # set by Stage for blocks after the first: their input is the previous
+        # block's output and nothing else reads it (see call)
+        self.grad_handoff = False
         self.shortcut = None
         if in_channels != out_channels:
             self.shortcut = Conv2D(in_channels, out_channels, 1, stride=stride, activation=None,
@@ -53,10 +56,17 @@ class BottleneckBlock(Layer):
         sc = self.shortcut(x) if self.shortcut is not None else x
         # relu(conv3(...) + shortcut) in one kernel.  conv1 -> conv2 -> conv3 is
         # a chain of sole consumers: each one's dgrad applies the previous
-        # ReLU's mask (no separate ReLU-backward pass).
-        h = self.conv2(self.conv1(x), relu_input_sole_consumer=True)
+        # ReLU's mask (no separate ReLU-backward pass).  With an identity
+        # shortcut, conv3 hands its residual gradient to conv1, whose dgrad adds
+        # it before applying the mask of x (the previous block's ReLU output,
+        # read by nothing else inside a stage): conv1 then carries x's whole
+        # gradient -- no autograd add, no separate ReLU backward.
+        link = ({} if self.grad_handoff and self.shortcut is None and torch.is_grad_enabled()
+                else None)
+        h = self.conv1(x, relu_input_sole_consumer=link is not None, grad_from=link)
+        h = self.conv2(h, relu_input_sole_consumer=True)
         return self.conv3(h, residual=sc.contiguous(), final_relu=True,
-                          relu_input_sole_consumer=True)
+                          relu_input_sole_consumer=True, res_grad_to=link)
 
 
 @add_arg_scope
@@ -89,6 +99,8 @@ class Stage(Layer):
             if i > 0:
                 kw["in_channels"] = block_kwargs["out_channels"]
             self.blocks.append(block_class(**kw))
+            if i > 0 and hasattr(self.blocks[-1], "grad_handoff"):
+                self.blocks[-1].grad_handoff = True
 
     def call(self, x):
         for b in self.blocks:

@@ -232,6 +232,19 @@ int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias
                         int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
                         int pad_end, int flags, void* workspace, size_t workspace_bytes,
                         void* stream);
+/* Gated form, for an input gradient (dgrad) of a ReLU output x that feeds
+ * two consumers -- the next bottleneck's conv1 and its identity shortcut
+ * (lib/modeling/backbone/blocks.py:143-186): writes
+ *   y = gate > 0 ? conv(x, w) + bias + residual : 0
+ * i.e. the conv's input gradient plus the shortcut's gradient (residual),
+ * passed through the producer's ReLU backward (gate = its output), in one
+ * pass.  residual / bias nullable; flags: bit2 split products, bit3 flipped
+ * taps only. */
+int d2mi_conv2d_nhwc_gated(const float* x, const float* w_packed, const float* bias,
+                           const float* residual, const float* gate, float* y, int N, int H,
+                           int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
+                           int pad_end, int flags, void* workspace, size_t workspace_bytes,
+                           void* stream);
 /* flags bit2 = "split" products: the same f32 operands, each split EXACTLY
  * into three bf16 terms (x = h + m + l, truncation), multiplied with six
  * bf16 MFMA products (v_mfma_f32_32x32x16_bf16; the dropped m*l, l*m, l*l

@@ -875,3 +875,57 @@ def test_conv2d_tail_split_matches_float64(dev, epi):
     np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
     # the tail rows (the last 14 tiles) are really there
     assert torch.isfinite(y[-1, -1]).all() and float(y[-1, -1].abs().sum()) > 0
+
+
+@pytest.mark.parametrize("shape", [(2, 50, 84, 256, 64, 1), (2, 25, 42, 512, 2048, 1),
+                                   (2, 12, 15, 64, 64, 3), (1, 100, 168, 128, 512, 1)])
+def test_gated_conv_adds_residual_then_masks(dev, shape):
+    """d2mi_conv2d_nhwc_gated: y = gate > 0 ? conv + residual : 0 equals the
+    ungated conv-with-residual masked afterwards, bit for bit -- whole tiles,
+    split-K (small M) and the tail split, flipped taps for the 3x3 dgrad."""
+    N, H, W, Cin, Cout, k = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    w = (torch.randn(k, k, Cout, Cin, generator=g) / Cin ** 0.5).to(dev)
+    res = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    gate = torch.relu(torch.randn(N, H, W, Cout, generator=g)).to(dev)
+    p = (k // 2, k // 2)
+    for flip in ([False, True] if k > 1 else [False]):
+        want = ops().conv2d_nhwc(x, w, None, 1, p, residual=res, flip_taps=flip)
+        want = torch.where(gate > 0, want, torch.zeros_like(want))
+        got = ops().conv2d_nhwc(x, w, None, 1, p, residual=res, relu_gate=gate, flip_taps=flip)
+        assert torch.equal(got, want)
+        plain = ops().conv2d_nhwc(x, w, None, 1, p, relu_gate=gate, flip_taps=flip)
+        ref = ops().conv2d_nhwc(x, w, None, 1, p, flip_taps=flip)
+        assert torch.equal(plain, torch.where(gate > 0, ref, torch.zeros_like(ref)))
+
+
+def test_bottleneck_residual_gradient_handoff_is_exact(dev):
+    """A res3-like stage (blocks 2..4 hand their identity-shortcut gradient to
+    conv1's gated dgrad) gives exactly the gradients of the same stage with the
+    hand-off off (autograd add + ReLU backward; the latter is checked against
+    float64 autograd by test_relu_gate_fused_into_consumer_dgrad)."""
+    from detectron2_tensorflow_amd.modeling.backbone.resnet import BottleneckBlock, Stage
+    torch.manual_seed(3)
+    st = Stage(BottleneckBlock, {"in_channels": 64, "out_channels": 128,
+                                 "bottleneck_channels": 32, "stride_in_1x1": True}, 3, 1,
+               scope="res_t").to(dev)
+    assert [b.grad_handoff for b in st.blocks] == [False, True, True]
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 20, 24, 64, generator=g).to(dev)
+    gy = torch.randn(2, 20, 24, 128, generator=g).to(dev)
+    res = {}
+    for handoff in (True, False):
+        for b in st.blocks[1:]:
+            b.grad_handoff = handoff
+        st.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        y = st(xi)
+        y.backward(gy)
+        res[handoff] = (y.detach(), xi.grad, {n: p.grad.clone() for n, p in st.named_parameters()})
+    ya, gxa, gpa = res[True]
+    yb, gxb, gpb = res[False]
+    assert torch.equal(ya, yb) and torch.equal(gxa, gxb)
+    assert gpa.keys() == gpb.keys() and gpa
+    for n in gpa:
+        assert torch.equal(gpa[n], gpb[n]), n

@@ -17,6 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="train")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--no-handoff", action="store_true",
+                    help="bottleneck residual-gradient hand-off off (A/B)")
     a = ap.parse_args()
     import bench
     sys.argv = [sys.argv[0], "--mode", a.mode]
@@ -27,6 +29,10 @@ def main():
     from detectron2_tensorflow_amd.layers.ops import KernelTimer
     _C.load()
     cfg, model = bench.build(args, dev)
+    if a.no_handoff:
+        for m in model.modules():
+            if hasattr(m, "grad_handoff"):
+                m.grad_handoff = False
     batch = bench.synthetic_batch(args, dev, 0)
     bench.calibrate_scores(model, batch)
     if a.mode == "train":
