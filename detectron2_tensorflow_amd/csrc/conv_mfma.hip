@@ -104,9 +104,9 @@ struct ConvArgs {
   int N, H, W, Cin, Cout, KH, KW, stride, pad, OH, OW, flags;
   int M, nM, nN, ntiles, splits, kt_per_split, nk, cchunks;
   // this launch covers tiles [tile_base, tile_base + ntiles); split-K
-  // partials cover output rows [m_base, M) (the tail launch of a grid whose
+  // partials cover output rows [m_base, m_end) (a main launch and a tail launch
   // last round would run mostly empty, see conv_core)
-  int tile_base, m_base;
+  int tile_base, m_base, m_end;
   int lds_epi;  // store_outputs_lds usable (Cout % 4 == 0, 16-B aligned operands)
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
   // pre-split operands (conv_x3_kernel): 3 bf16 planes each, plane strides in bytes
@@ -163,7 +163,8 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         continue;
       }
       if (a.splits > 1) {
-        float* pp = a.partial + ((size_t)split * (a.M - a.m_base) + (mb - a.m_base)) * a.Cout + co;
+        float* pp =
+            a.partial + ((size_t)split * (a.m_end - a.m_base) + (mb - a.m_base)) * a.Cout + co;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int dm = (r & 3) + 8 * (r >> 2);
@@ -243,7 +244,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
   const int tid = threadIdx.x;
   const int li = lane & 31, lh = lane >> 5;
   const bool part = a.splits > 1;
-  float* const dst = part ? a.partial + (size_t)split * (a.M - a.m_base) * a.Cout : a.y;
+  float* const dst = part ? a.partial + (size_t)split * (a.m_end - a.m_base) * a.Cout : a.y;
   const int mrow0 = part ? a.m_base : 0;
   const bool relu = (a.flags & kRelu) != 0, relu_after = (a.flags & kReluAfterResidual) != 0;
   __syncthreads();  // the main loop's last LDS reads are complete
@@ -732,7 +733,7 @@ __global__ void split3_kernel(const float4* __restrict__ x, int64_t n4, uint2* _
 
 // Fixed-order split-K reduction + epilogue (deterministic).
 __global__ void splitk_reduce_kernel(ConvArgs a) {
-  const int64_t total = (int64_t)(a.M - a.m_base) * a.Cout;
+  const int64_t total = (int64_t)(a.m_end - a.m_base) * a.Cout;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
@@ -777,6 +778,7 @@ struct Plan {
   // tail split: the first full_tiles run as whole tiles, the remaining
   // tail_tiles (whole pixel-row blocks) split K tail_splits ways
   int full_tiles, tail_tiles, tail_splits, tail_kt_per_split;
+  int main_m_end;  // output rows of the main launch (its split-K partial rows)
   size_t ws_bytes;
 };
 
@@ -821,6 +823,7 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   p.tail_tiles = 0;
   p.tail_splits = 1;
   p.tail_kt_per_split = p.nk;
+  p.main_m_end = M;
   const int G = wg_slots();
   if (p.splits == 1 && p.ntiles > G && p.nk >= 8) {
     const int full = (p.ntiles / G) * G / nN * nN;
@@ -951,12 +954,14 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     p.kt_per_split = p.nk;
     p.full_tiles = p.ntiles;
     p.tail_tiles = 0;
+    p.main_m_end = a.M;
   }
   a.nM = (a.M + p.BM - 1) / p.BM;
   a.nN = (Cout + p.BN - 1) / p.BN;
   a.ntiles = p.full_tiles;
   a.tile_base = 0;
   a.m_base = 0;
+  a.m_end = p.main_m_end;
   a.splits = p.splits;
   a.kt_per_split = p.kt_per_split;
   a.nk = p.nk;
@@ -971,9 +976,11 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     t.tile_base = p.full_tiles;
     t.ntiles = p.tail_tiles;
     t.m_base = p.full_tiles / a.nN * p.BM;
+    t.m_end = a.M;
     t.splits = p.tail_splits;
     t.kt_per_split = p.tail_kt_per_split;
-    t.partial = (float*)workspace;
+    t.partial = (float*)workspace +
+                (p.splits > 1 ? (size_t)p.splits * p.main_m_end * Cout : (size_t)0);
   }
   // 128x128 tiles: single-buffered LDS (two barriers per k-step, 2 workgroups
   // per CU) measured faster than double-buffered (1 workgroup per CU) on every
@@ -992,7 +999,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
       launch_conv<false>(p.cfg, db, g, st, c);
     D2MI_LAUNCH_CHECK();
     if (c.splits > 1) {
-      const int64_t total = (int64_t)(c.M - c.m_base) * Cout;
+      const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
       const int gr = (int)std::min<int64_t>((total + 255) / 256, 4096);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gr), dim3(256), 0, st, c);
       D2MI_LAUNCH_CHECK();

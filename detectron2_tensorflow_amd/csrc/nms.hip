@@ -135,14 +135,20 @@ __global__ __launch_bounds__(64) void nms_scan_kernel(const uint64_t* __restrict
       out[pos] = idx[base + row];
     }
     if (kept >= max_out) break;
-    // propagate kept rows of tile t into the removal words of later tiles
+    // propagate kept rows of tile t into the removal words of later tiles.
+    // Tile t is not the last, so all its 64 rows exist: their words are
+    // loaded unconditionally, 16 in flight at a time, and masked by keptm
+    // (a loop over the kept rows only would wait on one load per row).
     for (int t2 = t + 1 + lane; t2 < nt; t2 += 64) {
       uint64_t acc = 0;
-      uint64_t m = keptm;
-      while (m) {
-        const int r = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        acc |= mask[(base + t * 64 + r) * T + t2];
+      const uint64_t* col = mask + (base + (size_t)t * 64) * T + t2;
+#pragma unroll
+      for (int r0 = 0; r0 < 64; r0 += 16) {
+        uint64_t v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = col[(size_t)(r0 + r) * T];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc |= ((keptm >> (r0 + r)) & 1ull) ? v[r] : 0ull;
       }
       removed[t2] |= acc;
     }
