@@ -75,6 +75,8 @@ _SIGS = {
     "d2mi_wgrad_skinny": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "d2mi_column_sum_workspace_size": (c_size_t, [ctypes.c_longlong, c_int]),
     "d2mi_column_sum": (c_int, [P, ctypes.c_longlong, c_int, P, P, c_size_t, P]),
+    "d2mi_upsample2x_grad": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_stride_scatter": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_sgd_table_sizes": (c_int, [P, P, P]),
     "d2mi_momentum_sgd": (c_int, [P, P, c_int, P, c_float, c_float, c_float, P]),
     "d2mi_fold_many_sizes": (c_int, [P, P]),

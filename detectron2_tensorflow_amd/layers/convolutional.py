@@ -15,6 +15,8 @@ wgrad on the MFMA wgrad kernel or hipBLASLt / MIOpen, whichever measured
 faster for the shape (see _wgrad); stride-2 KxK dgrad and Cout % 4 != 0 use
 torch.nn.grad.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -58,6 +60,8 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
                                    residual=add, relu_gate=relu_gate)
         if KH == 1 and pb == 0 and pe == 0:
             g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
+            if Cin % 4 == 0:  # zero holes + scatter (+ add) in one pass
+                return ops.stride_scatter(g, x_shape, stride, add)
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
             gx[:, ::stride, ::stride] = g
             return gx if add is None else gx.add_(add)
@@ -70,12 +74,15 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
     return gx if add is None else gx + add
 
 
+_WGRAD_1X1_MIN_P = int(os.environ.get("D2MI_WGRAD_1X1_MIN_P", "8192"))
+
+
 def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
     """(weight gradient HWIO, bias gradient or None).
 
     Routed by measurement (tools/bench_kernels.py --only wgrad, MI355X):
     with split products (the default, ops.CONV_MATH) every KxK and every 1x1
-    over >= 32k output pixels runs on the MFMA wgrad kernel (bias gradient
+    over >= 8k output pixels runs on the MFMA wgrad kernel (bias gradient
     fused; FPN p2 3x3 154 TF/s vs MIOpen's 122, mask-head 3x3 147 vs 110);
     smaller 1x1 -> X^T . dY as one hipBLASLt GEMM.  With f32 products the
     KxK go to MIOpen's igemm wrw, which beats the f32 MFMA kernel there."""
@@ -84,7 +91,9 @@ def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
     eligible = Cin % 4 == 0 and Cout % 4 == 0
     if KH == 1 and KW == 1 and pb == 0 and pe == 0:
         P = gy.numel() // Cout
-        if P >= 32768 and eligible:
+        # tools/exp_wgrad_1x1.py: MFMA from 8400 pixels (res4: 54 vs 64-79 us
+        # on hipBLASLt), and the strided 1024->2048 at 2100; hipBLASLt below
+        if eligible and (P >= _WGRAD_1X1_MIN_P or (stride > 1 and Cin * Cout >= 2 ** 21)):
             if want_bias:
                 return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0), with_bias=True)
             return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0)), None
@@ -150,7 +159,9 @@ class _ConvMFMAFn(torch.autograd.Function):
             # relu is the last op whenever an add is fused (relu_after)
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)
         gtd = None
-        if has_td:
+        if has_td and gy.shape[-1] % 4 == 0:
+            gtd = ops.upsample2x_grad(gy)
+        elif has_td:
             N, OH, OW, C = gy.shape
             g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))

@@ -466,6 +466,36 @@ def fold_frozen_bn(w_hwio, bias, gamma, beta, mean, var, eps, want_packed=False)
                                  bool(want_packed))
 
 
+def upsample2x_grad(gy):
+    """Adjoint of the FPN top-down nearest 2x upsample (d2mi_upsample2x_grad):
+    gy [N, OH, OW, C] -> [N, ceil(OH/2), ceil(OW/2), C]."""
+    gy = _f32c(gy)
+    _C.require_device(gy)
+    N, OH, OW, C = gy.shape
+    out = torch.empty((N, (OH + 1) // 2, (OW + 1) // 2, C), dtype=torch.float32, device=gy.device)
+    rc = _C.lib().d2mi_upsample2x_grad(_C.ptr(gy), N, OH, OW, C, _C.ptr(out),
+                                       _C.stream_of(gy.device))
+    _C.check(rc, "d2mi_upsample2x_grad")
+    return out
+
+
+def stride_scatter(g, out_shape, stride, add=None):
+    """Input gradient of a 1x1 stride-s conv from its GEMM on the strided grid
+    (d2mi_stride_scatter): zeros off the grid, plus add (nullable)."""
+    g = _f32c(g)
+    add = _f32c(add) if add is not None else None
+    _C.require_device(g)
+    N, H, W, C = out_shape
+    if g.shape != (N, (H - 1) // stride + 1, (W - 1) // stride + 1, C):
+        raise ValueError(f"stride_scatter: {tuple(g.shape)} is not the stride-{stride} grid of "
+                         f"{tuple(out_shape)}")
+    out = torch.empty(tuple(out_shape), dtype=torch.float32, device=g.device)
+    rc = _C.lib().d2mi_stride_scatter(_C.ptr(g), _C.ptr(add), N, H, W, C, int(stride),
+                                      _C.ptr(out), _C.stream_of(g.device))
+    _C.check(rc, "d2mi_stride_scatter")
+    return out
+
+
 _FOLD_DT = np.dtype([(n, np.uint64) for n in (
     "w", "bias", "gamma", "beta", "mean", "var", "w_eff", "w_packed", "b_eff", "gw_eff", "gb_eff",
     "gw", "gbias", "ggamma", "gbeta")] + [("eps", np.float32)] + [(n, np.int32) for n in (

@@ -378,6 +378,18 @@ size_t d2mi_column_sum_workspace_size(long long rows, int cols);
 int d2mi_column_sum(const float* x, long long rows, int cols, float* out, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------ resampling gradients
+ * d2mi_upsample2x_grad: adjoint of the FPN top-down nearest 2x upsample
+ * (lib/modeling/backbone/fpn.py:138-149): gy [N,OH,OW,C] -> gtd
+ * [N,ceil(OH/2),ceil(OW/2),C], each the sum of the (up to) 2x2 pixels that
+ * copy it, in the order (0,0), (0,1), (1,0), (1,1).
+ * d2mi_stride_scatter: input gradient of a 1x1 stride-s conv from its GEMM on
+ * the strided grid: g [N,ceil(H/s),ceil(W/s),C] -> out [N,H,W,C] with zeros
+ * off the grid, plus add [N,H,W,C] (nullable).  C % 4 == 0, 16-B aligned. */
+int d2mi_upsample2x_grad(const float* gy, int N, int OH, int OW, int C, float* gtd, void* stream);
+int d2mi_stride_scatter(const float* g, const float* add, int N, int H, int W, int C, int stride,
+                        float* out, void* stream);
+
 /* ------------------------------------------------------ Momentum-SGD step
  * Replaces the update of lib/engine/trainer.py:116-139 for every trainable
  * tensor in two launches: g' = g + wd * w (slim.l2_regularizer gradient,

@@ -930,3 +930,24 @@ def test_bottleneck_residual_gradient_handoff_is_exact(dev):
     assert gpa.keys() == gpb.keys() and gpa
     for n in gpa:
         assert torch.equal(gpa[n], gpb[n]), n
+
+
+@pytest.mark.parametrize("shape", [(2, 25, 42, 256), (1, 7, 5, 8), (2, 200, 336, 16)])
+def test_upsample2x_grad_and_stride_scatter(dev, shape):
+    """d2mi_upsample2x_grad equals the 2x2 sum-pool of the zero-padded gradient
+    (odd maps included); d2mi_stride_scatter equals zeros + strided copy (+ add)."""
+    g = torch.Generator().manual_seed(sum(shape))
+    N, H, W, C = shape
+    gy = torch.randn(N, H, W, C, generator=g)
+    want = torch.nn.functional.pad(gy.double(), (0, 0, 0, W % 2, 0, H % 2))
+    want = want.reshape(N, (H + 1) // 2, 2, (W + 1) // 2, 2, C).sum((2, 4))
+    got = ops().upsample2x_grad(gy.to(dev)).cpu().double()
+    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-6, atol=1e-6)
+    for s in (2, 3):
+        gs = torch.randn(N, (H - 1) // s + 1, (W - 1) // s + 1, C, generator=g)
+        add = torch.randn(N, H, W, C, generator=g)
+        ref = torch.zeros(N, H, W, C)
+        ref[:, ::s, ::s] = gs
+        assert torch.equal(ops().stride_scatter(gs.to(dev), (N, H, W, C), s).cpu(), ref)
+        assert torch.equal(ops().stride_scatter(gs.to(dev), (N, H, W, C), s, add.to(dev)).cpu(),
+                           ref + add)
