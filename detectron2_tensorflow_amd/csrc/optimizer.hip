@@ -47,6 +47,16 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;  // valid in thread 0
 }
 
+// float4 body when every pointer of the tensor is 16-B aligned (chunk
+// boundaries are multiples of kChunk), scalar tail; 4 vectors in flight per
+// thread.  Per-thread sums are in a fixed order, so results stay deterministic.
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+__device__ __forceinline__ float sq_term(const SgdTensor& t, long long i) {
+  const float g = (t.g ? t.g[i] : 0.f) + t.wd * t.w[i];
+  return g * g;
+}
+
 __global__ __launch_bounds__(256) void sgd_sumsq_kernel(const SgdTensor* __restrict__ tensors,
                                                         const SgdChunk* __restrict__ chunks,
                                                         float* __restrict__ partial) {
@@ -54,18 +64,30 @@ __global__ __launch_bounds__(256) void sgd_sumsq_kernel(const SgdTensor* __restr
   const SgdChunk c = chunks[blockIdx.x];
   const SgdTensor t = tensors[c.tensor];
   float s = 0.f;
-  if (t.g && t.wd == 0.f) {
-    for (long long i = c.begin + threadIdx.x; i < c.end; i += blockDim.x) s += t.g[i] * t.g[i];
-  } else if (t.g) {
-    for (long long i = c.begin + threadIdx.x; i < c.end; i += blockDim.x) {
-      const float g = t.g[i] + t.wd * t.w[i];
-      s += g * g;
+  if (t.g || t.wd != 0.f) {
+    long long i0 = c.begin;
+    if (al16(t.w) && (!t.g || al16(t.g))) {
+      const long long n4 = (c.end - c.begin) / 4;
+      const float4* g4 = t.g ? reinterpret_cast<const float4*>(t.g + c.begin) : nullptr;
+      const float4* w4 = reinterpret_cast<const float4*>(t.w + c.begin);
+#pragma unroll 4
+      for (long long k = threadIdx.x; k < n4; k += blockDim.x) {
+        float4 g = g4 ? g4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t.wd != 0.f) {
+          const float4 w = w4[k];
+          g.x = g.x + t.wd * w.x;
+          g.y = g.y + t.wd * w.y;
+          g.z = g.z + t.wd * w.z;
+          g.w = g.w + t.wd * w.w;
+        }
+        s += g.x * g.x;
+        s += g.y * g.y;
+        s += g.z * g.z;
+        s += g.w * g.w;
+      }
+      i0 = c.begin + 4 * n4;
     }
-  } else if (t.wd != 0.f) {
-    for (long long i = c.begin + threadIdx.x; i < c.end; i += blockDim.x) {
-      const float g = t.wd * t.w[i];
-      s += g * g;
-    }
+    for (long long i = i0 + threadIdx.x; i < c.end; i += blockDim.x) s += sq_term(t, i);
   }
   const float tot = block_sum(s, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = tot;
@@ -88,13 +110,37 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(const SgdTensor* __rest
   }
   __syncthreads();
   const float div = scale_s;
-  for (long long i = c.begin + threadIdx.x; i < c.end; i += blockDim.x) {
-    const float w = t.w[i];
-    float g = (t.g ? t.g[i] : 0.f) + t.wd * w;
+  auto upd = [&](float w, float g, float a, float& wo, float& ao) {
+    g = g + t.wd * w;
     if (div > 0.f) g = g * clip / div;
-    const float a = t.accum[i] * momentum + g;
-    t.accum[i] = a;
-    t.w[i] = w - lr * a;
+    ao = a * momentum + g;
+    wo = w - lr * ao;
+  };
+  long long i0 = c.begin;
+  if (al16(t.w) && al16(t.accum) && (!t.g || al16(t.g))) {
+    const long long n4 = (c.end - c.begin) / 4;
+    float4* w4 = reinterpret_cast<float4*>(t.w + c.begin);
+    float4* a4 = reinterpret_cast<float4*>(t.accum + c.begin);
+    const float4* g4 = t.g ? reinterpret_cast<const float4*>(t.g + c.begin) : nullptr;
+#pragma unroll 4
+    for (long long k = threadIdx.x; k < n4; k += blockDim.x) {
+      const float4 w = w4[k], a = a4[k];
+      const float4 g = g4 ? g4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 wo, ao;
+      upd(w.x, g.x, a.x, wo.x, ao.x);
+      upd(w.y, g.y, a.y, wo.y, ao.y);
+      upd(w.z, g.z, a.z, wo.z, ao.z);
+      upd(w.w, g.w, a.w, wo.w, ao.w);
+      a4[k] = ao;
+      w4[k] = wo;
+    }
+    i0 = c.begin + 4 * n4;
+  }
+  for (long long i = i0 + threadIdx.x; i < c.end; i += blockDim.x) {
+    float wo, ao;
+    upd(t.w[i], t.g ? t.g[i] : 0.f, t.accum[i], wo, ao);
+    t.accum[i] = ao;
+    t.w[i] = wo;
   }
 }
 
