@@ -744,6 +744,34 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
   }
 }
 
+// float4 form (Cout % 4 == 0, 16-B aligned partial / y): same split order.
+__global__ void splitk_reduce4_kernel(ConvArgs a) {
+  const int64_t total = (int64_t)(a.m_end - a.m_base) * a.Cout;
+  const int64_t total4 = total / 4;
+  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int s = 0; s < a.splits; ++s) {
+      const float4 v = p4[(size_t)s * total4 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    const int64_t e = 4 * i;
+    const int ml = (int)(e / a.Cout), co = (int)(e - (int64_t)ml * a.Cout);
+    const int m = a.m_base + ml;
+    float4 o;
+    o.x = epilogue(a, acc.x, m, co);
+    o.y = epilogue(a, acc.y, m, co + 1);
+    o.z = epilogue(a, acc.z, m, co + 2);
+    o.w = epilogue(a, acc.w, m, co + 3);
+    *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
+  }
+}
+
 __global__ void pack_weights_kernel(const float* __restrict__ w, int taps, int Cin, int Cout,
                                     float* __restrict__ out) {
   const int64_t total = (int64_t)taps * Cin * Cout;
@@ -1000,8 +1028,13 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     D2MI_LAUNCH_CHECK();
     if (c.splits > 1) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
-      const int gr = (int)std::min<int64_t>((total + 255) / 256, 4096);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gr), dim3(256), 0, st, c);
+      if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+        const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);
+        hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(gr), dim3(256), 0, st, c);
+      } else {
+        const int gr = (int)std::min<int64_t>((total + 255) / 256, 4096);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gr), dim3(256), 0, st, c);
+      }
       D2MI_LAUNCH_CHECK();
     }
     return 0;

@@ -179,6 +179,34 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
 
 // Fixed split order (deterministic); the last Cout entries are the bias
 // gradient when pbias follows the weight partials.
+// float4 form (total % 4 == 0, 16-B aligned): the same per-element split
+// order, four elements and their split loads in flight per thread.
+__global__ void wgrad_reduce4_kernel(const float4* __restrict__ partial, int splits, size_t total4,
+                                     float4* __restrict__ dw, const float* __restrict__ pbias,
+                                     int Cout, float* __restrict__ dbias) {
+  const size_t n = total4 + (dbias ? (size_t)Cout : 0);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    if (i < total4) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+      for (int k = 0; k < splits; ++k) {
+        const float4 v = partial[(size_t)k * total4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      dw[i] = s;
+    } else {
+      const size_t c = i - total4;
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += pbias[(size_t)k * Cout + c];
+      dbias[c] = s;
+    }
+  }
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int splits, size_t total,
                                     float* __restrict__ dw, const float* __restrict__ pbias,
                                     int Cout, float* __restrict__ dbias) {
@@ -528,9 +556,17 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
   D2MI_LAUNCH_CHECK();
   if (a.splits > 1) {
     const size_t total = (size_t)KH * KW * Cin * Cout;
-    const int g = (int)std::min<size_t>((total + Cout + 255) / 256, 4096);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g), dim3(256), 0, st, a.partial, a.splits, total,
-                       dw_hwio, a.pbias, Cout, dbias);
+    if (total % 4 == 0 && ((uintptr_t)a.partial & 15) == 0 && ((uintptr_t)dw_hwio & 15) == 0) {
+      const size_t total4 = total / 4;
+      const int g4 = (int)std::min<size_t>((total4 + Cout + 255) / 256, 8192);
+      hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3(g4), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(a.partial), a.splits, total4,
+                         reinterpret_cast<float4*>(dw_hwio), a.pbias, Cout, dbias);
+    } else {
+      const int g = (int)std::min<size_t>((total + Cout + 255) / 256, 4096);
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g), dim3(256), 0, st, a.partial, a.splits,
+                         total, dw_hwio, a.pbias, Cout, dbias);
+    }
     D2MI_LAUNCH_CHECK();
   }
   return 0;

@@ -23,12 +23,12 @@ import sys
 # memsets and the rocPRIM radix sort it also launches are not attributable by
 # name and are left out).
 GROUPS = {
-    "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce_kernel"),
+    "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce4?_kernel"),
                      re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel")),
     "conv2d_mfma": (re.compile(r"conv_mfma_kernel<[^>]*, false>"), None),
     "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),
     "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_pixel_kernel")),
-    "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce_kernel"),
+    "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce4?_kernel"),
                          re.compile(r"conv_wgrad_split_kernel")),
     "conv_wgrad": (re.compile(r"conv_wgrad_kernel<"), None),
 }
