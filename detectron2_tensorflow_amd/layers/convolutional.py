@@ -130,11 +130,18 @@ class _ConvMFMAFn(torch.autograd.Function):
     in between) leaves the residual's gradient there instead of returning
     it, and the reader adds it inside its dgrad epilogue -- before the ReLU
     gate, so  gx = (dgrad + g_res) * (x > 0)  is one pass and autograd never
-    materialises the sum."""
+    materialises the sum.
+
+    Pair hand-off (``pair_grad``: the bottleneck's conv1 and projection
+    shortcut, both reading x): whichever backward runs first leaves its input
+    gradient in the shared dict and returns none for x; the second adds it in
+    its own dgrad epilogue / stride scatter and returns the sum.  Both always
+    run once the block output has a gradient (each feeds it)."""
 
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
-                relu_after=False, gate_input=False, res_grad_to=None, grad_from=None):
+                relu_after=False, gate_input=False, res_grad_to=None, grad_from=None,
+                pair_grad=None):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
@@ -145,6 +152,7 @@ class _ConvMFMAFn(torch.autograd.Function):
         ctx.in_info = getattr(x, "_d2mi_relu_info", None) if gate_input else None
         ctx.res_grad_to = res_grad_to if residual is not None else None
         ctx.grad_from = grad_from
+        ctx.pair_grad = pair_grad
         ctx.out_info = None
         if relu:  # (forward runs with grad mode off: tag unconditionally)
             ctx.out_info = {"masked": False}
@@ -172,18 +180,31 @@ class _ConvMFMAFn(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             add = ctx.grad_from.pop("g", None) if ctx.grad_from is not None else None
-            info = ctx.in_info
+            pair = ctx.pair_grad
+            deposit = False
+            if pair is not None:
+                other = pair.pop("g", None)
+                if other is None:
+                    deposit = True  # first of the pair: no gate, no add
+                elif add is None:
+                    add = other
+                else:
+                    add = add + other
+            info = None if deposit else ctx.in_info
             if info is not None and _gate_eligible(w.shape, stride, pb, pe):
                 gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=add)
                 info["masked"] = True
             else:
                 gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add)
+            if deposit:
+                pair["g"] = gx
+                gx = None
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
             gb = ops.column_sum(gy)
-        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None
+        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None
 
 
 class FoldGroup:
@@ -337,7 +358,7 @@ class Conv2D(Layer):
         return self._packed
 
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
-             relu_input_sole_consumer=False, res_grad_to=None, grad_from=None):
+             relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -365,7 +386,8 @@ class Conv2D(Layer):
                 packed = self.packed_weights(w)
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add,
-                                    bool(relu_input_sole_consumer), res_grad_to, grad_from)
+                                    bool(relu_input_sole_consumer), res_grad_to, grad_from,
+                                    pair_grad)
             if norm is not None:
                 ret = norm(ret)
             if self.act_fn is not None and not fuse_relu:

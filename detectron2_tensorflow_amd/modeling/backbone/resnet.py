@@ -40,6 +40,7 @@ class BottleneckBlock(Layer):
         # set by Stage for blocks after the first: their input is the previous
         # block's output and nothing else reads it (see call)
         self.grad_handoff = False
+        self.grad_pair = True  # conv1 / projection-shortcut pair hand-off (see call)
         self.shortcut = None
         if in_channels != out_channels:
             self.shortcut = Conv2D(in_channels, out_channels, 1, stride=stride, activation=None,
@@ -53,7 +54,11 @@ class BottleneckBlock(Layer):
                             scope="conv3")
 
     def call(self, x):
-        sc = self.shortcut(x) if self.shortcut is not None else x
+        # projection shortcut: it and conv1 both read x; their input gradients
+        # meet in the second one's epilogue instead of an autograd add
+        pair = ({} if self.grad_pair and self.shortcut is not None and torch.is_grad_enabled()
+                else None)
+        sc = self.shortcut(x, pair_grad=pair) if self.shortcut is not None else x
         # relu(conv3(...) + shortcut) in one kernel.  conv1 -> conv2 -> conv3 is
         # a chain of sole consumers: each one's dgrad applies the previous
         # ReLU's mask (no separate ReLU-backward pass).  With an identity
@@ -63,7 +68,7 @@ class BottleneckBlock(Layer):
         # gradient -- no autograd add, no separate ReLU backward.
         link = ({} if self.grad_handoff and self.shortcut is None and torch.is_grad_enabled()
                 else None)
-        h = self.conv1(x, relu_input_sole_consumer=link is not None, grad_from=link)
+        h = self.conv1(x, relu_input_sole_consumer=link is not None, grad_from=link, pair_grad=pair)
         h = self.conv2(h, relu_input_sole_consumer=True)
         return self.conv3(h, residual=sc.contiguous(), final_relu=True,
                           relu_input_sole_consumer=True, res_grad_to=link)

@@ -901,24 +901,27 @@ def test_gated_conv_adds_residual_then_masks(dev, shape):
         assert torch.equal(plain, torch.where(gate > 0, ref, torch.zeros_like(ref)))
 
 
-def test_bottleneck_residual_gradient_handoff_is_exact(dev):
-    """A res3-like stage (blocks 2..4 hand their identity-shortcut gradient to
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bottleneck_residual_gradient_handoff_is_exact(dev, stride):
+    """A res3-like stage (block 1's conv1 / projection shortcut meet in one
+    dgrad epilogue; blocks 2..3 hand their identity-shortcut gradient to
     conv1's gated dgrad) gives exactly the gradients of the same stage with the
-    hand-off off (autograd add + ReLU backward; the latter is checked against
+    hand-offs off (autograd add + ReLU backward; the latter is checked against
     float64 autograd by test_relu_gate_fused_into_consumer_dgrad)."""
     from detectron2_tensorflow_amd.modeling.backbone.resnet import BottleneckBlock, Stage
     torch.manual_seed(3)
     st = Stage(BottleneckBlock, {"in_channels": 64, "out_channels": 128,
-                                 "bottleneck_channels": 32, "stride_in_1x1": True}, 3, 1,
+                                 "bottleneck_channels": 32, "stride_in_1x1": True}, 3, stride,
                scope="res_t").to(dev)
     assert [b.grad_handoff for b in st.blocks] == [False, True, True]
     g = torch.Generator().manual_seed(4)
     x = torch.randn(2, 20, 24, 64, generator=g).to(dev)
-    gy = torch.randn(2, 20, 24, 128, generator=g).to(dev)
+    gy = torch.randn(2, 20 // stride, 24 // stride, 128, generator=g).to(dev)
     res = {}
     for handoff in (True, False):
         for b in st.blocks[1:]:
             b.grad_handoff = handoff
+        st.blocks[0].grad_pair = handoff
         st.zero_grad(set_to_none=True)
         xi = x.clone().requires_grad_(True)
         y = st(xi)
