@@ -466,6 +466,34 @@ def fold_frozen_bn(w_hwio, bias, gamma, beta, mean, var, eps, want_packed=False)
                                  bool(want_packed))
 
 
+def match_boxes(gt_boxes, gt_flags, boxes, thresholds, labels_of, allow_low_quality,
+                crowd_thr=1e-3, difficult_thr=float("inf")):
+    """Fused pairwise IoU + Matcher (d2mi_match_boxes): gt_boxes [N, G, 4],
+    gt_flags [N, G] int (bit0 matchable, bit1 crowd, bit2 difficult), boxes
+    [P, 4] (shared) or [N, P, 4]; thresholds with the -inf / +inf ends.
+    Returns (matches int64 [N, P], labels int64 [N, P])."""
+    gt_boxes = _f32c(gt_boxes)
+    boxes = _f32c(boxes)
+    gt_flags = _i32c(gt_flags)
+    _C.require_device(gt_boxes, gt_flags, boxes)
+    N, G = gt_flags.shape
+    per_image = boxes.dim() == 3
+    P = boxes.shape[-2]
+    matches = torch.empty((N, P), dtype=torch.int64, device=boxes.device)
+    labels = torch.empty((N, P), dtype=torch.int64, device=boxes.device)
+    thr = _C.host_array(_C.c_float, [float(t) for t in thresholds])
+    lab = _C.host_array(_C.ctypes.c_int32, [int(v) for v in labels_of])
+    wsb = _C.lib().d2mi_match_workspace_size(N, G)
+    ws = _C.workspace(wsb, boxes.device)
+    rc = _C.lib().d2mi_match_boxes(_C.ptr(gt_boxes), _C.ptr(gt_flags), _C.ptr(boxes),
+                                   int(per_image), N, G, P, thr, lab, len(labels_of),
+                                   int(bool(allow_low_quality)), float(crowd_thr),
+                                   float(difficult_thr), _C.ptr(matches), _C.ptr(labels),
+                                   _C.ptr(ws), wsb, _C.stream_of(boxes.device))
+    _C.check(rc, "d2mi_match_boxes")
+    return matches, labels
+
+
 def upsample2x_grad(gy):
     """Adjoint of the FPN top-down nearest 2x upsample (d2mi_upsample2x_grad):
     gy [N, OH, OW, C] -> [N, ceil(OH/2), ceil(OW/2), C]."""

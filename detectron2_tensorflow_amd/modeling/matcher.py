@@ -9,6 +9,8 @@ picks the k smallest of per-element uniform keys among the candidates
 """
 import torch
 
+from ..layers import ops
+
 
 def pairwise_iou(boxes1, boxes2):
     """box_list_ops.pairwise_iou (:295-372) batched: [N, G, 4] x [N, P, 4] -> [N, G, P];
@@ -62,6 +64,29 @@ class Matcher:
             diff = difficult_quality.max(dim=1).values > self.thresholds[1]
             labels = torch.where((labels == 0) & diff, torch.full_like(labels, -1), labels)
         return matches, labels
+
+
+def match_boxes(matcher, gt_boxes, matchable, boxes, crowd=None, difficult=None):
+    """pairwise_iou(gt_boxes, boxes) + matcher(...) with crowd / difficult
+    quality rows (rpn_outputs.py:306-330, roi_heads.py:160-216).  On the GPU
+    one fused HIP pass (ops.match_boxes: no [N, G, P] IoU matrix); elsewhere
+    the tensor formulation.  boxes [P, 4] shared or [N, P, 4]."""
+    N = gt_boxes.shape[0]
+    if boxes.is_cuda:
+        flags = matchable.to(torch.int32)
+        if crowd is not None:
+            flags = flags | (crowd.to(torch.int32) << 1)
+        if difficult is not None:
+            flags = flags | (difficult.to(torch.int32) << 2)
+        return ops.match_boxes(gt_boxes, flags, boxes, matcher.thresholds, matcher.labels,
+                               matcher.allow_low_quality_matches, crowd_thr=1e-3,
+                               difficult_thr=matcher.thresholds[1])
+    b = boxes if boxes.dim() == 3 else boxes[None].expand(N, -1, -1)
+    iou = pairwise_iou(gt_boxes, b)
+    zq = torch.zeros_like(iou)
+    crowd_q = torch.where(crowd[..., None], iou, zq) if crowd is not None else None
+    diff_q = torch.where(difficult[..., None], iou, zq) if difficult is not None else None
+    return matcher(iou, matchable, crowd_q, diff_q)
 
 
 def subsample_labels(labels, num_samples, positive_fraction, bg_label, generator=None):

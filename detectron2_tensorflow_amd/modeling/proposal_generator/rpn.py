@@ -12,7 +12,7 @@ from ...layers import Conv2D, Layer
 from ...layers import initializers as init
 from ...layers import ops
 from ...layers.loss import smooth_l1_loss
-from ..matcher import Matcher, pairwise_iou, subsample_labels
+from ..matcher import Matcher, match_boxes, subsample_labels
 from ...structures import BoxList
 from ...utils.arg_scope import arg_scope
 from ...utils.registry import Registry
@@ -160,9 +160,8 @@ class RPN(Layer):
         valid = gt["is_valid"]
         crowd = gt.get("gt_is_crowd")
         crowd = crowd.bool() if crowd is not None else torch.zeros_like(valid)
-        iou = pairwise_iou(gt_boxes, anchors[None].expand(N, -1, -1))
-        crowd_q = torch.where(crowd[..., None], iou, torch.zeros_like(iou))
-        matches, labels = self.anchor_matcher(iou, valid & ~crowd, crowd_q)
+        matches, labels = match_boxes(self.anchor_matcher, gt_boxes, valid & ~crowd, anchors,
+                                      crowd=crowd)
         if self.boundary_threshold >= 0:
             # legacy inside_window filter (rpn_outputs.py:268-277, box_list_ops.py:150)
             t = float(self.boundary_threshold)

@@ -15,7 +15,7 @@ from ...utils.registry import Registry
 from ..box_regression import Box2BoxTransform
 from ..poolers import ROIPooler
 from .box_head import build_box_head
-from ..matcher import Matcher, pairwise_iou, subsample_labels
+from ..matcher import Matcher, match_boxes, subsample_labels
 from .fast_rcnn import FastRCNNOutputLayers, fast_rcnn_inference, fast_rcnn_losses
 from .mask_head import build_mask_head, mask_rcnn_inference, mask_rcnn_loss
 
@@ -67,11 +67,8 @@ class ROIHeads(Layer):
             boxes = torch.cat([boxes, gt_boxes.to(boxes.dtype)], dim=1)
             pvalid = torch.cat([pvalid, gvalid], dim=1)
         M = boxes.shape[1]
-        iou = pairwise_iou(gt_boxes, boxes)
-        zq = torch.zeros_like(iou)
-        matches, labels = self.proposal_matcher(
-            iou, gvalid & ~crowd & ~difficult, torch.where(crowd[..., None], iou, zq),
-            torch.where(difficult[..., None], iou, zq))
+        matches, labels = match_boxes(self.proposal_matcher, gt_boxes, gvalid & ~crowd & ~difficult,
+                                      boxes, crowd=crowd, difficult=difficult)
         K = self.num_classes
         gcls = torch.gather(targets["gt_classes"].long(), 1, matches)
         gt_classes = torch.where(labels == 1, gcls,

@@ -378,6 +378,25 @@ size_t d2mi_column_sum_workspace_size(long long rows, int cols);
 int d2mi_column_sum(const float* x, long long rows, int cols, float* out, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------ IoU + Matcher
+ * box_list_ops.pairwise_iou (:295-372) of gt_boxes [N,G,4] against boxes
+ * ([P,4] shared by every image, or [N,P,4] with boxes_per_image = 1; yxyx
+ * f32, 16-B aligned) fused with Matcher.__call__ (lib/modeling/matcher.py:
+ * 8-173): matches [N,P] int64 = the first GT of maximal IoU among the
+ * matchable GT (gt_flags bit0), labels [N,P] int64 from the n_intervals
+ * intervals [thresholds[i], thresholds[i+1]) -> labels_of[i], low-quality
+ * matches (IoU equal to that GT's best over all boxes -> 1) when
+ * allow_low_quality, no matchable GT -> 0 / match 0, then -1 for background
+ * boxes whose max IoU with a crowd GT (bit1) exceeds crowd_thr or with a
+ * difficult GT (bit2) exceeds difficult_thr.  G <= 256; the workspace
+ * (d2mi_match_workspace_size) holds the per-GT best IoU. */
+size_t d2mi_match_workspace_size(int N, int G);
+int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, const float* boxes,
+                     int boxes_per_image, int N, int G, int P, const float* thresholds,
+                     const int* labels_of, int n_intervals, int allow_low_quality,
+                     float crowd_thr, float difficult_thr, long long* matches, long long* labels,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------ resampling gradients
  * d2mi_upsample2x_grad: adjoint of the FPN top-down nearest 2x upsample
  * (lib/modeling/backbone/fpn.py:138-149): gy [N,OH,OW,C] -> gtd

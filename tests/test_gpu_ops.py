@@ -954,3 +954,34 @@ def test_upsample2x_grad_and_stride_scatter(dev, shape):
         assert torch.equal(ops().stride_scatter(gs.to(dev), (N, H, W, C), s).cpu(), ref)
         assert torch.equal(ops().stride_scatter(gs.to(dev), (N, H, W, C), s, add.to(dev)).cpu(),
                            ref + add)
+
+
+@pytest.mark.parametrize("allow_low,per_image", [(True, False), (False, True)])
+def test_fused_match_equals_tensor_matcher(dev, allow_low, per_image):
+    """d2mi_match_boxes (IoU + Matcher in one pass) gives the tensor
+    formulation's matches and labels exactly: crowd and difficult GT, padded
+    (invalid) GT, an image without any matchable GT, IoU ties (duplicate GT),
+    boxes shared by the batch or per image."""
+    from detectron2_tensorflow_amd.modeling.matcher import Matcher, match_boxes
+    rng = np.random.default_rng(5 + int(allow_low))
+    N, G, P = 3, 9, 5000
+    def boxes(k):
+        cy, cx = rng.uniform(0, 400, k), rng.uniform(0, 600, k)
+        h, w = rng.uniform(4, 200, k), rng.uniform(4, 200, k)
+        return np.stack([cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2], -1).astype(F32)
+    gt = boxes(N * G).reshape(N, G, 4)
+    gt[0, 1] = gt[0, 0]  # a tie
+    bx = boxes(N * P).reshape(N, P, 4) if per_image else boxes(P)
+    bx[..., :7, :] = gt[0, :7] if not per_image else gt[:, :7]  # exact hits
+    valid = rng.random((N, G)) < 0.8
+    valid[2] = False
+    crowd = rng.random((N, G)) < 0.2
+    diff = rng.random((N, G)) < 0.2
+    m = Matcher([0.3, 0.7], [0, -1, 1], allow_low_quality_matches=allow_low)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    args = (t(gt), t(valid & ~crowd & ~diff), t(bx))
+    want = match_boxes(m, *args, crowd=t(crowd), difficult=t(diff))
+    got = match_boxes(m, *[a.to(dev) for a in args], crowd=t(crowd).to(dev),
+                      difficult=t(diff).to(dev))
+    assert torch.equal(got[0].cpu(), want[0]) and torch.equal(got[1].cpu(), want[1])
+    assert (want[1] == 1).any() and (want[1] == -1).any() and (want[1] == 0).any()
