@@ -115,6 +115,16 @@ def _smallest(keys, mask, k, limit):
     sel = torch.zeros_like(mask)
     if k <= 0:
         return sel
+    if keys.is_cuda:
+        # the HIP segmented radix select (one segment per row) on -key: the k
+        # largest of -key are the k smallest keys, ascending; unmasked -> -2
+        neg = torch.where(mask, -keys, torch.full_like(keys, -2.0))
+        start = torch.arange(N, device=keys.device, dtype=torch.int64) * P
+        vals, idx, _ = ops.topk_segments(neg.reshape(-1), start,
+                                         torch.full((N,), P, dtype=torch.int32,
+                                                    device=keys.device), k, P)
+        take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals > -2.0)
+        return sel.scatter_(1, idx.long(), take)
     kk = torch.where(mask, keys, torch.full_like(keys, 2.0))
     vals, idx = kk.topk(k, dim=1, largest=False, sorted=True)
     take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals < 2.0)

@@ -985,3 +985,21 @@ def test_fused_match_equals_tensor_matcher(dev, allow_low, per_image):
                       difficult=t(diff).to(dev))
     assert torch.equal(got[0].cpu(), want[0]) and torch.equal(got[1].cpu(), want[1])
     assert (want[1] == 1).any() and (want[1] == -1).any() and (want[1] == 0).any()
+
+
+def test_sampling_smallest_keys_on_hip_topk(dev):
+    """subsample_labels' k-smallest selection on the HIP segmented radix select
+    equals torch.topk's on the CPU (distinct keys): per-row limits, rows with
+    fewer candidates than k, an empty row."""
+    from detectron2_tensorflow_amd.modeling.matcher import _smallest
+    g = torch.Generator().manual_seed(9)
+    N, P, k = 3, 268569, 256
+    keys = torch.randperm(N * P, generator=g).reshape(N, P).float() / (N * P)
+    mask = torch.rand(N, P, generator=g) < 0.3
+    mask[1] = torch.rand(P, generator=g) < 1e-4  # fewer than k candidates
+    mask[2] = False
+    limit = torch.tensor([[200], [256], [10]])
+    want = _smallest(keys, mask, k, limit)
+    got = _smallest(keys.to(dev), mask.to(dev), k, limit.to(dev)).cpu()
+    assert torch.equal(got, want)
+    assert int(want[0].sum()) == 200 and int(want[1].sum()) == int(mask[1].sum())
