@@ -494,6 +494,21 @@ def match_boxes(gt_boxes, gt_flags, boxes, thresholds, labels_of, allow_low_qual
     return matches, labels
 
 
+def stem_pool(y, shift=None):
+    """relu(y + shift) -> zero pad 1 -> 3x3 / 2 VALID max pool, NHWC
+    (d2mi_stem_pool): the ResNet stem tail in one pass (no gradient)."""
+    y = _f32c(y)
+    shift = _f32c(shift) if shift is not None else None
+    _C.require_device(y)
+    N, H, W, C = y.shape
+    out = torch.empty((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, C), dtype=torch.float32,
+                      device=y.device)
+    rc = _C.lib().d2mi_stem_pool(_C.ptr(y), _C.ptr(shift), N, H, W, C, _C.ptr(out),
+                                 _C.stream_of(y.device))
+    _C.check(rc, "d2mi_stem_pool")
+    return out
+
+
 def upsample2x_grad(gy):
     """Adjoint of the FPN top-down nearest 2x upsample (d2mi_upsample2x_grad):
     gy [N, OH, OW, C] -> [N, ceil(OH/2), ceil(OW/2), C]."""

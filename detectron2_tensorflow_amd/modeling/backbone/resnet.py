@@ -12,7 +12,8 @@ from contextlib import ExitStack, contextmanager
 import torch
 import torch.nn.functional as F
 
-from ...layers import BatchNorm, Conv2D, Layer, get_norm
+from ...layers import BatchNorm, Conv2D, Layer, get_norm, ops
+from ...layers.activation import is_relu
 from ...layers import initializers as init
 from ...utils.arg_scope import add_arg_scope, arg_scope
 from .build import BACKBONE_REGISTRY, Backbone
@@ -82,7 +83,24 @@ class Stem(Layer):
                             normalizer_params={"channels": out_channels, "scope": "norm"},
                             scope="conv1")
 
+    def _fused_ok(self, x):
+        c = self.conv1
+        needs_grad = torch.is_grad_enabled() and (x.requires_grad or c.fold_trainable())
+        return (x.is_cuda and not needs_grad and is_relu(c.act_fn) and c.padding == "SAME"
+                and c.rate == 1 and c.num_groups == 1 and c.out_channels % 4 == 0)
+
     def call(self, x):
+        if self._fused_ok(x):
+            # frozen stem: MIOpen conv without its bias, then relu(+ shift),
+            # the zero pad and the 3x3/2 pool in one HIP pass (ops.stem_pool)
+            c = self.conv1
+            w, b, norm, _ = c.effective_params()
+            if norm is None:
+                p = (c.kernel_size - 1) // 2
+                y = F.conv2d(x.permute(0, 3, 1, 2),
+                             w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last),
+                             None, stride=c.stride, padding=p)
+                return ops.stem_pool(y.permute(0, 2, 3, 1), b)
         ret = self.conv1(x)
         ret = F.pad(ret.permute(0, 3, 1, 2), (1, 1, 1, 1))  # tf.pad zeros (resnet.py:80)
         ret = F.max_pool2d(ret, 3, 2)                        # VALID 3x3/2 (resnet.py:81)

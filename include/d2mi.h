@@ -397,6 +397,14 @@ int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, const float* bo
                      float crowd_thr, float difficult_thr, long long* matches, long long* labels,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------ ResNet stem tail
+ * relu(y + shift) -> zero pad 1 -> 3x3 stride-2 VALID max pool
+ * (lib/modeling/backbone/resnet.py:73-82) on the NHWC output y [N,H,W,C] of
+ * the stem conv (without its bias); out [N,(H-1)/2+1,(W-1)/2+1,C].  shift
+ * [C] nullable; C % 4 == 0; 16-B aligned. */
+int d2mi_stem_pool(const float* y, const float* shift, int N, int H, int W, int C, float* out,
+                   void* stream);
+
 /* ------------------------------------------------ resampling gradients
  * d2mi_upsample2x_grad: adjoint of the FPN top-down nearest 2x upsample
  * (lib/modeling/backbone/fpn.py:138-149): gy [N,OH,OW,C] -> gtd

@@ -1003,3 +1003,30 @@ def test_sampling_smallest_keys_on_hip_topk(dev):
     got = _smallest(keys.to(dev), mask.to(dev), k, limit.to(dev)).cpu()
     assert torch.equal(got, want)
     assert int(want[0].sum()) == 200 and int(want[1].sum()) == int(mask[1].sum())
+
+
+def test_fused_stem_pool_matches_unfused(dev):
+    """The frozen stem (MIOpen conv + d2mi_stem_pool: relu(+shift), zero pad,
+    3x3/2 VALID pool) equals conv + ReLU + F.pad + max_pool2d bit for bit."""
+    from detectron2_tensorflow_amd.layers import BatchNorm
+    from detectron2_tensorflow_amd.modeling.backbone.resnet import Stem
+    from detectron2_tensorflow_amd.utils.arg_scope import arg_scope
+    from detectron2_tensorflow_amd.layers import Conv2D
+    torch.manual_seed(2)
+    with arg_scope([Conv2D], normalizer=BatchNorm, activation="relu", use_bias=False,
+                   impl="auto"):
+        stem = Stem(3, 64, scope="stem").to(dev)
+    with torch.no_grad():
+        n = stem.conv1.normalizer_fn
+        n.moving_mean.normal_()
+        n.moving_variance.uniform_(0.5, 2.0)
+    for p in stem.parameters():
+        p.requires_grad_(False)
+    x = torch.randn(2, 101, 134, 3, device=dev) * 50
+    with torch.no_grad():
+        assert stem._fused_ok(x)
+        got = stem(x)
+        stem._fused_ok = lambda x: False
+        want = stem(x)
+    assert got.shape == want.shape == (2, 26, 34, 64)
+    assert torch.equal(got, want)
