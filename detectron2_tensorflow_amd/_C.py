@@ -81,6 +81,10 @@ _SIGS = {
     "d2mi_match_boxes": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_float,
                                  c_float, P, P, P, c_size_t, P]),
     "d2mi_stem_pool": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_rpn_loss_blocks": (c_int, []),
+    "d2mi_rpn_loss_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P]),
+    "d2mi_rpn_loss_bwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P, P,
+                                  P]),
     "d2mi_sgd_table_sizes": (c_int, [P, P, P]),
     "d2mi_momentum_sgd": (c_int, [P, P, c_int, P, c_float, c_float, c_float, P]),
     "d2mi_fold_many_sizes": (c_int, [P, P]),

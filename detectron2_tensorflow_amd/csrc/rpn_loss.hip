@@ -1,0 +1,175 @@
+// RPN losses in two passes (rpn_outputs.py:306-401, RPNOutputs.losses):
+// the sigmoid cross-entropy of the objectness logits over the sampled
+// anchors and the smooth-L1 of the box deltas over the positive anchors,
+// with the regression targets (box_regression.py:38-74, get_deltas) formed
+// on the fly from the anchor and its matched ground truth -- instead of the
+// gather / encode / cat / where / loss / sum chain of ~30 tensor passes over
+// [N, 268,569(, 4)].  Forward: per-workgroup partial sums (summed in a fixed
+// order by the caller); backward: d logits = g_cls (sigmoid(x) - z) on the
+// sampled anchors, d deltas = g_loc smooth-L1'(p - t) on the positives, with
+// (g_cls, g_loc) read from the device (no host synchronisation).
+// Element formulas follow ATen's binary_cross_entropy_with_logits and the
+// smooth_l1_loss of layers/loss.py.
+#include "common.h"
+
+namespace d2mi {
+namespace {
+
+struct RpnLossArgs {
+  const float* logits;        // [N, P]
+  const float4* deltas;       // [N, P] float4
+  const float4* anchors;      // [P]
+  const float4* gt;           // [N, G]
+  const long long* matches;   // [N, P]
+  const unsigned char* pos;   // [N, P]
+  const unsigned char* samp;  // [N, P]
+  int N, P, G;
+  float wy, wx, wh, ww, beta;
+};
+
+__device__ __forceinline__ float4 target_of(const RpnLossArgs& a, int n, int p) {
+  const float4 s = a.anchors[p];
+  const float4 t = a.gt[(size_t)n * a.G + (int)a.matches[(size_t)n * a.P + p]];
+  const float sh = s.z - s.x, sw = s.w - s.y;
+  const float scy = s.x + 0.5f * sh, scx = s.y + 0.5f * sw;
+  const float th = t.z - t.x, tw = t.w - t.y;
+  const float tcy = t.x + 0.5f * th, tcx = t.y + 0.5f * tw;
+  return make_float4(a.wy * (tcy - scy) / sh, a.wx * (tcx - scx) / sw, a.wh * logf(th / sh),
+                     a.ww * logf(tw / sw));
+}
+
+__device__ __forceinline__ float sl1(float t, float p, float beta) {
+  const float d = fabsf(t - p);
+  return beta < 1e-5f ? d : (d < beta ? 0.5f * (d * d) / beta : d - 0.5f * beta);
+}
+
+__device__ __forceinline__ float sl1_grad(float t, float p, float beta) {
+  const float d = p - t;  // d|t - p| / dp = sign(p - t)
+  const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+  if (beta < 1e-5f) return sg;
+  return fabsf(d) < beta ? d / beta : sg;
+}
+
+__global__ __launch_bounds__(256) void rpn_loss_fwd_kernel(RpnLossArgs a, float2* __restrict__ part) {
+  __shared__ float2 red[4];
+  const int n = blockIdx.y;
+  float cls = 0.f, loc = 0.f;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < a.P; p += gridDim.x * 256) {
+    const size_t i = (size_t)n * a.P + p;
+    if (a.samp[i]) {
+      const float x = a.logits[i], z = a.pos[i] ? 1.f : 0.f;
+      const float m = fmaxf(-x, 0.f);
+      cls += (1.f - z) * x + m + logf(expf(-m) + expf(-x - m));
+    }
+    if (a.pos[i]) {
+      const float4 t = target_of(a, n, p), d = a.deltas[i];
+      loc += ((sl1(t.x, d.x, a.beta) + sl1(t.y, d.y, a.beta)) + sl1(t.z, d.z, a.beta)) +
+             sl1(t.w, d.w, a.beta);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cls += __shfl_down(cls, o, 64);
+    loc += __shfl_down(loc, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[wv] = make_float2(cls, loc);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float2 s = red[0];
+    for (int k = 1; k < 4; ++k) {
+      s.x += red[k].x;
+      s.y += red[k].y;
+    }
+    part[(size_t)n * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void rpn_loss_bwd_kernel(RpnLossArgs a,
+                                                           const float* __restrict__ grads,
+                                                           float* __restrict__ d_logits,
+                                                           float4* __restrict__ d_deltas) {
+  const int n = blockIdx.y;
+  const float g_cls = grads[0], g_loc = grads[1];
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < a.P; p += gridDim.x * 256) {
+    const size_t i = (size_t)n * a.P + p;
+    float dl = 0.f;
+    if (a.samp[i]) {
+      const float x = a.logits[i], z = a.pos[i] ? 1.f : 0.f;
+      dl = g_cls * (1.f / (1.f + expf(-x)) - z);
+    }
+    d_logits[i] = dl;
+    float4 dd = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.pos[i]) {
+      const float4 t = target_of(a, n, p), d = a.deltas[i];
+      dd = make_float4(g_loc * sl1_grad(t.x, d.x, a.beta), g_loc * sl1_grad(t.y, d.y, a.beta),
+                       g_loc * sl1_grad(t.z, d.z, a.beta), g_loc * sl1_grad(t.w, d.w, a.beta));
+    }
+    d_deltas[i] = dd;
+  }
+}
+
+RpnLossArgs make_args(const float* logits, const float* deltas, const float* anchors,
+                      const float* gt, const long long* matches, const unsigned char* pos,
+                      const unsigned char* sampled, int N, int P, int G, const float* w,
+                      float beta) {
+  RpnLossArgs a;
+  a.logits = logits;
+  a.deltas = reinterpret_cast<const float4*>(deltas);
+  a.anchors = reinterpret_cast<const float4*>(anchors);
+  a.gt = reinterpret_cast<const float4*>(gt);
+  a.matches = matches;
+  a.pos = pos;
+  a.samp = sampled;
+  a.N = N;
+  a.P = P;
+  a.G = G;
+  a.wy = w[0];
+  a.wx = w[1];
+  a.wh = w[2];
+  a.ww = w[3];
+  a.beta = beta;
+  return a;
+}
+
+constexpr int kLossBlocks = 256;  // per image
+
+}  // namespace
+}  // namespace d2mi
+
+using namespace d2mi;
+
+extern "C" int d2mi_rpn_loss_blocks(void) { return kLossBlocks; }
+
+extern "C" int d2mi_rpn_loss_fwd(const float* logits, const float* deltas, const float* anchors,
+                                 const float* gt_boxes, const long long* matches,
+                                 const unsigned char* pos, const unsigned char* sampled, int N,
+                                 int P, int G, const float* weights, float beta, float* partial,
+                                 void* stream) {
+  D2MI_REQUIRE(N > 0 && P > 0 && G > 0, "bad rpn-loss shape");
+  D2MI_REQUIRE(((uintptr_t)deltas & 15) == 0 && ((uintptr_t)anchors & 15) == 0 &&
+                   ((uintptr_t)gt_boxes & 15) == 0,
+               "rpn loss: 16-byte aligned boxes / deltas");
+  const RpnLossArgs a = make_args(logits, deltas, anchors, gt_boxes, matches, pos, sampled, N, P,
+                                  G, weights, beta);
+  hipLaunchKernelGGL(rpn_loss_fwd_kernel, dim3(kLossBlocks, N), dim3(256), 0, as_stream(stream),
+                     a, reinterpret_cast<float2*>(partial));
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const float* anchors,
+                                 const float* gt_boxes, const long long* matches,
+                                 const unsigned char* pos, const unsigned char* sampled, int N,
+                                 int P, int G, const float* weights, float beta,
+                                 const float* grads, float* d_logits, float* d_deltas,
+                                 void* stream) {
+  D2MI_REQUIRE(N > 0 && P > 0 && G > 0, "bad rpn-loss shape");
+  D2MI_REQUIRE(((uintptr_t)d_deltas & 15) == 0, "rpn loss: 16-byte aligned d_deltas");
+  const RpnLossArgs a = make_args(logits, deltas, anchors, gt_boxes, matches, pos, sampled, N, P,
+                                  G, weights, beta);
+  hipLaunchKernelGGL(rpn_loss_bwd_kernel, dim3((P + 255) / 256 < 2048 ? (P + 255) / 256 : 2048, N),
+                     dim3(256), 0, as_stream(stream), a, grads, d_logits,
+                     reinterpret_cast<float4*>(d_deltas));
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}

@@ -494,6 +494,62 @@ def match_boxes(gt_boxes, gt_flags, boxes, thresholds, labels_of, allow_low_qual
     return matches, labels
 
 
+class _RPNLossFn(torch.autograd.Function):
+    """(loss_cls_sum, loss_loc_sum) of the RPN (d2mi_rpn_loss_fwd / _bwd);
+    differentiable w.r.t. logits and deltas."""
+
+    @staticmethod
+    def forward(ctx, logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta):
+        N, P = logits.shape
+        G = gt_boxes.shape[1]
+        nb = _C.lib().d2mi_rpn_loss_blocks()
+        part = torch.empty((N * nb, 2), dtype=torch.float32, device=logits.device)
+        w = _C.host_array(_C.c_float, [float(v) for v in weights])
+        rc = _C.lib().d2mi_rpn_loss_fwd(_C.ptr(logits), _C.ptr(deltas), _C.ptr(anchors),
+                                        _C.ptr(gt_boxes), _C.ptr(matches), _C.ptr(pos),
+                                        _C.ptr(sampled), N, P, G, w, float(beta), _C.ptr(part),
+                                        _C.stream_of(logits.device))
+        _C.check(rc, "d2mi_rpn_loss_fwd")
+        ctx.save_for_backward(logits, deltas, anchors, gt_boxes, matches, pos, sampled)
+        ctx.conf = (tuple(float(v) for v in weights), float(beta))
+        # fixed-size reductions of the partials (deterministic order)
+        return part[:, 0].sum(), part[:, 1].sum()
+
+    @staticmethod
+    def backward(ctx, g_cls, g_loc):
+        logits, deltas, anchors, gt_boxes, matches, pos, sampled = ctx.saved_tensors
+        weights, beta = ctx.conf
+        N, P = logits.shape
+        dev = logits.device
+        z = torch.zeros((), dtype=torch.float32, device=dev)
+        grads = torch.stack([g_cls if g_cls is not None else z,
+                             g_loc if g_loc is not None else z]).float().contiguous()
+        d_logits = torch.empty_like(logits)
+        d_deltas = torch.empty_like(deltas)
+        w = _C.host_array(_C.c_float, list(weights))
+        rc = _C.lib().d2mi_rpn_loss_bwd(_C.ptr(logits), _C.ptr(deltas), _C.ptr(anchors),
+                                        _C.ptr(gt_boxes), _C.ptr(matches), _C.ptr(pos),
+                                        _C.ptr(sampled), N, P, gt_boxes.shape[1], w, beta,
+                                        _C.ptr(grads), _C.ptr(d_logits), _C.ptr(d_deltas),
+                                        _C.stream_of(dev))
+        _C.check(rc, "d2mi_rpn_loss_bwd")
+        return d_logits, d_deltas, None, None, None, None, None, None, None
+
+
+def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta):
+    """Fused RPN losses (sums; the caller normalises): logits [N, P], deltas
+    [N, P, 4], anchors [P, 4], gt_boxes [N, G, 4], matches [N, P], pos /
+    sampled [N, P] bool -> (loss_cls_sum, loss_loc_sum)."""
+    logits, deltas = _f32c(logits), _f32c(deltas)
+    anchors, gt_boxes = _f32c(anchors), _f32c(gt_boxes)
+    matches = matches.to(torch.int64).contiguous()
+    pos = pos.to(torch.uint8).contiguous()
+    sampled = sampled.to(torch.uint8).contiguous()
+    _C.require_device(logits, deltas, anchors, gt_boxes, matches, pos, sampled)
+    return _RPNLossFn.apply(logits, deltas, anchors, gt_boxes, matches, pos, sampled,
+                            tuple(weights), float(beta))
+
+
 def stem_pool(y, shift=None):
     """relu(y + shift) -> zero pad 1 -> 3x3 / 2 VALID max pool, NHWC
     (d2mi_stem_pool): the ResNet stem tail in one pass (no gradient)."""

@@ -170,21 +170,28 @@ class RPN(Layer):
                       (anchors[None, :, 2] <= hw[:, :1] + t) & (anchors[None, :, 3] <= hw[:, 1:2] + t))
             labels = torch.where(inside, labels, torch.full_like(labels, -1))
         pos, neg = subsample_labels(labels, self.batch_size_per_image, self.positive_fraction, 0)
+        norm = 1.0 / (self.batch_size_per_image * N)
+        pl = torch.cat([x.reshape(N, -1) for x in logits], dim=1)
+        pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
+        if pl.is_cuda and gt_boxes.shape[1] > 0:
+            # one HIP pass each way: targets, sigmoid CE and smooth-L1 fused
+            loss_cls, loss_loc = ops.rpn_loss(pl, pd, anchors, gt_boxes, matches, pos, pos | neg,
+                                              self.box2box_transform.weights,
+                                              self.smooth_l1_beta)
+            return {"loss_rpn_cls": loss_cls * norm * self.loss_weight,
+                    "loss_rpn_loc": loss_loc * norm * self.loss_weight}
         matched = torch.gather(gt_boxes, 1, matches[..., None].expand(-1, -1, 4))
         gt_deltas = self.box2box_transform.get_deltas(
             anchors[None].expand(N, -1, -1).reshape(-1, 4), matched.reshape(-1, 4)).reshape(N, -1, 4)
         # only positive rows carry targets (dynamic_stitch of zeros, rpn_outputs.py:286-290);
         # other rows may be matched to padded GT whose log-size is -inf
         gt_deltas = torch.where(pos[..., None], gt_deltas, torch.zeros_like(gt_deltas))
-        pl = torch.cat([x.reshape(N, -1) for x in logits], dim=1)
-        pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
         sampled = pos | neg
         obj = torch.nn.functional.binary_cross_entropy_with_logits(
             pl, pos.to(pl.dtype), reduction="none")
         loss_cls = torch.where(sampled, obj, torch.zeros_like(obj)).sum()
         loc = smooth_l1_loss(labels=gt_deltas, predictions=pd, beta=self.smooth_l1_beta)
         loss_loc = torch.where(pos[..., None], loc, torch.zeros_like(loc)).sum()
-        norm = 1.0 / (self.batch_size_per_image * N)
         return {"loss_rpn_cls": loss_cls * norm * self.loss_weight,
                 "loss_rpn_loc": loss_loc * norm * self.loss_weight}
 

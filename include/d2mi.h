@@ -397,6 +397,25 @@ int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, const float* bo
                      float crowd_thr, float difficult_thr, long long* matches, long long* labels,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------ RPN losses
+ * RPNOutputs.losses (rpn_outputs.py:306-401) after matching and sampling:
+ * logits [N,P], deltas [N,P,4], anchors [P,4], gt_boxes [N,G,4] (yxyx),
+ * matches [N,P] int64, pos / sampled [N,P] bool (uint8).  Forward writes
+ * partial [N][d2mi_rpn_loss_blocks()] float2 = (sigmoid CE over sampled,
+ * smooth-L1(beta) over positives of the get_deltas targets with weights[4]),
+ * summed by the caller in a fixed order.  Backward: grads = device float[2]
+ * (d loss_cls_sum, d loss_loc_sum) -> d_logits [N,P], d_deltas [N,P,4]. */
+int d2mi_rpn_loss_blocks(void);
+int d2mi_rpn_loss_fwd(const float* logits, const float* deltas, const float* anchors,
+                      const float* gt_boxes, const long long* matches, const unsigned char* pos,
+                      const unsigned char* sampled, int N, int P, int G, const float* weights,
+                      float beta, float* partial, void* stream);
+int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const float* anchors,
+                      const float* gt_boxes, const long long* matches, const unsigned char* pos,
+                      const unsigned char* sampled, int N, int P, int G, const float* weights,
+                      float beta, const float* grads, float* d_logits, float* d_deltas,
+                      void* stream);
+
 /* ------------------------------------------------ ResNet stem tail
  * relu(y + shift) -> zero pad 1 -> 3x3 stride-2 VALID max pool
  * (lib/modeling/backbone/resnet.py:73-82) on the NHWC output y [N,H,W,C] of

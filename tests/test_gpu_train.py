@@ -269,3 +269,45 @@ def test_batched_frozen_bn_fold_matches_per_layer_fold(dev):
     assert la == lb == la2 and ga.keys() == gb.keys() == ga2.keys() and ga
     for n in ga:
         assert torch.equal(ga[n], gb[n]) and torch.equal(ga[n], ga2[n]), n
+
+
+def test_fused_rpn_loss_matches_tensor_formulation(dev):
+    """ops.rpn_loss (targets + sigmoid CE + smooth-L1 in one HIP pass, analytic
+    backward) equals the tensor formulation of RPNOutputs.losses in value and
+    in the gradients of logits and deltas."""
+    from detectron2_tensorflow_amd.layers import ops
+    from detectron2_tensorflow_amd.layers.loss import smooth_l1_loss
+    from detectron2_tensorflow_amd.modeling.box_regression import Box2BoxTransform
+    g = torch.Generator().manual_seed(4)
+    N, P, G, beta = 2, 5000, 6, 1.0 / 9
+    cy, cx = torch.rand(P, generator=g) * 500, torch.rand(P, generator=g) * 700
+    hh, ww = torch.rand(P, generator=g) * 100 + 8, torch.rand(P, generator=g) * 100 + 8
+    anchors = torch.stack([cy - hh / 2, cx - ww / 2, cy + hh / 2, cx + ww / 2], 1)
+    gt = anchors[torch.randint(0, P, (N * G,), generator=g)].reshape(N, G, 4) + \
+        torch.randn(N, G, 4, generator=g) * 3
+    matches = torch.randint(0, G, (N, P), generator=g)
+    pos = torch.rand(N, P, generator=g) < 0.05
+    sampled = pos | (torch.rand(N, P, generator=g) < 0.05)
+    logits = torch.randn(N, P, generator=g) * 3
+    deltas = torch.randn(N, P, 4, generator=g) * 0.3
+    weights = (1.0, 1.0, 1.0, 1.0)
+    t = lambda a: a.to(dev)
+    lf, df = t(logits).requires_grad_(True), t(deltas).requires_grad_(True)
+    cls, loc = ops.rpn_loss(lf, df, t(anchors), t(gt), t(matches), t(pos), t(sampled), weights,
+                            beta)
+    (cls * 0.7 + loc * 1.3).backward()
+    lr, dr = t(logits).requires_grad_(True), t(deltas).requires_grad_(True)
+    b2b = Box2BoxTransform(weights)
+    matched = torch.gather(t(gt), 1, t(matches)[..., None].expand(-1, -1, 4))
+    tgt = b2b.get_deltas(t(anchors)[None].expand(N, -1, -1).reshape(-1, 4),
+                         matched.reshape(-1, 4)).reshape(N, P, 4)
+    tgt = torch.where(t(pos)[..., None], tgt, torch.zeros_like(tgt))
+    obj = torch.nn.functional.binary_cross_entropy_with_logits(lr, t(pos).float(), reduction="none")
+    cls_r = torch.where(t(sampled), obj, torch.zeros_like(obj)).sum()
+    l1 = smooth_l1_loss(labels=tgt, predictions=dr, beta=beta)
+    loc_r = torch.where(t(pos)[..., None], l1, torch.zeros_like(l1)).sum()
+    (cls_r * 0.7 + loc_r * 1.3).backward()
+    assert cls.item() == pytest.approx(cls_r.item(), rel=1e-5)
+    assert loc.item() == pytest.approx(loc_r.item(), rel=1e-5)
+    torch.testing.assert_close(lf.grad, lr.grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(df.grad, dr.grad, rtol=1e-5, atol=1e-6)
