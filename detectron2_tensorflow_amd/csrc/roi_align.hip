@@ -271,18 +271,19 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 // the pad rows onto the edge rows, implicit in the clamped taps) as a GATHER:
 // device-scope float atomics on gfx950 resolve beyond the XCD-private L2 and a
 // scatter of them ran at ~120 GB/s.  Instead:
-//   1. geom: per-ROI geometry (level, image, normalised box, tap scales);
-//   2. emit: for every (ROI, sample, corner) contribution a 64-bit key
+//   1. emit: for every (ROI, sample, corner) contribution a 64-bit key
 //      pixel << low_bits | slot, slot = (roi * samples + sample) * 4 + corner,
-//      and its (grad_out row, y_lerp, x_lerp) record at index slot;
-//   3. radix-sort the keys: pixel-major, then the TF loop order;
-//   4. runs: first / end key of every touched pixel;
-//   5. pixels with more than kSeg contributions are split into kSeg-long
+//      and its (grad_out row, y_lerp, x_lerp) record at index slot (the ROI
+//      geometry is computed in place);
+//   2. stable onesweep radix sort on the pixel bits only: pixel-major, and
+//      within a pixel the emission (TF loop) order is kept;
+//   3. runs: first / end key of every touched pixel;
+//   4. pixels with more than kSeg contributions are split into kSeg-long
 //      segments (exclusive scan of their segment counts) summed by one wave
 //      each into a partial row — bounded work per wave however many ROIs pile
 //      onto one pixel (collapsed proposals at the image border do);
-//   6. the grad maps are zero-filled (memset, full bandwidth) and the touched
-//      pixels (compact list from step 4) are summed by waves striding over
+//   5. the grad maps are zero-filled (memset, full bandwidth) and the touched
+//      pixels (compact list from step 3) are summed by waves striding over
 //      that list, lanes over channels (float4): each sums its contributions
 //      (or its segments' partials) in order and stores the pixel once.
 // Summation order per pixel is (box, y, x, corner), the TF kernel's loop order
@@ -302,13 +303,39 @@ struct Contrib {
   int32_t pad;
 };
 
-__global__ void roi_bwd_geom_kernel(RoiArgs a, RoiGeom* geo) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < a.R) geo[r] = roi_geom(a, r);
+// One launch clears every buffer the backward starts from (the per-level grad
+// maps to 0, run_start to -1, the touched counter to 0) instead of a
+// hipMemsetAsync per buffer: each memset is its own ~5 us dispatch.
+constexpr int kMaxClear = D2MI_MAX_LEVELS + 2;
+struct ClearList {
+  uint32_t* ptr[kMaxClear];
+  long long words[kMaxClear];
+  uint32_t value[kMaxClear];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void roi_bwd_clear_kernel(ClearList cl) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (int k = 0; k < cl.n; ++k) {
+    uint32_t* p = cl.ptr[k];
+    const long long n = cl.words[k];
+    const uint32_t v = cl.value[k];
+    // 16-byte aligned body as uint4 stores, the unaligned head / tail as words
+    const long long head = std::min<long long>(n, (long long)((16 - ((uintptr_t)p & 15)) & 15) / 4);
+    const long long quads = (n - head) / 4;
+    uint4* q = reinterpret_cast<uint4*>(p + head);
+    const uint4 v4 = make_uint4(v, v, v, v);
+    for (long long i = tid; i < quads; i += stride) q[i] = v4;
+    const long long tail0 = head + quads * 4;
+    if (tid < head) p[tid] = v;
+    if (tid < n - tail0) p[tail0 + tid] = v;
+  }
 }
 
-__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, const RoiGeom* __restrict__ geo,
-                                    int low_bits, uint64_t* __restrict__ keys,
+// The ROI geometry is recomputed per sample (a few dozen flops against the
+// 40 B the thread stores) rather than staged by a separate launch.
+__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, uint64_t* __restrict__ keys,
                                     Contrib* __restrict__ rec) {
   const int S = a.sr > 0 ? a.sr : 1;
   const long long nsamp = (long long)a.out_h * a.out_w * S * S;
@@ -316,7 +343,7 @@ __global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, const RoiGeom* __restr
   if (t >= (long long)a.R * nsamp) return;
   const int r = (int)(t / nsamp);
   const int s = (int)(t - (long long)r * nsamp);
-  const RoiGeom g = geo[r];
+  const RoiGeom g = roi_geom(a, r);
   const uint64_t slot = (uint64_t)t * 4u;
   uint64_t* k = keys + slot;
   bool ok = g.ok;
@@ -659,7 +686,6 @@ int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, i
 
 template <typename WS>
 void bwd_layout(WS& w, int R, int C, const BwdPlan& p) {
-  w.template take<RoiGeom>((size_t)R + 1);
   w.template take<uint64_t>((size_t)p.n_keys + 1);          // keys
   w.template take<uint64_t>((size_t)p.n_keys + 1);          // sorted keys
   w.template take<Contrib>((size_t)p.n_samples + 1);        // records
@@ -671,7 +697,7 @@ void bwd_layout(WS& w, int R, int C, const BwdPlan& p) {
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
   w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
   w.template take<int32_t>(1);                              // their count
-  w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
+  w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
                             exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1)));
 }
 
@@ -717,7 +743,6 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
   if (p.total_pixels == 0) return 0;
   hipStream_t st = as_stream(stream);
   Workspace w(workspace, workspace_bytes);
-  RoiGeom* geo = w.take<RoiGeom>((size_t)R + 1);
   uint64_t* keys = w.take<uint64_t>((size_t)p.n_keys + 1);
   uint64_t* sorted = w.take<uint64_t>((size_t)p.n_keys + 1);
   Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
@@ -729,23 +754,35 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
   float* partial = w.take<float>((size_t)p.max_segs * C);
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
   int32_t* n_touched = w.take<int32_t>(1);
-  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.end_bit),
+  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
                                exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1));
   void* tmp = w.take<char>(tmp_bytes);
   const long long TP = p.total_pixels;
-  D2MI_HIP(hipMemsetAsync(run_start, 0xff, (size_t)TP * sizeof(int32_t), st));
-  D2MI_HIP(hipMemsetAsync(n_touched, 0, sizeof(int32_t), st));
+  ClearList cl = {};
+  long long clear_words = 0;
+  auto clear = [&](void* ptr, long long words, uint32_t value) {
+    cl.ptr[cl.n] = static_cast<uint32_t*>(ptr);
+    cl.words[cl.n] = words;
+    cl.value[cl.n] = value;
+    ++cl.n;
+    clear_words += words;
+  };
   for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero gradient
-    D2MI_HIP(hipMemsetAsync(a.gfeat[l], 0,
-                            (size_t)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C *
-                                sizeof(float), st));
+    clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
+  clear(run_start, TP, 0xffffffffu);
+  clear(n_touched, 1, 0u);
+  hipLaunchKernelGGL(roi_bwd_clear_kernel,
+                     dim3((unsigned)std::max(1LL, std::min((clear_words / 4 + 255) / 256, 8192LL))),
+                     dim3(256), 0, st, cl);
+  D2MI_LAUNCH_CHECK();
   if (p.n_keys > 0) {
-    hipLaunchKernelGGL(roi_bwd_geom_kernel, dim3((R + 255) / 256), dim3(256), 0, st, a, geo);
-    D2MI_LAUNCH_CHECK();
     hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((p.n_samples + 255) / 256)), dim3(256),
-                       0, st, a, p.pm, geo, p.low_bits, keys, rec);
+                       0, st, a, p.pm, p.low_bits, keys, rec);
     D2MI_LAUNCH_CHECK();
-    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.end_bit, tmp, tmp_bytes, st);
+    // pixel bits only: the sort is stable and the keys are emitted in slot
+    // (TF loop) order, so each pixel's run stays in that order
+    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.low_bits, p.end_bit, tmp, tmp_bytes,
+                        st);
     if (rc) return rc;
     hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
                        0, st, sorted, p.n_keys, p.low_bits, TP, run_start, run_end, touched,

@@ -100,20 +100,28 @@ int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32
   return 0;
 }
 
-size_t radix_sort_u64_workspace_size(size_t n, int end_bit) {
+// merge-sort limit 0: onesweep for everything above one block
+using OnesweepSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                      rocprim::default_config, 0>;
+
+size_t radix_sort_u64_workspace_size(size_t n, int begin_bit, int end_bit) {
   size_t bytes = 0;
-  rocprim::radix_sort_keys((void*)nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, n,
-                           0u, (unsigned)end_bit, (hipStream_t)0, false);
+  rocprim::radix_sort_keys<OnesweepSortConfig>((void*)nullptr, bytes, (const uint64_t*)nullptr,
+                                               (uint64_t*)nullptr, n, (unsigned)begin_bit,
+                                               (unsigned)end_bit, (hipStream_t)0, false);
   return bytes;
 }
 
-int radix_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, size_t n, int end_bit, void* ws,
-                   size_t ws_bytes, hipStream_t stream) {
+int radix_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, size_t n, int begin_bit,
+                   int end_bit, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (n == 0) return 0;
-  size_t need = radix_sort_u64_workspace_size(n, end_bit);
+  D2MI_REQUIRE(0 <= begin_bit && begin_bit < end_bit && end_bit <= 64, "bad sort bit range [%d, %d)",
+               begin_bit, end_bit);
+  size_t need = radix_sort_u64_workspace_size(n, begin_bit, end_bit);
   D2MI_REQUIRE(ws_bytes >= need, "radix sort workspace too small (%zu < %zu)", ws_bytes, need);
-  D2MI_HIP(rocprim::radix_sort_keys(ws, need, keys_in, keys_out, n, 0u, (unsigned)end_bit, stream,
-                                    false));
+  D2MI_HIP(rocprim::radix_sort_keys<OnesweepSortConfig>(ws, need, keys_in, keys_out, n,
+                                                        (unsigned)begin_bit, (unsigned)end_bit,
+                                                        stream, false));
   return 0;
 }
 
