@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 // bit-identical to the TF scatter for pixels with at most kSeg contributions
 // and no folded pad row.
 constexpr int kSeg = 64;    // contributions per wave before a pixel is split
-constexpr int kBatch = 8;   // contributions in flight per wave
+constexpr int kBatch = 2;   // contributions in flight per wave (r1 sweep, pixel kernel avg: 16 -> 103 us, 8 -> 64, 4 -> 49.5, 2 -> 46.7: occupancy, not loads in flight, binds)
 
 struct PixMap {
   long long base[D2MI_MAX_LEVELS + 1];  // first global pixel id per level
