@@ -41,6 +41,14 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     "mask_rcnn_R_50_FPN": "configs/COCO-InstanceSegmentation/mask_rcnn_R_50_FPN_1x.yaml",
     "faster_rcnn_R_50_FPN": "configs/COCO-Detection/faster_rcnn_R_50_FPN_1x.yaml",
+    "retinanet_R_50_FPN": "configs/COCO-Detection/retinanet_R_50_FPN_1x.yaml",
+    "retinanet_R_101_FPN": "configs/COCO-Detection/retinanet_R_101_FPN_3x.yaml",
+}
+METRICS = {
+    "mask_rcnn_R_50_FPN": "img/sec whole-node Mask R-CNN R50-FPN @1333x800",
+    "faster_rcnn_R_50_FPN": "img/sec Faster R-CNN R50-FPN @1333x800",
+    "retinanet_R_50_FPN": "img/sec RetinaNet R50-FPN",
+    "retinanet_R_101_FPN": "img/sec RetinaNet R101-FPN dense anchors",
 }
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32)
 # split products: every f32 multiply-add costs six v_mfma_f32_32x32x16_bf16
@@ -90,6 +98,21 @@ def build(args, device):
     return cfg, model
 
 
+def is_single_stage(model):
+    return hasattr(model, "detector")
+
+
+@torch.no_grad()
+def calibrate_retinanet(model, batch):
+    """BASELINE.md injection for RetinaNet: class logits ~ N(-3, 1), deltas ~
+    N(0, 0.1^2) on this batch's features (utils/synthetic.py)."""
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_retinanet_head
+    det = model.detector
+    feats = model.neck(model.backbone(model.preprocess_image(batch).tensor))
+    cls, box = det.head([feats[f] for f in det.in_features])
+    calibrate_retinanet_head(det.head, cls, box)
+
+
 @torch.no_grad()
 def calibrate_scores(model, batch):
     """Rescale the class / objectness logit weights so the random-init model
@@ -97,6 +120,8 @@ def calibrate_scores(model, batch):
     deltas to N(0, 0.1^2): the unnormalised features of a random-init ResNet
     otherwise give deltas of O(10), which collapse most proposals onto the
     image border (a random-init artefact, not a training distribution)."""
+    if is_single_stage(model):
+        return calibrate_retinanet(model, batch)
     stats = {}
 
     def grab(name):
@@ -166,7 +191,7 @@ def kernel_report(summary, mode="infer"):
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                      "traffic": pmc_traffic(pmc_group, mode), "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
-    for name in ("roi_align_fwd", "roi_align_bwd"):
+    for name in ("roi_align_fwd", "roi_align_bwd", "retinanet_topk"):
         if name not in summary:
             continue
         n, ms, byts = summary[name]
@@ -201,6 +226,15 @@ def cpu_baseline(args, model, batch, cfg=None):
             step.step(imgs, shapes, inst, threads=cores)
         dt = time.perf_counter() - t0
         what = "training iteration(s) (forward + losses + backward + Momentum-SGD update)"
+    elif is_single_stage(model):
+        from cpu_pipeline import CPURetinaNet
+        ref = CPURetinaNet(model.eval())
+        ref(imgs[:1, :256, :320], threads=cores)  # warm the libraries
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            ref(imgs, threads=cores)
+        dt = time.perf_counter() - t0
+        what = "inference forward(s) (backbone + FPN P6P7 + box tower + dense top-k/decode/NMS)"
     else:
         ref = CPUReference(model.eval())
         ref(imgs[:1, :256, :320], [[256, 320]], threads=cores)  # warm the libraries
@@ -223,6 +257,8 @@ def cpu_baseline(args, model, batch, cfg=None):
 
 def main():
     args = parse()
+    if args.model.startswith("retinanet") and args.mode == "train":
+        raise SystemExit("RetinaNet is benchmarked in --mode infer (config C4)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -253,7 +289,8 @@ def main():
         step = lambda: trainer.step(batch)
         grad_ctx = torch.enable_grad
     else:
-        step = lambda: model.inference(batch)
+        fwd = model if is_single_stage(model) else model.inference
+        step = lambda: fwd(batch)
         grad_ctx = torch.no_grad
 
     with grad_ctx():
@@ -308,8 +345,7 @@ def main():
     if rank == 0:
         kernels = kernel_report(summary, args.mode)
         result = {
-            "metric": "img/sec whole-node Mask R-CNN R50-FPN @1333x800"
-                      if args.model.startswith("mask") else "img/sec Faster R-CNN R50-FPN @1333x800",
+            "metric": METRICS[args.model],
             "value": round(world * args.batch * args.steps / elapsed, 3),
             "unit": "img/s",
             "n_gpus": world,

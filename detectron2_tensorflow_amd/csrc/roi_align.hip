@@ -458,7 +458,7 @@ __device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __re
         e[u] = rec[slot >> 2];
       }
     }
-    float4 v[kBatch];
+    float4 v[kBatch] = {};  // dead lanes accumulate zeros, never uninitialised registers
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) {
       if (u < m && live) {
@@ -810,7 +810,9 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
     D2MI_LAUNCH_CHECK();
   }
   if (p.n_keys == 0) return 0;
-  // fixed grid (the touched count stays on the device): ~8 waves per SIMD
+  // fixed grid (the touched count stays on the device): at most 8192
+  // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
+  // beyond residency start as earlier ones retire (the kBatch sweep above)
   const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
   if (vec4)
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,

@@ -1,8 +1,8 @@
 // Segmented sort of 64-bit (score, index) keys.
 // Small segments (<= 8192 keys: RPN levels, RetinaNet candidates, NMS inputs)
-// are sorted by one 1024-thread workgroup per segment with an in-LDS bitonic
-// network (64 KiB of keys); larger capacities fall back to rocPRIM's
-// segmented radix sort.
+// are sorted by a stable counting rank spread over len/64 workgroups per
+// segment (keys staged in LDS, 64 KiB at most); larger capacities fall back
+// to rocPRIM's segmented radix sort.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
@@ -12,36 +12,41 @@
 namespace d2mi {
 namespace {
 
-__global__ __launch_bounds__(1024) void bitonic_lds_kernel(const uint64_t* __restrict__ in,
-                                                           uint64_t* __restrict__ out,
-                                                           const int32_t* __restrict__ lens,
-                                                           int cap) {
+// Stable counting-rank sort: rank(i) = #{j : key_j < key_i} + #{j < i : key_j
+// == key_i}, a permutation of [0, len).  A workgroup ranks 64 keys of its
+// segment against all of them (each of its 4 waves a quarter of the segment,
+// keys broadcast from LDS), so a segment spreads over len/64 workgroups
+// instead of one workgroup running a bitonic network (13*14/2 LDS passes).
+constexpr int kRankI = 64;
+__global__ __launch_bounds__(256) void rank_sort_kernel(const uint64_t* __restrict__ in,
+                                                        uint64_t* __restrict__ out,
+                                                        const int32_t* __restrict__ lens,
+                                                        int cap) {
   extern __shared__ uint64_t s[];
-  const int seg = blockIdx.x;
+  __shared__ uint32_t part[256];
+  const int seg = blockIdx.y;
   const int len = min(lens[seg], cap);
-  int n = 1;
-  while (n < len) n <<= 1;
+  const int i0 = blockIdx.x * kRankI;
+  if (i0 >= len) return;
   const uint64_t* src = in + (size_t)seg * cap;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = i < len ? src[i] : ~0ull;
+  for (int j = threadIdx.x; j < len; j += 256) s[j] = src[j];
   __syncthreads();
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = s[i], b = s[ixj];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            s[i] = b;
-            s[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = i0 + lane;
+  const uint64_t mine = i < len ? s[i] : ~0ull;
+  const int q = (len + 3) >> 2;
+  const int j0 = w * q, j1 = min(len, j0 + q);
+  uint32_t r = 0;
+  for (int j = j0; j < j1; ++j) {
+    const uint64_t o = s[j];
+    r += (o < mine || (o == mine && j < i)) ? 1u : 0u;
   }
-  uint64_t* dst = out + (size_t)seg * cap;
-  for (int i = threadIdx.x; i < len; i += blockDim.x) dst[i] = s[i];
+  part[threadIdx.x] = r;
+  __syncthreads();
+  if (w == 0 && i < len) {
+    const uint32_t rank = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane];
+    out[(size_t)seg * cap + rank] = mine;
+  }
 }
 
 __global__ void seg_bounds_kernel(const int32_t* lens, int S, int cap, int* begin, int* end) {
@@ -76,11 +81,8 @@ int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32
                         int cap, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (S == 0 || cap == 0) return 0;
   if (cap <= kLdsSortCap) {
-    int n = 1;
-    while (n < cap) n <<= 1;
-    const int threads = n >= 1024 ? 1024 : (n < 64 ? 64 : n);
-    hipLaunchKernelGGL(bitonic_lds_kernel, dim3(S), dim3(threads), n * sizeof(uint64_t), stream,
-                       keys_in, keys_out, lens, cap);
+    hipLaunchKernelGGL(rank_sort_kernel, dim3((cap + kRankI - 1) / kRankI, S), dim3(256),
+                       cap * sizeof(uint64_t), stream, keys_in, keys_out, lens, cap);
     D2MI_LAUNCH_CHECK();
     return 0;
   }

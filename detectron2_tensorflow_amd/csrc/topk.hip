@@ -2,118 +2,257 @@
 // first) as a radix select on gfx950.
 //
 // Reference call sites: rpn_outputs.py:70 (per-level pre-NMS top-k over up to
-// 201,600 logits), rpn_outputs.py:106, retinanet.py:326 (up to 12.1 M sigmoid
-// scores per level per image).
+// 201,600 logits), rpn_outputs.py:106, retinanet.py:326 (top-k of the SIGMOID
+// of up to 12.1 M logits per level per image, key_mode 1).
 //
-// The selection is a most-significant-digit radix select on the order-preserving
-// uint32 image of the key (11 + 11 + 10 bits):
-//   hist   multi-workgroup LDS histogram per segment, merged with global atomics
-//   select one workgroup per segment finds the digit holding the k-th key and
-//          stops as soon as (keys above it) + (keys in it) fit the 8192-key LDS sort
-//   collect elements at or above the threshold digit are appended (unordered)
-//          as (key, index) sort keys; index order is restored by the final sort
-//   sort   one workgroup per segment, in-LDS bitonic sort, writes the first k.
-// A segment whose k-th key is tied with more than 8192 others (all digits
-// exhausted) takes the ordered path: one workgroup appends the tied keys in
-// index order until k is reached — the TF tie rule, at the cost of one serial pass.
-// Every kernel is launched unconditionally and reads the per-segment state, so
-// the whole select is a fixed launch sequence (no host synchronisation).
+// The select runs on the order-preserving uint32 image of the RAW value, for
+// both key modes: sigmoid is monotone, so the k-th largest sigmoid is the
+// sigmoid of the k-th largest logit, and the scan passes need no expf (at
+// 32 M scores per call the per-element sigmoid of every pass was the cost).
+// Only the few collected candidates are ranked on their sigmoid keys.
+//
+//   hist     (3 passes, 12 + 12 + 8 bits) per-workgroup LDS histogram of a
+//            16 K-element chunk (float4 loads, all in flight), flushed into 4
+//            replicated global histograms (low same-address atomic traffic)
+//   select   one workgroup per segment: suffix sums, the digit holding the
+//            k-th key; stops refining once (keys above) + (keys in it) fit the
+//            8192-key candidate buffer.  For key_mode 1 it also solves the
+//            sigmoid tie interval of the bin's lower edge (binary search over
+//            the key space): logits below the edge whose sigmoid equals the
+//            edge's sigmoid may still belong to the top-k (TF ranks the
+//            sigmoid values, ties by index).
+//   collect  one pass: keys >= edge -> buffer A; keys in the tie window below
+//            the edge whose sigmoid reaches the edge's -> buffer B.  One
+//            atomic per workgroup reserves its slots (no per-element atomics).
+//   resolve  one workgroup per segment: A + B when they fit; otherwise (a
+//            saturated sigmoid, or more than 8192 equal keys) the exact
+//            ordered path: keys strictly above the tie group, then the tied
+//            keys in index order until k (the TF tie rule).
+//   rank     counting rank of every candidate among all candidates on the
+//            final 64-bit (score desc, index asc) key, spread over many
+//            workgroups; rank < k scatters straight to the sorted output.
+// Every kernel is launched unconditionally and reads the per-segment state,
+// so the select is a fixed launch sequence (no host synchronisation).
 #include "internal.h"
 
 namespace d2mi {
 namespace {
 
-constexpr int kBins = 2048;
-constexpr int kCap = kLdsSortCap;  // candidates sortable in LDS
+constexpr int kBins = 4096;     // 12-bit digits
+constexpr int kRep = 4;         // replicated global histograms
+constexpr int kCap = kLdsSortCap;  // candidates (8192)
+constexpr int kThreads = 256;
 
 struct SegState {
-  uint32_t prefix;     // selected high bits so far
-  int32_t bits;        // number of resolved high bits
-  int32_t k_rem;       // k minus keys strictly above the current prefix
-  int32_t mode;        // 0 refine, 1 collect >= prefix, 2 collect all, 3 ordered ties, 4 empty
-  int32_t ncand;       // appended candidates
-  int32_t k;           // effective k
-  int32_t need_eq;     // mode 3: tied keys still to take (in index order)
-  int32_t pad;
+  uint32_t prefix;   // selected high bits so far
+  int32_t bits;      // number of resolved high bits
+  int32_t k_rem;     // k minus keys strictly above the current prefix
+  int32_t mode;      // 0 refine, 1 collect >= edge, 2 collect all, 3 resolved tie group, 4 empty
+  int32_t k;         // effective k
+  uint32_t edge;     // collect A: key >= edge (mode 1/3: lowest key of the prefix bin)
+  uint32_t win_lo;   // key_mode 1: keys in [win_lo, edge) are tested on their sigmoid
+  uint32_t tie_hi;   // key_mode 1: highest key whose sigmoid equals s_edge (mode 1/3)
+  float s_edge;      // sigmoid of the edge value (key_mode 1)
+  int32_t nA, nB;    // candidates appended to A / B
+  int32_t ncand;     // candidates after resolve (ranked)
 };
 
-__device__ __forceinline__ uint32_t value_key(float v, int key_mode) {
-  if (key_mode == 1) v = 1.f / (1.f + expf(-v));
-  return orderable(v);
+__device__ __forceinline__ float sigmoidf_tf(float v) { return 1.f / (1.f + expf(-v)); }
+
+__device__ __forceinline__ float key_value(float v, int key_mode) {
+  return key_mode == 1 ? sigmoidf_tf(v) : v;
 }
 
 __device__ __forceinline__ void digit_of(int pass, int& shift, int& nbits) {
-  if (pass == 0) { shift = 21; nbits = 11; }
-  else if (pass == 1) { shift = 10; nbits = 11; }
-  else { shift = 0; nbits = 10; }
+  if (pass == 0) { shift = 20; nbits = 12; }
+  else if (pass == 1) { shift = 8; nbits = 12; }
+  else { shift = 0; nbits = 8; }
 }
 
+// [lo, hi) element range of chunk b of a segment whose first element sits at
+// p: chunks are aligned to 16 B in memory; chunk 0 also owns the unaligned head.
+struct Chunk {
+  int head;  // elements before the first 16-B boundary
+  int64_t begin, end;
+};
+__device__ __forceinline__ Chunk chunk_of(const float* p, int len, int b, int per) {
+  Chunk c;
+  c.head = (int)((4 - (((uintptr_t)p >> 2) & 3)) & 3);
+  if (c.head > len) c.head = len;
+  c.begin = (int64_t)c.head + (int64_t)b * per;
+  c.end = c.begin + per;
+  if (c.end > len) c.end = len;
+  return c;
+}
+
+// The workgroup's chunk held in registers: the float4 body (all loads of a
+// thread issued before any use), plus at most one head element (chunk 0,
+// before the first 16-B boundary) and one tail element (last chunk) per thread.
+template <int V>
+struct ChunkRegs {
+  float4 v[V];
+  int64_t begin;
+  int n4;
+  float hv, tv;
+  int hi, ti;
+  bool has_h, has_t, empty;
+
+  __device__ __forceinline__ void load(const float* __restrict__ p, int len, int b) {
+    constexpr int per = kThreads * V * 4;
+    const Chunk c = chunk_of(p, len, b, per);
+    begin = c.begin;
+    empty = c.begin >= c.end && !(b == 0 && c.head > 0);
+    has_h = b == 0 && (int)threadIdx.x < c.head;
+    hi = threadIdx.x;
+    hv = has_h ? p[hi] : 0.f;
+    const int64_t n = c.end > c.begin ? c.end - c.begin : 0;
+    n4 = (int)(n >> 2);
+    const int nt = (int)(n - 4 * (int64_t)n4);
+    has_t = (int)threadIdx.x < nt;
+    ti = (int)(c.begin + 4 * (int64_t)n4) + threadIdx.x;
+    tv = has_t ? p[ti] : 0.f;
+    const float4* p4 = reinterpret_cast<const float4*>(p + c.begin);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int q = u * kThreads + threadIdx.x;
+      v[u] = q < n4 ? p4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  // f(index, value) for every element this thread holds
+  template <typename F>
+  __device__ __forceinline__ void visit(F f) const {
+    if (has_h) f(hi, hv);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int q = u * kThreads + threadIdx.x;
+      if (q < n4) {
+        const int i = (int)(begin + 4 * (int64_t)q);
+        f(i, v[u].x);
+        f(i + 1, v[u].y);
+        f(i + 2, v[u].z);
+        f(i + 3, v[u].w);
+      }
+    }
+    if (has_t) f(ti, tv);
+  }
+};
+
 __global__ void topk_init_kernel(SegState* st, uint32_t* hist, const int32_t* seg_len,
-                                 const int32_t* seg_k, int S, int k) {
-  const int s = blockIdx.x;
-  for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[(size_t)s * kBins + i] = 0;
-  if (threadIdx.x == 0) {
+                                 const int32_t* seg_k, int k) {
+  const int s = blockIdx.y;
+  uint32_t* h = hist + ((size_t)s * kRep + blockIdx.x) * kBins;
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int len = max(seg_len[s], 0);
     int kk = seg_k ? min(seg_k[s], k) : k;
-    kk = min(kk, len);
-    SegState x;
-    x.prefix = 0;
-    x.bits = 0;
+    kk = max(min(kk, len), 0);
+    SegState x = {};
     x.k_rem = kk;
     x.k = kk;
-    x.ncand = 0;
-    x.need_eq = 0;
-    x.pad = 0;
     x.mode = kk == 0 ? 4 : (len <= kCap ? 2 : 0);
     st[s] = x;
   }
 }
 
-__global__ __launch_bounds__(256) void topk_hist_kernel(const float* __restrict__ values,
-                                                        const int64_t* __restrict__ seg_start,
-                                                        const int32_t* __restrict__ seg_len,
-                                                        const SegState* __restrict__ st,
-                                                        uint32_t* __restrict__ hist, int pass,
-                                                        int key_mode) {
+template <int V>
+__global__ __launch_bounds__(kThreads) void topk_hist_kernel(
+    const float* __restrict__ values, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_len, const SegState* __restrict__ st,
+    uint32_t* __restrict__ hist, int pass) {
   const int s = blockIdx.y;
   const SegState x = st[s];
   if (x.mode != 0) return;
+  const int len = seg_len[s];
+  const int b = blockIdx.x;
+  const float* p = values + seg_start[s];
+  ChunkRegs<V> cr;
+  cr.load(p, len, b);
+  if (cr.empty) return;
   __shared__ uint32_t h[kBins];
-  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  for (int i = threadIdx.x; i < kBins; i += kThreads) h[i] = 0;
   __syncthreads();
   int shift, nbits;
   digit_of(pass, shift, nbits);
-  const float* v = values + seg_start[s];
-  const int len = seg_len[s];
   const int hs = shift + nbits;  // bits above this digit
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
-    const uint32_t key = value_key(v[i], key_mode);
-    if (hs == 32 || (key >> hs) == x.prefix) atomicAdd(&h[(key >> shift) & ((1u << nbits) - 1u)], 1u);
-  }
+  const uint32_t mask = (1u << nbits) - 1u;
+  cr.visit([&](int, float v) {
+    const uint32_t key = orderable(v);
+    if (hs == 32 || (key >> hs) == x.prefix) atomicAdd(&h[(key >> shift) & mask], 1u);
+  });
   __syncthreads();
-  uint32_t* g = hist + (size_t)s * kBins;
-  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+  uint32_t* g = hist + ((size_t)s * kRep + (b & (kRep - 1))) * kBins;
+  for (int i = threadIdx.x; i < kBins; i += kThreads)
     if (h[i]) atomicAdd(&g[i], h[i]);
 }
 
-__global__ __launch_bounds__(256) void topk_select_kernel(SegState* st, uint32_t* hist,
-                                                          int pass) {
+// sigmoid(from_orderable(u)) over a key range, as a function of the key:
+// monotone non-decreasing (sigmoid is).  Smallest key in [lo, hi] whose
+// sigmoid is >= s, or hi + 1.
+__device__ uint32_t lower_bound_sig(uint32_t lo, uint32_t hi, float s) {
+  uint32_t a = lo, b = hi + 1;  // search [a, b)
+  while (a < b) {
+    const uint32_t m = a + ((b - a) >> 1);
+    if (sigmoidf_tf(from_orderable(m)) >= s) b = m;
+    else a = m + 1;
+  }
+  return a;
+}
+// Largest key in [lo, hi] whose sigmoid is <= s (lo's sigmoid must be <= s).
+__device__ uint32_t upper_bound_sig(uint32_t lo, uint32_t hi, float s) {
+  uint32_t a = lo, b = hi;
+  while (a < b) {
+    const uint32_t m = a + ((b - a + 1) >> 1);
+    if (sigmoidf_tf(from_orderable(m)) <= s) a = m;
+    else b = m - 1;
+  }
+  return a;
+}
+
+constexpr uint32_t kKeyNegInf = 0x007fffffu;  // orderable(-inf)
+constexpr uint32_t kKeyPosInf = 0xff800000u;  // orderable(+inf)
+constexpr uint32_t kWindowMargin = 256;       // keys below the solved tie edge still tested
+
+__device__ void finish_state(SegState& x, int key_mode) {
+  // x.edge: lowest key of the prefix bin (mode 1) or the resolved key (mode 3)
+  x.win_lo = x.edge;
+  x.tie_hi = x.edge;
+  x.s_edge = 0.f;
+  if (key_mode == 1 && x.edge > kKeyNegInf && x.edge <= kKeyPosInf) {
+    const float se = sigmoidf_tf(from_orderable(x.edge));
+    x.s_edge = se;
+    const uint32_t lo = lower_bound_sig(kKeyNegInf, x.edge, se);
+    x.win_lo = lo > kKeyNegInf + kWindowMargin ? lo - kWindowMargin : kKeyNegInf;
+    x.tie_hi = upper_bound_sig(x.edge, kKeyPosInf, se);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void topk_select_kernel(SegState* st, uint32_t* hist,
+                                                               int pass, int key_mode) {
   const int s = blockIdx.x;
   SegState x = st[s];
   if (x.mode != 0) return;
   int shift, nbits;
   digit_of(pass, shift, nbits);
   const int nb = 1 << nbits;
-  uint32_t* g = hist + (size_t)s * kBins;
-  // suffix sums from the top bin: thread t owns bins [nb-1-8t-7, nb-1-8t] (top first)
-  __shared__ uint32_t part[256];
-  const int per = nb / 256;
+  uint32_t* g = hist + (size_t)s * kRep * kBins;
+  // suffix sums from the top bin: thread t owns bins [nb-1-per*t-(per-1), nb-1-per*t]
+  __shared__ uint32_t part[kThreads];
+  __shared__ uint32_t cnt[kBins];
+  const int per = nb / kThreads;
   const int t = threadIdx.x;
   uint32_t loc = 0;
-  for (int j = 0; j < per; ++j) loc += g[nb - 1 - (t * per + j)];
+  for (int j = 0; j < per; ++j) {
+    const int bin = nb - 1 - (t * per + j);
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) c += g[(size_t)r * kBins + bin];
+    cnt[bin] = c;
+    loc += c;
+  }
   part[t] = loc;
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
+  for (int o = 1; o < kThreads; o <<= 1) {
     const uint32_t add = t >= o ? part[t - o] : 0u;
     __syncthreads();
     part[t] += add;
@@ -127,10 +266,10 @@ __global__ __launch_bounds__(256) void topk_select_kernel(SegState* st, uint32_t
   if ((uint32_t)x.k_rem > before && (uint32_t)x.k_rem <= part[t]) {
     uint32_t acc = before;
     for (int j = 0; j < per; ++j) {
-      const int b = nb - 1 - (t * per + j);
-      const uint32_t c = g[b];
+      const int bin = nb - 1 - (t * per + j);
+      const uint32_t c = cnt[bin];
       if ((uint32_t)x.k_rem <= acc + c) {
-        found_bin = b;
+        found_bin = bin;
         found_gt = acc;
         found_eq = c;
         break;
@@ -139,140 +278,227 @@ __global__ __launch_bounds__(256) void topk_select_kernel(SegState* st, uint32_t
     }
   }
   __syncthreads();
-  // reset histogram for the next pass
-  for (int i = t; i < kBins; i += blockDim.x) g[i] = 0;
+  // reset the replicas for the next pass
+  for (int i = t; i < kRep * kBins; i += kThreads) g[i] = 0;
   if (t == 0) {
     if (found_bin < 0) {
-      x.mode = 2;  // should not happen (counts inconsistent); fall back to "all"
+      x.mode = 2;  // counts inconsistent (cannot happen): take everything, resolve decides
+      x.edge = 0;
     } else {
       x.prefix = (x.prefix << nbits) | (uint32_t)found_bin;
       x.bits += nbits;
-      const int gt_total = (x.k - x.k_rem) + (int)found_gt;  // keys strictly above prefix
+      const int gt_total = (x.k - x.k_rem) + (int)found_gt;  // keys strictly above the bin
       x.k_rem -= (int)found_gt;
-      if (gt_total + (int)found_eq <= kCap) x.mode = 1;
-      else if (x.bits == 32) {
-        x.mode = 3;
-        x.need_eq = x.k_rem;
+      if (gt_total + (int)found_eq <= kCap || x.bits == 32) {
+        x.mode = gt_total + (int)found_eq <= kCap ? 1 : 3;
+        x.edge = x.prefix << (32 - x.bits);
+        finish_state(x, key_mode);
       }
     }
     st[s] = x;
   }
 }
 
-__global__ __launch_bounds__(256) void topk_collect_kernel(const float* __restrict__ values,
-                                                           const int64_t* __restrict__ seg_start,
-                                                           const int32_t* __restrict__ seg_len,
-                                                           SegState* __restrict__ st,
-                                                           uint64_t* __restrict__ cand,
-                                                           int key_mode) {
+// Block-aggregated append: every thread contributes c items; returns the
+// thread's first slot (one atomic per workgroup on *counter).
+__device__ __forceinline__ int block_reserve(int c, int32_t* counter) {
+  __shared__ int wsum[kThreads / 64];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int wbefore = 0, total = 0;
+#pragma unroll
+  for (int j = 0; j < kThreads / 64; ++j) {
+    if (j < w) wbefore += wsum[j];
+    total += wsum[j];
+  }
+  if (threadIdx.x == 0) base = total ? atomicAdd(counter, total) : 0;
+  __syncthreads();
+  return base + wbefore + incl - c;
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void topk_collect_kernel(
+    const float* __restrict__ values, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_len, SegState* __restrict__ st,
+    uint64_t* __restrict__ candA, uint64_t* __restrict__ candB, int key_mode) {
   const int s = blockIdx.y;
   const SegState x = st[s];
   if (x.mode == 0 || x.mode == 4) return;
-  const float* v = values + seg_start[s];
   const int len = seg_len[s];
-  uint64_t* c = cand + (size_t)s * kCap;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
-    const float val = v[i];
-    const uint32_t key = value_key(val, key_mode);
-    bool take;
-    if (x.mode == 2) take = true;
-    else if (x.mode == 1) take = (key >> (32 - x.bits)) >= x.prefix;
-    else take = key > x.prefix;  // mode 3: strictly greater; ties appended in order below
-    if (take) {
-      const int pos = atomicAdd(&st[s].ncand, 1);
-      if (pos < kCap) c[pos] = ((uint64_t)(~key) << 32) | (uint32_t)i;
+  const int b = blockIdx.x;
+  const float* p = values + seg_start[s];
+  ChunkRegs<V> cr;
+  cr.load(p, len, b);
+  if (cr.empty) return;
+  // mode 2: all; mode 1: >= edge; mode 3: above the tie group (ties come in
+  // index order in resolve; tie_hi == UINT32_MAX: nothing is above it)
+  const bool none_above = x.mode == 3 && x.tie_hi == 0xffffffffu;
+  const uint32_t a_lo = x.mode == 2 ? 0u : (x.mode == 3 ? x.tie_hi + 1u : x.edge);
+  const bool win = key_mode == 1 && x.mode == 1 && x.win_lo < x.edge;
+  int na = 0, nb = 0;
+  cr.visit([&](int, float v) {
+    const uint32_t key = orderable(v);
+    if (none_above) return;
+    if (key >= a_lo) ++na;
+    else if (win && key >= x.win_lo && sigmoidf_tf(v) >= x.s_edge) ++nb;
+  });
+  int oa = block_reserve(na, &st[s].nA);
+  int ob = block_reserve(nb, &st[s].nB);
+  uint64_t* A = candA + (size_t)s * kCap;
+  uint64_t* B = candB + (size_t)s * kCap;
+  cr.visit([&](int i, float v) {
+    const uint32_t key = orderable(v);
+    if (none_above) return;
+    const uint64_t e = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)i;
+    if (key >= a_lo) {
+      if (oa < kCap) A[oa] = e;
+      ++oa;
+    } else if (win && key >= x.win_lo && sigmoidf_tf(v) >= x.s_edge) {
+      if (ob < kCap) B[ob] = e;
+      ++ob;
     }
-  }
+  });
 }
 
-// mode 3 only: append the first need_eq keys equal to prefix, in index order.
-__global__ __launch_bounds__(1024) void topk_ties_kernel(const float* __restrict__ values,
-                                                         const int64_t* __restrict__ seg_start,
-                                                         const int32_t* __restrict__ seg_len,
-                                                         SegState* __restrict__ st,
-                                                         uint64_t* __restrict__ cand,
-                                                         int key_mode) {
+// A + B when they fit; else the ordered path (module comment).
+__global__ __launch_bounds__(1024) void topk_resolve_kernel(
+    const float* __restrict__ values, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_len, SegState* __restrict__ st, uint64_t* __restrict__ candA,
+    const uint64_t* __restrict__ candB, int key_mode) {
   const int s = blockIdx.x;
-  const SegState x = st[s];
-  if (x.mode != 3) return;
-  const float* v = values + seg_start[s];
-  const int len = seg_len[s];
-  uint64_t* c = cand + (size_t)s * kCap;
+  SegState x = st[s];
   __shared__ int wsum[16];
-  __shared__ int base;
-  if (threadIdx.x == 0) base = st[s].ncand;
-  int need = x.need_eq;
+  __shared__ int base_sh;
+  if (x.mode == 0 || x.mode == 4) {
+    if (threadIdx.x == 0) st[s].ncand = 0;
+    return;
+  }
+  uint64_t* A = candA + (size_t)s * kCap;
+  const uint64_t* B = candB + (size_t)s * kCap;
+  const int nA = min(x.nA, kCap), nB = x.nB;
+  if (x.mode != 3 && nA + nB <= kCap) {
+    for (int i = threadIdx.x; i < nB; i += blockDim.x) A[nA + i] = B[i];
+    if (threadIdx.x == 0) st[s].ncand = nA + nB;
+    return;
+  }
+  // ordered path.  Tie group: keys in [tie_lo, tie_hi] whose key value equals
+  // the edge's (key_mode 1: sigmoid == s_edge, tested exactly).  1. keep the
+  // A entries strictly above the group, in place (order is irrelevant: ranked).
+  const uint32_t tie_hi = x.tie_hi;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (threadIdx.x == 0) base_sh = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int c0 = 0; c0 < len && need > 0; c0 += blockDim.x) {
+  for (int c0 = 0; c0 < nA; c0 += blockDim.x) {
     const int i = c0 + threadIdx.x;
-    const bool eq = i < len && value_key(v[i], key_mode) == x.prefix;
-    const uint64_t b = __ballot(eq);
-    const int wrank = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[wv] = __popcll(b);
+    uint64_t e = 0;
+    bool keep = false;
+    if (i < nA) {
+      e = A[i];
+      keep = orderable(__uint_as_float((uint32_t)(e >> 32))) > tie_hi;
+    }
+    const uint64_t bal = __ballot(keep);
+    const int wrank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(bal);
     __syncthreads();
     int before = 0, total = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+    for (int w = 0; w < nw; ++w) {
+      if (w < wv) before += wsum[w];
+      total += wsum[w];
+    }
+    const int pos = base_sh + before + wrank;
+    __syncthreads();  // every read of A[c0..] precedes the compacting writes
+    if (keep) A[pos] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) base_sh += total;
+    __syncthreads();
+  }
+  int have = base_sh;
+  int need = x.k - have;
+  // 2. the tied keys in index order until k
+  const float* v = values + seg_start[s];
+  const int len = seg_len[s];
+  const uint32_t tie_lo = key_mode == 1 ? x.win_lo : x.edge;
+  for (int c0 = 0; c0 < len && need > 0; c0 += blockDim.x) {
+    const int i = c0 + threadIdx.x;
+    bool eq = false;
+    float val = 0.f;
+    if (i < len) {
+      val = v[i];
+      const uint32_t key = orderable(val);
+      if (key >= tie_lo && key <= tie_hi)
+        eq = key_mode == 1 ? sigmoidf_tf(val) == x.s_edge : key == x.edge;
+    }
+    const uint64_t bal = __ballot(eq);
+    const int wrank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < nw; ++w) {
       if (w < wv) before += wsum[w];
       total += wsum[w];
     }
     const int rank = before + wrank;
-    if (eq && rank < need) c[base + rank] = ((uint64_t)(~x.prefix) << 32) | (uint32_t)i;
-    __syncthreads();
+    if (eq && rank < need) A[have + rank] = ((uint64_t)__float_as_uint(val) << 32) | (uint32_t)i;
     const int took = min(total, need);
-    if (threadIdx.x == 0) base += took;
+    have += took;
     need -= took;
     __syncthreads();
   }
-  if (threadIdx.x == 0) st[s].ncand = base;
+  if (threadIdx.x == 0) st[s].ncand = min(have, kCap);
 }
 
-__global__ __launch_bounds__(1024) void topk_final_kernel(const uint64_t* __restrict__ cand,
-                                                          const SegState* __restrict__ st,
-                                                          int kmax, int key_mode,
-                                                          float* __restrict__ vals_out,
-                                                          int32_t* __restrict__ idx_out,
-                                                          int32_t* __restrict__ count_out,
-                                                          int32_t* err) {
+// Counting rank on the final key (~orderable(score) << 32 | index): a block
+// ranks 64 candidates against all of its segment's, each wave a quarter of them.
+constexpr int kRankI = 64;
+__global__ __launch_bounds__(kThreads) void topk_rank_kernel(
+    const uint64_t* __restrict__ candA, const SegState* __restrict__ st, int kmax, int key_mode,
+    float* __restrict__ vals_out, int32_t* __restrict__ idx_out, int32_t* __restrict__ count_out) {
   extern __shared__ uint64_t sk[];
-  const int s = blockIdx.x;
+  __shared__ uint32_t part[kThreads];
+  const int s = blockIdx.y;
   const SegState x = st[s];
-  int len = x.mode == 4 ? 0 : x.ncand;
-  if (len > kCap) {
-    if (threadIdx.x == 0) atomicOr(err, kErrTopkCapacity);
-    len = kCap;
-  }
-  int n = 1;
-  while (n < len) n <<= 1;
-  const uint64_t* src = cand + (size_t)s * kCap;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) sk[i] = i < len ? src[i] : ~0ull;
-  __syncthreads();
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = sk[i], b = sk[ixj];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) { sk[i] = b; sk[ixj] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  const int kk = min(x.k, len);
-  for (int i = threadIdx.x; i < kmax; i += blockDim.x) {
-    if (i < kk) {
-      const uint64_t key = sk[i];
-      vals_out[(size_t)s * kmax + i] = from_orderable(~(uint32_t)(key >> 32));
-      idx_out[(size_t)s * kmax + i] = (int32_t)(key & 0xffffffffu);
-    } else {
+  const int n = x.mode == 4 ? 0 : x.ncand;
+  const int kk = min(x.k, n);
+  const int i0 = blockIdx.x * kRankI;
+  if (blockIdx.x == 0) {
+    for (int i = kk + threadIdx.x; i < kmax; i += kThreads) {
       vals_out[(size_t)s * kmax + i] = 0.f;
       idx_out[(size_t)s * kmax + i] = -1;
     }
+    if (threadIdx.x == 0) count_out[s] = kk;
   }
-  if (threadIdx.x == 0) count_out[s] = kk;
-  (void)key_mode;
+  if (i0 >= n) return;
+  const uint64_t* A = candA + (size_t)s * kCap;
+  for (int j = threadIdx.x; j < n; j += kThreads) {
+    const uint64_t e = A[j];
+    const float sc = key_value(__uint_as_float((uint32_t)(e >> 32)), key_mode);
+    sk[j] = ((uint64_t)(~orderable(sc)) << 32) | (uint32_t)e;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = i0 + lane;
+  const uint64_t mine = i < n ? sk[i] : ~0ull;
+  const int q = (n + 3) >> 2;
+  const int j0 = w * q, j1 = min(n, j0 + q);
+  uint32_t r = 0;
+  for (int j = j0; j < j1; ++j) r += sk[j] < mine ? 1u : 0u;
+  part[threadIdx.x] = r;
+  __syncthreads();
+  if (w == 0 && i < n) {
+    const uint32_t rank = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane];
+    if ((int)rank < kk) {
+      vals_out[(size_t)s * kmax + rank] = from_orderable(~(uint32_t)(mine >> 32));
+      idx_out[(size_t)s * kmax + rank] = (int32_t)(uint32_t)mine;
+    }
+  }
 }
 
 }  // namespace
@@ -281,7 +507,8 @@ size_t topk_workspace_size(int S, int k) {
   (void)k;
   WorkspaceSizer z;
   z.take<SegState>(S);
-  z.take<uint32_t>((size_t)S * kBins);
+  z.take<uint32_t>((size_t)S * kRep * kBins);
+  z.take<uint64_t>((size_t)S * kCap);
   z.take<uint64_t>((size_t)S * kCap);
   return z.off;
 }
@@ -295,29 +522,43 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
   if (S == 0) return 0;
   Workspace w(ws, ws_bytes);
   SegState* st = w.take<SegState>(S);
-  uint32_t* hist = w.take<uint32_t>((size_t)S * kBins);
-  uint64_t* cand = w.take<uint64_t>((size_t)S * kCap);
+  uint32_t* hist = w.take<uint32_t>((size_t)S * kRep * kBins);
+  uint64_t* candA = w.take<uint64_t>((size_t)S * kCap);
+  uint64_t* candB = w.take<uint64_t>((size_t)S * kCap);
   D2MI_REQUIRE(w.ok(), "top-k workspace too small (%zu < %zu)", ws_bytes, w.off);
-  const int per_block = 256 * 16;
-  const int gx = std::max(1, std::min((max_len + per_block - 1) / per_block, 4096));
-  hipLaunchKernelGGL(topk_init_kernel, dim3(S), dim3(256), 0, stream, st, hist, seg_len, seg_k, S,
-                     k);
+  // chunk per workgroup: 16 K elements for the dense RetinaNet levels, 4 K
+  // for RPN-sized segments (more workgroups over a smaller scan)
+  const bool big = max_len >= (1 << 20);
+  const int per = kThreads * 4 * (big ? 16 : 4);
+  const int gx = std::max(1, (max_len + 3 + per - 1) / per);
+  hipLaunchKernelGGL(topk_init_kernel, dim3(kRep, S), dim3(256), 0, stream, st, hist, seg_len,
+                     seg_k, k);
   D2MI_LAUNCH_CHECK();
   for (int pass = 0; pass < 3; ++pass) {
-    hipLaunchKernelGGL(topk_hist_kernel, dim3(gx, S), dim3(256), 0, stream, values, seg_start,
-                       seg_len, st, hist, pass, key_mode);
+    if (big)
+      hipLaunchKernelGGL(topk_hist_kernel<16>, dim3(gx, S), dim3(kThreads), 0, stream, values,
+                         seg_start, seg_len, st, hist, pass);
+    else
+      hipLaunchKernelGGL(topk_hist_kernel<4>, dim3(gx, S), dim3(kThreads), 0, stream, values,
+                         seg_start, seg_len, st, hist, pass);
     D2MI_LAUNCH_CHECK();
-    hipLaunchKernelGGL(topk_select_kernel, dim3(S), dim3(256), 0, stream, st, hist, pass);
+    hipLaunchKernelGGL(topk_select_kernel, dim3(S), dim3(kThreads), 0, stream, st, hist, pass,
+                       key_mode);
     D2MI_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(topk_collect_kernel, dim3(gx, S), dim3(256), 0, stream, values, seg_start,
-                     seg_len, st, cand, key_mode);
+  if (big)
+    hipLaunchKernelGGL(topk_collect_kernel<16>, dim3(gx, S), dim3(kThreads), 0, stream, values,
+                       seg_start, seg_len, st, candA, candB, key_mode);
+  else
+    hipLaunchKernelGGL(topk_collect_kernel<4>, dim3(gx, S), dim3(kThreads), 0, stream, values,
+                       seg_start, seg_len, st, candA, candB, key_mode);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(topk_ties_kernel, dim3(S), dim3(1024), 0, stream, values, seg_start, seg_len,
-                     st, cand, key_mode);
+  hipLaunchKernelGGL(topk_resolve_kernel, dim3(S), dim3(1024), 0, stream, values, seg_start,
+                     seg_len, st, candA, candB, key_mode);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(topk_final_kernel, dim3(S), dim3(1024), kCap * sizeof(uint64_t), stream, cand,
-                     st, k, key_mode, vals_out, idx_out, count_out, error_word());
+  hipLaunchKernelGGL(topk_rank_kernel, dim3(kCap / kRankI, S), dim3(kThreads),
+                     kCap * sizeof(uint64_t), stream, candA, st, k, key_mode, vals_out, idx_out,
+                     count_out);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

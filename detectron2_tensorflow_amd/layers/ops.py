@@ -851,11 +851,15 @@ def retinanet_inference(box_cls, box_delta, strides, cell_anchors, num_classes, 
     wsb = _C.lib().d2mi_retinanet_workspace_size(N, L, lhw, A, int(num_classes),
                                                  int(topk_candidates))
     ws = _C.workspace(wsb, dev)
+    ev = KernelTimer.start()
     rc = _C.lib().d2mi_retinanet_inference(
         cp, bp, lhw, st, cells, L, A, int(num_classes), N, int(topk_candidates),
         float(score_threshold), float(nms_threshold), int(max_detections),
         _C.host_array(_C.c_float, [float(w) for w in weights]), float(scale_clamp), _C.ptr(ob),
         _C.ptr(os_), _C.ptr(oc), _C.ptr(ov), _C.ptr(ws), wsb, _C.stream_of(dev))
+    # algorithmic bytes: the dense logit scan, 4 B per (anchor, class) score
+    # (64.5 MB per image at 1333x800)
+    KernelTimer.stop(ev, "retinanet_topk", 4 * sum(t.numel() for t in box_cls))
     _C.check(rc, "d2mi_retinanet_inference")
     return ob, os_, oc, ov.bool()
 

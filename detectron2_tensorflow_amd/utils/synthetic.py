@@ -46,3 +46,24 @@ def synthetic_train_batch(batch, height, width, seed, device, **kw):
     out = synthetic_images(batch, height, width, seed, device)
     out["instances"] = synthetic_instances(batch, height, width, seed, device, **kw)
     return out
+
+
+@torch.no_grad()
+def calibrate_retinanet_head(tower, box_cls, box_delta, cls_mean=-3.0, cls_std=1.0,
+                             delta_std=0.1):
+    """BASELINE.md score injection for a random-init RetinaNet: rescale the
+    cls_score / bbox_pred conv weights (the convs are linear in their weights)
+    so that, on the features that produced ``box_cls`` / ``box_delta`` (the
+    head's outputs, any device), the class logits are ~ N(cls_mean, cls_std^2)
+    and the deltas ~ N(0, delta_std^2).  A random-init ResNet's unnormalised
+    features otherwise give logits of std ~20 (every sigmoid saturates to 1.0)
+    and deltas of O(10)."""
+    def std_wo_bias(outs, bias):
+        return float(torch.cat([(o - bias.to(o.device)).reshape(-1) for o in outs]).double().std())
+
+    s = std_wo_bias(box_cls, tower.cls_score.bias)
+    tower.cls_score.weights.mul_(cls_std / max(s, 1e-12))
+    tower.cls_score.bias.fill_(cls_mean)
+    s = std_wo_bias(box_delta, tower.bbox_pred.bias)
+    tower.bbox_pred.weights.mul_(delta_std / max(s, 1e-12))
+    tower.bbox_pred.bias.zero_()

@@ -62,7 +62,9 @@ def _backbone(bb, x):
 
 
 def _fpn(neck, x_feats):
-    """FPN.call (fpn.py:121-159) + LastLevelMaxPool (fpn.py:171-183)."""
+    """FPN.call (fpn.py:121-159) + LastLevelMaxPool (fpn.py:171-183) or
+    LastLevelP6P7 (fpn.py:186-217: p6 = ReLU(conv3x3/2(res5)) — the post-ReLU
+    p6 is what the head sees — and p7 = conv3x3/2(p6), no activation)."""
     x = [x_feats[f] for f in neck.in_features[::-1]]
     prev = _conv(x[0], neck.lateral_convs[0])
     results = [_conv(prev, neck.output_convs[0])]
@@ -70,7 +72,12 @@ def _fpn(neck, x_feats):
         top = prev.repeat_interleave(2, 1).repeat_interleave(2, 2)
         prev = _conv(f, lat) + top
         results.insert(0, _conv(prev, out))
-    results.append(results[-1][:, ::2, ::2, :])  # LastLevelMaxPool
+    tb = neck.top_block_type
+    if tb == "MAXPOOL":
+        results.append(results[-1][:, ::2, ::2, :])  # max_pool k1 s2 VALID
+    elif tb == "P6P7":
+        p6 = _conv(x_feats["res5"], neck.top_block.p6)
+        results.extend([p6, _conv(p6, neck.top_block.p7)])
     return dict(zip(neck._out_features, results))
 
 
@@ -159,6 +166,78 @@ class CPUReference:
                 out["masks"] = np.stack([
                     oracle.paste_masks(masks[n], out["boxes"][n], paste_to, valid=out["is_valid"][n])
                     for n in range(N)])
+        return out
+
+
+class CPURetinaNet:
+    """SingleStageDetector + RetinaNetHead inference on CPU
+    (single_stage_detector.py:33-83, retinanet.py:110-145, :285-387,
+    :418-450): preprocess -> ResNet -> FPN with the P6P7 top block -> box tower
+    (NUM_CONVS x conv3x3+ReLU per branch, cls_score / bbox_pred conv3x3) ->
+    ALL anchors materialised per level (anchor_generator.py:92-109) ->
+    oracle.retinanet_inference (per level sigmoid + top_k(1000) + 0.05
+    threshold + decode with MODEL.RPN.BBOX_REG_WEIGHTS, class-offset NMS,
+    pad to DETECTIONS_PER_IMAGE)."""
+
+    def __init__(self, model):
+        self.m = copy.deepcopy(model).cpu().eval()
+        for p in self.m.parameters():
+            p.requires_grad_(False)
+
+    def features(self, images):
+        m = self.m
+        x = (torch.from_numpy(np.asarray(images, F32)) - m.pixel_mean) / m.pixel_std
+        if m.input_format == "BGR":
+            x = x.flip(-1)
+        H, W = x.shape[1:3]
+        d = m.neck.size_divisibility
+        x = F.pad(x, (0, 0, 0, (-W) % d, 0, (-H) % d))
+        return _fpn(m.neck, _backbone(m.backbone, x.contiguous()))
+
+    def head(self, feats):
+        """RetinaNetBoxTower.call (retinanet.py:431-450): [N,H,W,A*K], [N,H,W,A*4]."""
+        det = self.m.detector
+        tower = det.head
+        cls, box = [], []
+        for f in det.in_features:
+            y = feats[f]
+            for c in tower.cls_layers:
+                y = _conv(y, c)
+            cls.append(_conv(y, tower.cls_score))
+            y = feats[f]
+            for c in tower.box_layers:
+                y = _conv(y, c)
+            box.append(_conv(y, tower.bbox_pred))
+        return cls, box
+
+    def postprocess(self, cls, box):
+        """RetinaNetHead.inference on given head outputs (numpy or torch)."""
+        det = self.m.detector
+        ag = det.anchor_generator
+        K = det.num_classes
+        cls = [np.asarray(c, F32) for c in cls]
+        box = [np.asarray(b, F32) for b in box]
+        N = cls[0].shape[0]
+        anchors = [oracle.grid_anchors(c.shape[1], c.shape[2], ag.strides[i],
+                                       ag.cell_anchors[i].numpy())
+                   for i, c in enumerate(cls)]
+        res = oracle.retinanet_inference([c.reshape(N, -1, K) for c in cls],
+                                         [b.reshape(N, -1, 4) for b in box], anchors, K,
+                                         det.topk_candidates, det.score_threshold,
+                                         det.nms_threshold, det.max_detections_per_image,
+                                         det.box2box_transform.weights,
+                                         det.box2box_transform.scale_clamp)
+        return {"boxes": np.stack([r[0] for r in res]), "scores": np.stack([r[1] for r in res]),
+                "classes": np.stack([r[2] for r in res]),
+                "is_valid": np.stack([r[3] for r in res])}
+
+    @torch.no_grad()
+    def __call__(self, images, image_shapes=None, threads=None):
+        if threads:
+            torch.set_num_threads(threads)
+        cls, box = self.head(self.features(images))
+        out = self.postprocess([c.numpy() for c in cls], [b.numpy() for b in box])
+        out["head"] = (cls, box)
         return out
 
 

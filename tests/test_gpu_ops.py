@@ -108,6 +108,40 @@ def test_roi_align_backward_raw_matches_tf_grad(dev):
     np.testing.assert_array_equal(x.grad.cpu().numpy(), want)
 
 
+def test_roi_align_backward_unaligned_grad_maps(dev):
+    """d2mi_roi_align_bwd on caller-owned gradient maps that start 4 B past a
+    16-B boundary (a sliced tensor): the clear kernel's unaligned head and
+    tail paths.  Untouched pixels come back zero, touched ones equal the TF
+    CropAndResizeGradImage restatement, and the guard words around the maps
+    are not written."""
+    from detectron2_tensorflow_amd import _C
+    rng = np.random.default_rng(44)
+    N, H, W, C, R, oh, ow = 2, 13, 19, 8, 40, 6, 5
+    boxes = rng.uniform(-0.1, 0.9, size=(R, 4)).astype(F32)
+    bimg = rng.integers(0, N, size=R).astype(np.int32)
+    g = rng.normal(size=(R, oh, ow, C)).astype(F32)
+    want = oracle.crop_and_resize_grad_image(g, boxes, bimg, (N, H, W))
+    n = N * H * W * C
+    buf = torch.full((n + 2,), 7.0, dtype=torch.float32, device=dev)  # guard word each side
+    grad = buf[1:n + 1]
+    assert grad.data_ptr() % 16 == 4
+    bt, it, gt = (torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
+                  torch.from_numpy(g).to(dev))
+    gp = _C.host_array(_C.c_void_p, [grad.data_ptr()])
+    dims = _C.host_array(_C.ctypes.c_int32, [N, H, W])
+    sc = _C.host_array(_C.c_float, [1.0])
+    wsb = _C.lib().d2mi_roi_align_bwd_workspace_size(dims, 1, C, R, oh, ow, 0)
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_roi_align_bwd(gp, dims, sc, 1, C, _C.ptr(bt), _C.ptr(it), R, oh, ow, 0,
+                                     ops().BOX_MODE_RAW, 0, 0, 0, 0, 224, 4, _C.ptr(gt),
+                                     _C.ptr(ws), wsb, _C.stream_of(dev))
+    _C.check(rc, "d2mi_roi_align_bwd")
+    got = buf.cpu().numpy()
+    assert got[0] == 7.0 and got[-1] == 7.0
+    np.testing.assert_array_equal(got[1:n + 1].reshape(N, H, W, C), want)
+    assert (want == 0).any()  # some pixels untouched: the clear path is exercised
+
+
 @pytest.mark.parametrize("C,crop,sr", [(300, (14, 14), 0), (64, (7, 7), 2), (3, (28, 20), 0)])
 def test_roi_align_backward_raw_large_crops_and_ragged_channels(dev, C, crop, sr):
     """More samples than one 64-lane block, channel counts off the 64-chunk grid,
@@ -253,11 +287,16 @@ def test_nms_large_segment_uses_radix_sort_path(dev):
 # --------------------------------------------------------------------- top-k
 def test_topk_segments_vs_oracle(dev):
     rng = np.random.default_rng(12)
-    lens = [1, 10, 999, 5000, 9000, 201600, 300000]
+    lens = [1, 10, 999, 5000, 9000, 201600, 300000, 300001, 1 << 20]
     vals = [rng.normal(size=n).astype(F32) for n in lens]
     vals[3] = np.round(vals[3], 1)           # heavy ties
     vals[4][:] = 0.5                          # all tied: ordered-ties path
     vals[6] = np.round(vals[6] * 4) / 4       # ties straddling the threshold bin
+    # saturated logits: every sigmoid is exactly 1.0 (both sides), so key_mode 1
+    # takes the ordered path over the sigmoid tie group (lowest indices first)
+    # while the raw values are all distinct; odd length + odd start (unaligned)
+    vals[7] = np.maximum(rng.normal(40, 5, size=lens[7]), 25).astype(F32)
+    vals[8] = (rng.normal(-3, 1, size=lens[8])).astype(F32)  # RetinaNet-like, big-chunk path
     flat = np.concatenate(vals)
     start = np.cumsum([0] + lens[:-1]).astype(np.int64)
     for k in (1, 1000, 2000):
@@ -273,8 +312,11 @@ def test_topk_segments_vs_oracle(dev):
                 assert c[s] == len(wi)
                 if sig:
                     # GPU expf vs CPU expf may differ by 1 ulp: compare values,
-                    # and indices wherever the oracle keys are untied
+                    # and indices on the saturated segment (exact ties at 1.0)
                     np.testing.assert_allclose(v[s, : c[s]], wv, rtol=1e-6, atol=0)
+                    if s == 7:
+                        assert (wv == 1.0).all()
+                        np.testing.assert_array_equal(i[s, : c[s]], wi)
                 else:
                     np.testing.assert_array_equal(i[s, : c[s]], wi)
                     np.testing.assert_array_equal(v[s, : c[s]], wv)

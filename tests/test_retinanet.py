@@ -1,0 +1,198 @@
+"""RetinaNet model path (BASELINE configs C1 and C4): SingleStageDetector +
+RetinaNetHead (lib/modeling/meta_arch/single_stage_detector.py:33-83,
+lib/modeling/single_stage_heads/retinanet.py:110-145, :285-387, :418-450).
+
+C1 — R50-FPN forward of one synthetic 640x640 image on the CPU restatement
+(oracle/cpu_pipeline.py: CPURetinaNet; the reference config is CPU plumbing).
+C4 — the GPU path: R50 at 640x640 against the CPU restatement (head outputs,
+post-processing bit-exact on identical head outputs, detections end to end),
+and R101-FPN at 1333x800 (201,600 anchors x 80 classes = 16.1 M sigmoid
+scores per image) against the oracle's post-processing on the GPU's own head
+outputs, plus determinism and the padded output layout.
+
+Random-init weights give logits of std ~20 (every sigmoid saturates at 1.0):
+the cls_score / bbox_pred weights are rescaled once so logits ~ N(-3, 1) and
+deltas ~ N(0, 0.1^2) (BASELINE.md score injection), on both sides.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F32 = np.float32
+CM = {"num_thing_classes": 80, "num_stuff_classes": 53, "stuff_ignore_value": 0}
+
+
+def _cfg(depth=50):
+    from detectron2_tensorflow_amd.config import finalize, get_cfg
+    cfg = get_cfg()
+    name = "retinanet_R_50_FPN_1x.yaml" if depth == 50 else "retinanet_R_101_FPN_3x.yaml"
+    cfg.merge_from_file(os.path.join(ROOT, "configs", "COCO-Detection", name))
+    finalize(cfg, False, 1, CM)
+    return cfg
+
+
+def _model(depth=50):
+    from detectron2_tensorflow_amd.modeling import build_model
+    torch.manual_seed(0)
+    return build_model(_cfg(depth)).eval()
+
+
+def _check_layout(boxes, scores, classes, valid, num_classes=80):
+    """pad_or_clip_boxlist layout (retinanet.py:365-367): the kept detections
+    first, in NMS selection order (scores non-increasing), zeros after."""
+    for n in range(valid.shape[0]):
+        v = valid[n]
+        m = int(v.sum())
+        assert v[:m].all() and not v[m:].any()
+        assert (boxes[n][m:] == 0).all() and (scores[n][m:] == 0).all()
+        assert (np.diff(scores[n][:m]) <= 0).all()
+        assert ((classes[n][:m] >= 0) & (classes[n][:m] < num_classes)).all()
+        assert np.isfinite(boxes[n][:m]).all()
+
+
+def _same_class_overlap_ok(boxes, classes, valid, thr=0.5):
+    """No two kept detections of one class overlap by IoU > thr (the class-offset
+    NMS of retinanet.py:349-355)."""
+    import oracle
+    for n in range(valid.shape[0]):
+        m = int(valid[n].sum())
+        b, c = boxes[n][:m], classes[n][:m]
+        for k in np.unique(c):
+            bb = b[c == k]
+            if len(bb) < 2:
+                continue
+            keep = oracle.nms(bb, np.linspace(1, 0, len(bb), dtype=F32), len(bb), thr)
+            assert len(keep) == len(bb)
+
+
+# ---------------------------------------------------------------- C1 (CPU)
+def test_c1_retinanet_r50_640_cpu_plumbing():
+    """C1: one synthetic 640x640 image through the CPU restatement of the
+    RetinaNet R50-FPN forward: 76,725 anchors, a full
+    [1, 100] padded result with the reference layout."""
+    import cpu_pipeline as cp
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_retinanet_head
+    model = _model(50)
+    ref = cp.CPURetinaNet(model)
+    img = np.random.default_rng(0).uniform(0, 255, (1, 640, 640, 3)).astype(F32)
+    with torch.no_grad():
+        cls, box = ref.head(ref.features(img))
+        calibrate_retinanet_head(ref.m.detector.head, cls, box)
+        cls, box = ref.head(ref.features(img))
+    A, K = 9, 80
+    assert sum(c.shape[1] * c.shape[2] * A for c in cls) == 76725
+    assert [c.shape[-1] for c in cls] == [A * K] * 5 and [b.shape[-1] for b in box] == [A * 4] * 5
+    allc = torch.cat([c.reshape(-1) for c in cls])
+    assert abs(float(allc.mean()) + 3.0) < 0.1 and abs(float(allc.std()) - 1.0) < 0.1
+    out = ref.postprocess([c.numpy() for c in cls], [b.numpy() for b in box])
+    assert out["boxes"].shape == (1, 100, 4) and out["classes"].dtype == np.int32
+    assert int(out["is_valid"].sum()) == 100  # 5 x 1000 candidates above 0.05 -> 100 kept
+    _check_layout(out["boxes"], out["scores"], out["classes"], out["is_valid"])
+    _same_class_overlap_ok(out["boxes"], out["classes"], out["is_valid"])
+
+
+# ------------------------------------------------------------- C4 (GPU)
+def _gpu_head(model, batch):
+    det = model.detector
+    images = model.preprocess_image(batch)
+    feats = model.neck(model.backbone(images.tensor))
+    return det.head([feats[f] for f in det.in_features])
+
+
+def _calibrated_gpu_model(dev, depth, batch):
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_retinanet_head
+    model = _model(depth).to(dev)
+    with torch.no_grad():
+        cls, box = _gpu_head(model, batch)
+        calibrate_retinanet_head(model.detector.head, cls, box)
+    return model
+
+
+def _assert_post_matches_oracle(ref, cls, box, got):
+    """Post-processing parity on identical head outputs: valid flags and class
+    ids bit-exact, scores to 2e-7 relative (the sigmoid's expf), boxes within
+    max(1e-4, 2 ulp)."""
+    from test_gpu_ops import assert_boxes_close
+    want = ref.postprocess([c.cpu().numpy() for c in cls], [b.cpu().numpy() for b in box])
+    g = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(g["is_valid"], want["is_valid"])
+    np.testing.assert_array_equal(g["classes"], want["classes"])
+    np.testing.assert_allclose(g["scores"], want["scores"], rtol=2e-7, atol=0)
+    for n in range(g["boxes"].shape[0]):
+        assert_boxes_close(g["boxes"][n], want["boxes"][n])
+    return want
+
+
+@pytest.mark.gpu
+def test_c4_retinanet_r50_640_vs_cpu_restatement(dev):
+    import cpu_pipeline as cp
+    rng = np.random.default_rng(5)
+    img = rng.uniform(0, 255, (2, 640, 640, 3)).astype(F32)
+    shapes = np.array([[640, 640], [600, 620]], np.int32)
+    batch = {"image": torch.from_numpy(img).to(dev), "image_shape": torch.from_numpy(shapes).to(dev)}
+    model = _calibrated_gpu_model(dev, 50, batch)
+    with torch.no_grad():
+        cls, box = _gpu_head(model, batch)
+        out = model(batch)["instances"]
+        post = model.detector.inference(cls, box)
+    ref = cp.CPURetinaNet(model)
+    # 1. the model's own forward == its head + post-processing
+    for k, f in (("boxes", post.boxes), ("scores", post.get_field("scores")),
+                 ("classes", post.get_field("pred_classes")), ("is_valid", post.get_field("is_valid"))):
+        assert torch.equal(out[k], f), k
+    # 2. post-processing on identical head outputs: bit-exact vs the oracle
+    got = {"boxes": out["boxes"], "scores": out["scores"], "classes": out["classes"],
+           "is_valid": out["is_valid"]}
+    _assert_post_matches_oracle(ref, cls, box, got)
+    # 3. head outputs vs the CPU restatement of backbone + FPN(P6P7) + tower
+    with torch.no_grad():
+        wcls, wbox = ref.head(ref.features(img))
+    for g_, w_ in zip(list(cls) + list(box), list(wcls) + list(wbox)):
+        err = (g_.cpu() - w_).abs().max().item()
+        assert err <= 1e-3 * max(w_.abs().max().item(), 1.0), err
+    # 4. end to end: detections of the whole GPU model vs the whole CPU restatement
+    want = ref.postprocess([c.numpy() for c in wcls], [b.numpy() for b in wbox])
+    g = {k: v.cpu().numpy() for k, v in got.items()}
+    for n in range(2):
+        wv, gv = want["is_valid"][n], g["is_valid"][n]
+        hits = 0
+        for b, c in zip(want["boxes"][n][wv], want["classes"][n][wv]):
+            d = np.abs(g["boxes"][n][gv] - b).max(axis=1)
+            hits += bool(((d < 1e-2) & (g["classes"][n][gv] == c)).any())
+        assert hits >= 0.95 * wv.sum(), (n, hits, int(wv.sum()))
+    _check_layout(g["boxes"], g["scores"], g["classes"], g["is_valid"])
+
+
+@pytest.mark.gpu
+def test_c4_retinanet_r101_1333x800_dense_anchors(dev):
+    """C4 geometry: 800x1333 padded to 800x1344, p3..p7 = 100x168 ... 7x11,
+    201,600 anchors/img x 80 classes (p3 alone 12.1 M scores).  Post-processing
+    bit-exact vs the oracle on the GPU's own head outputs at full size;
+    two runs identical; reference output layout."""
+    import cpu_pipeline as cp
+    g = torch.Generator(device="cpu").manual_seed(9)
+    img = torch.rand(2, 800, 1333, 3, generator=g) * 255
+    batch = {"image": img.to(dev), "image_shape": torch.tensor([[800, 1333], [800, 1333]], device=dev)}
+    model = _calibrated_gpu_model(dev, 101, batch)
+    old = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # the MIOpen stem: no atomic split-K
+    try:
+        with torch.no_grad():
+            cls, box = _gpu_head(model, batch)
+            a = model(batch)["instances"]
+            b = model(batch)["instances"]
+    finally:
+        torch.backends.cudnn.deterministic = old
+    assert [tuple(c.shape[1:3]) for c in cls] == [(100, 168), (50, 84), (25, 42), (13, 21), (7, 11)]
+    assert sum(c.shape[1] * c.shape[2] * 9 for c in cls) == 201600
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    ref = cp.CPURetinaNet(model)
+    _assert_post_matches_oracle(ref, cls, box, a)
+    h = {k: v.cpu().numpy() for k, v in a.items()}
+    _check_layout(h["boxes"], h["scores"], h["classes"], h["is_valid"])
+    _same_class_overlap_ok(h["boxes"], h["classes"], h["is_valid"])
+    assert int(h["is_valid"].sum()) == 200

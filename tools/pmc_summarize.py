@@ -19,9 +19,12 @@ import sys
 
 # (kernels of the group, the group's one-per-op kernel).  The split-K /
 # partial reductions are counted with their group; per-launch figures divide
-# by the op's main kernel count.  ROIAlign backward: its own kernels (the
-# memsets and the rocPRIM radix sort it also launches are not attributable by
-# name and are left out).
+# by the op's main kernel count.  ROIAlign backward: its own roi_bwd_* kernels,
+# including roi_bwd_clear_kernel (the grad-map / run-start / counter clear,
+# 183 MB of writes at 1333x800).  The rocPRIM onesweep sort it launches (about
+# 40 us of the ~170 us per backward) is not attributable by name and is left
+# out, so `traffic` covers fewer kernels than the HIP-event time does
+# (DESIGN.md section 5 says so).
 GROUPS = {
     "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce4?_kernel"),
                      re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel")),
