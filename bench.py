@@ -43,12 +43,14 @@ CONFIGS = {
     "faster_rcnn_R_50_FPN": "configs/COCO-Detection/faster_rcnn_R_50_FPN_1x.yaml",
     "retinanet_R_50_FPN": "configs/COCO-Detection/retinanet_R_50_FPN_1x.yaml",
     "retinanet_R_101_FPN": "configs/COCO-Detection/retinanet_R_101_FPN_3x.yaml",
+    "solo_v2_R_50_FPN": "configs/COCO-InstanceSegmentation/solo_v2_R_50_FPN_1x.yaml",
 }
 METRICS = {
     "mask_rcnn_R_50_FPN": "img/sec whole-node Mask R-CNN R50-FPN @1333x800",
     "faster_rcnn_R_50_FPN": "img/sec Faster R-CNN R50-FPN @1333x800",
     "retinanet_R_50_FPN": "img/sec RetinaNet R50-FPN",
     "retinanet_R_101_FPN": "img/sec RetinaNet R101-FPN dense anchors",
+    "solo_v2_R_50_FPN": "img/sec SOLOv2 R50-FPN (dynamic-conv masks + Matrix NMS)",
 }
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32)
 # split products: every f32 multiply-add costs six v_mfma_f32_32x32x16_bf16
@@ -114,12 +116,30 @@ def calibrate_retinanet(model, batch):
 
 
 @torch.no_grad()
+def calibrate_solo(model, batch):
+    """Score injection for SOLOv2: category logits ~ N(-4.5, 1) (a few hundred
+    to a few thousand candidates above 0.1 after point NMS), dynamic kernels
+    of std 0.1 (utils/synthetic.py)."""
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_solo_head
+    b = model.detector.mask_kernel_branch
+    feats = model.neck(model.backbone(model.preprocess_image(batch).tensor))
+    cls, ker = b(feats)
+    calibrate_solo_head(b, cls, ker)
+
+
+def is_solo(model):
+    return hasattr(getattr(model, "detector", None), "mask_kernel_branch")
+
+
+@torch.no_grad()
 def calibrate_scores(model, batch):
     """Rescale the class / objectness logit weights so the random-init model
     emits BASELINE.md's synthetic score distributions, and the RPN anchor
     deltas to N(0, 0.1^2): the unnormalised features of a random-init ResNet
     otherwise give deltas of O(10), which collapse most proposals onto the
     image border (a random-init artefact, not a training distribution)."""
+    if is_solo(model):
+        return calibrate_solo(model, batch)
     if is_single_stage(model):
         return calibrate_retinanet(model, batch)
     stats = {}
@@ -191,7 +211,8 @@ def kernel_report(summary, mode="infer"):
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                      "traffic": pmc_traffic(pmc_group, mode), "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
-    for name in ("roi_align_fwd", "roi_align_bwd", "retinanet_topk"):
+    for name in ("roi_align_fwd", "roi_align_bwd", "retinanet_topk", "solo_mask_stats",
+                 "solo_matrix_nms", "solo_paste"):
         if name not in summary:
             continue
         n, ms, byts = summary[name]
@@ -226,6 +247,16 @@ def cpu_baseline(args, model, batch, cfg=None):
             step.step(imgs, shapes, inst, threads=cores)
         dt = time.perf_counter() - t0
         what = "training iteration(s) (forward + losses + backward + Momentum-SGD update)"
+    elif is_solo(model):
+        from cpu_pipeline import CPUSOLOv2
+        ref = CPUSOLOv2(model.eval())
+        ref(imgs[:1, :256, :320], threads=cores)  # warm the libraries
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            ref(imgs, threads=cores)
+        dt = time.perf_counter() - t0
+        what = ("inference forward(s) (backbone + FPN + SOLOv2 kernel / feature branches + "
+                "dynamic conv, Matrix NMS, masks to the image)")
     elif is_single_stage(model):
         from cpu_pipeline import CPURetinaNet
         ref = CPURetinaNet(model.eval())
@@ -259,6 +290,8 @@ def main():
     args = parse()
     if args.model.startswith("retinanet") and args.mode == "train":
         raise SystemExit("RetinaNet is benchmarked in --mode infer (config C4)")
+    if args.model.startswith("solo") and args.mode == "train":
+        raise SystemExit("SOLOv2 is benchmarked in --mode infer (config C5: the inference tail)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

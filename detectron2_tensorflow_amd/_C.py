@@ -51,6 +51,19 @@ _SIGS = {
                                          c_float, c_int, P, c_float, P, P, P, P, P, c_size_t, P]),
     "d2mi_matrix_nms_workspace_size": (c_size_t, [c_int]),
     "d2mi_matrix_nms": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, P, P, c_size_t, P]),
+    "d2mi_resize_bilinear": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                                     P]),
+    "d2mi_solo_cells": (c_int, [P, P, c_int, c_int, c_int, c_float, P, P, P, P, P]),
+    "d2mi_solo_mask_stats": (c_int, [P, c_int, c_int, c_float, P, P, P]),
+    "d2mi_solo_select_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "d2mi_solo_select": (c_int, [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float,
+                                 c_float, c_int, P, P, P, P, P, P, c_size_t, P]),
+    "d2mi_solo_matrix_nms_workspace_size": (c_size_t, [c_int, c_int]),
+    "d2mi_solo_matrix_nms": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, P, P,
+                                     c_size_t, P]),
+    "d2mi_solo_finalize_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "d2mi_solo_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int,
+                                   c_float, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),
     "d2mi_conv_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_int, P]),

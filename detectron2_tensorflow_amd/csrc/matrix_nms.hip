@@ -41,24 +41,33 @@ __device__ __forceinline__ float iou_at(const float* inter, const float* s, cons
   return it / uni;
 }
 
-// comp[j] = max over i of iou[i][j]   (one thread per column)
-__global__ void comp_kernel(const float* inter, const float* s, const int64_t* cls, int M,
-                            float* comp) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= M) return;
+// comp[j] = max over i of iou[i][j]: one 256-thread workgroup per column,
+// threads over the rows, tree max (exact in any order).
+__global__ __launch_bounds__(256) void comp_kernel(const float* inter, const float* s,
+                                                   const int64_t* cls, int M, float* comp) {
+  __shared__ float red[256];
+  const int j = blockIdx.x;
   float mx = 0.f;  // every column has the zero entries of the lower triangle
-  for (int i = 0; i < M; ++i) mx = fmaxf(mx, iou_at(inter, s, cls, M, i, j));
-  comp[j] = mx;
+  for (int i = threadIdx.x; i < j; i += blockDim.x) mx = fmaxf(mx, iou_at(inter, s, cls, M, i, j));
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) comp[j] = red[0];
 }
 
-__global__ void decay_kernel(const float* inter, const float* s, const int64_t* cls,
-                             const float* comp, const float* scores, int M, int kernel,
-                             float sigma, float* out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= M) return;
+// one workgroup per column: min over the rows of the decay, tree min
+__global__ __launch_bounds__(256) void decay_kernel(const float* inter, const float* s,
+                                                    const int64_t* cls, const float* comp,
+                                                    const float* scores, int M, int kernel,
+                                                    float sigma, float* out) {
+  __shared__ float red[256];
+  const int j = blockIdx.x;
   float mn = INFINITY;
   const float ns = -1.f * sigma;
-  for (int i = 0; i < M; ++i) {
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
     const float v = iou_at(inter, s, cls, M, i, j);
     const float c = comp[i];
     float d;
@@ -66,7 +75,13 @@ __global__ void decay_kernel(const float* inter, const float* s, const int64_t* 
     else d = (1.f - v) / (1.f - c);
     mn = fminf(mn, d);
   }
-  out[j] = scores[j] * mn;
+  red[threadIdx.x] = mn;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] = fminf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = scores[j] * red[0];
 }
 
 }  // namespace
@@ -107,10 +122,10 @@ extern "C" int d2mi_matrix_nms(const float* masks, const int64_t* classes, const
     D2MI_LAUNCH_CHECK();
     s = sums;
   }
-  hipLaunchKernelGGL(comp_kernel, dim3((M + 63) / 64), dim3(64), 0, st, inter, s, classes, M, comp);
+  hipLaunchKernelGGL(comp_kernel, dim3(M), dim3(256), 0, st, inter, s, classes, M, comp);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(decay_kernel, dim3((M + 63) / 64), dim3(64), 0, st, inter, s, classes, comp,
-                     scores, M, kernel, sigma, out_scores);
+  hipLaunchKernelGGL(decay_kernel, dim3(M), dim3(256), 0, st, inter, s, classes, comp, scores, M,
+                     kernel, sigma, out_scores);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

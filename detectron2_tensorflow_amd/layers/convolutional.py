@@ -8,8 +8,8 @@ implicit-GEMM kernel (d2mi_conv2d_nhwc) — the FPN lateral/output convs, the
 RPN head and the mask head use it — and raises if the tensor is not on the GPU.
 ``impl="torch"`` is stock PyTorch-ROCm conv2d in channels_last, used for the
 backbone (a caller of the hot path, outside its scope).
-``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation,
-Cin % 4 == 0) and the input is on the GPU.
+``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation)
+and the input is on the GPU; Cin % 4 != 0 runs with zero channels appended.
 Backward of the mfma path: dgrad on the same MFMA kernel (flipped kernel);
 wgrad on the MFMA wgrad kernel or hipBLASLt / MIOpen, whichever measured
 faster for the shape (see _wgrad); stride-2 KxK dgrad and Cout % 4 != 0 use
@@ -298,8 +298,10 @@ class Conv2D(Layer):
         self._packed_key = None
 
     def _mfma_eligible(self, x):
-        return (x.is_cuda and self.num_groups == 1 and self.rate == 1
-                and self.in_channels % 4 == 0)
+        # Cin % 4 != 0 (e.g. SOLOv2's 256 + 2 coordinate channels) runs with
+        # zero channels appended to the input and the weights (exact: the
+        # extra products are 0)
+        return x.is_cuda and self.num_groups == 1 and self.rate == 1
 
     def _param_key(self):
         key = [self.weights.data_ptr(), self.weights._version]
@@ -382,6 +384,11 @@ class Conv2D(Layer):
             relu_after_add = relu_after_add or final_relu
             if (topdown is not None or residual is not None) and fuse_relu and not relu_after_add:
                 raise ValueError("relu(conv) + add cannot be fused; use relu_after_add")
+            padc = (-self.in_channels) % 4
+            if padc:
+                inputs = F.pad(inputs, (0, padc))
+                w = F.pad(w, (0, 0, 0, padc))
+                packed = None
             if packed is None:
                 packed = self.packed_weights(w)
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,

@@ -11,12 +11,20 @@ from . import ops
 
 
 def resize_images(images, size, method="bilinear", **kwargs):
-    """tf.compat.v2.image.resize (half-pixel centres, no antialias) on NHWC."""
+    """resize_images (:9-36) on NHWC.  With TF >= 1.14 the reference takes the
+    tf.compat.v2.image.resize branch, whose kwargs filter drops align_corners:
+    bilinear is ResizeBilinear with half-pixel centres and no antialias, run
+    here by the HIP kernel (d2mi_resize_bilinear, TF 1.15 arithmetic; GPU
+    tensors only).  Other methods are not on the hot path: PyTorch's
+    interpolate (half-pixel for bicubic / area; nearest is floor-indexed)."""
     x = images if images.dim() == 4 else images[None]
-    mode = {"bilinear": "bilinear", "nearest": "nearest", "bicubic": "bicubic", "area": "area"}[method]
-    kw = {"align_corners": False} if mode in ("bilinear", "bicubic") else {}
-    y = F.interpolate(x.permute(0, 3, 1, 2), size=tuple(int(s) for s in size), mode=mode, **kw)
-    y = y.permute(0, 2, 3, 1)
+    if method == "bilinear":
+        y = ops.resize_bilinear(x, size)
+    else:
+        mode = {"nearest": "nearest", "bicubic": "bicubic", "area": "area"}[method]
+        kw = {"align_corners": False} if mode == "bicubic" else {}
+        y = F.interpolate(x.permute(0, 3, 1, 2), size=tuple(int(s) for s in size), mode=mode,
+                          **kw).permute(0, 2, 3, 1)
     return y if images.dim() == 4 else y[0]
 
 

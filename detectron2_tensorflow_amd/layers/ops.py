@@ -294,7 +294,7 @@ def _presplit_ok(x, Cin):
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
                 residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None,
-                flip_taps=False, relu_gate=None):
+                flip_taps=False, relu_gate=None, out=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
@@ -315,7 +315,13 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     pb, pe = pad
     OH = (H + pb + pe - KH) // stride + 1
     OW = (W + pb + pe - KW) // stride + 1
-    y = torch.empty((N, OH, OW, Cout), dtype=torch.float32, device=x.device)
+    if out is not None:
+        if (tuple(out.shape) != (N, OH, OW, Cout) or out.dtype != torch.float32
+                or not out.is_contiguous() or out.device != x.device):
+            raise ValueError(f"out must be a contiguous f32 {(N, OH, OW, Cout)} tensor on {x.device}")
+        y = out
+    else:
+        y = torch.empty((N, OH, OW, Cout), dtype=torch.float32, device=x.device)
     if topdown is not None:
         topdown = _f32c(topdown)
         if topdown.shape != (N, (OH + 1) // 2, (OW + 1) // 2, Cout):
@@ -757,6 +763,136 @@ def matrix_nms_scores(masks, classes, scores, sum_masks=None, kernel="gaussian",
                                   _C.ptr(out), _C.ptr(ws), wsb, _C.stream_of(masks.device))
     _C.check(rc, "d2mi_matrix_nms")
     return out
+
+
+# ------------------------------------------------------------ resize / SOLOv2
+def resize_bilinear(x, size, align_corners=False, half_pixel_centers=True):
+    """TF ResizeBilinear on NHWC f32 (d2mi_resize_bilinear): x [N,H,W,C] ->
+    [N, size[0], size[1], C]."""
+    x = _f32c(x)
+    _C.require_device(x)
+    N, H, W, C = x.shape
+    OH, OW = int(size[0]), int(size[1])
+    y = torch.empty((N, OH, OW, C), dtype=torch.float32, device=x.device)
+    rc = _C.lib().d2mi_resize_bilinear(_C.ptr(x), N, H, W, C, OH, OW, int(bool(align_corners)),
+                                       int(bool(half_pixel_centers)), _C.ptr(y),
+                                       _C.stream_of(x.device))
+    _C.check(rc, "d2mi_resize_bilinear")
+    return y
+
+
+def solo_inference(cate_logits, kernels, mask_features, strides, out_hw, score_thresh=0.1,
+                   mask_thresh=0.5, update_thresh=0.05, pre_nms_topk=500, max_detections=100,
+                   nms_kernel="gaussian", nms_sigma=2.0, debug=None):
+    """MaskKernelBranch.inference (solo_v2.py:476-627) on the HIP stages of
+    csrc/solo.hip.  cate_logits[l] [N,S_l,S_l,K] (pre-sigmoid), kernels[l]
+    [N,S_l,S_l,D], mask_features [N,Hm,Wm,D], strides[l] (the per-level
+    sum_masks floor), out_hw the padded image size.  Returns masks uint8
+    [N,max_det,OH,OW], boxes [N,max_det,4], scores, classes int64, is_valid.
+    One host read (the live-cell counts that size the dynamic-conv GEMMs).
+    debug: a dict to receive the intermediates (tests)."""
+    if nms_kernel not in ("gaussian", "linear"):
+        raise NotImplementedError(f"NMS kernel {nms_kernel} not implemented yet.")
+    cate = [_f32c(t) for t in cate_logits]
+    kern = [_f32c(t) for t in kernels]
+    feats = _f32c(mask_features)
+    _C.require_device(feats, *cate, *kern)
+    N, K = cate[0].shape[0], cate[0].shape[-1]
+    D = kern[0].shape[-1]
+    _, Hm, Wm, D2 = feats.shape
+    if D != D2:
+        raise ValueError(f"kernel dims {D} != mask feature dims {D2}")
+    P = Hm * Wm
+    L = len(cate)
+    grids = [int(t.shape[1]) for t in cate]
+    T = sum(g * g for g in grids)
+    dev = feats.device
+    st = _C.stream_of(dev)
+    lib = _C.lib()
+    g_arr = _C.host_array(_C.ctypes.c_int32, grids)
+    s_arr = _C.host_array(_C.c_float, [float(s) for s in strides])
+    probs = torch.empty((N, T, K), dtype=torch.float32, device=dev)
+    live_cells = torch.empty((N, T), dtype=torch.int32, device=dev)
+    live_row = torch.empty((N, T), dtype=torch.int32, device=dev)
+    live_count = torch.empty((N,), dtype=torch.int32, device=dev)
+    rc = lib.d2mi_solo_cells(_C.host_array(_C.c_void_p, [t.data_ptr() for t in cate]), g_arr, L,
+                             N, K, float(score_thresh), _C.ptr(probs), _C.ptr(live_cells),
+                             _C.ptr(live_row), _C.ptr(live_count), st)
+    _C.check(rc, "d2mi_solo_cells")
+    counts = [int(c) for c in live_count.cpu()]  # the one host synchronisation
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    R = offs[-1]
+    row_off = torch.tensor(offs[:-1], dtype=torch.int32, device=dev)
+    kern_all = torch.cat([k.reshape(N, -1, D) for k in kern], 1)  # [N, T, D]
+    logits = torch.empty((max(R, 1), P), dtype=torch.float32, device=dev)
+    for n in range(N):
+        c = counts[n]
+        if c == 0:
+            continue
+        rows = kern_all[n].index_select(0, live_cells[n, :c].long()).reshape(1, 1, c, D)
+        # dynamic 1x1 conv (solo_v2.py:509-511): one MFMA GEMM per image,
+        # [c, D] x [P, D]^T -> [c, P] written straight into the shared buffer
+        conv2d_nhwc(rows, feats[n].reshape(1, 1, P, D), out=logits[offs[n]:offs[n + 1]].view(
+            1, 1, c, P))
+    sum_masks = torch.empty((max(R, 1),), dtype=torch.float32, device=dev)
+    sum_scores = torch.empty_like(sum_masks)
+    ev = KernelTimer.start()
+    rc = lib.d2mi_solo_mask_stats(_C.ptr(logits), R, P, float(mask_thresh), _C.ptr(sum_masks),
+                                  _C.ptr(sum_scores), st)
+    KernelTimer.stop(ev, "solo_mask_stats", 4 * R * P)  # the dynamic-conv logits read once
+    _C.check(rc, "d2mi_solo_mask_stats")
+    k = int(min(pre_nms_topk, T * K))
+    top_scores = torch.empty((N, k), dtype=torch.float32, device=dev)
+    top_classes = torch.empty((N, k), dtype=torch.int64, device=dev)
+    top_sum = torch.empty((N, k), dtype=torch.float32, device=dev)
+    top_count = torch.empty((N,), dtype=torch.int32, device=dev)
+    W64 = (P + 63) // 64
+    bits = torch.empty((N, k, W64), dtype=torch.int64, device=dev)
+    wsb = lib.d2mi_solo_select_workspace_size(N, T, K, k)
+    ws = _C.workspace(wsb, dev)
+    rc = lib.d2mi_solo_select(_C.ptr(probs), _C.ptr(live_row), _C.ptr(row_off), _C.ptr(logits),
+                              _C.ptr(sum_masks), _C.ptr(sum_scores), g_arr, s_arr, L, N, K, P,
+                              float(score_thresh), float(mask_thresh), k, _C.ptr(top_scores),
+                              _C.ptr(top_classes), _C.ptr(top_sum), _C.ptr(top_count),
+                              _C.ptr(bits), _C.ptr(ws), wsb, st)
+    _C.check(rc, "d2mi_solo_select")
+    # Matrix NMS (solo_v2.py:541-545) over the padded top-k rows, all images
+    decayed = torch.empty((N, k), dtype=torch.float32, device=dev)
+    mwsb = lib.d2mi_solo_matrix_nms_workspace_size(N, k)
+    mws = _C.workspace(mwsb, dev)
+    ev = KernelTimer.start()
+    rc = lib.d2mi_solo_matrix_nms(_C.ptr(bits), _C.ptr(top_classes), _C.ptr(top_scores),
+                                  _C.ptr(top_sum), N, k, P, 0 if nms_kernel == "gaussian" else 1,
+                                  float(nms_sigma), _C.ptr(decayed), _C.ptr(mws), mwsb, st)
+    # algorithmic bytes: the bit-packed masks read once (SURVEY D4 prices the
+    # f32 GEMM at 2 N^2 HW flop; the AND + popcount form is bound by bytes)
+    KernelTimer.stop(ev, "solo_matrix_nms", N * k * W64 * 8)
+    _C.check(rc, "d2mi_solo_matrix_nms")
+    OH, OW = int(out_hw[0]), int(out_hw[1])
+    out_masks = torch.empty((N, max_detections, OH, OW), dtype=torch.uint8, device=dev)
+    out_boxes = torch.empty((N, max_detections, 4), dtype=torch.float32, device=dev)
+    out_scores = torch.empty((N, max_detections), dtype=torch.float32, device=dev)
+    out_classes = torch.empty((N, max_detections), dtype=torch.int64, device=dev)
+    out_valid = torch.empty((N, max_detections), dtype=torch.uint8, device=dev)
+    fwsb = lib.d2mi_solo_finalize_workspace_size(N, max_detections, OH)
+    fws = _C.workspace(fwsb, dev)
+    ev = KernelTimer.start()
+    rc = lib.d2mi_solo_finalize(_C.ptr(decayed), _C.ptr(top_classes), _C.ptr(top_count),
+                                _C.ptr(bits), N, k, Hm, Wm, float(update_thresh),
+                                int(max_detections), float(mask_thresh), OH, OW,
+                                _C.ptr(out_masks), _C.ptr(out_boxes), _C.ptr(out_scores),
+                                _C.ptr(out_classes), _C.ptr(out_valid), _C.ptr(fws), fwsb, st)
+    # algorithmic bytes: the uint8 canvas written once (the bit masks are L2-resident)
+    KernelTimer.stop(ev, "solo_paste", N * max_detections * OH * OW)
+    _C.check(rc, "d2mi_solo_finalize")
+    if debug is not None:
+        debug.update(probs=probs, live_cells=live_cells, live_row=live_row, counts=counts,
+                     row_off=offs, logits=logits[:R], sum_masks=sum_masks[:R],
+                     sum_scores=sum_scores[:R], top_scores=top_scores, top_classes=top_classes,
+                     top_sum=top_sum, top_count=top_count, mask_bits=bits, decayed=decayed)
+    return out_masks, out_boxes, out_scores, out_classes, out_valid.bool()
 
 
 # ------------------------------------------------------- fused post-processing

@@ -23,6 +23,8 @@ class SingleStageDetector(_Preprocess, Layer):
         results, losses = self.detector(images, features, gt)
         if self.training:
             return losses
-        return {"instances": {"boxes": results.boxes, "classes": results.get_field("pred_classes"),
-                              "scores": results.get_field("scores"),
-                              "is_valid": results.get_field("is_valid")}}
+        out = {"boxes": results.boxes, "classes": results.get_field("pred_classes"),
+               "scores": results.get_field("scores"), "is_valid": results.get_field("is_valid")}
+        if results.has_field("pred_masks"):  # single_stage_detector.py:75-76 (SOLOv2)
+            out["masks"] = results.get_field("pred_masks")
+        return {"instances": out}

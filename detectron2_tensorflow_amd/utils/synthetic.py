@@ -49,6 +49,26 @@ def synthetic_train_batch(batch, height, width, seed, device, **kw):
 
 
 @torch.no_grad()
+def calibrate_solo_head(branch, pred_cls, pred_kernels, cls_mean=-4.5, cls_std=1.0,
+                        kernel_std=0.1):
+    """Score injection for a random-init SOLOv2 MaskKernelBranch: rescale
+    solo_cate so the category logits are ~ N(cls_mean, cls_std^2) (a few
+    hundred to a few thousand (cell, class) candidates above
+    SCORE_THRESH_TEST = 0.1 after point NMS) and solo_kernel so the dynamic
+    kernels have std kernel_std (mask logits of O(1): masks neither empty nor
+    full).  pred_cls / pred_kernels: the branch's outputs on the features the
+    calibration is for."""
+    def std_wo_bias(outs, bias):
+        return float(torch.cat([(o - bias.to(o.device)).reshape(-1) for o in outs]).double().std())
+
+    s = std_wo_bias(pred_cls, branch.solo_cate.bias)
+    branch.solo_cate.weights.mul_(cls_std / max(s, 1e-12))
+    branch.solo_cate.bias.fill_(cls_mean)
+    s = std_wo_bias(pred_kernels, branch.solo_kernel.bias)
+    branch.solo_kernel.weights.mul_(kernel_std / max(s, 1e-12))
+    branch.solo_kernel.bias.zero_()
+
+
 def calibrate_retinanet_head(tower, box_cls, box_delta, cls_mean=-3.0, cls_std=1.0,
                              delta_std=0.1):
     """BASELINE.md score injection for a random-init RetinaNet: rescale the

@@ -200,6 +200,77 @@ int d2mi_matrix_nms(const float* masks, const int64_t* classes, const float* sco
                     const float* sum_masks, int M, int HW, int kernel, float sigma,
                     float* out_scores, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------- ResizeBilinear
+ * tf.compat.v2.image.resize(method="bilinear") as the reference's
+ * resize_images calls it (lib/layers/functional.py:9-36; TF >= 1.14 takes the
+ * v2 branch, which drops align_corners: half-pixel centres, no antialias),
+ * TF 1.15 resize_bilinear_op.cc arithmetic.  x [N,H,W,C] -> y [N,OH,OW,C]. */
+int d2mi_resize_bilinear(const float* x, int N, int H, int W, int C, int OH, int OW,
+                         int align_corners, int half_pixel_centers, float* y, void* stream);
+
+/* ------------------------------------------------- SOLOv2 inference tail
+ * MaskKernelBranch.inference (lib/modeling/single_stage_heads/solo_v2.py:476-627)
+ * in four stages around the caller's dynamic-conv GEMM and d2mi_matrix_nms.
+ *
+ * d2mi_solo_cells: cate[l] device float [N, S_l, S_l, K] category logits
+ * (grids host int32 [L] = S_l, T = sum S_l^2 cells) -> probs [N, T, K] =
+ * point_nms(sigmoid(cate)) (solo_v2.py:29-40, :267-269) in the reference's
+ * flattened order (:567-586); live_cells [N, T]: the cells with any prob >
+ * score_thr in cell order, first live_count[n] valid; live_row [N, T]: a live
+ * cell's position in live_cells, -1 otherwise.  cate is a host array of L
+ * device pointers. */
+int d2mi_solo_cells(const float* const* cate, const int32_t* grids, int L, int N, int K,
+                    float score_thr, float* probs, int32_t* live_cells, int32_t* live_row,
+                    int32_t* live_count, void* stream);
+
+/* d2mi_solo_mask_stats: logits [R, P] (one dynamic-conv row per live cell,
+ * :509-511) -> sum_masks[r] = #(sigmoid > mask_thr) (:513-517) and
+ * sum_scores[r] = sum of those sigmoids (:529-531).  16-B aligned. */
+int d2mi_solo_mask_stats(const float* logits, int R, int P, float mask_thr, float* sum_masks,
+                         float* sum_scores, void* stream);
+
+/* d2mi_solo_select: candidates (cell, class) with prob > score_thr and
+ * sum_masks > stride of the cell's level (:482-526), scored prob *
+ * sum_scores / sum_masks (:528-532); exact top-k (k = TOPK_CANDIDATES_TEST,
+ * tf.nn.top_k sorted, ties by candidate order, :535-539); the top-k's binary
+ * masks bit-packed, mask_bits [N, k, ceil(P/64)] uint64 (bit p % 64 of word
+ * p / 64), classes [N, k] int64 (rows past top_count: zero masks, classes
+ * -1 - t), sum_masks [N, k], scores [N, k] (:537-539).  row_off [N] device:
+ * first logits row of each image; grids / strides host [L]. */
+size_t d2mi_solo_select_workspace_size(int N, int T, int K, int k);
+int d2mi_solo_select(const float* probs, const int32_t* live_row, const int32_t* row_off,
+                     const float* logits, const float* sum_masks, const float* sum_scores,
+                     const int32_t* grids, const float* strides, int L, int N, int K, int P,
+                     float score_thr, float mask_thr, int k, float* top_scores,
+                     int64_t* top_classes, float* top_sum_masks, int32_t* top_count,
+                     uint64_t* mask_bits, void* workspace, size_t workspace_bytes, void* stream);
+
+/* d2mi_solo_matrix_nms: matrix_nms (lib/layers/nms.py:29-83, called at
+ * solo_v2.py:541-545) for N images of k binary masks at once: the
+ * intersection matrix M M^T as popcounts of AND-ed mask words (exact), then
+ * the IoU / class / compensation / decay arithmetic of d2mi_matrix_nms.
+ * kernel 0 = gaussian, 1 = linear.  out_scores [N, k]. */
+size_t d2mi_solo_matrix_nms_workspace_size(int N, int k);
+int d2mi_solo_matrix_nms(const uint64_t* mask_bits, const int64_t* classes, const float* scores,
+                         const float* sum_masks, int N, int k, int P, int kernel, float sigma,
+                         float* out_scores, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* d2mi_solo_finalize: decayed Matrix-NMS scores [N, k] > update_thr in
+ * candidate order, pad / clip to max_det (:547-557); the bit-packed masks
+ * resized from [Hm, Wm] to the padded image [OH, OW] with TF bilinear
+ * (half-pixel) and > mask_thr (:598-602) -> out_masks uint8
+ * [N, max_det, OH, OW] (the reference's float 0/1 values); out_boxes
+ * [N, max_det, 4] from the masks (:604-623); out_scores, out_classes int64,
+ * out_valid uint8 [N, max_det]. */
+size_t d2mi_solo_finalize_workspace_size(int N, int max_det, int OH);
+int d2mi_solo_finalize(const float* nms_scores, const int64_t* top_classes,
+                       const int32_t* top_count, const uint64_t* mask_bits, int N, int k, int Hm,
+                       int Wm, float update_thr, int max_det, float mask_thr, int OH, int OW,
+                       uint8_t* out_masks, float* out_boxes, float* out_scores,
+                       int64_t* out_classes, uint8_t* out_valid, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* --------------------------------------------------------------- conv2d
  * NHWC implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32),
  * lib/layers/convolutional.py:12-23 (fix_padding: symmetric pad) and
