@@ -142,30 +142,8 @@ def calibrate_scores(model, batch):
         return calibrate_solo(model, batch)
     if is_single_stage(model):
         return calibrate_retinanet(model, batch)
-    stats = {}
-
-    def grab(name):
-        def hook(mod, inp, out):
-            x = inp[0]
-            stats[name] = float((x.reshape(-1, x.shape[-1]) ** 2).sum(-1).mean())
-        return hook
-
-    rh = model.roi_heads
-    h1 = rh.box_predictor.register_forward_hook(grab("box"))
-    rpn_head = model.proposal_generator.rpn_head
-    h2 = rpn_head.conv.register_forward_hook(lambda m, i, o: stats.__setitem__(
-        "rpn", float((o.reshape(-1, o.shape[-1]) ** 2).sum(-1).mean())))
-    was = model.training
-    model.eval()
-    model.inference(batch)
-    model.train(was)
-    h1.remove()
-    h2.remove()
-    cls = rh.box_predictor.cls_score
-    cls.weights.normal_(0.0, 3.0 / math.sqrt(max(stats["box"], 1e-12)))
-    obj = rpn_head.objectness_logits
-    obj.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["rpn"], 1e-12)))
-    rpn_head.anchor_deltas.weights.normal_(0.0, 0.1 / math.sqrt(max(stats["rpn"], 1e-12)))
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_rcnn_scores
+    calibrate_rcnn_scores(model, batch)
 
 
 def synthetic_batch(args, device, rank):
@@ -211,7 +189,8 @@ def kernel_report(summary, mode="infer"):
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                      "traffic": pmc_traffic(pmc_group, mode), "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
-    for name in ("roi_align_fwd", "roi_align_bwd", "retinanet_topk", "solo_mask_stats",
+    for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_topk",
+                 "solo_mask_stats",
                  "solo_matrix_nms", "solo_paste"):
         if name not in summary:
             continue
@@ -226,9 +205,10 @@ def kernel_report(summary, mode="infer"):
 
 def cpu_baseline(args, model, batch, cfg=None):
     """The oracle's CPU restatement timed on this host (rank 0, N=1): for
-    --mode train one training iteration (oracle/cpu_train.py: forward with
-    autograd, losses, backward, update) on ONE image of the same size — the
-    bounded sample; for --mode infer the inference forward (cpu_pipeline.py)."""
+    --mode train --cpu-iters training iterations (oracle/cpu_train.py: forward
+    with autograd, losses, backward, update) of min(--cpu-images, --batch)
+    images of the same size (default 3 x 2) — the bounded sample; for --mode
+    infer the inference forward of the model (cpu_pipeline.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cpu_pipeline import CPUReference, cpu_cores
     cores = cpu_cores()

@@ -8,8 +8,9 @@ implicit-GEMM kernel (d2mi_conv2d_nhwc) — the FPN lateral/output convs, the
 RPN head and the mask head use it — and raises if the tensor is not on the GPU.
 ``impl="torch"`` is stock PyTorch-ROCm conv2d in channels_last, used for the
 backbone (a caller of the hot path, outside its scope).
-``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation)
-and the input is on the GPU; Cin % 4 != 0 runs with zero channels appended.
+``impl="auto"`` picks mfma when the shape is eligible (no groups/dilation,
+Cin % 4 == 0) and the input is on the GPU; ``impl="mfma"`` with Cin % 4 != 0
+runs with zero channels appended.
 Backward of the mfma path: dgrad on the same MFMA kernel (flipped kernel);
 wgrad on the MFMA wgrad kernel or hipBLASLt / MIOpen, whichever measured
 faster for the shape (see _wgrad); stride-2 KxK dgrad and Cout % 4 != 0 use
@@ -297,11 +298,13 @@ class Conv2D(Layer):
         self._packed = None
         self._packed_key = None
 
-    def _mfma_eligible(self, x):
-        # Cin % 4 != 0 (e.g. SOLOv2's 256 + 2 coordinate channels) runs with
-        # zero channels appended to the input and the weights (exact: the
-        # extra products are 0)
-        return x.is_cuda and self.num_groups == 1 and self.rate == 1
+    def _mfma_eligible(self, x, padded=False):
+        # impl="mfma" with Cin % 4 != 0 (e.g. SOLOv2's 256 + 2 coordinate
+        # channels) runs with zero channels appended to the input and the
+        # weights (exact: the extra products are 0); "auto" keeps such convs
+        # (the 3-channel stem) on MIOpen
+        return (x.is_cuda and self.num_groups == 1 and self.rate == 1
+                and (padded or self.in_channels % 4 == 0))
 
     def _param_key(self):
         key = [self.weights.data_ptr(), self.weights._version]
@@ -375,7 +378,7 @@ class Conv2D(Layer):
             if impl == "torch":
                 return torch.relu_(self.call(inputs, topdown, residual))
         if impl == "mfma":
-            if not self._mfma_eligible(inputs):
+            if not self._mfma_eligible(inputs, padded=True):
                 raise ValueError(f"{self.scope}: shape/device not supported by the MFMA conv "
                                  f"(groups={self.num_groups}, rate={self.rate}, "
                                  f"Cin={self.in_channels}, device={inputs.device})")

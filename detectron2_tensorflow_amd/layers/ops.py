@@ -98,9 +98,12 @@ class _RoIAlignFn(torch.autograd.Function):
         S = max(sr, 1) ** 2
         # algorithmic bytes: 4 f32 corner reads per sample + 1 f32
         # write per output.  Feature-pyramid pooling (C >= 64, the hot path) and
-        # narrow crops (the C = 1 mask-target crop_and_resize) are timed apart.
-        KernelTimer.stop(ev, "roi_align_fwd" if C >= 64 else "crop_and_resize_fwd_narrow",
-                         R * out_h * out_w * C * (16 * S + 4))
+        # narrow crops (the C = 1 mask-target crop_and_resize) are timed apart,
+        # and the box pooler (7x7) apart from the mask pooler (14x14, a few
+        # dozen ROIs per step: latency-bound)
+        name = ("crop_and_resize_fwd_narrow" if C < 64 else
+                "roi_align_fwd" if out_h * out_w <= 49 else "roi_align_fwd_mask")
+        KernelTimer.stop(ev, name, R * out_h * out_w * C * (16 * S + 4))
         _C.check(rc, "d2mi_roi_align_fwd")
         ctx.params = params
         ctx.shapes = [f.shape for f in feats]
@@ -198,6 +201,9 @@ def non_max_suppression(boxes, scores, max_output_size, iou_threshold=0.5):
 
 
 # --------------------------------------------------------------------- top-k
+TOPK_MAX_K = 8192  # d2mi_topk's largest k (kCap in csrc/topk.hip)
+
+
 def topk_segments(values, seg_start, seg_len, k, max_seg_len, sigmoid=False):
     """Exact segmented top-k (tf.nn.top_k sorted=True order)."""
     values = _f32c(values)

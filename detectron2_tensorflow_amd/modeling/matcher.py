@@ -115,7 +115,7 @@ def _smallest(keys, mask, k, limit):
     sel = torch.zeros_like(mask)
     if k <= 0:
         return sel
-    if keys.is_cuda:
+    if keys.is_cuda and k <= ops.TOPK_MAX_K:
         # the HIP segmented radix select (one segment per row) on -key: the k
         # largest of -key are the k smallest keys, ascending; unmasked -> -2
         neg = torch.where(mask, -keys, torch.full_like(keys, -2.0))
@@ -125,6 +125,8 @@ def _smallest(keys, mask, k, limit):
                                                     device=keys.device), k, P)
         take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals > -2.0)
         return sel.scatter_(1, idx.long(), take)
+    # beyond the HIP select's capacity (batch sizes above 8192 per image, e.g.
+    # every anchor sampled) or off the GPU: torch's top-k, same selection
     kk = torch.where(mask, keys, torch.full_like(keys, 2.0))
     vals, idx = kk.topk(k, dim=1, largest=False, sorted=True)
     take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals < 2.0)

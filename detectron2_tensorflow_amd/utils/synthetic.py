@@ -49,6 +49,42 @@ def synthetic_train_batch(batch, height, width, seed, device, **kw):
 
 
 @torch.no_grad()
+def calibrate_rcnn_scores(model, batch):
+    """BASELINE.md score injection for a random-init (Mask / Faster) R-CNN:
+    rescale the box-head class logits to ~ N(0, 3^2), the RPN objectness to
+    ~ N(0, 1) and the RPN anchor deltas to N(0, 0.1^2) on this batch's
+    features.  The unnormalised features of a random-init ResNet otherwise
+    give class logits in the hundreds (a Fast R-CNN CE loss of ~750) and
+    deltas of O(10), which collapse most proposals onto the image border (a
+    random-init artefact, not a training distribution)."""
+    import math
+    stats = {}
+
+    def grab(name):
+        def hook(mod, inp, out):
+            x = inp[0]
+            stats[name] = float((x.reshape(-1, x.shape[-1]) ** 2).sum(-1).mean())
+        return hook
+
+    rh = model.roi_heads
+    h1 = rh.box_predictor.register_forward_hook(grab("box"))
+    rpn_head = model.proposal_generator.rpn_head
+    h2 = rpn_head.conv.register_forward_hook(lambda m, i, o: stats.__setitem__(
+        "rpn", float((o.reshape(-1, o.shape[-1]) ** 2).sum(-1).mean())))
+    was = model.training
+    model.eval()
+    model.inference({"image": batch["image"], "image_shape": batch["image_shape"]})
+    model.train(was)
+    h1.remove()
+    h2.remove()
+    cls = rh.box_predictor.cls_score
+    cls.weights.normal_(0.0, 3.0 / math.sqrt(max(stats["box"], 1e-12)))
+    obj = rpn_head.objectness_logits
+    obj.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["rpn"], 1e-12)))
+    rpn_head.anchor_deltas.weights.normal_(0.0, 0.1 / math.sqrt(max(stats["rpn"], 1e-12)))
+
+
+@torch.no_grad()
 def calibrate_solo_head(branch, pred_cls, pred_kernels, cls_mean=-4.5, cls_std=1.0,
                         kernel_std=0.1):
     """Score injection for a random-init SOLOv2 MaskKernelBranch: rescale

@@ -379,7 +379,10 @@ def matrix_nms(masks, classes, scores, sum_masks=None, kernel="gaussian", sigma=
     cls = np.asarray(classes)
     cmat = (cls[None, :] == cls[:, None]).astype(F32)
     iou = iou * cmat
-    comp = iou.max(axis=0)
+    # reduce_max / reduce_min: Eigen's scalar Max/MinReducer update only when
+    # `t < accum` (`t > accum`) holds, i.e. they skip NaN (the linear kernel's
+    # 0 / 0 where comp = 1 and iou = 1): fmax / fmin reductions
+    comp = np.fmax.reduce(iou, axis=0)
     comp = np.tile(comp[None, :], (n, 1)).T
     if kernel == "gaussian":
         decay = np.exp(F32(-1 * sigma) * (iou ** 2 - comp ** 2))
@@ -387,7 +390,7 @@ def matrix_nms(masks, classes, scores, sum_masks=None, kernel="gaussian", sigma=
         decay = (F32(1.0) - iou) / (F32(1.0) - comp)
     else:
         raise NotImplementedError(kernel)
-    return (_f32(scores) * decay.min(axis=0)).astype(F32)
+    return (_f32(scores) * np.fmin.reduce(decay, axis=0)).astype(F32)
 
 
 def paste_masks(box_masks, boxes, out_shape, valid=None, yx_scale=None, threshold=0.5):

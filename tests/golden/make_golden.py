@@ -1,4 +1,5 @@
-"""Generates tests/golden/nms_golden.npz from the REFERENCE's own numpy NMS.
+"""Generates tests/golden/nms_golden.npz from the REFERENCE's own numpy NMS,
+and tests/golden/box_ops_golden.npz from its numpy IoU, clip and decode.
 
 Runs only in the build container (needs /root/reference): loads
 lib/structures/np_box_list.py, np_box_ops.py and np_box_list_ops.py by file
@@ -13,6 +14,18 @@ tie-free inputs and rejects sets with any pairwise IoU within 1e-4 of the
 threshold.  The committed .npz is data (inputs + expected outputs); no
 reference source travels with it.
 
+box_ops_golden.npz (same loader):
+  * np_box_ops.iou (np_box_ops.py:48-63: intersection in float64 through
+    np.zeros, float32 areas) of two seeded box sets -> float64 IoU matrix;
+    the sets avoid near-ties (each GT's best IoU, and each overlapped box's
+    best GT, leads the runner-up by > 1e-4) and IoUs within 1e-4 of the
+    matcher thresholds 0.3 / 0.5 / 0.7;
+  * np_box_list_ops.clip_to_window (np_box_list_ops.py:319-350: fmin / fmax,
+    then the boxes with area > 0 kept) -> clipped boxes + kept indices;
+  * np_box_ops.apply_box_deltas (np_box_ops.py:85-113: weights (1, 1, 1, 1),
+    ymax = ymin + h) -> decoded boxes, |dh|, |dw| below Box2BoxTransform's
+    clamp log(1000/16) so the two formulas differ only by rounding.
+
     python tests/golden/make_golden.py [/root/reference]
 """
 import importlib.util
@@ -23,6 +36,7 @@ import types
 import numpy as np
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "nms_golden.npz")
+OUT_BOX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "box_ops_golden.npz")
 
 
 def load_reference_np_ops(ref_root):
@@ -81,6 +95,45 @@ def make_case(rng, mods, n, thr, max_out, clusters):
     raise RuntimeError("could not draw a threshold-safe case")
 
 
+def box_ops_cases(mods, rng):
+    ops, lops, bl = mods["np_box_ops"], mods["np_box_list_ops"], mods["np_box_list"]
+    data = {}
+    for _ in range(200):
+        gt = random_boxes(rng, 20, extent=600.0, min_side=16.0, max_side=300.0)
+        anchors = random_boxes(rng, 3000, extent=600.0, min_side=8.0, max_side=300.0,
+                               clusters=60)
+        # many anchors close to the GT so every matcher label occurs
+        near = gt[rng.integers(0, 20, size=1000)] + rng.normal(0, 6, size=(1000, 4)).astype(np.float32)
+        anchors[:1000] = np.concatenate([np.minimum(near[:, :2], near[:, 2:] - 2),
+                                         np.maximum(near[:, 2:], near[:, :2] + 2)], 1)
+        iou = ops.iou(gt.astype(np.float32), anchors.astype(np.float32))
+        srt = np.sort(iou, axis=0)
+        if np.any((srt[-1] > 0) & (srt[-1] - srt[-2] < 1e-4)):
+            continue
+        srt_g = np.sort(iou, axis=1)
+        if np.any(srt_g[:, -1] - srt_g[:, -2] < 1e-4):
+            continue
+        if any(np.any(np.abs(iou - t) < 1e-4) for t in (0.3, 0.5, 0.7)):
+            continue
+        data.update(iou_gt=gt, iou_boxes=anchors, iou=iou)
+        break
+    else:
+        raise RuntimeError("could not draw a tie-free IoU case")
+    boxes = random_boxes(rng, 500, extent=900.0, min_side=4.0, max_side=400.0) - np.float32(100)
+    window = np.array([0, 0, 640, 853], np.float32)
+    blist = bl.BoxList(boxes.copy())
+    blist.add_field("idx", np.arange(500))
+    clipped = lops.clip_to_window(blist, window)
+    data.update(clip_boxes=boxes, clip_window=window, clip_out=clipped.get().astype(np.float32),
+                clip_keep=clipped.get_field("idx").astype(np.int32))
+    dboxes = random_boxes(rng, 2000, extent=1333.0, min_side=4.0, max_side=800.0)
+    deltas = rng.normal(0, 0.5, size=(2000, 4)).astype(np.float32)
+    deltas[:, 2:] = np.clip(deltas[:, 2:], -4.0, 4.0)
+    data.update(dec_boxes=dboxes, dec_deltas=deltas,
+                dec_out=ops.apply_box_deltas(dboxes.copy(), deltas.copy()).astype(np.float32))
+    return data
+
+
 def main(ref_root="/root/reference"):
     mods = load_reference_np_ops(ref_root)
     rng = np.random.default_rng(20261015)
@@ -98,6 +151,9 @@ def main(ref_root="/root/reference"):
     data["num_cases"] = np.array(len(cases))
     np.savez_compressed(OUT, **data)
     print("wrote", OUT, {k: v.shape for k, v in data.items() if k.endswith("_keep")})
+    box = box_ops_cases(mods, np.random.default_rng(20261016))
+    np.savez_compressed(OUT_BOX, **box)
+    print("wrote", OUT_BOX, {k: v.shape for k, v in box.items()})
 
 
 if __name__ == "__main__":

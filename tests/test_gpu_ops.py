@@ -60,10 +60,18 @@ def test_roi_align_multilevel_matches_oracle(dev, C):
         got, lv = ops().roi_align([torch.from_numpy(f).to(dev) for f in feats],
                                   torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
                                   (oh, oh), scales, 0, True, return_levels=True)
-        lv = lv.cpu().numpy()
+        lv, got = lv.cpu().numpy(), got.cpu().numpy()
         same = lv == lv_want
-        assert same.mean() > 0.99, "level assignment disagrees beyond boundary cases"
-        np.testing.assert_allclose(got.cpu().numpy()[same], want[same], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(got[same], want[same], rtol=0, atol=1e-5)
+        # a level differs only for log-boundary boxes (logf rounding on either
+        # side), and the GPU's output is the oracle's ROIAlign on its level
+        b = boxes.astype(np.float64)
+        v = 4 + np.log(np.sqrt((b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])) / 224 + 2.0 ** -52) / math.log(2)
+        for i in np.nonzero(~same)[0]:
+            assert abs(v[i] - round(v[i])) < 1e-5, (i, v[i], lv[i], lv_want[i])
+            w1 = oracle.roi_align(feats[lv[i]], boxes[i:i + 1], bimg[i:i + 1], (oh, oh),
+                                  scales[lv[i]], 0, True)
+            np.testing.assert_allclose(got[i:i + 1], w1, rtol=0, atol=1e-5)
 
 
 @pytest.mark.parametrize("aligned,sr,pad", [(True, 0, True), (False, 0, True), (True, 2, True),
@@ -471,7 +479,13 @@ def test_matrix_nms_vs_oracle(dev):
         want = oracle.matrix_nms(masks, classes, scores, kernel=kern, sigma=2.0)
         got = ops().matrix_nms_scores(torch.from_numpy(masks).to(dev), torch.from_numpy(classes).to(dev),
                                       torch.from_numpy(scores).to(dev), kernel=kern, sigma=2.0)
-        np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-5, atol=1e-6)
+        g = got.cpu().numpy()
+        fin = np.isfinite(want)
+        # the finite decays (the linear kernel divides by 1 - comp, which is 0
+        # for the duplicated masks: those columns are +inf on both sides)
+        np.testing.assert_allclose(g[fin], want[fin], rtol=1e-5, atol=1e-6)
+        np.testing.assert_array_equal(g[~fin], want[~fin])
+        assert fin.sum() > M // 2
 
 
 # ------------------------------------------------------------------ conv

@@ -311,3 +311,75 @@ def test_fused_rpn_loss_matches_tensor_formulation(dev):
     assert loc.item() == pytest.approx(loc_r.item(), rel=1e-5)
     torch.testing.assert_close(lf.grad, lr.grad, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(df.grad, dr.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_whole_training_step_matches_cpu_restatement(dev):
+    """One HIP Trainer.step vs oracle/cpu_train.py's CPUTrainStep.step on
+    identical weights and batch (lib/engine/trainer.py:116-139,
+    model_deploy.py:203-205), with EVERY candidate sampled: the RPN and ROI
+    batch sizes exceed the candidate counts (2^20 anchors per image at
+    positive fraction 0.5; 200 train proposals + GT per image under 512 at
+    fraction 1.0), so the random subsampling is a permutation and every loss
+    is order-invariant.  Pins A14 (RPN losses), A18 (label + sample), A19
+    (box losses), A20 (mask loss) and A23 (clip_by_norm + Momentum-SGD)
+    together: losses to 1e-4 relative, the updated FPN / RPN / ROI-head
+    weights to 1e-4 of their scale, and their updates w1 - w0 to 5e-3 of the
+    update's scale per tensor plus 4 ulp of the weight (an f32 weight of 0.03
+    rounds its update to ~2e-9; ReLU units within f32 noise of zero pass or
+    block their gradient differently: the box head's updates differ by
+    ~1.5e-3), for the tensors whose update exceeds 100 such ulps."""
+    import cpu_train
+    from detectron2_tensorflow_amd.config import finalize, get_cfg
+    from detectron2_tensorflow_amd.engine import Trainer
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.utils.synthetic import (calibrate_rcnn_scores,
+                                                           synthetic_train_batch)
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(ROOT, "configs", "COCO-InstanceSegmentation",
+                                     "mask_rcnn_R_50_FPN_1x.yaml"))
+    cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT = "raw"
+    cfg.SOLVER.BASE_LR = 0.02
+    cfg.SOLVER.WARMUP_ITERS = 0
+    cfg.SOLVER.IMS_PER_BATCH_BASE = 2
+    cfg.MODEL.RPN.BATCH_SIZE_PER_IMAGE = 1 << 20
+    cfg.MODEL.RPN.POST_NMS_TOPK_TRAIN = 200
+    cfg.MODEL.ROI_HEADS.BATCH_SIZE_PER_IMAGE = 512
+    cfg.MODEL.ROI_HEADS.POSITIVE_FRACTION = 1.0
+    finalize(cfg, True, 1, CATS)
+    torch.manual_seed(0)
+    model = build_model(cfg).to(dev)
+    model.train()
+    batch = synthetic_train_batch(2, 256, 320, 3, dev)
+    calibrate_rcnn_scores(model, batch)               # BASELINE.md logit scales
+    cpu = cpu_train.CPUTrainStep(model, cfg)          # deep copy of the same weights
+    names = [n for n, p in model.named_parameters() if p.requires_grad
+             and not n.startswith("backbone.")]
+    before = {n: p.detach().cpu().clone() for n, p in model.named_parameters() if n in names}
+    trainer = Trainer(cfg, model)
+    g_losses = {k: float(v.detach()) for k, v in trainer.step(batch).items()}
+    c_losses = cpu.step(batch["image"].cpu().numpy(), batch["image_shape"].cpu().numpy(),
+                        {k: v.cpu() for k, v in batch["instances"].items()}, threads=16)
+    for k, v in c_losses.items():
+        assert abs(g_losses[k] - v) <= 1e-4 * max(abs(v), 1e-3), (k, g_losses[k], v)
+    cparams = dict(cpu.m.named_parameters())
+    checked, worst_w, worst_d = 0, 0.0, 0.0
+    for n, p in model.named_parameters():
+        if n not in before:
+            continue
+        g, c, w0 = p.detach().cpu(), cparams[n].detach(), before[n]
+        dg, dc = g - w0, c - w0
+        upd = dc.abs().max().item()
+        diff = (g - c).abs().max().item()
+        # weights to 1e-4 of their scale (zero-initialised biases: of the update)
+        assert diff <= max(1e-4 * c.abs().max().item(), 5e-3 * upd, 1e-12), (n, diff)
+        worst_w = max(worst_w, diff / max(c.abs().max().item(), 1e-12))
+        # the update is stored rounded to the weight's ulp: allow 4 ulp of it
+        ulp4 = 4 * torch.finfo(torch.float32).eps * w0.abs().max().item()
+        if upd > 100 * ulp4:
+            dd = (dg - dc).abs().max().item()
+            assert dd <= 5e-3 * upd + ulp4, (n, dd, upd)
+            worst_d = max(worst_d, dd / upd)
+            checked += 1
+    print(f"losses gpu {g_losses}\nlosses cpu {c_losses}\nworst weight rel diff {worst_w:.3g}, "
+          f"worst update rel diff {worst_d:.3g} over {checked} tensors")
+    assert checked > 25, checked

@@ -163,3 +163,48 @@ def test_paste_masks_kat_in_range_region():
     z = oracle.paste_masks(np.full((2, mh, mh), 0.5, np.float32), np.repeat(box, 2, 0), (H, W),
                            valid=np.array([True, False]))
     assert z.sum() == 0
+
+
+# ------------------------------------------------ reference-held box-op goldens
+BOX_GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "box_ops_golden.npz")
+
+
+def test_pairwise_iou_matches_reference_numpy_iou():
+    """oracle/training.py pairwise_iou (the TF box_list_ops formula, float32)
+    vs the reference's np_box_ops.iou (np_box_ops.py:48-63, float64
+    intersection): equal to float32 rounding; the matcher decisions on the
+    two matrices are identical (tie- and threshold-safe inputs)."""
+    import training
+    g = np.load(BOX_GOLDEN)
+    ours = training.pairwise_iou(g["iou_gt"], g["iou_boxes"])
+    np.testing.assert_allclose(ours, g["iou"], rtol=2e-6, atol=1e-7)
+    for thr, labels in (((0.3, 0.7), (0, -1, 1)), ((0.5,), (0, 1))):
+        m1, l1 = training.matcher(ours, thr, labels, True)
+        m2, l2 = training.matcher(g["iou"].astype(np.float32), thr, labels, True)
+        np.testing.assert_array_equal(m1, m2)
+        np.testing.assert_array_equal(l1, l2)
+    assert len(set(l1.tolist())) == 2 and (l1 == 1).sum() > 100
+
+
+def test_clip_to_window_matches_reference_numpy_clip():
+    """clip_to_window (box_list_ops.py:112-147) vs np_box_list_ops.clip_to_window
+    (np_box_list_ops.py:319-350): identical clipped corners; the reference's
+    numpy version then drops zero-area boxes (the TF op with
+    filter_nonoverlapping=True does the same)."""
+    g = np.load(BOX_GOLDEN)
+    out = oracle.clip_to_window(g["clip_boxes"], g["clip_window"])
+    area = (out[:, 2] - out[:, 0]) * (out[:, 3] - out[:, 1])
+    keep = np.nonzero(area > 0)[0]
+    np.testing.assert_array_equal(keep, g["clip_keep"])
+    np.testing.assert_array_equal(out[keep], g["clip_out"])
+
+
+def test_apply_deltas_matches_reference_numpy_decode():
+    """Box2BoxTransform.apply_deltas with weights (1, 1, 1, 1) vs the reference's
+    np_box_ops.apply_box_deltas (np_box_ops.py:85-113): the same decode up to
+    rounding (numpy forms ymax = ymin + h, the transform cy + h / 2)."""
+    g = np.load(BOX_GOLDEN)
+    got = oracle.apply_deltas(g["dec_deltas"], g["dec_boxes"], (1, 1, 1, 1))
+    want = g["dec_out"]
+    tol = np.maximum(np.float32(1e-4), 4 * np.spacing(np.abs(want).max(axis=1, keepdims=True)))
+    assert (np.abs(got - want) <= tol).all()

@@ -294,6 +294,86 @@ def test_bucketed_allreduce_gloo_world2_matches_single_process(tmp_path):
         torch.testing.assert_close(r0[k], v, rtol=1e-5, atol=1e-6)
 
 
+class _SharedBranchModel(torch.nn.Module):
+    """A head shared across "levels" (used 3 times per forward, as the RPN head
+    over p2..p6) and a branch that only runs when its input is non-empty (as
+    a mask head on a rank with no foreground)."""
+
+    def __init__(self, seed):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.stem = torch.nn.Linear(16, 32)
+        self.shared = torch.nn.Linear(32, 32)
+        self.branch = torch.nn.Linear(32, 3)
+        self.out = torch.nn.Linear(32, 3)
+
+    def forward(self, x, use_branch):
+        h = torch.relu(self.stem(x))
+        y = 0
+        for s in (1.0, 0.5, 0.25):  # one parameter, three uses
+            y = y + self.out(torch.relu(self.shared(h * s)))
+        if use_branch:
+            y = y + self.branch(h)
+        return y
+
+
+def _dp_shared_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from detectron2_tensorflow_amd.engine import BucketedAllReduce, broadcast_parameters
+    from detectron2_tensorflow_amd.solver import MomentumSGD
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = _SharedBranchModel(seed=rank)
+    broadcast_parameters(model)
+    params = list(model.parameters())
+    opt = MomentumSGD([{"params": params, "weight_decay": 0.0}], 0.9, 0.0)
+    red = BucketedAllReduce(params, bucket_bytes=2048)  # the branch gets a bucket of its own
+    for it in range(3):
+        opt.zero_grad()
+        red.reset()
+        x, y = _batch(rank * 10 + it)
+        # rank 1 never runs the branch: its .grad stays None there, and
+        # finish() must contribute zeros for it (same collective sequence)
+        torch.nn.functional.mse_loss(model(x, use_branch=(rank == 0)), y).backward()
+        red.finish()
+        opt.step(0.05)
+    torch.save({k: v.detach().clone() for k, v in model.state_dict().items()},
+               os.path.join(out_dir, f"shared{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_shared_and_rank_local_params(tmp_path):
+    """engine/reducer.py with a parameter used several times per forward (its
+    post-accumulate hook fires once, on the summed gradient) and a parameter
+    that gets no gradient on one rank only (the finish() zero fill): replicas
+    stay bit-identical and equal the single-process mean-gradient update."""
+    import torch.multiprocessing as mp
+    from detectron2_tensorflow_amd.solver import MomentumSGD
+    world = 2
+    mp.spawn(_dp_shared_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "shared0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "shared1.pt", weights_only=True)
+    for k in r0:
+        torch.testing.assert_close(r0[k], r1[k], rtol=0, atol=0)
+    model = _SharedBranchModel(seed=0)
+    params = list(model.parameters())
+    opt = MomentumSGD([{"params": params, "weight_decay": 0.0}], 0.9, 0.0)
+    for it in range(3):
+        grads = []
+        for rank in range(world):
+            model.zero_grad(set_to_none=True)
+            x, y = _batch(rank * 10 + it)
+            torch.nn.functional.mse_loss(model(x, use_branch=(rank == 0)), y).backward()
+            grads.append([p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+                          for p in params])
+        for i, p in enumerate(params):
+            p.grad = (grads[0][i] + grads[1][i]) / world
+        opt.step(0.05)
+    for k, v in model.state_dict().items():
+        torch.testing.assert_close(r0[k], v, rtol=1e-5, atol=1e-6)
+    assert not torch.equal(r0["branch.weight"], _SharedBranchModel(seed=0).branch.weight)
+
+
 def test_cpu_training_step_restatement_runs_and_updates():
     """oracle/cpu_train.py (bench.py's training cpu_baseline): one step on a tiny
     image gives finite losses and moves the trainable weights only."""

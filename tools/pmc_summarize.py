@@ -29,7 +29,7 @@ GROUPS = {
     "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce4?_kernel"),
                      re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel")),
     "conv2d_mfma": (re.compile(r"conv_mfma_kernel<[^>]*, false>"), None),
-    "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),
+    "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),  # split below
     "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_pixel_kernel")),
     "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce4?_kernel"),
                          re.compile(r"conv_wgrad_split_kernel")),
@@ -40,6 +40,7 @@ GROUPS = {
 def load(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     per = collections.defaultdict(lambda: [0, 0.0])
+    disp = []  # (name, grid size, value) per dispatch
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
@@ -47,13 +48,28 @@ def load(d, counter):
             name = r.get("Kernel_Name", "")
             per[name][0] += 1
             per[name][1] += float(r["Counter_Value"])
-    return per
+            disp.append((name, int(float(r.get("Grid_Size", 0) or 0)), float(r["Counter_Value"])))
+    return per, disp
+
+
+def split_roi_fwd(disp):
+    """The ROIAlign forward's box-pooler (7x7, ~1000 ROIs) and mask-pooler
+    (14x14, a few dozen ROIs) launches, told apart by grid size: the box
+    launches have the largest grids.  -> {"roi_align_fwd": [values],
+    "roi_align_fwd_mask": [values]}"""
+    rx = re.compile(r"roi_align_fwd_kernel<true>")
+    xs = [(g, v) for n, g, v in disp if rx.search(n)]
+    if not xs:
+        return {}
+    gmax = max(g for g, _ in xs)
+    return {"roi_align_fwd": [v for g, v in xs if g * 2 > gmax],
+            "roi_align_fwd_mask": [v for g, v in xs if g * 2 <= gmax]}
 
 
 def main():
     fd, wd, out = sys.argv[1:4]
-    fetch = load(fd, "FETCH_SIZE")
-    write = load(wd, "WRITE_SIZE")
+    fetch, fdisp = load(fd, "FETCH_SIZE")
+    write, wdisp = load(wd, "WRITE_SIZE")
     res = {"units": "bytes per dispatch", "fetch_correction": 2.0,
            "note": "FETCH_SIZE x2 (gfx950 16 B/lane reads); WRITE_SIZE as reported",
            "groups": {}}
@@ -73,6 +89,14 @@ def main():
         }
         res["groups"][g]["traffic_bytes_per_launch"] = (
             res["groups"][g]["fetch_bytes_per_launch"] + res["groups"][g]["write_bytes_per_launch"])
+    # the ROIAlign forward per launch kind (grid size), replacing the average
+    fs, ws = split_roi_fwd(fdisp), split_roi_fwd(wdisp)
+    for g in fs:
+        if fs[g]:
+            fb, wb = 2.0 * sum(fs[g]) * 1024 / len(fs[g]), sum(ws.get(g, [])) * 1024 / max(len(ws.get(g, [])), 1)
+            res["groups"][g] = {"dispatches": len(fs[g]), "main_kernel_dispatches": len(fs[g]),
+                                "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                                "traffic_bytes_per_launch": fb + wb, "split_by": "grid size"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
