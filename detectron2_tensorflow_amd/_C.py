@@ -33,6 +33,9 @@ _SIGS = {
     "d2mi_roi_align_bwd_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int]),
     "d2mi_roi_align_bwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_size_t, P]),
+    "d2mi_roi_align_bwd_ex": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int,
+                                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
+                                      P, c_size_t, P]),
     "d2mi_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
     "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),
@@ -64,6 +67,9 @@ _SIGS = {
     "d2mi_solo_finalize_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "d2mi_solo_finalize": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int,
                                    c_float, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),
+    "d2mi_group_norm_workspace_size": (c_size_t, [c_int] * 5),
+    "d2mi_group_norm_nhwc": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_float, c_int,
+                                     c_int, c_int, P, P, c_size_t, P]),
     "d2mi_conv_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_int, P]),

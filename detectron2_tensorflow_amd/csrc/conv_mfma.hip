@@ -233,14 +233,14 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
 // loaded as float4s BEFORE its LDS barrier (their latency overlaps the
 // transpose).  Same arithmetic order as epilogue(); split-K partials are
 // written raw.  smem: >= 32 * (BN + 4) floats of the kernel's LDS.
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int NT = 256>
 __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&acc)[TM][TN],
                                                   int m0, int n0, int wr, int wc, int lane,
                                                   int split, float* smem) {
   constexpr int BN = WN * TN * 32;
   constexpr int LS = BN + 4;        // slab row stride (floats)
   constexpr int F4 = BN / 4;        // float4 per tile row
-  constexpr int Q = 32 * F4 / 256;  // float4 per thread per slab
+  constexpr int Q = 32 * F4 / NT;   // float4 per thread per slab
   const int tid = threadIdx.x;
   const int li = lane & 31, lh = lane >> 5;
   const bool part = a.splits > 1;
@@ -253,7 +253,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
     float4 res[Q], gt[Q], td[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int idx = tid + 256 * q;
+      const int idx = tid + NT * q;
       const int row = idx / F4, c4 = idx - row * F4;
       const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
       res[q] = gt[q] = td[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -280,7 +280,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int idx = tid + 256 * q;
+      const int idx = tid + NT * q;
       const int row = idx / F4, c4 = idx - row * F4;
       const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
       if (m >= a.M || co >= a.Cout) continue;

@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
 // -> records -> grad_out rows) overlaps across waves instead of a wave per
 // feature-map pixel (most of which only stored zeros) -- that launch was bound
 // by wave start-up and latency, at ~1/4 of its store bandwidth.
-template <bool VEC4>
+template <bool VEC4, bool ACC>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
     RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
     int low_bits, const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
@@ -559,8 +559,21 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
         }
       }
       if (live) {
-        if (VEC4) *reinterpret_cast<float4*>(dst + c) = acc;
-        else dst[c] = acc.x;
+        // ACC: the map already holds another ROI set's gradient (the
+        // hand-off of the box and mask poolers' backwards): old + new, the
+        // same rounding as autograd's sum of the two maps
+        if (VEC4) {
+          if (ACC) {
+            const float4 o = *reinterpret_cast<const float4*>(dst + c);
+            acc.x = o.x + acc.x;
+            acc.y = o.y + acc.y;
+            acc.z = o.z + acc.z;
+            acc.w = o.w + acc.w;
+          }
+          *reinterpret_cast<float4*>(dst + c) = acc;
+        } else {
+          dst[c] = ACC ? dst[c] + acc.x : acc.x;
+        }
       }
     }
   }
@@ -715,13 +728,14 @@ extern "C" size_t d2mi_roi_align_bwd_workspace_size(const int32_t* dims, int num
   return w.off;
 }
 
-extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
-                                  const float* scales, int num_levels, int C, const float* boxes,
-                                  const int32_t* box_ind, int R, int out_h, int out_w,
-                                  int sampling_ratio, int box_mode, int pad_border, int assign,
-                                  int min_level, int max_level, int canonical_box_size,
-                                  int canonical_level, const float* grad_out, void* workspace,
-                                  size_t workspace_bytes, void* stream) {
+extern "C" int d2mi_roi_align_bwd_ex(float* const* grad_feats, const int32_t* dims,
+                                     const float* scales, int num_levels, int C,
+                                     const float* boxes, const int32_t* box_ind, int R, int out_h,
+                                     int out_w, int sampling_ratio, int box_mode, int pad_border,
+                                     int assign, int min_level, int max_level,
+                                     int canonical_box_size, int canonical_level,
+                                     const float* grad_out, int accumulate, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
   RoiArgs a = {};
   int rc = fill_args(a, dims, scales, num_levels, C, boxes, box_ind, R, out_h, out_w,
                      sampling_ratio, box_mode, pad_border, assign, min_level, max_level,
@@ -767,8 +781,9 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
     ++cl.n;
     clear_words += words;
   };
-  for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero gradient
-    clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
+  if (!accumulate)  // untouched pixels: zero gradient (accumulate: left as they are)
+    for (int l = 0; l < num_levels; ++l)
+      clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
   clear(run_start, TP, 0xffffffffu);
   clear(n_touched, 1, 0u);
   hipLaunchKernelGGL(roi_bwd_clear_kernel,
@@ -814,14 +829,27 @@ extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
   // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
   // beyond residency start as earlier ones retire (the kBatch sweep above)
   const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
-  if (vec4)
-    hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
-                       p.low_bits, run_start, run_end, nseg, seg_first, partial, touched,
-                       n_touched);
-  else
-    hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, sorted, rec,
-                       p.low_bits, run_start, run_end, nseg, seg_first, partial, touched,
-                       n_touched);
+#define PIX(V, A)                                                                            \
+  hipLaunchKernelGGL((roi_bwd_pixel_kernel<V, A>), grid, dim3(256), 0, st, a, p.pm, sorted, rec, \
+                     p.low_bits, run_start, run_end, nseg, seg_first, partial, touched, n_touched)
+  if (vec4 && accumulate) PIX(true, true);
+  else if (vec4) PIX(true, false);
+  else if (accumulate) PIX(false, true);
+  else PIX(false, false);
+#undef PIX
   D2MI_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,
+                                  const float* scales, int num_levels, int C, const float* boxes,
+                                  const int32_t* box_ind, int R, int out_h, int out_w,
+                                  int sampling_ratio, int box_mode, int pad_border, int assign,
+                                  int min_level, int max_level, int canonical_box_size,
+                                  int canonical_level, const float* grad_out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  return d2mi_roi_align_bwd_ex(grad_feats, dims, scales, num_levels, C, boxes, box_ind, R, out_h,
+                               out_w, sampling_ratio, box_mode, pad_border, assign, min_level,
+                               max_level, canonical_box_size, canonical_level, grad_out, 0,
+                               workspace, workspace_bytes, stream);
 }

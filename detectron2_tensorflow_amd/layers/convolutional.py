@@ -363,7 +363,8 @@ class Conv2D(Layer):
         return self._packed
 
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
-             relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None):
+             relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None,
+             raw=False):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -398,6 +399,11 @@ class Conv2D(Layer):
                                     fuse_relu, topdown, residual, relu_after_add,
                                     bool(relu_input_sole_consumer), res_grad_to, grad_from,
                                     pair_grad)
+            if raw:  # the conv (+ bias) alone: the caller applies the normalizer / activation
+                return ret
+            if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \
+                    and norm.fused_ok(ret):
+                return norm(ret, relu=True)  # GroupNorm + ReLU in one HIP pass
             if norm is not None:
                 ret = norm(ret)
             if self.act_fn is not None and not fuse_relu:

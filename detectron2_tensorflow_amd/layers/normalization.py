@@ -10,6 +10,7 @@ normalization.py:121-168) are not part of the hot path.
 import torch
 
 from ..utils.arg_scope import add_arg_scope
+from . import ops
 from .base import Layer
 
 
@@ -46,10 +47,29 @@ class GroupNorm(Layer):
         self.gamma = torch.nn.Parameter(torch.ones(channels), requires_grad=trainable)
         self.beta = torch.nn.Parameter(torch.zeros(channels), requires_grad=trainable)
 
-    def call(self, x):
+    def fused_ok(self, x):
+        """The HIP GroupNorm (d2mi_group_norm_nhwc) takes inference on the GPU."""
+        C = self.channels
+        return (x.is_cuda and not (torch.is_grad_enabled() and self.gamma.requires_grad)
+                and C % self.num_groups == 0 and (C // self.num_groups) % 4 == 0 and C <= 1024
+                and self.num_groups <= 64)
+
+    def call(self, x, relu=False, up2=False, accumulate_into=None):
+        """GroupNorm.call (normalization.py:235-260) on NHWC.  relu / up2 /
+        accumulate_into fuse the ops that follow it in the SOLOv2 heads (HIP
+        path); training (autograd) runs on torch's group_norm."""
+        if self.fused_ok(x):
+            return ops.group_norm(x, self.num_groups, self.gamma, self.beta, self.epsilon,
+                                  relu, up2, accumulate_into)
         y = torch.nn.functional.group_norm(x.permute(0, 3, 1, 2), self.num_groups, self.gamma,
-                                           self.beta, self.epsilon)
-        return y.permute(0, 2, 3, 1)
+                                           self.beta, self.epsilon).permute(0, 2, 3, 1)
+        if relu:
+            y = torch.relu(y)
+        if up2:
+            y = y.repeat_interleave(2, 1).repeat_interleave(2, 2)
+        if accumulate_into is not None:
+            return accumulate_into.add_(y)
+        return y
 
 
 def get_norm(norm):

@@ -71,10 +71,18 @@ def _i32c(t):
 # ------------------------------------------------------------------ ROIAlign
 class _RoIAlignFn(torch.autograd.Function):
     """ROIAlign forward/backward over 1..8 feature levels.  Boxes carry no
-    gradient (crop_and_resize stop_gradient, lib/layers/functional.py:120)."""
+    gradient (crop_and_resize stop_gradient, lib/layers/functional.py:120).
+
+    grad_share (a dict shared by two poolings of the SAME feature maps, the
+    box and mask poolers of a training step, both of whose backwards always
+    run): the first backward writes the full maps and leaves them in the
+    dict, returning no gradient for the features; the second adds its
+    contributions into them (d2mi_roi_align_bwd_ex accumulate: no second
+    183 MB clear at 1333x800, no autograd add of two maps) and returns the
+    sum — bit-identical to autograd's add of the two maps."""
 
     @staticmethod
-    def forward(ctx, boxes, box_ind, params, *feats):
+    def forward(ctx, boxes, box_ind, params, grad_share, *feats):
         feats = [_f32c(f) for f in feats]
         boxes = _f32c(boxes)
         box_ind = _i32c(box_ind)
@@ -106,6 +114,7 @@ class _RoIAlignFn(torch.autograd.Function):
         KernelTimer.stop(ev, name, R * out_h * out_w * C * (16 * S + 4))
         _C.check(rc, "d2mi_roi_align_fwd")
         ctx.params = params
+        ctx.share = grad_share
         ctx.shapes = [f.shape for f in feats]
         ctx.save_for_backward(boxes, box_ind)
         ctx.set_materialize_grads(False)  # level (non-differentiable): no zero grad
@@ -116,12 +125,17 @@ class _RoIAlignFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out, _grad_level):
         if grad_out is None:
-            return (None,) * (3 + len(ctx.shapes))
+            return (None,) * (4 + len(ctx.shapes))
         boxes, box_ind = ctx.saved_tensors
         (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
          _) = ctx.params
-        # every element is written by d2mi_roi_align_bwd (zero-fill + touched pixels)
-        grads = [torch.empty(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
+        share = ctx.share
+        prior = share.pop("maps", None) if share is not None else None
+        if prior is not None:  # second of a pair: add into the first's maps
+            grads = prior
+        else:
+            # every element is written by d2mi_roi_align_bwd (zero-fill + touched pixels)
+            grads = [torch.empty(s, dtype=torch.float32, device=boxes.device) for s in ctx.shapes]
         g = _f32c(grad_out)
         gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
         dims = _C.host_array(_C.ctypes.c_int32, [v for s in ctx.shapes for v in (s[0], s[1], s[2])])
@@ -130,25 +144,30 @@ class _RoIAlignFn(torch.autograd.Function):
         wsb = _C.lib().d2mi_roi_align_bwd_workspace_size(dims, len(grads), C, R, out_h, out_w, sr)
         ws = _C.workspace(wsb, boxes.device)
         ev = KernelTimer.start()
-        rc = _C.lib().d2mi_roi_align_bwd(gp, dims, sc, len(grads), C, _C.ptr(boxes),
-                                         _C.ptr(box_ind), R, out_h, out_w, sr, mode, pad, assign,
-                                         min_l, max_l, canon_s, canon_l, _C.ptr(g), _C.ptr(ws), wsb,
-                                         _C.stream_of(boxes.device))
+        rc = _C.lib().d2mi_roi_align_bwd_ex(gp, dims, sc, len(grads), C, _C.ptr(boxes),
+                                            _C.ptr(box_ind), R, out_h, out_w, sr, mode, pad,
+                                            assign, min_l, max_l, canon_s, canon_l, _C.ptr(g),
+                                            int(prior is not None), _C.ptr(ws), wsb,
+                                            _C.stream_of(boxes.device))
         # algorithmic bytes: R*oh*ow*C*(4 + 32*S) = the grad_out read
         # + 4 corner read-modify-writes per sample of the reference's scatter
         S = max(sr, 1) ** 2
         KernelTimer.stop(ev, "roi_align_bwd" if C >= 64 else "crop_and_resize_bwd_narrow",
                          R * out_h * out_w * C * (4 + 32 * S))
         _C.check(rc, "d2mi_roi_align_bwd")
-        return (None, None, None, *grads)
+        if share is not None and prior is None:  # first of a pair: hand the maps over
+            share["maps"] = grads
+            return (None,) * (4 + len(grads))
+        return (None, None, None, None, *grads)
 
 
 def roi_align(features, boxes, box_ind, output_size, scales, sampling_ratio=0, aligned=True,
               pad_border=True, assign_levels=True, min_level=None, max_level=None,
               canonical_box_size=224, canonical_level=4, return_levels=False,
-              box_mode=None):
+              box_mode=None, grad_share=None):
     """Multi-level ROIAlign (poolers.py:134-180 + roi_align.py:45-66 +
-    functional.py:100-166) in one launch; output rows in input order."""
+    functional.py:100-166) in one launch; output rows in input order.
+    grad_share: see _RoIAlignFn (two poolings of one set of maps)."""
     if not isinstance(features, (list, tuple)):
         features = [features]
     L = len(features)
@@ -162,7 +181,7 @@ def roi_align(features, boxes, box_ind, output_size, scales, sampling_ratio=0, a
               int(box_mode), int(bool(pad_border)), int(bool(assign_levels and L > 1)),
               int(min_level), int(max_level), int(canonical_box_size), int(canonical_level),
               bool(return_levels))
-    out, level = _RoIAlignFn.apply(boxes, box_ind, params, *features)
+    out, level = _RoIAlignFn.apply(boxes, box_ind, params, grad_share, *features)
     return (out, level) if return_levels else out
 
 
@@ -769,6 +788,33 @@ def matrix_nms_scores(masks, classes, scores, sum_masks=None, kernel="gaussian",
                                   _C.ptr(out), _C.ptr(ws), wsb, _C.stream_of(masks.device))
     _C.check(rc, "d2mi_matrix_nms")
     return out
+
+
+# ---------------------------------------------------------------- GroupNorm
+def group_norm(x, num_groups, gamma, beta, eps, relu=False, up2=False, accumulate_into=None):
+    """GroupNorm (+ ReLU) on NHWC with the SOLOv2 feature-branch tail fused
+    (d2mi_group_norm_nhwc): up2 writes the nearest x2 upsample; accumulate_into
+    adds the result into that tensor (returned).  Inference only (no grad)."""
+    x = _f32c(x)
+    gamma, beta = _f32c(gamma), _f32c(beta)
+    _C.require_device(x, gamma, beta)
+    N, H, W, C = x.shape
+    oshape = (N, 2 * H, 2 * W, C) if up2 else (N, H, W, C)
+    if accumulate_into is not None:
+        y = accumulate_into
+        if tuple(y.shape) != oshape or not y.is_contiguous() or y.dtype != torch.float32:
+            raise ValueError(f"accumulate_into must be a contiguous f32 {oshape} tensor")
+    else:
+        y = torch.empty(oshape, dtype=torch.float32, device=x.device)
+    lib = _C.lib()
+    wsb = lib.d2mi_group_norm_workspace_size(N, H, W, C, int(num_groups))
+    ws = _C.workspace(wsb, x.device)
+    rc = lib.d2mi_group_norm_nhwc(_C.ptr(x), N, H, W, C, int(num_groups), _C.ptr(gamma),
+                                  _C.ptr(beta), float(eps), int(bool(relu)), int(bool(up2)),
+                                  int(accumulate_into is not None), _C.ptr(y), _C.ptr(ws), wsb,
+                                  _C.stream_of(x.device))
+    _C.check(rc, "d2mi_group_norm_nhwc")
+    return y
 
 
 # ------------------------------------------------------------ resize / SOLOv2

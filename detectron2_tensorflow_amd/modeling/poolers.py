@@ -51,15 +51,18 @@ class ROIPooler(Layer):
         assert canonical_box_size > 0
         self.canonical_box_size = canonical_box_size
 
-    def pool(self, x, boxes, box_img, return_levels=False):
-        """x: list of NHWC maps; boxes [R, 4] image px; box_img [R] image index."""
+    def pool(self, x, boxes, box_img, return_levels=False, grad_share=None):
+        """x: list of NHWC maps; boxes [R, 4] image px; box_img [R] image index.
+        grad_share: a dict shared with another pooling of the same maps whose
+        backward also runs (ops._RoIAlignFn): one gradient map set, no add."""
         assert len(x) == len(self.scales), (
             f"unequal value, num_level_assignments={len(self.scales)}, but x is list of {len(x)} Tensors")
         return ops.roi_align(x, boxes, box_img, self.output_size, self.scales, self.sampling_ratio,
                              aligned=self.aligned, min_level=self.min_level,
                              max_level=self.max_level,
                              canonical_box_size=self.canonical_box_size,
-                             canonical_level=self.canonical_level, return_levels=return_levels)
+                             canonical_level=self.canonical_level, return_levels=return_levels,
+                             grad_share=grad_share)
 
     def call(self, x, instances):
         """instances: SparseBoxList (boxes in .data, image index in .indices[:, 0])."""

@@ -140,9 +140,12 @@ class StandardROIHeads(ROIHeads):
             if targets is None:
                 raise ValueError("ROI-head training needs targets")
             sampled = self.label_and_sample_proposals(proposals, targets)
-            losses = self._box_losses(feats, sampled)
+            # the box and mask poolers read the same p2..p5: one gradient map
+            # set for both backwards (ops._RoIAlignFn grad_share)
+            share = {} if self.mask_on else None
+            losses = self._box_losses(feats, sampled, share)
             if self.mask_on:
-                losses["loss_mask"] = self._mask_loss(feats, sampled, targets)
+                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share)
             return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
         pred = self.forward_with_given_boxes(features, pred)
@@ -170,17 +173,18 @@ class StandardROIHeads(ROIHeads):
         res.set_tracking("image_shape", image_shapes)
         return res
 
-    def _box_losses(self, feats, sampled):
+    def _box_losses(self, feats, sampled, grad_share=None):
         boxes = sampled["boxes"]
         N, S = boxes.shape[:2]
         img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(S)
-        x = self.box_pooler.pool(feats, boxes.reshape(-1, 4).contiguous(), img)
+        x = self.box_pooler.pool(feats, boxes.reshape(-1, 4).contiguous(), img,
+                                 grad_share=grad_share)
         logits, deltas = self.box_predictor(self.box_head(x))
         return fast_rcnn_losses(logits, deltas, boxes.reshape(-1, 4), sampled["gt_classes"].reshape(-1),
                                 sampled["gt_boxes"].reshape(-1, 4), sampled["is_valid"].reshape(-1),
                                 self.box2box_transform, self.smooth_l1_beta)
 
-    def _mask_loss(self, feats, sampled, targets):
+    def _mask_loss(self, feats, sampled, targets, grad_share=None):
         """_forward_mask training branch (roi_heads.py:594-600) over the first
         int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
         foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
@@ -209,7 +213,7 @@ class StandardROIHeads(ROIHeads):
             rows = key.sort().values[:R] % B
             boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))
             self.last_mask_rows = R
-        x = self.mask_pooler.pool(feats, boxes.contiguous(), img)
+        x = self.mask_pooler.pool(feats, boxes.contiguous(), img, grad_share=grad_share)
         _, logits = self.mask_head(x)
         return mask_rcnn_loss(logits, boxes, gt_boxes, cls, gm.reshape(N * G, *gm.shape[2:]), mind,
                               fg, self.use_mini_masks)

@@ -180,14 +180,33 @@ class MaskFeatureBranch(Layer):
                                     scope="predictor")
 
     def call(self, features):
+        """res = sum of the scale heads (solo_v2.py:705-721).  On the GPU in
+        inference every head's last GroupNorm writes its ReLU'd, upsampled
+        output straight into the running sum (d2mi_group_norm_nhwc up2 +
+        accumulate): no upsampled copy, no separate add."""
         res = None
         for i, f in enumerate(self.in_features):
             x = features[f]
             if i > 0 and f == self.in_features[-1]:
                 N, H, W, _ = x.shape
                 x = torch.cat([x, coord_channels(N, H, W, x.device)], dim=3)
-            y = self.scale_heads[i](x)
-            res = y if res is None else res + y
+            layers = self.scale_heads[i]._layers
+            convs = [m for m in layers if isinstance(m, Conv2D)]
+            up = any(isinstance(m, Upsample) for m in layers)
+            last = convs[-1]
+            norm = last.normalizer_fn
+            fusable = (res is not None and isinstance(norm, GroupNorm) and norm.fused_ok(x)
+                       and last.act_fn is not None)
+            if not fusable:
+                y = self.scale_heads[i](x)
+                res = y if res is None else res + y
+                continue
+            for conv in convs[:-1]:  # conv -> GN + ReLU (-> up2) chain before the last
+                x = conv(x)
+                if up:
+                    x = x.repeat_interleave(2, 1).repeat_interleave(2, 2)
+            y = last(x, raw=True)
+            norm(y, relu=True, up2=up, accumulate_into=res)
         return self.predictor(res)
 
 

@@ -90,6 +90,18 @@ int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims, const floa
                        int pad_border, int assign, int min_level, int max_level,
                        int canonical_box_size, int canonical_level, const float* grad_out,
                        void* workspace, size_t workspace_bytes, void* stream);
+/* d2mi_roi_align_bwd_ex with accumulate = 1: the maps already hold another
+ * ROI set's gradient of the same features (the box pooler's, when the mask
+ * pooler's backward runs second: lib/modeling/roi_heads/roi_heads.py:545-605
+ * pool the same p2..p5 twice, and TF's AddN sums the two
+ * CropAndResizeGradImage maps); touched pixels become old + new, untouched
+ * ones are left unwritten (no clear, no separate add pass). */
+int d2mi_roi_align_bwd_ex(float* const* grad_feats, const int32_t* dims, const float* scales,
+                          int num_levels, int C, const float* boxes, const int32_t* box_ind,
+                          int R, int out_h, int out_w, int sampling_ratio, int box_mode,
+                          int pad_border, int assign, int min_level, int max_level,
+                          int canonical_box_size, int canonical_level, const float* grad_out,
+                          int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------- NMS
  * Segmented greedy NMS with TF NonMaxSuppressionV3 semantics
@@ -270,6 +282,21 @@ int d2mi_solo_finalize(const float* nms_scores, const int64_t* top_classes,
                        uint8_t* out_masks, float* out_boxes, float* out_scores,
                        int64_t* out_classes, uint8_t* out_valid, void* workspace,
                        size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------- GroupNorm
+ * GroupNorm.call (lib/layers/normalization.py:235-260) on NHWC x [N,H,W,C]:
+ * tf.nn.moments over (H, W, C/G) (two-pass mean / variance), then
+ * y = x * inv + (beta - mean * inv), inv = rsqrt(var + eps) * gamma;
+ * relu: max(y, 0) (the conv's activation after its normalizer,
+ * convolutional.py:251-262); up2: y written to the 2x2 block of the nearest
+ * x2 upsample (out [N,2H,2W,C], wrappers.py:104-116); accumulate: y added to
+ * the output (the SOLOv2 scale-head sum, solo_v2.py:705-721).  C / G % 4 == 0,
+ * C <= 1024, G <= 64, 16-B aligned; workspace from
+ * d2mi_group_norm_workspace_size. */
+size_t d2mi_group_norm_workspace_size(int N, int H, int W, int C, int G);
+int d2mi_group_norm_nhwc(const float* x, int N, int H, int W, int C, int G, const float* gamma,
+                         const float* beta, float eps, int relu, int up2, int accumulate,
+                         float* y, void* workspace, size_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------- conv2d
  * NHWC implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32),

@@ -1086,3 +1086,32 @@ def test_fused_stem_pool_matches_unfused(dev):
         want = stem(x)
     assert got.shape == want.shape == (2, 26, 34, 64)
     assert torch.equal(got, want)
+
+
+def test_roi_align_backward_grad_share_matches_autograd_sum(dev):
+    """Two poolings of the same p2..p5 maps (the box 7x7 and mask 14x14 poolers
+    of a training step) with grad_share: one gradient map set written by the
+    first backward and accumulated into by the second (d2mi_roi_align_bwd_ex
+    accumulate) == autograd's sum of two independent backwards, bit for bit."""
+    rng = np.random.default_rng(45)
+    N, IH, IW, C = 2, 256, 320, 64
+    strides = [4, 8, 16, 32]
+    scales = [1.0 / s for s in strides]
+    feats = [rng.normal(size=(N, IH // s, IW // s, C)).astype(F32) for s in strides]
+    b1, b2 = rand_boxes(rng, 400, IH, IW, 2.0, 300.0), rand_boxes(rng, 64, IH, IW, 8.0, 300.0)
+    i1 = rng.integers(0, N, size=400).astype(np.int32)
+    i2 = rng.integers(0, N, size=64).astype(np.int32)
+    g1 = torch.from_numpy(rng.normal(size=(400, 7, 7, C)).astype(F32)).to(dev)
+    g2 = torch.from_numpy(rng.normal(size=(64, 14, 14, C)).astype(F32)).to(dev)
+    grads = []
+    for share in (None, {}):
+        xs = [torch.from_numpy(f).to(dev).requires_grad_(True) for f in feats]
+        o1 = ops().roi_align(xs, torch.from_numpy(b1).to(dev), torch.from_numpy(i1).to(dev), (7, 7),
+                             scales, 0, True, grad_share=share)
+        o2 = ops().roi_align(xs, torch.from_numpy(b2).to(dev), torch.from_numpy(i2).to(dev),
+                             (14, 14), scales, 0, True, grad_share=share)
+        torch.autograd.backward([o1, o2], [g1, g2])
+        grads.append([x.grad.clone() for x in xs])
+        assert share is None or not share  # the second backward took the maps
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)

@@ -333,3 +333,35 @@ def test_solo_r50_1333x800_geometry(dev):
         assert not a["masks"][n][m:].any()
         bx = a["boxes"][n][:m]
         assert (bx[:, 0] <= bx[:, 2]).all() and (bx[:, 1] <= bx[:, 3]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,G,relu,up2,acc", [(128, 32, True, False, False), (512, 32, True, False, False),
+                                              (128, 32, True, True, True), (256, 32, False, True, False),
+                                              (128, 32, True, False, True)])
+def test_group_norm_hip_vs_float64(dev, C, G, relu, up2, acc):
+    """d2mi_group_norm_nhwc vs the GroupNorm.call formula in float64
+    (normalization.py:235-260: moments over H, W and the group's channels,
+    x * inv + (beta - mean * inv)), with the fused ReLU / nearest-x2 / sum."""
+    from detectron2_tensorflow_amd.layers import ops
+    rng = np.random.default_rng(C + G)
+    N, H, W = 2, 25, 42
+    x = (rng.normal(size=(N, H, W, C)) * 3 + 1).astype(F32)
+    gamma = rng.uniform(0.5, 1.5, size=C).astype(F32)
+    beta = rng.normal(size=C).astype(F32)
+    xr = x.astype(np.float64).reshape(N, H, W, G, C // G)
+    mu = xr.mean(axis=(1, 2, 4), keepdims=True)
+    var = ((xr - mu) ** 2).mean(axis=(1, 2, 4), keepdims=True)
+    inv = 1 / np.sqrt(var + 1e-5) * gamma.reshape(1, 1, 1, G, C // G)
+    want = (xr * inv + (beta.reshape(1, 1, 1, G, C // G) - mu * inv)).reshape(N, H, W, C)
+    if relu:
+        want = np.maximum(want, 0)
+    if up2:
+        want = want.repeat(2, 1).repeat(2, 2)
+    base = rng.normal(size=want.shape).astype(F32) if acc else None
+    if acc:
+        want = want + base
+    out = ops.group_norm(torch.from_numpy(x).to(dev), G, torch.from_numpy(gamma).to(dev),
+                         torch.from_numpy(beta).to(dev), 1e-5, relu, up2,
+                         torch.from_numpy(base).to(dev) if acc else None)
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=2e-5, atol=2e-5)
