@@ -153,7 +153,14 @@ def synthetic_batch(args, device, rank):
     return synthetic_images(args.batch, args.height, args.width, 1000 + rank, device)
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_train_pmc.json")
+def _latest_pmc():
+    """The newest round's committed PMC summary (profiles/rNN_train_pmc.json)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_train_pmc.json")))
+    return files[-1] if files else os.path.join(ROOT, "profiles", "r1_train_pmc.json")
+
+
+PMC_FILE = _latest_pmc()
 
 
 def pmc_traffic(group, mode):
