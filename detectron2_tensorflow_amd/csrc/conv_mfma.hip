@@ -310,8 +310,8 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
-template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT>
-__global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
+template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
   constexpr int NB = DB ? 2 : 1;
@@ -369,7 +369,8 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   // the other set) and a 1-deep prefetch of the weight tile (small and
   // L2-resident): an activation gather has two compute phases to return, one
   // phase (~0.6 us at 2 workgroups/CU) being below its loaded latency.
-  float4 ra[2][RA], rb[RB];
+  // OCC 3 (three workgroups per CU): a 1-deep activation prefetch (fewer VGPRs)
+  float4 ra[OCC >= 3 ? 1 : 2][RA], rb[RB];
   // channel-chunk-major, tap-minor K order: consecutive k-steps read the
   // same 32 channels at neighbouring pixels (the 3x3 taps), which are still
   // in L2 (tap-major order re-fetched them Cin/32 steps later)
@@ -521,11 +522,29 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
         __syncthreads();
         buf ^= 1;
       }
+    } else if constexpr (OCC >= 3) {
+      load_a(kt0, ra[0]);
+      load_b(kt0);
+      store_tile(0, ra[0], rb);
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) {
+          load_b(kt + 1);
+          load_a(kt + 1, ra[0]);
+        }
+        compute(0);
+        __syncthreads();
+        if (more) {
+          store_tile(0, ra[0], rb);
+          __syncthreads();
+        }
+      }
     } else {
       // step(kt): activation set F is free (its k-step is in LDS), set X
       // holds kt + 1.  B(kt+1) is issued before A(kt+2), so the store of
       // k-step kt+1 leaves only A(kt+2) in flight.
-      auto step = [&](int kt, float4 (&F)[RA], const float4 (&X)[RA]) {
+      auto step = [&](int kt, float4 (&F)[RA], const float4 (&X)[RA]) {  // (OCC 2 only)
         if (kt + 1 < kt1) load_b(kt + 1);
         if (kt + 2 < kt1) load_a(kt + 2, F);
         compute(0);
@@ -811,17 +830,28 @@ struct Plan {
 };
 
 // Resident workgroups of the 128-wide conv tiles: 2 per CU.
-static int wg_slots() {
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, cus = 0;
+// Resident workgroups per CU of a plan's kernel: the 128x128 split kernel
+// runs three (168 VGPRs, 48 KiB LDS: conv_mfma_kernel<..., OCC = 3>), the
+// others two.  D2MI_CONV_OCC=2 keeps the 128x128 split kernel at two (A/B).
+static bool occ3_enabled() {
+  static const int on = [] {
+    const char* e = getenv("D2MI_CONV_OCC");
+    return !(e && e[0] == '2');
+  }();
+  return on;
+}
+
+static int wg_slots(int cfg) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;  // MI355X
-    slots = 2 * cus;
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        c <= 0)
+      c = 256;  // MI355X
+    cus = c;
   }
-  return slots;
+  return (cfg == 0 && occ3_enabled() ? 3 : 2) * cus;
 }
 
 // wide_ok: the 128x128 tile may be used -- its kernels only carry the LDS
@@ -835,9 +865,10 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   p.ntiles = nM * nN;
   p.nk = KH * KW * ((Cin + BK - 1) / BK);
   p.splits = 1;
-  // Fewer tiles than 2 workgroups per CU (512) and a long K: split K.
-  if (p.ntiles < 384 && p.nk >= 16) {
-    p.splits = std::min(std::max(1, 512 / p.ntiles), std::min(p.nk / 8, 16));
+  const int G = wg_slots(p.cfg);
+  // Fewer tiles than resident workgroups and a long K: split K.
+  if (4 * p.ntiles < 3 * G && p.nk >= 16) {
+    p.splits = std::min(std::max(1, G / p.ntiles), std::min(p.nk / 8, 16));
   }
   p.kt_per_split = (p.nk + p.splits - 1) / p.splits;
   p.splits = (p.nk + p.kt_per_split - 1) / p.kt_per_split;
@@ -852,8 +883,8 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   p.tail_splits = 1;
   p.tail_kt_per_split = p.nk;
   p.main_m_end = M;
-  const int G = wg_slots();
-  if (p.splits == 1 && p.ntiles > G && p.nk >= 8) {
+  static const char* tail_env = getenv("D2MI_CONV_TAIL");  // "0": no tail split (A/B)
+  if (p.splits == 1 && p.ntiles > G && p.nk >= 8 && !(tail_env && tail_env[0] == '0')) {
     const int full = (p.ntiles / G) * G / nN * nN;
     const int tail = p.ntiles - full;
     if (tail > 0 && 2 * tail <= G) {
@@ -897,6 +928,10 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
 
 template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  if (cfg == 0 && !db && occ3_enabled()) {
+    hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3>), grid, dim3(256), 0, st, a);
+    return;
+  }
   if (cfg == 0) {
     if (db)
       hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
