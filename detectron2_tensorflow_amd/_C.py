@@ -150,14 +150,22 @@ def check(rc, what):
 
 
 def ptr(t):
-    """Device pointer of a tensor (None -> NULL)."""
-    if t is None:
-        return None
-    return c_void_p(t.data_ptr())
+    """Device pointer of a tensor as a plain int (None -> NULL); ctypes
+    converts it for the c_void_p argument without a wrapper object."""
+    return None if t is None else t.data_ptr()
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_of(device=None):
-    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """hipStream_t (as an int) of the current torch stream on ``device``."""
+    if _raw_stream is not None:
+        idx = device.index if isinstance(device, torch.device) else device
+        if idx is None:
+            idx = torch.cuda.current_device()
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def require_device(*tensors):
@@ -175,6 +183,26 @@ def host_array(ctype, values):
 
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+_scratch = {}
+
+
+def scratch(nbytes, device):
+    """A grow-only per-(device, stream) scratch buffer for workspaces that live
+    only inside one C call (split-K partials, reductions): every use is
+    ordered on that stream, so consecutive calls can share it without an
+    allocation each.  Never hand it to anything that outlives the call."""
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None:
+        idx = torch.cuda.current_device()
+    key = (idx, stream_of(idx))
+    buf = _scratch.get(key)
+    n = max(int(nbytes), 1)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=torch.device("cuda", idx))
+        _scratch[key] = buf
+    return buf
 
 
 _ERR_BITS = {1: "box index out of range", 2: "NMS candidate capacity exceeded",

@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 from .. import _C
+from ..utils import host_sync
 
 _DEFAULT_SCALE_CLAMP = math.log(1000.0 / 16)  # lib/modeling/box_regression.py:10
 
@@ -61,10 +62,14 @@ class KernelTimer:
 
 
 def _f32c(t):
+    if t.dtype is torch.float32 and t.is_contiguous():
+        return t
     return t.to(torch.float32).contiguous()
 
 
 def _i32c(t):
+    if t.dtype is torch.int32 and t.is_contiguous():
+        return t
     return t.to(torch.int32).contiguous()
 
 
@@ -372,29 +377,29 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     flags = (1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
     if math_mode == "split" and not presplit:
         flags |= 4
-    wsb = _C.lib().d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
-                                              int(pe))
-    ws = _C.workspace(wsb, x.device) if wsb else None
+    lib = _C.lib()
+    wsb = lib.d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
+                                         int(pe))
+    ws = _C.scratch(wsb, x.device) if wsb else None
+    st = _C.stream_of(x.device)
     if presplit:
         x3 = x_split if x_split is not None else split_bf16x3(x)
         w3 = w_split if w_split is not None else split_bf16x3(w_packed)
     ev = KernelTimer.start()
     if presplit:
-        rc = _C.lib().d2mi_conv2d_nhwc_x3(_C.ptr(x3), _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
-                                          _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
-                                          int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb,
-                                          _C.stream_of(x.device))
+        rc = lib.d2mi_conv2d_nhwc_x3(_C.ptr(x3), _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
+                                     _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
+                                     int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb, st)
     elif relu_gate is not None:
-        rc = _C.lib().d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
-                                             _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,
-                                             H, W, Cin, Cout, KH, KW, int(stride), int(pb),
-                                             int(pe), flags, _C.ptr(ws), wsb,
-                                             _C.stream_of(x.device))
+        rc = lib.d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
+                                        _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,
+                                        H, W, Cin, Cout, KH, KW, int(stride), int(pb),
+                                        int(pe), flags, _C.ptr(ws), wsb, st)
     else:
-        rc = _C.lib().d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
-                                          _C.ptr(topdown), _C.ptr(residual), _C.ptr(y), N, H, W,
-                                          Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
-                                          _C.ptr(ws), wsb, _C.stream_of(x.device))
+        rc = lib.d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
+                                     _C.ptr(topdown), _C.ptr(residual), _C.ptr(y), N, H, W,
+                                     Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
+                                     _C.ptr(ws), wsb, st)
     fl = 2.0 * N * OH * OW * Cout * KH * KW * Cin
     KernelTimer.stop(ev, "conv2d_split" if math_mode == "split" else "conv2d_mfma", fl)
     if KernelTimer.detail and ev is not None:
@@ -422,7 +427,7 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math
     db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
     args = (N, H, W, Cin, Cout, KH, KW, int(stride), int(pb), int(pe))
     wsb = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
-    ws = _C.workspace(wsb, x.device) if wsb else None
+    ws = _C.scratch(wsb, x.device) if wsb else None
     ev = KernelTimer.start()
     flags = 4 if math_mode == "split" else 0
     rc = _C.lib().d2mi_conv2d_wgrad_ex(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
@@ -686,23 +691,30 @@ class _FoldManyFn(torch.autograd.Function):
     def forward(ctx, spec, *ts):
         n = len(spec)
         dev = ts[0].device
-        tab = np.zeros(n, _FOLD_DT)
-        outs, saved = [], []
+        rows, outs = [], []
         fwd = bwd = cob = part = 0
         table, chunks = _fold_table("fwd", n, dev)
+        ws_ = [ts[6 * i] for i in range(n)]
+        for w in ws_:
+            if not (w.is_contiguous() and w.dtype == torch.float32 and w.device == dev):
+                raise ValueError("fold_frozen_bn_many: contiguous f32 weights on one device")
+        # the outputs are views of three flat buffers (3 allocations, not 3n)
+        sizes = [w.numel() for w in ws_]
+        couts = [w.shape[3] for w in ws_]
+        w_effs = torch.empty(sum(sizes), dtype=torch.float32, device=dev).split(sizes)
+        b_effs = torch.empty(sum(couts), dtype=torch.float32, device=dev).split(couts)
+        psz = [sz if sp[1] else 0 for sz, sp in zip(sizes, spec)]
+        packs = torch.empty(max(sum(psz), 1), dtype=torch.float32, device=dev).split(psz)
         for i, (eps, want_packed) in enumerate(spec):
             w, bias, gamma, beta, mean, var = ts[6 * i:6 * i + 6]
             KH, KW, Cin, Cout = w.shape
-            if not (w.is_contiguous() and w.dtype == torch.float32 and w.device == dev):
-                raise ValueError("fold_frozen_bn_many: contiguous f32 weights on one device")
-            w_eff = torch.empty_like(w)
-            b_eff = torch.empty((Cout,), dtype=torch.float32, device=dev)
-            packed = (torch.empty((KH, KW, Cout, Cin), dtype=torch.float32, device=dev)
-                      if want_packed else None)
+            w_eff = w_effs[i].view(KH, KW, Cin, Cout)
+            b_eff = b_effs[i]
+            packed = packs[i].view(KH, KW, Cout, Cin) if want_packed else None
             nco, taps = -(-Cout // 64), KH * KW
-            tab[i] = (_addr(w), _addr(bias), _addr(gamma), _addr(beta),
-                      _addr(mean), _addr(var), _addr(w_eff), _addr(packed), _addr(b_eff),
-                      0, 0, 0, 0, 0, 0, eps, taps, Cin, Cout, fwd, bwd, cob, 0, part)
+            rows.append((_addr(w), _addr(bias), _addr(gamma), _addr(beta),
+                         _addr(mean), _addr(var), _addr(w_eff), _addr(packed), _addr(b_eff),
+                         0, 0, 0, 0, 0, 0, eps, taps, Cin, Cout, fwd, bwd, cob, 0, part))
             fwd += nco * -(-Cin // 64) * taps
             bwd += nco * chunks
             cob += Cout
@@ -710,6 +722,7 @@ class _FoldManyFn(torch.autograd.Function):
             outs += [w_eff, b_eff, packed]
             if packed is not None:
                 ctx.mark_non_differentiable(packed)
+        tab = np.array(rows, dtype=_FOLD_DT)
         rc = _C.lib().d2mi_fold_frozen_bn_many(_C.ptr(table.upload(tab)), n, fwd,
                                                _C.stream_of(dev))
         _C.check(rc, "d2mi_fold_frozen_bn_many")
@@ -871,7 +884,7 @@ def solo_inference(cate_logits, kernels, mask_features, strides, out_hw, score_t
                              N, K, float(score_thresh), _C.ptr(probs), _C.ptr(live_cells),
                              _C.ptr(live_row), _C.ptr(live_count), st)
     _C.check(rc, "d2mi_solo_cells")
-    counts = [int(c) for c in live_count.cpu()]  # the one host synchronisation
+    counts = host_sync.read_ints(live_count)  # the one host synchronisation
     offs = [0]
     for c in counts:
         offs.append(offs[-1] + c)

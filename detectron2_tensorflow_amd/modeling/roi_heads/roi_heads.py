@@ -11,6 +11,7 @@ import torch
 
 from ...layers import ShapeSpec
 from ...structures import BoxList
+from ...utils import host_sync
 from ...utils.registry import Registry
 from ..box_regression import Box2BoxTransform
 from ..poolers import ROIPooler
@@ -206,7 +207,7 @@ class StandardROIHeads(ROIHeads):
             # host read of the foreground count; the rows are gathered fg-first
             # (image order kept) and padded to a multiple of MASK_ROW_BUCKET
             # with masked-out rows, which bounds the number of distinct shapes.
-            nfg = int(fg.sum())
+            nfg = host_sync.read_ints(fg.sum())[0]
             B = fg.numel()
             R = min(B, max(self.MASK_ROW_BUCKET, -(-nfg // self.MASK_ROW_BUCKET) * self.MASK_ROW_BUCKET))
             key = (~fg).to(torch.int64) * B + torch.arange(B, device=dev)

@@ -3,8 +3,11 @@
 
 Each step starts on an idle device: host_ms = time for step() to return
 (Python + launches, plus any host syncs inside the step), wall_ms = time
-until the device has finished it.  host_ms close to wall_ms means the step is
-launch-bound, not kernel-bound.
+until the device has finished it.  blocked_in_syncs_ms = time the host sat
+in the step's synchronising reads (utils/host_sync.py: the mask branch's
+foreground count), waiting for the device to catch up; host_busy_ms =
+host_ms - blocked: the host's own enqueue work.  host_busy close to wall_ms
+means the step is launch-bound, not kernel-bound.
 
 usage: python tools/host_time.py [--mode train|infer] [--steps 5]
 """
@@ -42,12 +45,14 @@ def main():
     else:
         step = lambda: model.inference(batch)
         ctx = torch.no_grad
+    from detectron2_tensorflow_amd.utils import host_sync
     with ctx():
         for _ in range(3):
             step()
         torch.cuda.synchronize()
-        hs, ws = [], []
+        hs, ws, bs = [], [], []
         for _ in range(a.steps):
+            host_sync.reset()
             t0 = time.perf_counter()
             step()
             t1 = time.perf_counter()
@@ -55,10 +60,12 @@ def main():
             t2 = time.perf_counter()
             hs.append((t1 - t0) * 1e3)
             ws.append((t2 - t0) * 1e3)
-    hs.sort()
-    ws.sort()
-    print(f"host_ms median {hs[len(hs) // 2]:.2f}  wall_ms median {ws[len(ws) // 2]:.2f}  "
-          f"(min {hs[0]:.2f} / {ws[0]:.2f})")
+            bs.append(host_sync.blocked_s * 1e3)
+    med = lambda v: sorted(v)[len(v) // 2]
+    busy = [h - b for h, b in zip(hs, bs)]
+    print(f"host_ms median {med(hs):.2f}  blocked_in_syncs_ms {med(bs):.2f}  "
+          f"host_busy_ms {med(busy):.2f}  wall_ms median {med(ws):.2f}  "
+          f"host_busy/wall {med(busy) / med(ws):.2f}")
 
 
 if __name__ == "__main__":
