@@ -318,6 +318,11 @@ def split_bf16x3(x):
     return out
 
 
+# workspace sizes per conv / wgrad shape (pure functions of the shape and the
+# device's CU count: one ctypes query per distinct shape)
+_CONV_WS, _WGRAD_WS = {}, {}
+
+
 def _presplit_ok(x, Cin):
     return Cin % 8 == 0 and 6 * x.numel() < 2 ** 31
 
@@ -378,8 +383,11 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     if math_mode == "split" and not presplit:
         flags |= 4
     lib = _C.lib()
-    wsb = lib.d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
-                                         int(pe))
+    wkey = (N, H, W, Cin, Cout, KH, KW, stride, pb, pe)
+    wsb = _CONV_WS.get(wkey)
+    if wsb is None:
+        wsb = _CONV_WS[wkey] = lib.d2mi_conv2d_workspace_size(N, H, W, Cin, Cout, KH, KW,
+                                                              int(stride), int(pb), int(pe))
     ws = _C.scratch(wsb, x.device) if wsb else None
     st = _C.stream_of(x.device)
     if presplit:
@@ -426,7 +434,9 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math
     dw = torch.empty((KH, KW, Cin, Cout), dtype=torch.float32, device=x.device)
     db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
     args = (N, H, W, Cin, Cout, KH, KW, int(stride), int(pb), int(pe))
-    wsb = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
+    wsb = _WGRAD_WS.get(args)
+    if wsb is None:
+        wsb = _WGRAD_WS[args] = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
     ws = _C.scratch(wsb, x.device) if wsb else None
     ev = KernelTimer.start()
     flags = 4 if math_mode == "split" else 0
