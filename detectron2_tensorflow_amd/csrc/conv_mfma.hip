@@ -49,6 +49,7 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32, LDSP = 36, LDSB = 32;
+constexpr int kMaxConvLevels = 6;
 
 // bf16 LDS images: 64-B rows (32 bf16 = one BK step) whose four 16-B chunks
 // are XOR-swizzled by (row >> 2) & 3.  ds_read_b128 phases (lanes
@@ -114,33 +115,96 @@ struct ConvArgs {
   const uint16_t* w3;
   int x_plane_bytes, w_plane_bytes;
   int tdH, tdW;
+  int dbg;  // ablation bits (D2MI_CONV_DBG, timing experiments only; 0 in production)
+  // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
+  // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
+  // input / output / gate maps.  The kernel swaps them into the fields above
+  // at start, so everything after that is the single-level code.
+  int nlev;
+  const float* lv_x[kMaxConvLevels];
+  float* lv_y[kMaxConvLevels];
+  const float* lv_gate[kMaxConvLevels];
+  int lv_H[kMaxConvLevels], lv_W[kMaxConvLevels], lv_OH[kMaxConvLevels], lv_OW[kMaxConvLevels];
+  int lv_N[kMaxConvLevels], lv_xbytes[kMaxConvLevels], lv_tile0[kMaxConvLevels + 1];
+  int lv_moff[kMaxConvLevels + 1];  // first row of each level in the split-K slab; [6] = total
 };
+
+// The per-level part of a launch's arguments: a single-level launch takes
+// it from ConvArgs; a multi-level one (nlev > 0) from the tile's level, whose
+// tile index it makes level-local.  A small struct of scalars (the kernels
+// keep it in SGPRs; swapping fields of the whole ConvArgs put it in scratch).
+struct Geo {
+  const float* x;
+  float* y;
+  const float* gate;
+  int N, H, W, OH, OW, M, m_end, x_bytes;
+  // split-K partial rows: slab stride (rows per split) and the row that maps
+  // to slab row 0 (single level: m_base; multi-level: minus the level's row
+  // offset in the concatenated slab)
+  int pstride, prow0;
+};
+
+__device__ __forceinline__ Geo geo_of(const ConvArgs& a) {
+  return Geo{a.x, a.y, a.gate, a.N, a.H, a.W, a.OH, a.OW, a.M, a.m_end, a.x_bytes,
+             a.m_end - a.m_base, a.m_base};
+}
+
+__device__ __forceinline__ Geo select_level(const ConvArgs& a, int& tile) {
+  Geo r = geo_of(a);
+  if (a.nlev == 0) return r;
+  // unrolled over the level slots (constant indices: a runtime index into the
+  // by-value kernel argument would copy it to scratch)
+  int base = 0;
+#pragma unroll
+  for (int l = 0; l < kMaxConvLevels; ++l) {
+    if (l < a.nlev && tile >= a.lv_tile0[l]) {
+      base = a.lv_tile0[l];
+      r.x = a.lv_x[l];
+      r.y = a.lv_y[l];
+      r.gate = a.lv_gate[l];
+      r.N = a.lv_N[l];
+      r.H = a.lv_H[l];
+      r.W = a.lv_W[l];
+      r.OH = a.lv_OH[l];
+      r.OW = a.lv_OW[l];
+      r.x_bytes = a.lv_xbytes[l];
+      r.prow0 = -a.lv_moff[l];
+    }
+  }
+  tile -= base;
+  r.M = r.N * r.OH * r.OW;
+  r.m_end = r.M;
+  r.pstride = a.lv_moff[a.nlev > 0 ? kMaxConvLevels : 0];  // total rows (slot kMaxConvLevels)
+  return r;
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-__device__ __forceinline__ float epilogue(const ConvArgs& a, float acc, int m, int co) {
+__device__ __forceinline__ float epilogue(const ConvArgs& a, const Geo& g, float acc, int m,
+                                          int co) {
   float v = acc + (a.bias ? a.bias[co] : 0.f);
   if ((a.flags & kRelu) && !(a.flags & kReluAfterResidual)) v = fmaxf(v, 0.f);
   if (a.topdown) {
-    const int n = m / (a.OH * a.OW);
-    const int rem = m - n * a.OH * a.OW;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int n = m / (g.OH * g.OW);
+    const int rem = m - n * g.OH * g.OW;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
     v = v + a.topdown[(((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout + co];
   }
   if (a.residual) v = v + a.residual[(size_t)m * a.Cout + co];
   if ((a.flags & kRelu) && (a.flags & kReluAfterResidual)) v = fmaxf(v, 0.f);
-  if (a.gate && !(a.gate[(size_t)m * a.Cout + co] > 0.f)) v = 0.f;
+  if (g.gate && !(g.gate[(size_t)m * a.Cout + co] > 0.f)) v = 0.f;
   return v;
 }
 
 // Epilogue shared by the conv kernels: bias, ReLU, top-down / residual adds
 // (or the split-K partial slab), written straight from the MFMA accumulators.
 template <int WN, int TM, int TN>
-__device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)[TM][TN], int m0,
+__device__ __forceinline__ void store_outputs(const ConvArgs& a, const Geo& g,
+                                              floatx16 (&acc)[TM][TN], int m0,
                                               int n0, int wr, int wc, int lane, int split) {
   const int li = lane & 31, lh = lane >> 5;
   // C/D map for 32x32: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const bool simple = a.splits == 1 && !a.topdown && !a.residual && !a.gate;
+  const bool simple = a.splits == 1 && !a.topdown && !a.residual && !g.gate;
   const bool relu = (a.flags & kRelu) != 0;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -151,11 +215,11 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
     for (int i = 0; i < TM; ++i) {
       const int mb = m0 + (wr * TM + i) * 32 + 4 * lh;
       if (simple) {  // bias (+ relu) only: the common case, no per-element branches
-        float* yp = a.y + (size_t)mb * a.Cout + co;
+        float* yp = g.y + (size_t)mb * a.Cout + co;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int dm = (r & 3) + 8 * (r >> 2);
-          if (mb + dm < a.M) {
+          if (mb + dm < g.M) {
             float v = acc[i][j][r] + bv;
             yp[(size_t)dm * a.Cout] = relu ? fmaxf(v, 0.f) : v;
           }
@@ -164,11 +228,11 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
       }
       if (a.splits > 1) {
         float* pp =
-            a.partial + ((size_t)split * (a.m_end - a.m_base) + (mb - a.m_base)) * a.Cout + co;
+            a.partial + ((size_t)split * g.pstride + (mb - g.prow0)) * a.Cout + co;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int dm = (r & 3) + 8 * (r >> 2);
-          if (mb + dm < a.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
+          if (mb + dm < g.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
         }
         continue;
       }
@@ -178,11 +242,11 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
       // pixel coordinates of row mb, then stepped (dm < 32): no per-element division
       int tn = 0, toh = 0, tow = 0, last = 0;
       if (a.topdown) {
-        const int mm = min(mb, a.M - 1);
-        tn = mm / (a.OH * a.OW);
-        const int rem = mm - tn * a.OH * a.OW;
-        toh = rem / a.OW;
-        tow = rem - toh * a.OW;
+        const int mm = min(mb, g.M - 1);
+        tn = mm / (g.OH * g.OW);
+        const int rem = mm - tn * g.OH * g.OW;
+        toh = rem / g.OW;
+        tow = rem - toh * g.OW;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -192,12 +256,12 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
         if (a.topdown) {  // advance (n, oh, ow) from row mb + last to mb + dm
           tow += dm - last;
           last = dm;
-          while (tow >= a.OW) {
-            tow -= a.OW;
-            if (++toh == a.OH) { toh = 0; ++tn; }
+          while (tow >= g.OW) {
+            tow -= g.OW;
+            if (++toh == g.OH) { toh = 0; ++tn; }
           }
         }
-        if (m < a.M) {
+        if (m < g.M) {
           if (a.residual) v = a.residual[(size_t)m * a.Cout + co];
           if (a.topdown)
             v = v + a.topdown[(((size_t)tn * a.tdH + (toh >> 1)) * a.tdW + (tow >> 1)) * a.Cout +
@@ -209,18 +273,18 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mb + (r & 3) + 8 * (r >> 2);
-        if (m >= a.M) continue;
+        if (m >= g.M) continue;
         float v = acc[i][j][r] + bv;
         if (relu && !relu_after) v = fmaxf(v, 0.f);
         // epilogue() order: conv + bias, (+ top-down) (+ residual), gate last
         // (the gate comes with Cout % 4 == 0 dgrads: normally the LDS epilogue)
-        if ((a.topdown && a.residual) || a.gate) {
-          v = epilogue(a, acc[i][j][r], m, co);
+        if ((a.topdown && a.residual) || g.gate) {
+          v = epilogue(a, g, acc[i][j][r], m, co);
         } else {
           v = v + add[r];
           if (relu && relu_after) v = fmaxf(v, 0.f);
         }
-        a.y[(size_t)m * a.Cout + co] = v;
+        g.y[(size_t)m * a.Cout + co] = v;
       }
     }
   }
@@ -234,7 +298,8 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, floatx16 (&acc)
 // transpose).  Same arithmetic order as epilogue(); split-K partials are
 // written raw.  smem: >= 32 * (BN + 4) floats of the kernel's LDS.
 template <int WM, int WN, int TM, int TN, int NT = 256>
-__device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&acc)[TM][TN],
+__device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& g,
+                                                  floatx16 (&acc)[TM][TN],
                                                   int m0, int n0, int wr, int wc, int lane,
                                                   int split, float* smem) {
   constexpr int BN = WN * TN * 32;
@@ -244,8 +309,8 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
   const int tid = threadIdx.x;
   const int li = lane & 31, lh = lane >> 5;
   const bool part = a.splits > 1;
-  float* const dst = part ? a.partial + (size_t)split * (a.m_end - a.m_base) * a.Cout : a.y;
-  const int mrow0 = part ? a.m_base : 0;
+  float* const dst = part ? a.partial + (size_t)split * g.pstride * a.Cout : g.y;
+  const int mrow0 = part ? g.prow0 : 0;
   const bool relu = (a.flags & kRelu) != 0, relu_after = (a.flags & kReluAfterResidual) != 0;
   __syncthreads();  // the main loop's last LDS reads are complete
 #pragma unroll
@@ -257,14 +322,14 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
       const int row = idx / F4, c4 = idx - row * F4;
       const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
       res[q] = gt[q] = td[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!part && m < a.M && co < a.Cout) {
+      if (!part && m < g.M && co < a.Cout) {
         const size_t o = (size_t)m * a.Cout + co;
         if (a.residual) res[q] = ld4(a.residual + o);
-        if (a.gate) gt[q] = ld4(a.gate + o);
+        if (g.gate) gt[q] = ld4(g.gate + o);
         if (a.topdown) {
-          const int n = m / (a.OH * a.OW);
-          const int rem = m - n * a.OH * a.OW;
-          const int oh = rem / a.OW, ow = rem - oh * a.OW;
+          const int n = m / (g.OH * g.OW);
+          const int rem = m - n * g.OH * g.OW;
+          const int oh = rem / g.OW, ow = rem - oh * g.OW;
           td[q] = ld4(a.topdown + (((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout +
                       co);
         }
@@ -283,7 +348,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
       const int idx = tid + NT * q;
       const int row = idx / F4, c4 = idx - row * F4;
       const int m = m0 + s * 32 + row, co = n0 + c4 * 4;
-      if (m >= a.M || co >= a.Cout) continue;
+      if (m >= g.M || co >= a.Cout) continue;
       float4 v = *reinterpret_cast<const float4*>(&smem[row * LS + c4 * 4]);
       if (!part) {
         float* vv = reinterpret_cast<float*>(&v);
@@ -297,7 +362,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
           if (a.topdown) x = x + tt[e];
           if (a.residual) x = x + rr[e];
           if (relu && relu_after) x = fmaxf(x, 0.f);
-          if (a.gate && !(gg[e] > 0.f)) x = 0.f;
+          if (g.gate && !(gg[e] > 0.f)) x = 0.f;
           vv[e] = x;
         }
       }
@@ -310,7 +375,7 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, floatx16 (&
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
-template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2>
+template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false>
 __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
@@ -326,8 +391,9 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
   const int orig = blockIdx.x;
   const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  const int tile =
+  int tile =
       a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const Geo g = ML ? select_level(a, tile) : geo_of(a);  // ML: a multi-level launch
   const int mt = tile / a.nN, nt = tile - mt * a.nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int split = blockIdx.y;
@@ -349,17 +415,17 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
   for (int p = 0; p < RA; ++p) {
     const int m = m0 + srow + 32 * p;
-    const int mm = m < a.M ? m : 0;
-    const int n = mm / (a.OH * a.OW);
-    const int rem = mm - n * a.OH * a.OW;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int mm = m < g.M ? m : 0;
+    const int n = mm / (g.OH * g.OW);
+    const int rem = mm - n * g.OH * g.OW;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
     const int ihv = oh * a.stride - a.pad;
-    ih0[p] = m < a.M ? ihv : -(1 << 29);
+    ih0[p] = m < g.M ? ihv : -(1 << 29);
     iw0[p] = ow * a.stride - a.pad;
-    base[p] = ((n * a.H + ihv) * a.W + iw0[p]) * a.Cin + schunk;
+    base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + schunk;
   }
   const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.x), 0, a.x_bytes, 0x00020000);
+      const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
   constexpr uint32_t kOOB = 0x80000000u;
@@ -381,12 +447,12 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
     const int cc = chunk * BK;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const bool cok = cc + schunk < a.Cin;
-    const int toff = (kh * a.W + kw) * a.Cin + cc;
+    const int toff = (kh * g.W + kw) * a.Cin + cc;
 #pragma unroll
     for (int p = 0; p < RA; ++p) {
       // bitwise &: no short-circuit branches around the loads
-      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)a.H) &
-                      ((unsigned)(iw0[p] + kw) < (unsigned)a.W);
+      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
+                      ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
       const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
       la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
     }
@@ -527,16 +593,17 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
       load_b(kt0);
       store_tile(0, ra[0], rb);
       __syncthreads();
+      const int dbg = a.dbg;
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (more) {
+        if (more && !(dbg & 1)) {
           load_b(kt + 1);
           load_a(kt + 1, ra[0]);
         }
-        compute(0);
+        if (!(dbg & 4)) compute(0);
         __syncthreads();
         if (more) {
-          store_tile(0, ra[0], rb);
+          if (!(dbg & 2)) store_tile(0, ra[0], rb);
           __syncthreads();
         }
       }
@@ -566,10 +633,11 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
+  if (a.dbg & 8) return;
   if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
-    store_outputs_lds<WM, WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split, &As[0][0]);
+    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, &As[0][0]);
   else
-    store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
 }
 
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
@@ -579,6 +647,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 // one 16-B buffer load per (row, plane).  Requires Cin % 8 == 0.
 template <int WM, int WN, int TM, int TN, bool DB>
 __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
+  const Geo g = geo_of(a);
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int PA = (BM * 4 + 255) / 256, PB = (BN * 4 + 255) / 256;
   constexpr int NB = DB ? 2 : 1;
@@ -605,14 +674,14 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
 #pragma unroll
   for (int p = 0; p < PA; ++p) {
     const int m = m0 + r4 + 64 * p;
-    const int mm = m < a.M ? m : 0;
-    const int n = mm / (a.OH * a.OW);
-    const int rem = mm - n * a.OH * a.OW;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int mm = m < g.M ? m : 0;
+    const int n = mm / (g.OH * g.OW);
+    const int rem = mm - n * g.OH * g.OW;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
     const int ihv = oh * a.stride - a.pad;
-    ih0[p] = m < a.M ? ihv : -(1 << 29);
+    ih0[p] = m < g.M ? ihv : -(1 << 29);
     iw0[p] = ow * a.stride - a.pad;
-    base[p] = ((n * a.H + ihv) * a.W + iw0[p]) * a.Cin + c8;
+    base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + c8;
   }
   __amdgpu_buffer_rsrc_t xr[3], wr3[3];
 #pragma unroll
@@ -637,11 +706,11 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
     const int cc = chunk * BK;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const bool cok = cc + c8 < a.Cin;
-    const int toff = (kh * a.W + kw) * a.Cin + cc;
+    const int toff = (kh * g.W + kw) * a.Cin + cc;
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
-      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)a.H) &
-                      ((unsigned)(iw0[p] + kw) < (unsigned)a.W);
+      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
+                      ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
       const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 2u : kOOB;
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
@@ -732,10 +801,10 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
     }
   }
   if (WN * TN * 32 == 128 || a.lds_epi)
-    store_outputs_lds<WM, WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split,
+    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split,
                                       reinterpret_cast<float*>(&As[0][0]));
   else
-    store_outputs<WN, TM, TN>(a, acc, m0, n0, wr, wc, lane, split);
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
 }
 
 // x [n] f32 -> [3][n] bf16 planes (h, m, l of the exact truncation split).
@@ -752,6 +821,7 @@ __global__ void split3_kernel(const float4* __restrict__ x, int64_t n4, uint2* _
 
 // Fixed-order split-K reduction + epilogue (deterministic).
 __global__ void splitk_reduce_kernel(ConvArgs a) {
+  const Geo g = geo_of(a);
   const int64_t total = (int64_t)(a.m_end - a.m_base) * a.Cout;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -759,12 +829,13 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
     for (int s = 0; s < a.splits; ++s) acc += a.partial[(size_t)s * total + i];
     const int ml = (int)(i / a.Cout), co = (int)(i - (int64_t)ml * a.Cout);
     const int m = a.m_base + ml;
-    a.y[(size_t)m * a.Cout + co] = epilogue(a, acc, m, co);
+    a.y[(size_t)m * a.Cout + co] = epilogue(a, g, acc, m, co);
   }
 }
 
 // float4 form (Cout % 4 == 0, 16-B aligned partial / y): same split order.
 __global__ void splitk_reduce4_kernel(ConvArgs a) {
+  const Geo g = geo_of(a);
   const int64_t total = (int64_t)(a.m_end - a.m_base) * a.Cout;
   const int64_t total4 = total / 4;
   const float4* p4 = reinterpret_cast<const float4*>(a.partial);
@@ -783,11 +854,45 @@ __global__ void splitk_reduce4_kernel(ConvArgs a) {
     const int ml = (int)(e / a.Cout), co = (int)(e - (int64_t)ml * a.Cout);
     const int m = a.m_base + ml;
     float4 o;
-    o.x = epilogue(a, acc.x, m, co);
-    o.y = epilogue(a, acc.y, m, co + 1);
-    o.z = epilogue(a, acc.z, m, co + 2);
-    o.w = epilogue(a, acc.w, m, co + 3);
+    o.x = epilogue(a, g, acc.x, m, co);
+    o.y = epilogue(a, g, acc.y, m, co + 1);
+    o.z = epilogue(a, g, acc.z, m, co + 2);
+    o.w = epilogue(a, g, acc.w, m, co + 3);
     *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
+  }
+}
+
+// Multi-level split-K: rows of the concatenated slab -> (level, row), fixed
+// split order, + bias (+ ReLU); float4 over channels (Cout % 4 == 0).
+__global__ void splitk_reduce_levels_kernel(ConvArgs a) {
+  const int C4 = a.Cout / 4;
+  const int rows = a.lv_moff[kMaxConvLevels];
+  const int64_t total = (int64_t)rows * C4;
+  const bool relu = (a.flags & kRelu) != 0;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / C4), c = (int)(e - (int64_t)r * C4) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < a.splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(a.partial + ((size_t)sp * rows + r) * a.Cout + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (a.bias) {
+      acc.x += a.bias[c]; acc.y += a.bias[c + 1]; acc.z += a.bias[c + 2]; acc.w += a.bias[c + 3];
+    }
+    if (relu) {
+      acc.x = fmaxf(acc.x, 0.f); acc.y = fmaxf(acc.y, 0.f);
+      acc.z = fmaxf(acc.z, 0.f); acc.w = fmaxf(acc.w, 0.f);
+    }
+    float* y = a.lv_y[0];
+    int m = r;
+#pragma unroll
+    for (int l = 1; l < kMaxConvLevels; ++l)
+      if (l < a.nlev && r >= a.lv_moff[l]) {
+        y = a.lv_y[l];
+        m = r - a.lv_moff[l];
+      }
+    *reinterpret_cast<float4*>(y + (size_t)m * a.Cout + c) = acc;
   }
 }
 
@@ -944,6 +1049,25 @@ static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvA
   }
 }
 
+// Multi-level launches (ConvArgs::nlev > 0): no split-K, single-buffered.
+template <bool SPLIT>
+static void launch_conv_levels(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  if (cfg == 0) {
+    if (occ3_enabled())
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3, true>), grid, dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 2, true>), grid, dim3(256), 0,
+                         st, a);
+  } else if (cfg == 1) {
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT, 2, true>), grid, dim3(256), 0, st,
+                       a);
+  } else {
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT, 2, true>), grid, dim3(256), 0, st,
+                       a);
+  }
+}
+
 static void launch_x3(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
   if (cfg == 0) {
     if (db)
@@ -1010,6 +1134,10 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     static const char* off = getenv("D2MI_CONV_LDS_EPI");  // "0": register epilogue (A/B)
     a.lds_epi = Cout % 4 == 0 && al16(y) && al16(residual) && al16(gate) && al16(topdown) &&
                 al16(workspace) && !(off && off[0] == '0');
+  }
+  {
+    static const char* dbg = getenv("D2MI_CONV_DBG");
+    a.dbg = dbg ? atoi(dbg) : 0;
   }
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
@@ -1159,6 +1287,145 @@ extern "C" int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const flo
   D2MI_REQUIRE(act == 0 || act == 1, "act must be 0 (none) or 1 (relu)");
   return d2mi_conv2d_nhwc_ex(x, w_packed, bias, topdown, residual, y, N, H, W, Cin, Cout, KH, KW,
                              stride, pad_beg, pad_end, act ? kRelu : 0, nullptr, 0, stream);
+}
+
+// Split-K plan of a multi-level launch: the single-level rule on the total
+// tile count (Cout % 4 == 0 for the level-aware reduce).
+static int levels_splits(const int32_t* dims, int nlev, int Cin, int Cout, int KH, int KW,
+                         int stride, int pad_beg, int pad_end, int64_t* rows, int* ntiles) {
+  const Plan p0 = make_plan(1, Cout, KH, KW, Cin, Cout % 4 == 0);
+  const int nN = (Cout + p0.BN - 1) / p0.BN;
+  int64_t r = 0;
+  int t = 0;
+  for (int l = 0; l < nlev; ++l) {
+    int OH = 0, OW = 0;
+    conv_dims(dims[3 * l + 1], dims[3 * l + 2], KH, KW, stride, pad_beg, pad_end, OH, OW);
+    const int64_t M = (int64_t)dims[3 * l] * OH * OW;
+    r += M;
+    t += (int)((M + p0.BM - 1) / p0.BM) * nN;
+  }
+  *rows = r;
+  *ntiles = t;
+  const int G = wg_slots(p0.cfg);
+  const int nk = KH * KW * ((Cin + BK - 1) / BK);
+  if (Cout % 4 || !(4 * t < 3 * G && nk >= 16)) return 1;
+  const int S = std::min(std::max(1, G / std::max(t, 1)), std::min(nk / 8, 16));
+  const int kps = (nk + S - 1) / S;
+  return (nk + kps - 1) / kps;
+}
+
+extern "C" size_t d2mi_conv2d_levels_workspace_size(const int32_t* dims, int nlev, int Cin,
+                                                    int Cout, int KH, int KW, int stride,
+                                                    int pad_beg, int pad_end) {
+  if (nlev < 1 || nlev > kMaxConvLevels) return 0;
+  int64_t rows;
+  int t;
+  const int S = levels_splits(dims, nlev, Cin, Cout, KH, KW, stride, pad_beg, pad_end, &rows, &t);
+  return S > 1 ? (size_t)S * rows * Cout * sizeof(float) : 0;
+}
+
+extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* dims, int nlev,
+                                       const float* w_packed, const float* bias, float* const* ys,
+                                       int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
+                                       int pad_end, int flags, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(nlev >= 1 && nlev <= kMaxConvLevels, "nlev=%d out of [1,%d]", nlev, kMaxConvLevels);
+  D2MI_REQUIRE(Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0, "bad conv shape");
+  D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
+  D2MI_REQUIRE((flags & ~(kRelu | kSplit3)) == 0,
+               "multi-level conv flags: bit0 relu, bit2 split-bf16 MFMA products");
+  D2MI_REQUIRE(((uintptr_t)w_packed & 15) == 0, "w must be 16-byte aligned");
+  D2MI_REQUIRE((int64_t)KH * KW * Cin * Cout * sizeof(float) < (1ll << 31),
+               "conv weights must be < 2 GiB");
+  ConvArgs a = {};
+  a.w = w_packed;
+  a.w_bytes = (int)((int64_t)KH * KW * Cin * Cout * 4);
+  a.bias = bias;
+  a.Cin = Cin;
+  a.Cout = Cout;
+  a.KH = KH;
+  a.KW = KW;
+  a.stride = stride;
+  a.pad = pad_beg;
+  a.flags = flags;
+  a.nlev = nlev;
+  bool al = (Cout % 4) == 0;
+  int64_t Mtot = 0;
+  for (int l = 0; l < nlev; ++l) {
+    const int N = dims[3 * l], H = dims[3 * l + 1], W = dims[3 * l + 2];
+    int OH, OW;
+    D2MI_REQUIRE(N > 0 && H > 0 && W > 0 &&
+                     conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH, OW) == 0,
+                 "level %d: bad or empty conv geometry", l);
+    D2MI_REQUIRE((int64_t)N * H * W * Cin * 4 < (1ll << 31), "level %d input must be < 2 GiB", l);
+    D2MI_REQUIRE(((uintptr_t)xs[l] & 15) == 0, "level %d input must be 16-byte aligned", l);
+    al = al && ((uintptr_t)ys[l] & 15) == 0;
+    a.lv_x[l] = xs[l];
+    a.lv_y[l] = ys[l];
+    a.lv_gate[l] = nullptr;
+    a.lv_N[l] = N;
+    a.lv_H[l] = H;
+    a.lv_W[l] = W;
+    a.lv_OH[l] = OH;
+    a.lv_OW[l] = OW;
+    a.lv_xbytes[l] = (int)((int64_t)N * H * W * Cin * 4);
+    Mtot += (int64_t)N * OH * OW;
+  }
+  a.lds_epi = al;
+  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al);
+  a.nN = (Cout + p.BN - 1) / p.BN;
+  int t = 0;
+  for (int l = 0; l < nlev; ++l) {
+    a.lv_tile0[l] = t;
+    t += (a.lv_N[l] * a.lv_OH[l] * a.lv_OW[l] + p.BM - 1) / p.BM * a.nN;
+  }
+  a.lv_tile0[nlev] = t;
+  a.ntiles = t;
+  a.tile_base = 0;
+  a.nk = KH * KW * ((Cin + BK - 1) / BK);
+  {
+    int64_t rows;
+    int tt;
+    int S = levels_splits(dims, nlev, Cin, Cout, KH, KW, stride, pad_beg, pad_end, &rows, &tt);
+    if (S > 1 && (workspace == nullptr || workspace_bytes < (size_t)S * rows * Cout * 4 ||
+                  ((uintptr_t)workspace & 15) != 0 || !al))
+      S = 1;  // no (usable) workspace: one pass per tile
+    a.splits = S;
+    a.kt_per_split = (a.nk + S - 1) / S;
+    a.partial = S > 1 ? (float*)workspace : nullptr;
+    int64_t off = 0;
+    for (int l = 0; l <= kMaxConvLevels; ++l) {
+      a.lv_moff[l] = (int)off;
+      if (l < nlev) off += (int64_t)a.lv_N[l] * a.lv_OH[l] * a.lv_OW[l];
+    }
+    for (int l = nlev; l <= kMaxConvLevels; ++l) a.lv_moff[l] = (int)rows;
+  }
+  a.cchunks = (Cin + BK - 1) / BK;
+  // level 0's geometry in the single-level fields (unused by the kernel)
+  a.x = xs[0];
+  a.y = ys[0];
+  a.N = a.lv_N[0];
+  a.H = a.lv_H[0];
+  a.W = a.lv_W[0];
+  a.OH = a.lv_OH[0];
+  a.OW = a.lv_OW[0];
+  a.M = a.N * a.OH * a.OW;
+  a.m_end = a.M;
+  a.x_bytes = a.lv_xbytes[0];
+  a.tdH = a.tdW = 1;
+  const dim3 grid(a.ntiles, a.splits);
+  if (flags & kSplit3)
+    launch_conv_levels<true>(p.cfg, grid, as_stream(stream), a);
+  else
+    launch_conv_levels<false>(p.cfg, grid, as_stream(stream), a);
+  D2MI_LAUNCH_CHECK();
+  if (a.splits > 1) {
+    const int64_t total = (int64_t)a.lv_moff[kMaxConvLevels] * (Cout / 4);
+    const int gr = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(splitk_reduce_levels_kernel, dim3(gr), dim3(256), 0, as_stream(stream), a);
+    D2MI_LAUNCH_CHECK();
+  }
+  return 0;
 }
 
 extern "C" int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream) {

@@ -362,6 +362,42 @@ class Conv2D(Layer):
             self._packed_key = key
         return self._packed
 
+    def call_levels(self, inputs):
+        """This layer applied to each of ``inputs`` (feature levels sharing the
+        layer, as the reference's per-level head calls do), as ONE multi-level
+        MFMA launch (ops.conv2d_nhwc_levels) when nothing needs a gradient;
+        per-level calls otherwise.  The normalizer / activation follow per
+        level (GroupNorm + ReLU fused where it can be)."""
+        padded = self.impl == "mfma"  # explicit MFMA: Cin padded to a multiple of 4
+        ok = (not torch.is_grad_enabled() and self.impl in ("mfma", "auto") and len(inputs) <= 6
+              and all(self._mfma_eligible(x, padded) for x in inputs)
+              and not isinstance(self.normalizer_fn, BatchNorm))
+        if not ok:
+            return [self(x) for x in inputs]
+        w, b, norm, packed = self.effective_params(want_packed=True)
+        padc = (-self.in_channels) % 4
+        if padc:
+            inputs = [F.pad(x, (0, padc)) for x in inputs]
+            w = F.pad(w, (0, 0, 0, padc))
+            packed = None
+        if packed is None:
+            packed = self.packed_weights(w)
+        pads = same_pads(self.kernel_size, self.rate) if self.padding == "SAME" else (0, 0)
+        fuse_relu = norm is None and is_relu(self.act_fn)
+        ys = ops.conv2d_nhwc_levels(inputs, packed, b, self.stride, pads, relu=fuse_relu)
+        out = []
+        for y in ys:
+            if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \
+                    and norm.fused_ok(y):
+                out.append(norm(y, relu=True))
+                continue
+            if norm is not None:
+                y = norm(y)
+            if self.act_fn is not None and not fuse_relu:
+                y = self.act_fn(y)
+            out.append(y)
+        return out
+
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
              relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None,
              raw=False):

@@ -418,6 +418,50 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
     return y
 
 
+def conv2d_nhwc_levels(xs, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, math_mode=None):
+    """One launch of the same conv over up to 6 feature levels (a head shared
+    across FPN levels: RetinaNet / SOLOv2 towers): xs[l] [N_l, H_l, W_l, Cin]
+    -> [N_l, OH_l, OW_l, Cout] each (d2mi_conv2d_nhwc_levels).  Every level's
+    tiles run in one grid, so the small levels neither serialise behind the
+    big one nor need split-K; per-tile arithmetic is conv2d_nhwc's."""
+    math_mode = math_mode or CONV_MATH
+    if math_mode not in ("f32", "split"):
+        raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
+    xs = [_f32c(x) for x in xs]
+    _C.require_device(w_packed, *xs)
+    if not 1 <= len(xs) <= 6:
+        raise ValueError(f"conv2d_nhwc_levels takes 1..6 levels, got {len(xs)}")
+    KH, KW, Cout, Cin = w_packed.shape
+    pb, pe = pad
+    ys, dims = [], []
+    for x in xs:
+        N, H, W, C = x.shape
+        if C != Cin:
+            raise ValueError(f"conv input has {C} channels, weights expect {Cin}")
+        OH = (H + pb + pe - KH) // stride + 1
+        OW = (W + pb + pe - KW) // stride + 1
+        ys.append(torch.empty((N, OH, OW, Cout), dtype=torch.float32, device=x.device))
+        dims += [N, H, W]
+    if math_mode == "split" and Cout <= 64:
+        math_mode = "f32"
+    flags = (1 if relu else 0) | (4 if math_mode == "split" else 0)
+    xp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in xs])
+    yp = _C.host_array(_C.c_void_p, [y.data_ptr() for y in ys])
+    dm = _C.host_array(_C.ctypes.c_int32, dims)
+    lib = _C.lib()
+    wsb = lib.d2mi_conv2d_levels_workspace_size(dm, len(xs), Cin, Cout, KH, KW, int(stride),
+                                                int(pb), int(pe))
+    ws = _C.scratch(wsb, xs[0].device) if wsb else None
+    ev = KernelTimer.start()
+    rc = lib.d2mi_conv2d_nhwc_levels(xp, dm, len(xs), _C.ptr(w_packed), _C.ptr(bias), yp, Cin,
+                                     Cout, KH, KW, int(stride), int(pb), int(pe), flags,
+                                     _C.ptr(ws), wsb, _C.stream_of(xs[0].device))
+    fl = sum(2.0 * y.shape[0] * y.shape[1] * y.shape[2] * Cout * KH * KW * Cin for y in ys)
+    KernelTimer.stop(ev, "conv2d_split" if math_mode == "split" else "conv2d_mfma", fl)
+    _C.check(rc, "d2mi_conv2d_nhwc_levels")
+    return ys
+
+
 def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math_mode=None):
     """HWIO weight gradient of conv2d_nhwc on the MFMA wgrad kernel; with_bias
     also returns the bias gradient (dy summed over pixels) from the same pass.

@@ -44,11 +44,15 @@ class RetinaNetBoxTower(Layer):
             self.bbox_pred = Conv2D(cin, A * 4, activation=None, scope="bbox_pred")
 
     def call(self, features):
-        logits, bbox_reg = [], []
-        for f in features:
-            logits.append(self.cls_score(self.cls_subnet(f)))
-            bbox_reg.append(self.bbox_pred(self.bbox_subnet(f)))
-        return logits, bbox_reg
+        """Per level: cls_score(cls_subnet(f)), bbox_pred(bbox_subnet(f))
+        (retinanet.py:110-145, variables shared across levels).  Each layer
+        runs over all levels in one multi-level launch (Conv2D.call_levels)."""
+        c, b = list(features), list(features)
+        for layer in self.cls_layers:
+            c = layer.call_levels(c)
+        for layer in self.box_layers:
+            b = layer.call_levels(b)
+        return self.cls_score.call_levels(c), self.bbox_pred.call_levels(b)
 
 
 @SINGLE_STAGE_HEADS_REGISTRY.register()

@@ -140,11 +140,15 @@ class MaskKernelBranch(Layer):
     def call(self, features):
         """(category logits [N,S,S,K] per level, kernels [N,S,S,D] per level);
         the sigmoid + point NMS of the inference path run in ops.solo_inference."""
-        pred_cls, pred_kernels = [], []
-        for g, gk in self.grid_inputs(features):
-            pred_cls.append(self.solo_cate(self.cls_subnet(g)))
-            pred_kernels.append(self.solo_kernel(self.kernel_subnet(gk)))
-        return pred_cls, pred_kernels
+        ins = self.grid_inputs(features)
+        c = [g for g, _ in ins]
+        k = [gk for _, gk in ins]
+        # each tower layer over all five grids in one multi-level launch
+        for layer in self.cls_layers:
+            c = layer.call_levels(c)
+        for layer in self.kernel_layers:
+            k = layer.call_levels(k)
+        return self.solo_cate.call_levels(c), self.solo_kernel.call_levels(k)
 
 
 class MaskFeatureBranch(Layer):

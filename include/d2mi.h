@@ -343,6 +343,22 @@ int d2mi_conv2d_nhwc_gated(const float* x, const float* w_packed, const float* b
                            int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
                            int pad_end, int flags, void* workspace, size_t workspace_bytes,
                            void* stream);
+/* Multi-level form: the same conv (shared weights) over nlev <= 6 feature
+ * levels in ONE launch -- the heads the reference applies per FPN level with
+ * shared variables: RetinaNet towers / predictors (retinanet.py:110-145),
+ * SOLOv2 kernel / category towers (solo_v2.py:173-272).  xs[l]
+ * [N_l,H_l,W_l,Cin]; dims = {N_l, H_l, W_l} per level; ys[l]
+ * [N_l,OH_l,OW_l,Cout]; flags bit0 ReLU, bit2 split products.  Every level's
+ * tiles share one grid: the small levels run beside the big one instead of
+ * after it; when all levels together are under a round of workgroups, K is
+ * split over the levels' concatenated rows (workspace of
+ * d2mi_conv2d_levels_workspace_size bytes; fixed-order reduce). */
+size_t d2mi_conv2d_levels_workspace_size(const int32_t* dims, int nlev, int Cin, int Cout,
+                                         int KH, int KW, int stride, int pad_beg, int pad_end);
+int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* dims, int nlev,
+                            const float* w_packed, const float* bias, float* const* ys, int Cin,
+                            int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
+                            int flags, void* workspace, size_t workspace_bytes, void* stream);
 /* flags bit2 = "split" products: the same f32 operands, each split EXACTLY
  * into three bf16 terms (x = h + m + l, truncation), multiplied with six
  * bf16 MFMA products (v_mfma_f32_32x32x16_bf16; the dropped m*l, l*m, l*l

@@ -1115,3 +1115,30 @@ def test_roi_align_backward_grad_share_matches_autograd_sum(dev):
         assert share is None or not share  # the second backward took the maps
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cout,relu", [(256, True), (720, False), (36, False)])
+def test_conv_levels_matches_per_level_convs(dev, cout, relu):
+    """d2mi_conv2d_nhwc_levels (one launch over RetinaNet's P3..P7 at 640x640,
+    shared weights) == conv2d_nhwc per level: the same per-tile arithmetic,
+    summation order differing only where a small level alone would split K;
+    and level 0 vs float64.  Cout 720 = the cls_score head (a partial N tile),
+    36 = bbox_pred (narrow: f32 MFMA)."""
+    from detectron2_tensorflow_amd.layers import ops
+    g = torch.Generator(device="cpu").manual_seed(11)
+    shapes = [(2, 80, 80), (2, 40, 40), (2, 20, 20), (2, 10, 10), (2, 5, 5)]
+    xs = [torch.randn(n, h, w, 256, generator=g).to(dev) for n, h, w in shapes]
+    w = (torch.randn(3, 3, 256, cout, generator=g) * 0.02).to(dev)
+    b = (torch.randn(cout, generator=g) * 0.1).to(dev)
+    wp = ops.pack_conv_weights(w)
+    ys = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
+    for x, y in zip(xs, ys):
+        ref = ops.conv2d_nhwc(x, wp, b, 1, (1, 1), relu=relu)
+        assert y.shape == ref.shape
+        torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+    x64 = xs[0].double().permute(0, 3, 1, 2)
+    r64 = torch.nn.functional.conv2d(x64, w.double().permute(3, 2, 0, 1), b.double(), padding=1)
+    r64 = r64.permute(0, 2, 3, 1)
+    if relu:
+        r64 = r64.clamp_min(0)
+    torch.testing.assert_close(ys[0].double(), r64, rtol=1e-4, atol=1e-4)

@@ -1,6 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-T="tests/test_gpu_train.py::test_mask_head_on_foreground_rows_matches_fixed_layout"
-timeout -k 10 200 python -u -m pytest $T -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/t1.log 2>&1 || true
-D2MI_CONV_OCC=2 timeout -k 10 200 python -u -m pytest $T -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/t2.log 2>&1 || true
-tail -1 gpurun_out/t1.log; tail -1 gpurun_out/t2.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py tests/test_retinanet.py tests/test_solo.py -x -q -k "levels or retinanet or solo" --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/t_lv.log 2>&1
+tail -2 gpurun_out/t_lv.log
+timeout -k 10 300 python bench.py --model retinanet_R_101_FPN --mode infer --cpu-baseline 0 > gpurun_out/b_ret.log 2>&1
+tail -1 gpurun_out/b_ret.log | cut -c1-300
+timeout -k 10 300 python bench.py --model solo_v2_R_50_FPN --mode infer --cpu-baseline 0 > gpurun_out/b_solo.log 2>&1
+tail -1 gpurun_out/b_solo.log | cut -c1-300
