@@ -65,6 +65,16 @@ class StandardRPNHead(Layer):
     def call(self, features):
         rpn_features, logits, deltas = [], [], []
         fuse = features[0].is_cuda
+        if fuse and not torch.is_grad_enabled() and len(features) <= 6:
+            # inference: the shared 3x3 and the fused 16-wide 1x1 each as ONE
+            # multi-level launch over p2..p6
+            shares = self.conv.call_levels(list(features))
+            w16, wp, b16 = self._fused_1x1()
+            A, D = self.objectness_logits.weights.shape[3], self.anchor_deltas.weights.shape[3]
+            for y in ops.conv2d_nhwc_levels(shares, wp, b16):
+                logits.append(y[..., :A].contiguous())
+                deltas.append(y[..., A:A + D].contiguous())
+            return shares, logits, deltas
         for x in features:
             share = self.conv(x)
             rpn_features.append(share)

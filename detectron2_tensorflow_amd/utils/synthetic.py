@@ -69,8 +69,9 @@ def calibrate_rcnn_scores(model, batch):
     rh = model.roi_heads
     h1 = rh.box_predictor.register_forward_hook(grab("box"))
     rpn_head = model.proposal_generator.rpn_head
-    h2 = rpn_head.conv.register_forward_hook(lambda m, i, o: stats.__setitem__(
-        "rpn", float((o.reshape(-1, o.shape[-1]) ** 2).sum(-1).mean())))
+    # the shared conv's output on the last level (the head returns them all)
+    h2 = rpn_head.register_forward_hook(lambda m, i, o: stats.__setitem__(
+        "rpn", float((o[0][-1].reshape(-1, o[0][-1].shape[-1]) ** 2).sum(-1).mean())))
     was = model.training
     model.eval()
     model.inference({"image": batch["image"], "image_shape": batch["image_shape"]})
