@@ -269,9 +269,9 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (__umulhi(n, f.m) + n) >> f.l;
 }
 
-template <int TM, int TN>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_split_kernel(WgradArgs a, FastDiv fd_hw,
-                                                                  FastDiv fd_w) {
+template <int TM, int TN, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void conv_wgrad_split_kernel(WgradArgs a, FastDiv fd_hw,
+                                                                    FastDiv fd_w) {
   constexpr int BM = 2 * TM * 32, BN = 2 * TN * 32;
   constexpr int GA = BM / 4, GB = BN / 4;  // 4-channel groups
   __shared__ __attribute__((aligned(16))) uint16_t As[3 * BM * LDW];
@@ -444,7 +444,21 @@ FastDiv make_fastdiv(uint32_t d) {
 
 struct WPlan {
   int TM, TN, BM, BN, ntiles, splits, chunks_per_split, nchunks;
+  bool occ3;
 };
+
+// The 128x128 split wgrad can run three workgroups per CU (168 VGPRs, 52 KiB
+// LDS).  Measured (tools/conv_ab.py --set wgrad): 3% faster on the FPN p2 3x3
+// (134,400 pixels), slower on everything smaller (the extra pixel splits cost
+// more partial traffic than the occupancy gains), so only pixel counts of
+// 64k and up take it.  D2MI_WGRAD_OCC=2 disables it (A/B).
+static bool wgrad_occ3() {
+  static const int on = [] {
+    const char* e = getenv("D2MI_WGRAD_OCC");
+    return !(e && e[0] == '2');
+  }();
+  return on;
+}
 
 WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
   WPlan p;
@@ -456,8 +470,11 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
   p.ntiles = KH * KW * ((Cin + p.BM - 1) / p.BM) * ((Cout + p.BN - 1) / p.BN);
   const long long P = (long long)N * OH * OW;
   p.nchunks = (int)((P + KP - 1) / KP);
-  // about 2 workgroups per CU in total, each walking >= 16 chunks
-  int splits = std::max(1, 512 / p.ntiles);
+  // about one round of resident workgroups (2 or 3 per CU), each walking
+  // >= 16 chunks
+  p.occ3 = p.TM == 2 && p.TN == 2 && P >= 65536 && wgrad_occ3();
+  const int G = p.occ3 ? 768 : 512;
+  int splits = std::max(1, G / p.ntiles);
   splits = std::min(splits, std::max(1, p.nchunks / 16));
   splits = std::min(splits, 64);
   p.chunks_per_split = (p.nchunks + splits - 1) / splits;
@@ -537,7 +554,9 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
     a.x_bytes = (int)((int64_t)N * H * W * Cin * 4);
     a.dy_bytes = (int)((int64_t)a.P * Cout * 4);
     const FastDiv fhw = make_fastdiv((uint32_t)(a.OH * a.OW)), fw = make_fastdiv((uint32_t)a.OW);
-    if (p.TM == 2 && p.TN == 2)
+    if (p.occ3)
+      hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 2, 3>), grid, dim3(256), 0, st, a, fhw, fw);
+    else if (p.TM == 2 && p.TN == 2)
       hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 2>), grid, dim3(256), 0, st, a, fhw, fw);
     else if (p.TM == 2)
       hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 1>), grid, dim3(256), 0, st, a, fhw, fw);

@@ -1,8 +1,11 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py tests/test_retinanet.py tests/test_solo.py -x -q -k "levels or retinanet or solo" --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/t_lv.log 2>&1
-tail -2 gpurun_out/t_lv.log
-timeout -k 10 300 python bench.py --model retinanet_R_101_FPN --mode infer --cpu-baseline 0 > gpurun_out/b_ret.log 2>&1
-tail -1 gpurun_out/b_ret.log | cut -c1-300
-timeout -k 10 300 python bench.py --model solo_v2_R_50_FPN --mode infer --cpu-baseline 0 > gpurun_out/b_solo.log 2>&1
-tail -1 gpurun_out/b_solo.log | cut -c1-300
+o=gpurun_out/ab_w.log; : > $o
+for occ in 2 3; do
+echo "wocc=$occ" >> $o
+D2MI_WGRAD_OCC=$occ timeout -k 10 120 python tools/conv_ab.py --set wgrad --iters 20 2>&1 | grep -v amdgpu >> $o
+D2MI_WGRAD_OCC=$occ timeout -k 10 200 python bench.py --cpu-baseline 0 --steps 20 2>&1 | tail -1 | cut -c1-100 >> $o
+done
+D2MI_WGRAD_OCC=2 timeout -k 10 200 python bench.py --cpu-baseline 0 --steps 20 2>&1 | tail -1 | cut -c1-100 >> $o
+timeout -k 10 200 python bench.py --cpu-baseline 0 --steps 20 2>&1 | tail -1 | cut -c1-100 >> $o
+cat $o

@@ -6,7 +6,7 @@ one process: for A/B runs of kernel knobs set through the environment.
 
 Each shape: N,H,W,Cin,Cout,k,stride,form with form in
   plain | r (residual add + ReLU after) | g (ReLU gate: a dgrad epilogue) |
-  gr (gate + residual).
+  gr (gate + residual) | w (the weight gradient, conv2d_wgrad, with bias).
 """
 import argparse
 import os
@@ -23,6 +23,9 @@ SETS = {
                 "2,25,42,512,2048,1,1,r", "2,50,84,256,1024,1,1,gr", "2,50,84,1024,256,1,1,g",
                 "2,50,84,1024,256,1,1,plain", "2,100,168,512,128,1,1,g",
                 "2,200,336,256,64,1,1,plain", "2,200,336,64,64,1,1,plain"],
+    "wgrad": ["2,200,336,256,256,3,1,w", "2,100,168,256,256,3,1,w", "2,50,84,256,256,3,1,w",
+              "2,100,168,128,128,3,1,w", "2,25,42,512,512,3,1,w", "32,14,14,256,256,3,1,w",
+              "2,50,84,1024,256,1,1,w", "2,50,84,256,1024,1,1,w", "2,200,336,64,64,3,1,w"],
     "kxk": ["2,200,336,256,256,3,1,plain", "2,50,84,256,256,3,1,plain",
             "2,100,168,128,128,3,1,plain", "2,25,42,512,512,3,1,plain",
             "2,200,336,64,64,3,1,plain", "32,14,14,256,256,3,1,plain"],
@@ -48,6 +51,21 @@ def main():
         wp = ops.pack_conv_weights(w)
         p = (k - 1) // 2
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        if form == "w":
+            dy = torch.randn(N, OH, OW, Cout, generator=g).to(dev)
+            ref = ops.conv2d_wgrad(x, dy, k, s, (p, p), with_bias=True)[0]
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                y = ops.conv2d_wgrad(x, dy, k, s, (p, p), with_bias=True)[0]
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / a.iters * 1e3
+            fl = 2.0 * N * OH * OW * Cout * k * k * Cin
+            print(f"{spec:32s} {us:8.1f} us {fl / us / 1e6:7.1f} TF/s  "
+                  f"sum {float(y.double().sum()):.6e}", flush=True)
+            continue
         res = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "r" in form else None
         gate = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "g" in form else None
         kw = dict(residual=res, relu_gate=gate, relu_after_add=(form == "r"), relu=(form == "r"))
