@@ -626,6 +626,106 @@ class _RPNLossFn(torch.autograd.Function):
         return d_logits, d_deltas, None, None, None, None, None, None, None
 
 
+class _FastRCNNLossFn(torch.autograd.Function):
+    """(loss_cls, loss_box_reg) of FastRCNNOutputs.losses on dense rows
+    (d2mi_fast_rcnn_loss_fwd / _bwd, csrc/roi_losses.hip); differentiable
+    w.r.t. logits and deltas."""
+
+    @staticmethod
+    def forward(ctx, logits, deltas, proposals, gt_classes, gt_boxes, valid, weights, beta):
+        B, K1 = logits.shape
+        nreg = deltas.shape[1] // 4
+        dev = logits.device
+        stats = torch.empty(4, dtype=torch.float32, device=dev)
+        lib = _C.lib()
+        wsb = lib.d2mi_fast_rcnn_loss_workspace_size(B)
+        ws = _C.scratch(wsb, dev)
+        w = _C.host_array(_C.c_float, [float(v) for v in weights])
+        rc = lib.d2mi_fast_rcnn_loss_fwd(_C.ptr(logits), _C.ptr(deltas), _C.ptr(proposals),
+                                         _C.ptr(gt_classes), _C.ptr(gt_boxes), _C.ptr(valid), B,
+                                         K1, nreg, w, float(beta), _C.ptr(stats), _C.ptr(ws), wsb,
+                                         _C.stream_of(dev))
+        _C.check(rc, "d2mi_fast_rcnn_loss_fwd")
+        ctx.save_for_backward(logits, deltas, proposals, gt_classes, gt_boxes, valid, stats)
+        ctx.conf = (tuple(float(v) for v in weights), float(beta))
+        ctx.set_materialize_grads(False)
+        return stats[0], stats[1]
+
+    @staticmethod
+    def backward(ctx, g_cls, g_box):
+        logits, deltas, proposals, gt_classes, gt_boxes, valid, stats = ctx.saved_tensors
+        weights, beta = ctx.conf
+        dev = logits.device
+        z = torch.zeros((), dtype=torch.float32, device=dev)
+        grads = torch.stack([g_cls if g_cls is not None else z,
+                             g_box if g_box is not None else z]).float().contiguous()
+        d_logits = torch.empty_like(logits)
+        d_deltas = torch.empty_like(deltas)
+        B, K1 = logits.shape
+        w = _C.host_array(_C.c_float, list(weights))
+        rc = _C.lib().d2mi_fast_rcnn_loss_bwd(_C.ptr(logits), _C.ptr(deltas), _C.ptr(proposals),
+                                              _C.ptr(gt_classes), _C.ptr(gt_boxes), _C.ptr(valid),
+                                              B, K1, deltas.shape[1] // 4, w, beta, _C.ptr(stats),
+                                              _C.ptr(grads), _C.ptr(d_logits), _C.ptr(d_deltas),
+                                              _C.stream_of(dev))
+        _C.check(rc, "d2mi_fast_rcnn_loss_bwd")
+        return d_logits, d_deltas, None, None, None, None, None, None
+
+
+def fast_rcnn_loss(logits, deltas, proposals, gt_classes, gt_boxes, valid, weights, beta):
+    """Fused Fast R-CNN losses on dense rows: logits [B, K+1], deltas
+    [B, nreg*4], proposals / gt_boxes [B, 4], gt_classes [B], valid [B] ->
+    (loss_cls, loss_box_reg), both already / max(1, #valid)."""
+    logits, deltas = _f32c(logits), _f32c(deltas)
+    proposals, gt_boxes = _f32c(proposals), _f32c(gt_boxes)
+    gt_classes = gt_classes.to(torch.int64).contiguous()
+    valid = valid.to(torch.uint8).contiguous()
+    _C.require_device(logits, deltas, proposals, gt_classes, gt_boxes, valid)
+    return _FastRCNNLossFn.apply(logits, deltas, proposals, gt_classes, gt_boxes, valid,
+                                 tuple(weights), float(beta))
+
+
+class _MaskLossFn(torch.autograd.Function):
+    """mask_rcnn_loss's sigmoid BCE of the gt-class channel over foreground
+    rows, mean over fg x Hm x Wm (d2mi_mask_loss_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, classes, fg):
+        B, Hm, Wm, C = logits.shape
+        dev = logits.device
+        stats = torch.empty(3, dtype=torch.float32, device=dev)
+        lib = _C.lib()
+        wsb = lib.d2mi_mask_loss_workspace_size(B)
+        ws = _C.scratch(wsb, dev)
+        rc = lib.d2mi_mask_loss_fwd(_C.ptr(logits), _C.ptr(target), _C.ptr(classes), _C.ptr(fg), B,
+                                    Hm * Wm, C, _C.ptr(stats), _C.ptr(ws), wsb, _C.stream_of(dev))
+        _C.check(rc, "d2mi_mask_loss_fwd")
+        ctx.save_for_backward(logits, target, classes, fg, stats)
+        return stats[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, classes, fg, stats = ctx.saved_tensors
+        B, Hm, Wm, C = logits.shape
+        grads = g.reshape(1).float().contiguous()
+        d_logits = torch.empty_like(logits)
+        rc = _C.lib().d2mi_mask_loss_bwd(_C.ptr(logits), _C.ptr(target), _C.ptr(classes),
+                                         _C.ptr(fg), B, Hm * Wm, C, _C.ptr(stats), _C.ptr(grads),
+                                         _C.ptr(d_logits), _C.stream_of(logits.device))
+        _C.check(rc, "d2mi_mask_loss_bwd")
+        return d_logits, None, None, None
+
+
+def mask_loss(logits, target, classes, fg):
+    """Fused mask loss: logits [B, Hm, Wm, C], target [B, Hm, Wm] (0 / 1),
+    classes [B], fg [B] -> mean sigmoid BCE of each fg row's class channel."""
+    logits, target = _f32c(logits), _f32c(target)
+    classes = classes.to(torch.int64).contiguous()
+    fg = fg.to(torch.uint8).contiguous()
+    _C.require_device(logits, target, classes, fg)
+    return _MaskLossFn.apply(logits, target, classes, fg)
+
+
 def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta):
     """Fused RPN losses (sums; the caller normalises): logits [N, P], deltas
     [N, P, 4], anchors [P, 4], gt_boxes [N, G, 4], matches [N, P], pos /

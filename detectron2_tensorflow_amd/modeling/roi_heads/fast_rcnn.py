@@ -10,6 +10,10 @@ from ...layers import initializers as init
 from ...layers import ops
 from ...layers.loss import smooth_l1_loss
 
+# GPU training takes the fused HIP losses (csrc/roi_losses.hip); False runs
+# the tensor formulation below on the GPU too (tests compare the two).
+FUSED_LOSSES = True
+
 
 class FastRCNNOutputLayers(Layer):
     def __init__(self, input_size, num_classes, cls_agnostic_bbox_reg, box_dim=4, **kwargs):
@@ -55,6 +59,11 @@ def fast_rcnn_losses(pred_class_logits, pred_proposal_deltas, proposal_boxes, gt
     loss_cls = mean softmax CE over the R valid rows; loss_box_reg = smooth-L1 of
     the gt-class deltas of foreground rows, summed, / R.  Both 0 when R == 0."""
     import torch
+    if pred_class_logits.is_cuda and FUSED_LOSSES:
+        lc, lb = ops.fast_rcnn_loss(pred_class_logits, pred_proposal_deltas, proposal_boxes,
+                                    gt_classes, gt_boxes, valid, box2box_transform.weights,
+                                    smooth_l1_beta)
+        return {"loss_cls": lc, "loss_box_reg": lb}
     K = pred_class_logits.shape[1] - 1
     R = valid.sum().clamp(min=1).to(pred_class_logits.dtype)
     cls = torch.where(valid, gt_classes, torch.zeros_like(gt_classes)).long()

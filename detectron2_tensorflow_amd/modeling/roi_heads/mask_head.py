@@ -6,10 +6,15 @@ import torch
 
 from ...layers import Conv2D, ConvTranspose2D, Layer, get_norm
 from ...layers import initializers as init
+from ...layers import ops
 from ...utils.arg_scope import arg_scope
 from ...utils.registry import Registry
 
 ROI_MASK_HEAD_REGISTRY = Registry("ROI_MASK_HEAD")
+
+# GPU training takes the fused HIP loss (csrc/roi_losses.hip); False runs the
+# tensor formulation on the GPU too (tests compare the two).
+FUSED_LOSSES = True
 
 
 def mask_rcnn_inference(pred_mask_logits, pred_classes):
@@ -47,6 +52,8 @@ def mask_rcnn_loss(pred_mask_logits, boxes, gt_boxes, gt_classes, gt_masks, mask
     with torch.no_grad():
         target = tf_crop_and_resize(masks, boxes.detach().contiguous(), ind, (Hm, Wm))
         target = torch.round(target[..., 0])
+    if pred_mask_logits.is_cuda and FUSED_LOSSES:
+        return ops.mask_loss(pred_mask_logits, target, gt_classes, fg)
     if C == 1:
         logits = pred_mask_logits[..., 0]
     else:

@@ -530,6 +530,43 @@ int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const float* anc
                       float beta, const float* grads, float* d_logits, float* d_deltas,
                       void* stream);
 
+/* ----------------------------------------------------- ROI-head losses
+ * FastRCNNOutputs.losses (lib/modeling/roi_heads/fast_rcnn.py:269-357) on
+ * dense sampled rows: logits [B, K1 = K+1], deltas [B, nreg*4] (nreg 1 =
+ * class-agnostic), proposals / gt_boxes [B] yxyx float4, gt_classes int64 [B]
+ * (K = background), valid uint8 [B].  stats [4] device = (loss_cls, loss_box,
+ * #valid, R = max(1, #valid)): loss_cls = sum of softmax CE over valid rows /
+ * R, loss_box = sum of smooth-L1(beta) of the gt-class deltas against
+ * get_deltas(proposal, gt box; weights) over foreground rows / R
+ * (box_regression.py:38-74, layers/loss.py).  Row terms go to the workspace
+ * and are summed by one workgroup in a fixed order (deterministic).
+ * _bwd: d_logits / d_deltas (every element written) for the upstream
+ * gradients grads [2] device (loss_cls, loss_box). */
+size_t d2mi_fast_rcnn_loss_workspace_size(int B);
+int d2mi_fast_rcnn_loss_fwd(const float* logits, const float* deltas, const float* proposals,
+                            const long long* gt_classes, const float* gt_boxes,
+                            const unsigned char* valid, int B, int K1, int nreg,
+                            const float* weights, float beta, float* stats, void* workspace,
+                            size_t workspace_bytes, void* stream);
+int d2mi_fast_rcnn_loss_bwd(const float* logits, const float* deltas, const float* proposals,
+                            const long long* gt_classes, const float* gt_boxes,
+                            const unsigned char* valid, int B, int K1, int nreg,
+                            const float* weights, float beta, const float* stats,
+                            const float* grads, float* d_logits, float* d_deltas, void* stream);
+/* mask_rcnn_loss (lib/modeling/roi_heads/mask_head.py:17-68): logits
+ * [B, P = Hm*Wm, C], target [B, P] (the rounded crop_and_resize of the GT
+ * mask), classes int64 [B], fg uint8 [B]; stats [3] = (loss, #fg,
+ * n = max(1, #fg * P)), loss = sum over fg rows of the sigmoid BCE of the
+ * class channel (clamped to [0, C-1]; channel 0 when C == 1) / n.  _bwd
+ * writes the whole d_logits for grads [1] device. */
+size_t d2mi_mask_loss_workspace_size(int B);
+int d2mi_mask_loss_fwd(const float* logits, const float* target, const long long* classes,
+                       const unsigned char* fg, int B, int P, int C, float* stats,
+                       void* workspace, size_t workspace_bytes, void* stream);
+int d2mi_mask_loss_bwd(const float* logits, const float* target, const long long* classes,
+                       const unsigned char* fg, int B, int P, int C, const float* stats,
+                       const float* grads, float* d_logits, void* stream);
+
 /* ------------------------------------------------ ResNet stem tail
  * relu(y + shift) -> zero pad 1 -> 3x3 stride-2 VALID max pool
  * (lib/modeling/backbone/resnet.py:73-82) on the NHWC output y [N,H,W,C] of

@@ -157,8 +157,11 @@ def test_mask_head_on_foreground_rows_matches_fixed_layout(dev):
         # summation order differs with the row count (split-K / wgrad partitions
         # of every dgrad and wgrad in the head): weight gradients are sums over
         # ~10^5 pixel terms with cancellation, so the bound is relative to the
-        # tensor's largest entry (measured: up to 1.2e-4 of it)
-        torch.testing.assert_close(res[True][1][n], g, rtol=1e-4, atol=3e-4 * g.abs().max().item())
+        # tensor's largest entry (measured: up to 1.2e-3 of it on a handful of
+        # the 262,144 deconv-weight entries; a wrong row or class would be O(1))
+        torch.testing.assert_close(res[True][1][n], g, rtol=1e-4, atol=2e-3 * g.abs().max().item())
+        bad = ((res[True][1][n] - g).abs() > 3e-4 * g.abs().max()).float().mean().item()
+        assert bad < 1e-3, (n, bad)
 
 
 def test_rpn_head_fused_1x1_matches_separate_convs(dev):
@@ -386,3 +389,72 @@ def test_whole_training_step_matches_cpu_restatement(dev):
     print(f"losses gpu {g_losses}\nlosses cpu {c_losses}\nworst weight rel diff {worst_w:.3g}, "
           f"worst update rel diff {worst_d:.3g} over {checked} tensors")
     assert checked > 25, checked
+
+
+@pytest.mark.parametrize("nreg", [80, 1])
+def test_fused_fast_rcnn_loss_matches_tensor_formulation(dev, nreg):
+    """ops.fast_rcnn_loss (csrc/roi_losses.hip: per-row CE + smooth-L1 with the
+    targets formed in place, fixed-order reduction, analytic backward) equals
+    FastRCNNOutputs.losses' tensor formulation (fast_rcnn_losses with
+    FUSED_LOSSES off) in value and in the logits / deltas gradients; rows that
+    are padding (valid False), background and foreground all present."""
+    from detectron2_tensorflow_amd.modeling.box_regression import Box2BoxTransform
+    from detectron2_tensorflow_amd.modeling.roi_heads import fast_rcnn as fr
+    g = torch.Generator().manual_seed(5)
+    B, K = 1024, 80
+    cy, cx = torch.rand(B, generator=g) * 700, torch.rand(B, generator=g) * 1200
+    hh, ww = torch.rand(B, generator=g) * 200 + 8, torch.rand(B, generator=g) * 200 + 8
+    props = torch.stack([cy - hh / 2, cx - ww / 2, cy + hh / 2, cx + ww / 2], 1)
+    gtb = props + torch.randn(B, 4, generator=g) * 6
+    gtb[:, 2:] = torch.maximum(gtb[:, 2:], gtb[:, :2] + 2)
+    cls = torch.randint(0, K + 1, (B,), generator=g)  # K = background
+    valid = torch.rand(B, generator=g) < 0.85
+    logits = torch.randn(B, K + 1, generator=g) * 3
+    deltas = torch.randn(B, nreg * 4, generator=g) * 0.5
+    b2b = Box2BoxTransform((10.0, 10.0, 5.0, 5.0))
+    t = lambda a: a.to(dev)
+    res = {}
+    for fused in (True, False):
+        fr.FUSED_LOSSES = fused
+        try:
+            lg, dl = t(logits).requires_grad_(True), t(deltas).requires_grad_(True)
+            out = fr.fast_rcnn_losses(lg, dl, t(props), t(cls), t(gtb), t(valid), b2b, 0.5)
+            (out["loss_cls"] * 0.7 + out["loss_box_reg"] * 1.3).backward()
+            res[fused] = (out["loss_cls"].item(), out["loss_box_reg"].item(), lg.grad, dl.grad)
+        finally:
+            fr.FUSED_LOSSES = True
+    a, b = res[True], res[False]
+    assert a[0] == pytest.approx(b[0], rel=2e-6) and a[1] == pytest.approx(b[1], rel=2e-6)
+    torch.testing.assert_close(a[2], b[2], rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(a[3], b[3], rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("C", [80, 1])
+def test_fused_mask_loss_matches_tensor_formulation(dev, C):
+    """ops.mask_loss (csrc/roi_losses.hip) == mask_rcnn_loss's tensor
+    formulation: value and the logits gradient (only each foreground row's
+    class channel nonzero)."""
+    from detectron2_tensorflow_amd.modeling.roi_heads import mask_head as mh
+    rng = np.random.default_rng(3)
+    B, G = 64, 6
+    gt = np.stack([rng.uniform(0, 100, G), rng.uniform(0, 100, G),
+                   rng.uniform(120, 300, G), rng.uniform(120, 300, G)], 1).astype(np.float32)
+    masks = (rng.random((G, 56, 56)) < 0.5).astype(np.uint8)
+    gi = rng.integers(0, G, B)
+    boxes = (gt[gi] + rng.normal(0, 15, (B, 4))).astype(np.float32)
+    cls = rng.integers(0, 80, B)
+    fg = rng.random(B) < 0.6
+    logits = rng.standard_normal((B, 28, 28, C)).astype(np.float32) * 2
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    res = {}
+    for fused in (True, False):
+        mh.FUSED_LOSSES = fused
+        try:
+            lg = t(logits).requires_grad_(True)
+            loss = mh.mask_rcnn_loss(lg, t(boxes), t(gt[gi]), t(cls), t(masks), t(gi), t(fg), True)
+            (loss * 1.7).backward()
+            res[fused] = (loss.item(), lg.grad)
+        finally:
+            mh.FUSED_LOSSES = True
+    assert res[True][0] == pytest.approx(res[False][0], rel=2e-6)
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-9)
