@@ -971,9 +971,16 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   p.nk = KH * KW * ((Cin + BK - 1) / BK);
   p.splits = 1;
   const int G = wg_slots(p.cfg);
-  // Fewer tiles than resident workgroups and a long K: split K.
-  if (4 * p.ntiles < 3 * G && p.nk >= 16) {
-    p.splits = std::min(std::max(1, G / p.ntiles), std::min(p.nk / 8, 16));
+  // Fewer tiles than resident workgroups and a long K: split K (to about
+  // GS workgroups: every split writes and the reduce reads one more partial
+  // slab of the output).
+  static const int GS = [] {
+    const char* e = getenv("D2MI_CONV_SPLIT_SLOTS");
+    return e ? atoi(e) : 0;
+  }();
+  const int gs = GS > 0 ? GS : G;
+  if (4 * p.ntiles < 3 * gs && p.nk >= 16) {
+    p.splits = std::min(std::max(1, gs / p.ntiles), std::min(p.nk / 8, 16));
   }
   p.kt_per_split = (p.nk + p.splits - 1) / p.splits;
   p.splits = (p.nk + p.kt_per_split - 1) / p.kt_per_split;

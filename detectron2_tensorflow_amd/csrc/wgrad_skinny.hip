@@ -65,6 +65,105 @@ __global__ __launch_bounds__(256) void wgrad_skinny_partial_kernel(
   }
 }
 
+// float4 form (Cin % 4 == 0, 16-B aligned x): a lane owns 4 input channels,
+// the four waves take every 4th pixel of the chunk (each row read is one
+// 1 KiB float4 wave load for Cin = 256, four rows in flight per wave: 4x the
+// bytes per load of the scalar form, which left this pass latency-bound),
+// and the waves' sums are combined in wave order through LDS before the
+// chunk partial is written.  kChunk4 pixels per workgroup.
+constexpr int kChunk4 = 128;
+
+__global__ __launch_bounds__(256, 2) void wgrad_skinny_partial4_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, int P, int Cin, int Cout,
+    float* __restrict__ partial /* [chunks][Cin + 1][Cout] */) {
+  // gs: the chunk's G rows (16 KiB); reused for the wave combine (3 x 64
+  // lanes x 64 floats = 48 KiB)
+  __shared__ float4 lds[3 * 64 * 16];
+  float* gs = reinterpret_cast<float*>(lds);
+  const int chunk = blockIdx.x;
+  const int p0 = chunk * kChunk4;
+  const int np = min(kChunk4, P - p0);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* out = partial + (size_t)chunk * (Cin + 1) * Cout;
+  for (int cb = 0; cb < Cin; cb += 256) {  // 256 input channels per pass
+    __syncthreads();
+    for (int i = threadIdx.x; i < kChunk4 * kMaxCout; i += blockDim.x) {
+      const int p = i / kMaxCout, j = i - p * kMaxCout;
+      gs[i] = (p < np && j < Cout) ? g[(size_t)(p0 + p) * Cout + j] : 0.f;
+    }
+    __syncthreads();
+    const int c = cb + 4 * lane;
+    const bool live = c < Cin;
+    float4 acc[kMaxCout];
+#pragma unroll
+    for (int j = 0; j < kMaxCout; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (live) {
+      const float* xp = x + (size_t)p0 * Cin + c;
+      int p = wv;
+      for (; p + 12 < np; p += 16) {  // 4 rows in flight per wave
+        float4 xv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xv[u] = *reinterpret_cast<const float4*>(xp + (size_t)(p + 4 * u) * Cin);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* gr = gs + (p + 4 * u) * kMaxCout;
+#pragma unroll
+          for (int j = 0; j < kMaxCout; ++j) {
+            const float gv = gr[j];
+            acc[j].x = fmaf(xv[u].x, gv, acc[j].x);
+            acc[j].y = fmaf(xv[u].y, gv, acc[j].y);
+            acc[j].z = fmaf(xv[u].z, gv, acc[j].z);
+            acc[j].w = fmaf(xv[u].w, gv, acc[j].w);
+          }
+        }
+      }
+      for (; p < np; p += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xp + (size_t)p * Cin);
+        const float* gr = gs + p * kMaxCout;
+#pragma unroll
+        for (int j = 0; j < kMaxCout; ++j) {
+          const float gv = gr[j];
+          acc[j].x = fmaf(xv.x, gv, acc[j].x);
+          acc[j].y = fmaf(xv.y, gv, acc[j].y);
+          acc[j].z = fmaf(xv.z, gv, acc[j].z);
+          acc[j].w = fmaf(xv.w, gv, acc[j].w);
+        }
+      }
+    }
+    // bias row of this chunk (once): column sums of G in pixel order
+    float bsum = 0.f;
+    if (cb == 0 && threadIdx.x < Cout)
+      for (int q = 0; q < np; ++q) bsum += gs[q * kMaxCout + threadIdx.x];
+    __syncthreads();  // gs no longer read: the region takes the wave sums
+    if (wv > 0) {
+#pragma unroll
+      for (int j = 0; j < kMaxCout; ++j) lds[((wv - 1) * 64 + lane) * kMaxCout + j] = acc[j];
+    }
+    __syncthreads();
+    if (wv == 0 && live) {
+      // ((w0 + w1) + w2) + w3 per output, one output column at a time
+#pragma unroll
+      for (int j = 0; j < kMaxCout; ++j) {
+        float4 t = acc[j];
+        for (int w = 0; w < 3; ++w) {
+          const float4 v = lds[(w * 64 + lane) * kMaxCout + j];
+          t.x += v.x;
+          t.y += v.y;
+          t.z += v.z;
+          t.w += v.w;
+        }
+        if (j < Cout) {
+          out[(size_t)c * Cout + j] = t.x;
+          out[(size_t)(c + 1) * Cout + j] = t.y;
+          out[(size_t)(c + 2) * Cout + j] = t.z;
+          out[(size_t)(c + 3) * Cout + j] = t.w;
+        }
+      }
+    }
+    if (cb == 0 && threadIdx.x < Cout) out[(size_t)Cin * Cout + threadIdx.x] = bsum;
+  }
+}
+
 // Sum the chunk partials (gw rows, then the gb row) in a fixed order: 16
 // outputs per workgroup, 16 chunk segments per output summed in chunk order
 // by 16 threads, then the 16 segment sums in segment order (one thread per
@@ -151,7 +250,7 @@ extern "C" int d2mi_column_sum(const float* x, long long rows, int cols, float* 
 
 extern "C" size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout) {
   if (P <= 0 || Cin <= 0 || Cout <= 0) return 0;
-  const size_t chunks = ((size_t)P + kChunk - 1) / kChunk;
+  const size_t chunks = ((size_t)P + kChunk - 1) / kChunk;  // >= the float4 form's
   return chunks * (size_t)(Cin + 1) * Cout * sizeof(float);
 }
 
@@ -163,11 +262,16 @@ extern "C" int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin,
   const size_t need = d2mi_wgrad_skinny_workspace_size(P, Cin, Cout);
   D2MI_REQUIRE(workspace && workspace_bytes >= need, "wgrad_skinny workspace too small: %zu < %zu",
                workspace_bytes, need);
-  const int chunks = (P + kChunk - 1) / kChunk;
+  const bool v4 = Cin % 4 == 0 && ((uintptr_t)x & 15) == 0;
+  const int chunks = v4 ? (P + kChunk4 - 1) / kChunk4 : (P + kChunk - 1) / kChunk;
   hipStream_t st = as_stream(stream);
   float* partial = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(wgrad_skinny_partial_kernel, dim3(chunks), dim3(256), 0, st, x, g, P, Cin,
-                     Cout, partial);
+  if (v4)
+    hipLaunchKernelGGL(wgrad_skinny_partial4_kernel, dim3(chunks), dim3(256), 0, st, x, g, P, Cin,
+                       Cout, partial);
+  else
+    hipLaunchKernelGGL(wgrad_skinny_partial_kernel, dim3(chunks), dim3(256), 0, st, x, g, P, Cin,
+                       Cout, partial);
   D2MI_LAUNCH_CHECK();
   const int n = (Cin + 1) * Cout;
   hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((n + kRedOut - 1) / kRedOut), dim3(256), 0,
