@@ -36,6 +36,11 @@ _SIGS = {
     "d2mi_roi_align_bwd_ex": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int,
                                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int,
                                       P, c_size_t, P]),
+    "d2mi_roi_align_bwd2_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                                   c_int, c_int, c_int, c_int]),
+    "d2mi_roi_align_bwd2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int,
+                                    c_int, c_int, c_int, P, c_int, P, c_size_t, P]),
     "d2mi_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
     "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),

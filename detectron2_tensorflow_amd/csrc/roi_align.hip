@@ -37,6 +37,11 @@ struct RoiArgs {
   const float* gout;
   int32_t* err;
   int bpb;  // forward: output bins per workgroup (16, 32 or 64)
+  // backward over one or two ROI sets of the same maps (Contrib::set picks):
+  // each set's grad_out and its sampling ratio (the avg-pool divisor)
+  const float* gout_s[2];
+  int sr_s[2];
+  int acc_mask;  // backward: bit l = level l's map already holds a gradient to add to
 };
 
 struct RoiGeom {
@@ -298,9 +303,9 @@ struct PixMap {
 };
 
 struct Contrib {
-  int32_t row;  // grad_out row index r * nbins + bin
+  int32_t row;  // grad_out row index r * nbins + bin (of its set's grad_out)
   float yl, xl;
-  int32_t pad;
+  int32_t set;  // ROI set (0 / 1) of a merged backward
 };
 
 // One launch clears every buffer the backward starts from (the per-level grad
@@ -335,15 +340,20 @@ __global__ __launch_bounds__(256) void roi_bwd_clear_kernel(ClearList cl) {
 
 // The ROI geometry is recomputed per sample (a few dozen flops against the
 // 40 B the thread stores) rather than staged by a separate launch.
-__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, uint64_t* __restrict__ keys,
+// set / sample_base: a merged backward emits its second ROI set after the
+// first (samples from sample_base on) with pair keys pixel * 2 + set
+// (set_bits = 1): each set's contributions of a pixel form their own run.
+__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, int set, int set_bits,
+                                    long long sample_base, uint64_t* __restrict__ keys,
                                     Contrib* __restrict__ rec) {
   const int S = a.sr > 0 ? a.sr : 1;
   const long long nsamp = (long long)a.out_h * a.out_w * S * S;
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long long)a.R * nsamp) return;
-  const int r = (int)(t / nsamp);
-  const int s = (int)(t - (long long)r * nsamp);
+  const long long tl = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tl >= (long long)a.R * nsamp) return;
+  const int r = (int)(tl / nsamp);
+  const int s = (int)(tl - (long long)r * nsamp);
   const RoiGeom g = roi_geom(a, r);
+  const long long t = sample_base + tl;
   const uint64_t slot = (uint64_t)t * 4u;
   uint64_t* k = keys + slot;
   bool ok = g.ok;
@@ -365,26 +375,34 @@ __global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, uint64_t
   c.row = r * (a.out_h * a.out_w) + (iy / S) * a.out_w + ix / S;
   c.yl = ty.lerp;
   c.xl = tx.lerp;
-  c.pad = 0;
+  c.set = set;
   rec[t] = c;  // shared by the 4 corners: slot >> 2
   const uint64_t img = (uint64_t)pm.base[g.lvl] + (uint64_t)g.n * g.H * g.W;
-  k[0] = ((img + (uint64_t)ty.r0 * g.W + tx.r0) << low_bits) | (slot + 0);
-  k[1] = ((img + (uint64_t)ty.r0 * g.W + tx.r1) << low_bits) | (slot + 1);
-  k[2] = ((img + (uint64_t)ty.r1 * g.W + tx.r0) << low_bits) | (slot + 2);
-  k[3] = ((img + (uint64_t)ty.r1 * g.W + tx.r1) << low_bits) | (slot + 3);
+  const int sh = low_bits + set_bits;
+  const uint64_t sb = (uint64_t)set << low_bits;
+  k[0] = ((img + (uint64_t)ty.r0 * g.W + tx.r0) << sh) | sb | (slot + 0);
+  k[1] = ((img + (uint64_t)ty.r0 * g.W + tx.r1) << sh) | sb | (slot + 1);
+  k[2] = ((img + (uint64_t)ty.r1 * g.W + tx.r0) << sh) | sb | (slot + 2);
+  k[3] = ((img + (uint64_t)ty.r1 * g.W + tx.r1) << sh) | sb | (slot + 3);
 }
 
 // run_start[p] = first sorted index of pixel p (-1 untouched), run_end[p] = one past its last.
 // Every touched pixel is also appended to touched[] (*n_touched entries; the
 // list order varies run to run, the per-pixel sums do not).
+// With set_bits = 1 the runs are per (pixel, set) pair (run_start / run_end
+// indexed by pixel * 2 + set) and touched[] lists each pixel once.
 __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
-                                    long long total_pixels, int32_t* __restrict__ run_start,
+                                    int set_bits, long long total_pixels,
+                                    int32_t* __restrict__ run_start,
                                     int32_t* __restrict__ run_end, int32_t* __restrict__ touched,
                                     int32_t* __restrict__ n_touched) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t p = i < n ? keys[i] >> low_bits : ~0ull;
+  const uint64_t q = i < n ? keys[i] >> low_bits : ~0ull;  // pair
+  const uint64_t p = q >> set_bits;                         // pixel
   const bool live = i < n && (long long)p < total_pixels;  // invalid contributions sort last
-  const bool first = live && (i == 0 || (keys[i - 1] >> low_bits) != p);
+  const uint64_t qprev = (live && i > 0) ? keys[i - 1] >> low_bits : ~0ull;
+  const bool first = live && (i == 0 || (qprev >> set_bits) != p);  // first of the pixel
+  const bool first_pair = live && (i == 0 || qprev != q);
   // one global counter atomic per 1024-thread workgroup: same-address device
   // atomics serialise (one per wave still cost ~20 us per launch); the waves'
   // offsets come from an LDS counter
@@ -400,11 +418,9 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __re
   if (threadIdx.x == 0) wg_base = wg_count ? atomicAdd(n_touched, wg_count) : 0;
   __syncthreads();
   base += wg_base;
-  if (first) {
-    run_start[p] = (int32_t)i;
-    touched[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
-  }
-  if (live && (i == n - 1 || (keys[i + 1] >> low_bits) != p)) run_end[p] = (int32_t)(i + 1);
+  if (first) touched[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+  if (first_pair) run_start[q] = (int32_t)i;
+  if (live && (i == n - 1 || (keys[i + 1] >> low_bits) != q)) run_end[q] = (int32_t)(i + 1);
 }
 
 // nseg[p] = number of kSeg segments of pixel p when it has more than kSeg
@@ -443,7 +459,7 @@ __device__ __forceinline__ float weigh(int corner, float yl, float xl, float v) 
 template <bool VEC4>
 __device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __restrict__ keys,
                                           const Contrib* __restrict__ rec, uint64_t low_mask,
-                                          int i0, int i1, int c, bool live, float inv, bool avg) {
+                                          int i0, int i1, int c, bool live) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int C = a.C;
   for (int i = i0; i < i1; i += kBatch) {
@@ -462,7 +478,7 @@ __device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __re
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) {
       if (u < m && live) {
-        const float* src = a.gout + (size_t)e[u].row * C + c;
+        const float* src = a.gout_s[e[u].set] + (size_t)e[u].row * C + c;
         if (VEC4) v[u] = *reinterpret_cast<const float4*>(src);
         else v[u].x = *src;
       }
@@ -471,7 +487,11 @@ __device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __re
     for (int u = 0; u < kBatch; ++u) {
       if (u < m) {
         float4 g = v[u];
-        if (avg) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
+        const int sr = a.sr_s[e[u].set];
+        if (sr > 0) {  // the avg-pool divisor of the set's sampling ratio
+          const float inv = (float)(sr * sr);
+          g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv;
+        }
         acc.x += weigh(corner[u], e[u].yl, e[u].xl, g.x);
         if (VEC4) {
           acc.y += weigh(corner[u], e[u].yl, e[u].xl, g.y);
@@ -499,12 +519,11 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
   const int i0 = run_start[p] + k * kSeg;
   const int i1 = min(i0 + kSeg, run_end[p]);
   const uint64_t low_mask = (1ull << low_bits) - 1ull;
-  const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
   const int step = VEC4 ? 256 : 64;
   for (int c0 = 0; c0 < a.C; c0 += step) {
     const int c = c0 + (VEC4 ? lane * 4 : lane);
     const bool live = c < a.C;
-    const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
+    const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
     if (live) {
       float* dst = partial + (size_t)seg * a.C + c;
       if (VEC4) *reinterpret_cast<float4*>(dst) = acc;
@@ -519,60 +538,75 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
 // -> records -> grad_out rows) overlaps across waves instead of a wave per
 // feature-map pixel (most of which only stored zeros) -- that launch was bound
 // by wave start-up and latency, at ~1/4 of its store bandwidth.
-template <bool VEC4, bool ACC>
+template <bool VEC4>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
     RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
-    int low_bits, const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
-    const int32_t* __restrict__ nseg, const int32_t* __restrict__ seg_first,
-    const float* __restrict__ partial, const int32_t* __restrict__ touched,
-    const int32_t* __restrict__ n_touched) {
+    int low_bits, int set_bits, const int32_t* __restrict__ run_start,
+    const int32_t* __restrict__ run_end, const int32_t* __restrict__ nseg,
+    const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
+    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched) {
   const int lane = threadIdx.x & 63;
   const int C = a.C;
   const uint64_t low_mask = (1ull << low_bits) - 1ull;
-  const float inv = a.sr > 0 ? (float)(a.sr * a.sr) : 1.f;
   const int step = VEC4 ? 256 : 64;
   const int nt = *n_touched;
+  const int nsets = 1 << set_bits;
   for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += gridDim.x * 4) {
     const long long pix = touched[t];
     int l = 0;
     while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
-    const int i0 = run_start[pix];
-    const int i1 = run_end[pix];
-    const int ns = nseg[pix];
-    const int f = ns ? seg_first[pix] : 0;
+    const bool acc_lv = (a.acc_mask >> l) & 1;
     for (int c0 = 0; c0 < C; c0 += step) {
       const int c = c0 + (VEC4 ? lane * 4 : lane);
       const bool live = c < C;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ns == 0) {
-        acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live, inv, a.sr > 0);
-      } else if (live) {
-        for (int j = 0; j < ns; ++j) {
-          const float* src = partial + (size_t)(f + j) * C + c;
-          if (VEC4) {
-            const float4 v = *reinterpret_cast<const float4*>(src);
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-          } else {
-            acc.x += *src;
+      float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+      bool any = false;
+      // each set's contributions summed apart (its own TF-order run), then
+      // set 0 + set 1: the rounding of the sum of two separate backwards
+      for (int sidx = 0; sidx < nsets; ++sidx) {
+        const long long q = (pix << set_bits) | sidx;
+        const int i0 = run_start[q];
+        if (i0 < 0) continue;
+        const int i1 = run_end[q];
+        const int ns = nseg[q];
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ns == 0) {
+          acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
+        } else if (live) {
+          const int f = seg_first[q];
+          for (int j = 0; j < ns; ++j) {
+            const float* src = partial + (size_t)(f + j) * C + c;
+            if (VEC4) {
+              const float4 v = *reinterpret_cast<const float4*>(src);
+              acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            } else {
+              acc.x += *src;
+            }
           }
+        }
+        if (any) {
+          res.x = res.x + acc.x; res.y = res.y + acc.y; res.z = res.z + acc.z; res.w = res.w + acc.w;
+        } else {
+          res = acc;
+          any = true;
         }
       }
       if (live) {
-        // ACC: the map already holds another ROI set's gradient (the
-        // hand-off of the box and mask poolers' backwards): old + new, the
-        // same rounding as autograd's sum of the two maps
+        // accumulate: the level's map already holds another gradient of the
+        // same features (a hand-off between backward calls): old + new, the
+        // rounding of autograd's sum of the two maps
         if (VEC4) {
-          if (ACC) {
+          if (acc_lv) {
             const float4 o = *reinterpret_cast<const float4*>(dst + c);
-            acc.x = o.x + acc.x;
-            acc.y = o.y + acc.y;
-            acc.z = o.z + acc.z;
-            acc.w = o.w + acc.w;
+            res.x = o.x + res.x;
+            res.y = o.y + res.y;
+            res.z = o.z + res.z;
+            res.w = o.w + res.w;
           }
-          *reinterpret_cast<float4*>(dst + c) = acc;
+          *reinterpret_cast<float4*>(dst + c) = res;
         } else {
-          dst[c] = ACC ? dst[c] + acc.x : acc.x;
+          dst[c] = acc_lv ? dst[c] + res.x : res.x;
         }
       }
     }
@@ -670,16 +704,18 @@ int bits_for(unsigned long long v) {  // smallest b with 2^b > v
 }
 
 struct BwdPlan {
-  long long total_pixels, n_keys, n_samples, max_segs, max_touched;
-  int low_bits, end_bit;
+  long long total_pixels, pairs, n_keys, n_samples, max_segs, max_touched;
+  int low_bits, end_bit, set_bits;
   PixMap pm;
 };
 
-int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, int sr,
-             BwdPlan* p) {
-  const long long S = sr > 0 ? sr : 1;
-  p->n_samples = (long long)R * out_h * out_w * S * S;
+// n_samples: the sampling points of all ROI sets; set_bits: 1 for a merged
+// two-set backward (runs per (pixel, set) pair), else 0.
+int bwd_plan_n(const int32_t* dims, int num_levels, long long n_samples, int set_bits,
+               BwdPlan* p) {
+  p->n_samples = n_samples;
   p->n_keys = p->n_samples * 4;
+  p->set_bits = set_bits;
   long long t = 0;
   for (int l = 0; l < num_levels; ++l) {
     p->pm.base[l] = t;
@@ -687,31 +723,149 @@ int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, i
   }
   p->pm.base[num_levels] = t;
   p->total_pixels = t;
-  // every split pixel has > kSeg contributions: segments <= 2 * n / kSeg
+  p->pairs = t << set_bits;
+  // every split run has > kSeg contributions: segments <= 2 * n / kSeg
   p->max_segs = 2 * (p->n_keys / kSeg) + 1;
   p->max_touched = std::min(p->n_keys, t);
   p->low_bits = max(1, bits_for(p->n_keys > 0 ? (unsigned long long)(p->n_keys - 1) : 0ull));
-  p->end_bit = p->low_bits + bits_for((unsigned long long)t);
+  p->end_bit = p->low_bits + set_bits + bits_for((unsigned long long)t);
   D2MI_REQUIRE(p->end_bit <= 64, "ROIAlign backward key space too large (%d bits)", p->end_bit);
-  D2MI_REQUIRE(p->n_keys < (1LL << 31) && t < (1LL << 31), "ROIAlign backward too large");
+  D2MI_REQUIRE(p->n_keys < (1LL << 31) && p->pairs < (1LL << 31), "ROIAlign backward too large");
   return 0;
 }
 
-template <typename WS>
-void bwd_layout(WS& w, int R, int C, const BwdPlan& p) {
+int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, int sr,
+             BwdPlan* p) {
+  const long long S = sr > 0 ? sr : 1;
+  return bwd_plan_n(dims, num_levels, (long long)R * out_h * out_w * S * S, 0, p);
+}
+
+template <class WS>
+void bwd_layout(WS& w, int C, const BwdPlan& p) {
   w.template take<uint64_t>((size_t)p.n_keys + 1);          // keys
   w.template take<uint64_t>((size_t)p.n_keys + 1);          // sorted keys
   w.template take<Contrib>((size_t)p.n_samples + 1);        // records
-  w.template take<int32_t>((size_t)p.total_pixels + 1);     // run_start
-  w.template take<int32_t>((size_t)p.total_pixels + 1);     // run_end
-  w.template take<int32_t>((size_t)p.total_pixels + 1);     // nseg
-  w.template take<int32_t>((size_t)p.total_pixels + 1);     // seg_first
+  w.template take<int32_t>((size_t)p.pairs + 1);            // run_start
+  w.template take<int32_t>((size_t)p.pairs + 1);            // run_end
+  w.template take<int32_t>((size_t)p.pairs + 1);            // nseg
+  w.template take<int32_t>((size_t)p.pairs + 1);            // seg_first
   w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
   w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
   w.template take<int32_t>(1);                              // their count
   w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
-                            exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1)));
+                            exclusive_scan_i32_workspace_size((size_t)p.pairs + 1)));
+}
+
+// The backward over nsets (1 or 2) ROI sets of the same maps; sets[k] holds
+// each set's ROIs / crop / grad_out (everything else equal).
+int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_levels, int C,
+                 int acc_mask, bool vec4, void* workspace, size_t workspace_bytes,
+                 hipStream_t st) {
+  RoiArgs a = sets[0];
+  a.acc_mask = acc_mask;
+  long long ns[2] = {0, 0};
+  for (int k = 0; k < nsets; ++k) {
+    const long long S = sets[k].sr > 0 ? sets[k].sr : 1;
+    ns[k] = (long long)sets[k].R * sets[k].out_h * sets[k].out_w * S * S;
+    a.gout_s[k] = sets[k].gout;
+    a.sr_s[k] = sets[k].sr;
+  }
+  const int sb = nsets > 1 ? 1 : 0;
+  BwdPlan p;
+  int rc = bwd_plan_n(dims, num_levels, ns[0] + ns[1], sb, &p);
+  if (rc) return rc;
+  WorkspaceSizer z;
+  bwd_layout(z, C, p);
+  D2MI_REQUIRE(workspace_bytes >= z.off && (workspace || z.off == 0),
+               "ROIAlign backward workspace too small: %zu < %zu", workspace_bytes, z.off);
+  if (p.total_pixels == 0) return 0;
+  Workspace w(workspace, workspace_bytes);
+  uint64_t* keys = w.take<uint64_t>((size_t)p.n_keys + 1);
+  uint64_t* sorted = w.take<uint64_t>((size_t)p.n_keys + 1);
+  Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
+  int32_t* run_start = w.take<int32_t>((size_t)p.pairs + 1);
+  int32_t* run_end = w.take<int32_t>((size_t)p.pairs + 1);
+  int32_t* nseg = w.take<int32_t>((size_t)p.pairs + 1);
+  int32_t* seg_first = w.take<int32_t>((size_t)p.pairs + 1);
+  int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
+  float* partial = w.take<float>((size_t)p.max_segs * C);
+  int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
+  int32_t* n_touched = w.take<int32_t>(1);
+  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
+                               exclusive_scan_i32_workspace_size((size_t)p.pairs + 1));
+  void* tmp = w.take<char>(tmp_bytes);
+  const long long TQ = p.pairs;
+  ClearList cl = {};
+  long long clear_words = 0;
+  auto clear = [&](void* ptr, long long words, uint32_t value) {
+    cl.ptr[cl.n] = static_cast<uint32_t*>(ptr);
+    cl.words[cl.n] = words;
+    cl.value[cl.n] = value;
+    ++cl.n;
+    clear_words += words;
+  };
+  for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero (accumulated levels: kept)
+    if (!((acc_mask >> l) & 1))
+      clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
+  clear(run_start, TQ, 0xffffffffu);
+  clear(n_touched, 1, 0u);
+  hipLaunchKernelGGL(roi_bwd_clear_kernel,
+                     dim3((unsigned)std::max(1LL, std::min((clear_words / 4 + 255) / 256, 8192LL))),
+                     dim3(256), 0, st, cl);
+  D2MI_LAUNCH_CHECK();
+  if (p.n_keys > 0) {
+    long long base = 0;
+    for (int k = 0; k < nsets; ++k) {
+      if (ns[k] > 0) {
+        hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((ns[k] + 255) / 256)), dim3(256),
+                           0, st, sets[k], p.pm, p.low_bits, k, sb, base, keys, rec);
+        D2MI_LAUNCH_CHECK();
+      }
+      base += ns[k];
+    }
+    // pair bits only: the sort is stable and the keys are emitted in slot
+    // (TF loop) order, so each (pixel, set) run stays in that order
+    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.low_bits, p.end_bit, tmp, tmp_bytes,
+                        st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
+                       0, st, sorted, p.n_keys, p.low_bits, sb, p.total_pixels, run_start, run_end,
+                       touched, n_touched);
+    D2MI_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(roi_bwd_nseg_kernel, dim3((unsigned)((TQ + 1 + 255) / 256)), dim3(256), 0, st,
+                     run_start, run_end, TQ, nseg);
+  D2MI_LAUNCH_CHECK();
+  rc = exclusive_scan_i32(nseg, seg_first, (size_t)TQ + 1, tmp, tmp_bytes, st);
+  if (rc) return rc;
+  if (p.n_keys == 0) return 0;
+  hipLaunchKernelGGL(roi_bwd_segpix_kernel, dim3((unsigned)((TQ + 255) / 256)), dim3(256), 0, st,
+                     nseg, seg_first, TQ, seg_pixel);
+  D2MI_LAUNCH_CHECK();
+  const dim3 sgrid((unsigned)((p.max_segs + 3) / 4));
+  if (vec4)
+    hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted, rec,
+                       p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TQ,
+                       partial);
+  else
+    hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted, rec,
+                       p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TQ,
+                       partial);
+  D2MI_LAUNCH_CHECK();
+  // fixed grid (the touched count stays on the device): at most 8192
+  // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
+  // beyond residency start as earlier ones retire (the kBatch sweep above)
+  const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
+#define PIX(V)                                                                            \
+  hipLaunchKernelGGL((roi_bwd_pixel_kernel<V>), grid, dim3(256), 0, st, a, p.pm, sorted, rec, \
+                     p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,  \
+                     n_touched)
+  if (vec4) PIX(true);
+  else PIX(false);
+#undef PIX
+  D2MI_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace
@@ -724,7 +878,7 @@ extern "C" size_t d2mi_roi_align_bwd_workspace_size(const int32_t* dims, int num
   BwdPlan p;
   if (bwd_plan(dims, num_levels, R, out_h, out_w, sampling_ratio, &p)) return 0;
   WorkspaceSizer w;
-  bwd_layout(w, R, C, p);
+  bwd_layout(w, C, p);
   return w.off;
 }
 
@@ -747,98 +901,55 @@ extern "C" int d2mi_roi_align_bwd_ex(float* const* grad_feats, const int32_t* di
     vec4 = vec4 && (((uintptr_t)grad_feats[l] & 15) == 0);
   }
   a.gout = grad_out;
+  return roi_bwd_core(&a, 1, dims, num_levels, C, accumulate ? (1 << num_levels) - 1 : 0, vec4,
+                      workspace, workspace_bytes, as_stream(stream));
+}
+
+extern "C" size_t d2mi_roi_align_bwd2_workspace_size(const int32_t* dims, int num_levels, int C,
+                                                     int R0, int out_h0, int out_w0, int sr0,
+                                                     int R1, int out_h1, int out_w1, int sr1) {
+  if (!dims || num_levels < 1 || num_levels > D2MI_MAX_LEVELS || R0 < 0 || R1 < 0 || C < 1)
+    return 0;
+  const long long S0 = sr0 > 0 ? sr0 : 1, S1 = sr1 > 0 ? sr1 : 1;
   BwdPlan p;
-  rc = bwd_plan(dims, num_levels, R, out_h, out_w, sampling_ratio, &p);
+  if (bwd_plan_n(dims, num_levels,
+                 (long long)R0 * out_h0 * out_w0 * S0 * S0 + (long long)R1 * out_h1 * out_w1 * S1 * S1,
+                 1, &p))
+    return 0;
+  WorkspaceSizer w;
+  bwd_layout(w, C, p);
+  return w.off;
+}
+
+extern "C" int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims,
+                                   const float* scales, int num_levels, int C, int box_mode,
+                                   int pad_border, int assign, int min_level, int max_level,
+                                   int canonical_box_size, int canonical_level,
+                                   const float* boxes0, const int32_t* box_ind0, int R0,
+                                   int out_h0, int out_w0, int sr0, const float* grad_out0,
+                                   const float* boxes1, const int32_t* box_ind1, int R1,
+                                   int out_h1, int out_w1, int sr1, const float* grad_out1,
+                                   int accumulate_mask, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+  RoiArgs sets[2] = {};
+  int rc = fill_args(sets[0], dims, scales, num_levels, C, boxes0, box_ind0, R0, out_h0, out_w0,
+                     sr0, box_mode, pad_border, assign, min_level, max_level, canonical_box_size,
+                     canonical_level);
   if (rc) return rc;
-  const size_t need = d2mi_roi_align_bwd_workspace_size(dims, num_levels, C, R, out_h, out_w,
-                                                        sampling_ratio);
-  D2MI_REQUIRE(workspace_bytes >= need && (workspace || need == 0),
-               "ROIAlign backward workspace too small: %zu < %zu", workspace_bytes, need);
-  if (p.total_pixels == 0) return 0;
-  hipStream_t st = as_stream(stream);
-  Workspace w(workspace, workspace_bytes);
-  uint64_t* keys = w.take<uint64_t>((size_t)p.n_keys + 1);
-  uint64_t* sorted = w.take<uint64_t>((size_t)p.n_keys + 1);
-  Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
-  int32_t* run_start = w.take<int32_t>((size_t)p.total_pixels + 1);
-  int32_t* run_end = w.take<int32_t>((size_t)p.total_pixels + 1);
-  int32_t* nseg = w.take<int32_t>((size_t)p.total_pixels + 1);
-  int32_t* seg_first = w.take<int32_t>((size_t)p.total_pixels + 1);
-  int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
-  float* partial = w.take<float>((size_t)p.max_segs * C);
-  int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
-  int32_t* n_touched = w.take<int32_t>(1);
-  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
-                               exclusive_scan_i32_workspace_size((size_t)p.total_pixels + 1));
-  void* tmp = w.take<char>(tmp_bytes);
-  const long long TP = p.total_pixels;
-  ClearList cl = {};
-  long long clear_words = 0;
-  auto clear = [&](void* ptr, long long words, uint32_t value) {
-    cl.ptr[cl.n] = static_cast<uint32_t*>(ptr);
-    cl.words[cl.n] = words;
-    cl.value[cl.n] = value;
-    ++cl.n;
-    clear_words += words;
-  };
-  if (!accumulate)  // untouched pixels: zero gradient (accumulate: left as they are)
-    for (int l = 0; l < num_levels; ++l)
-      clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
-  clear(run_start, TP, 0xffffffffu);
-  clear(n_touched, 1, 0u);
-  hipLaunchKernelGGL(roi_bwd_clear_kernel,
-                     dim3((unsigned)std::max(1LL, std::min((clear_words / 4 + 255) / 256, 8192LL))),
-                     dim3(256), 0, st, cl);
-  D2MI_LAUNCH_CHECK();
-  if (p.n_keys > 0) {
-    hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((p.n_samples + 255) / 256)), dim3(256),
-                       0, st, a, p.pm, p.low_bits, keys, rec);
-    D2MI_LAUNCH_CHECK();
-    // pixel bits only: the sort is stable and the keys are emitted in slot
-    // (TF loop) order, so each pixel's run stays in that order
-    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.low_bits, p.end_bit, tmp, tmp_bytes,
-                        st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
-                       0, st, sorted, p.n_keys, p.low_bits, TP, run_start, run_end, touched,
-                       n_touched);
-    D2MI_LAUNCH_CHECK();
-  }
-  hipLaunchKernelGGL(roi_bwd_nseg_kernel, dim3((unsigned)((TP + 1 + 255) / 256)), dim3(256), 0, st,
-                     run_start, run_end, TP, nseg);
-  D2MI_LAUNCH_CHECK();
-  rc = exclusive_scan_i32(nseg, seg_first, (size_t)TP + 1, tmp, tmp_bytes, st);
+  rc = fill_args(sets[1], dims, scales, num_levels, C, boxes1, box_ind1, R1, out_h1, out_w1, sr1,
+                 box_mode, pad_border, assign, min_level, max_level, canonical_box_size,
+                 canonical_level);
   if (rc) return rc;
-  if (p.n_keys > 0) {
-    hipLaunchKernelGGL(roi_bwd_segpix_kernel, dim3((unsigned)((TP + 255) / 256)), dim3(256), 0, st,
-                       nseg, seg_first, TP, seg_pixel);
-    D2MI_LAUNCH_CHECK();
-    const dim3 sgrid((unsigned)((p.max_segs + 3) / 4));
-    if (vec4)
-      hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                         p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TP,
-                         partial);
-    else
-      hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                         p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TP,
-                         partial);
-    D2MI_LAUNCH_CHECK();
+  bool vec4 = (C % 4) == 0 && ((uintptr_t)grad_out0 & 15) == 0 && ((uintptr_t)grad_out1 & 15) == 0;
+  for (int l = 0; l < num_levels; ++l) {
+    sets[0].gfeat[l] = sets[1].gfeat[l] = grad_feats[l];
+    vec4 = vec4 && (((uintptr_t)grad_feats[l] & 15) == 0);
   }
-  if (p.n_keys == 0) return 0;
-  // fixed grid (the touched count stays on the device): at most 8192
-  // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
-  // beyond residency start as earlier ones retire (the kBatch sweep above)
-  const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
-#define PIX(V, A)                                                                            \
-  hipLaunchKernelGGL((roi_bwd_pixel_kernel<V, A>), grid, dim3(256), 0, st, a, p.pm, sorted, rec, \
-                     p.low_bits, run_start, run_end, nseg, seg_first, partial, touched, n_touched)
-  if (vec4 && accumulate) PIX(true, true);
-  else if (vec4) PIX(true, false);
-  else if (accumulate) PIX(false, true);
-  else PIX(false, false);
-#undef PIX
-  D2MI_LAUNCH_CHECK();
-  return 0;
+  sets[0].gout = grad_out0;
+  sets[1].gout = grad_out1;
+  D2MI_REQUIRE((accumulate_mask >> num_levels) == 0, "accumulate_mask has bits past the levels");
+  return roi_bwd_core(sets, 2, dims, num_levels, C, accumulate_mask, vec4, workspace,
+                      workspace_bytes, as_stream(stream));
 }
 
 extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,

@@ -121,6 +121,9 @@ class _RoIAlignFn(torch.autograd.Function):
         ctx.params = params
         ctx.share = grad_share
         ctx.shapes = [f.shape for f in feats]
+        # per-level input-gradient hand-off with another consumer of the same
+        # maps (the RPN head conv: ops / convolutional pair_grad protocol)
+        ctx.pairs = [getattr(f, "_d2mi_grad_pair", None) for f in feats]
         ctx.save_for_backward(boxes, box_ind)
         ctx.set_materialize_grads(False)  # level (non-differentiable): no zero grad
         if level is not None:
@@ -135,6 +138,28 @@ class _RoIAlignFn(torch.autograd.Function):
         (out_h, out_w, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l,
          _) = ctx.params
         share = ctx.share
+        if share is not None and MERGED_BWD and grad_out.shape[-1] >= 64:
+            # a pair of poolings of the same maps: the first backward only
+            # leaves its grad_out; the second runs ONE backward over both ROI
+            # sets (one emit per set, one sort, one gather pass summing each
+            # set's run apart, set 0 + set 1)
+            first = share.pop("set0", None)
+            g = _f32c(grad_out)
+            if first is None:
+                share["set0"] = (boxes, box_ind, g, ctx.params)
+                return (None,) * (4 + len(ctx.shapes))
+            # levels whose other consumer already left its input gradient:
+            # accumulate into it; the others: written here and left for it
+            given = [pr.pop("g", None) if pr is not None else None for pr in ctx.pairs]
+            grads = _roi_align_bwd2(first, (boxes, box_ind, g, ctx.params), ctx.shapes, given)
+            out = []
+            for pr, gv, gr in zip(ctx.pairs, given, grads):
+                if pr is not None and gv is None:
+                    pr["g"] = gr  # the other consumer adds it in its dgrad epilogue
+                    out.append(None)
+                else:
+                    out.append(gr)
+            return (None, None, None, None, *out)
         prior = share.pop("maps", None) if share is not None else None
         if prior is not None:  # second of a pair: add into the first's maps
             grads = prior
@@ -164,6 +189,55 @@ class _RoIAlignFn(torch.autograd.Function):
             share["maps"] = grads
             return (None,) * (4 + len(grads))
         return (None, None, None, None, *grads)
+
+
+# The box and mask poolers' backwards as one merged backward (False: two
+# backwards, the second accumulating into the first's maps; tests compare).
+MERGED_BWD = True
+
+
+def _roi_align_bwd2(set0, set1, shapes, given=None):
+    """d2mi_roi_align_bwd2 over two (boxes, box_ind, grad_out, params) sets
+    of the same feature maps (equal level / box-mode parameters).  given[l]:
+    a gradient map of level l to accumulate into (returned), or None."""
+    b0, i0, g0, p0 = set0
+    b1, i1, g1, p1 = set1
+    if p0[2] != p1[2] or p0[4:11] != p1[4:11]:  # scales, box mode .. canonical level
+        raise ValueError("merged ROIAlign backward: the two poolings differ beyond their crops")
+    (oh0, ow0, scales, sr0, mode, pad, assign, min_l, max_l, canon_s, canon_l, _) = p0
+    oh1, ow1, sr1 = p1[0], p1[1], p1[3]
+    dev = b0.device
+    given = given or [None] * len(shapes)
+    grads, acc_mask = [], 0
+    for l, (s, gv) in enumerate(zip(shapes, given)):
+        if gv is not None and tuple(gv.shape) == tuple(s) and gv.dtype == torch.float32 \
+                and gv.is_contiguous():
+            grads.append(gv)
+            acc_mask |= 1 << l
+        elif gv is not None:
+            grads.append(_f32c(gv).clone())
+            acc_mask |= 1 << l
+        else:
+            grads.append(torch.empty(s, dtype=torch.float32, device=dev))
+    gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
+    dims = _C.host_array(_C.ctypes.c_int32, [v for s in shapes for v in (s[0], s[1], s[2])])
+    sc = _C.host_array(_C.c_float, list(scales))
+    C = shapes[0][-1]
+    R0, R1 = b0.shape[0], b1.shape[0]
+    lib = _C.lib()
+    wsb = lib.d2mi_roi_align_bwd2_workspace_size(dims, len(grads), C, R0, oh0, ow0, sr0, R1, oh1,
+                                                 ow1, sr1)
+    ws = _C.workspace(wsb, dev)
+    ev = KernelTimer.start()
+    rc = lib.d2mi_roi_align_bwd2(gp, dims, sc, len(grads), C, mode, pad, assign, min_l, max_l,
+                                 canon_s, canon_l, _C.ptr(b0), _C.ptr(i0), R0, oh0, ow0, sr0,
+                                 _C.ptr(g0), _C.ptr(b1), _C.ptr(i1), R1, oh1, ow1, sr1, _C.ptr(g1),
+                                 acc_mask, _C.ptr(ws), wsb, _C.stream_of(dev))
+    S0, S1 = max(sr0, 1) ** 2, max(sr1, 1) ** 2
+    KernelTimer.stop(ev, "roi_align_bwd", R0 * oh0 * ow0 * C * (4 + 32 * S0) +
+                     R1 * oh1 * ow1 * C * (4 + 32 * S1))
+    _C.check(rc, "d2mi_roi_align_bwd2")
+    return grads
 
 
 def roi_align(features, boxes, box_ind, output_size, scales, sampling_ratio=0, aligned=True,

@@ -57,12 +57,32 @@ class GeneralizedRCNN(_Preprocess, Layer):
         self.segmentation_output_format = cfg.MODEL.SEGMENTATION_OUTPUT.FORMAT
         self.segmentation_output_resolution = cfg.MODEL.SEGMENTATION_OUTPUT.FIXED_RESOLUTION
 
+    def _tag_shared_levels(self, features):
+        """FPN levels read by both the RPN head conv and the ROI poolers get a
+        gradient hand-off dict (the pair_grad protocol): whichever backward
+        runs first leaves its input gradient there and the other adds into it
+        (the RPN dgrad epilogue, or the merged ROIAlign backward accumulating
+        at touched pixels) -- no autograd add of two full maps, no zero-fill
+        of the pooled levels.  Only when the ROI heads take the merged
+        backward (box + mask poolers), which always consumes the hand-off."""
+        from ...layers import ops
+        rh, pg = self.roi_heads, self.proposal_generator
+        if (pg is None or not getattr(rh, "mask_on", False) or not ops.MERGED_BWD
+                or not hasattr(pg, "rpn_head")):
+            return
+        shared = set(rh.in_features) & set(getattr(pg, "in_features", ()))
+        for f in shared:
+            t = features[f]
+            if t.is_cuda and t.requires_grad and t.shape[-1] >= 64:
+                t._d2mi_grad_pair = {}
+
     def call(self, batched_inputs):
         if not self.training:
             return self.inference(batched_inputs)
         images = self.preprocess_image(batched_inputs)
         gt = batched_inputs.get("instances", batched_inputs.get("targets"))
         features = self.neck(self.backbone(images.tensor))
+        self._tag_shared_levels(features)
         if self.proposal_generator is not None:
             proposals, proposal_losses, _ = self.proposal_generator(images, features, gt)
         else:

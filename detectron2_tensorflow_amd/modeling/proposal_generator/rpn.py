@@ -76,7 +76,9 @@ class StandardRPNHead(Layer):
                 deltas.append(y[..., A:A + D].contiguous())
             return shares, logits, deltas
         for x in features:
-            share = self.conv(x)
+            # a level the ROI poolers also read hands its input gradient over
+            # (GeneralizedRCNN tags them; the pair_grad protocol)
+            share = self.conv(x, pair_grad=getattr(x, "_d2mi_grad_pair", None))
             rpn_features.append(share)
             if fuse:
                 w16, wp, b16 = self._fused_1x1()

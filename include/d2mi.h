@@ -103,6 +103,29 @@ int d2mi_roi_align_bwd_ex(float* const* grad_feats, const int32_t* dims, const f
                           int canonical_box_size, int canonical_level, const float* grad_out,
                           int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
+/* One backward over TWO ROI sets pooled from the same maps -- the box (7x7)
+ * and mask (14x14) poolers of a training step (roi_heads.py:497-605), whose
+ * CropAndResizeGradImage maps TF sums (AddN): one emit per set, ONE sort on
+ * (pixel, set) keys, one gather pass that sums each set's contributions in
+ * its TF order and writes set0 + set1 (untouched pixels 0).  Every element
+ * of grad_feats is written, except for the levels whose bit is set in
+ * accumulate_mask: their maps already hold another gradient of the same
+ * features (the RPN head's input gradient, rpn.py:83-96 reading the same
+ * p2..p5) and get old + (set0 + set1) at touched pixels only (no clear, no
+ * separate add).  Geometry / level parameters are shared; each set has its
+ * ROIs, crop size, sampling ratio and grad_out. */
+size_t d2mi_roi_align_bwd2_workspace_size(const int32_t* dims, int num_levels, int C, int R0,
+                                          int out_h0, int out_w0, int sr0, int R1, int out_h1,
+                                          int out_w1, int sr1);
+int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims, const float* scales,
+                        int num_levels, int C, int box_mode, int pad_border, int assign,
+                        int min_level, int max_level, int canonical_box_size, int canonical_level,
+                        const float* boxes0, const int32_t* box_ind0, int R0, int out_h0,
+                        int out_w0, int sr0, const float* grad_out0, const float* boxes1,
+                        const int32_t* box_ind1, int R1, int out_h1, int out_w1, int sr1,
+                        const float* grad_out1, int accumulate_mask, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------- NMS
  * Segmented greedy NMS with TF NonMaxSuppressionV3 semantics
  * (score_threshold = -inf; IoU with min/max-normalised corners, 0 when an

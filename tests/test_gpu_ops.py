@@ -1088,11 +1088,24 @@ def test_fused_stem_pool_matches_unfused(dev):
     assert torch.equal(got, want)
 
 
-def test_roi_align_backward_grad_share_matches_autograd_sum(dev):
+@pytest.mark.parametrize("merged", [True, False])
+def test_roi_align_backward_grad_share_matches_autograd_sum(dev, merged):
     """Two poolings of the same p2..p5 maps (the box 7x7 and mask 14x14 poolers
-    of a training step) with grad_share: one gradient map set written by the
-    first backward and accumulated into by the second (d2mi_roi_align_bwd_ex
-    accumulate) == autograd's sum of two independent backwards, bit for bit."""
+    of a training step) with grad_share == autograd's sum of two independent
+    backwards, bit for bit: merged = ONE backward over both ROI sets
+    (d2mi_roi_align_bwd2: one sort on (pixel, set) keys, each set's run summed
+    apart, then added); else the first backward writes the maps and the second
+    accumulates into them (d2mi_roi_align_bwd_ex accumulate).  Small boxes
+    pile > 64 contributions onto single pixels (the split-run path)."""
+    import detectron2_tensorflow_amd.layers.ops as O
+    O.MERGED_BWD = merged
+    try:
+        _grad_share_case(dev)
+    finally:
+        O.MERGED_BWD = True
+
+
+def _grad_share_case(dev):
     rng = np.random.default_rng(45)
     N, IH, IW, C = 2, 256, 320, 64
     strides = [4, 8, 16, 32]
