@@ -282,15 +282,19 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 //      geometry is computed in place);
 //   2. stable onesweep radix sort on the pixel bits only: pixel-major, and
 //      within a pixel the emission (TF loop) order is kept;
-//   3. runs: first / end key of every touched pixel;
-//   4. pixels with more than kSeg contributions are split into kSeg-long
-//      segments (exclusive scan of their segment counts) summed by one wave
-//      each into a partial row — bounded work per wave however many ROIs pile
-//      onto one pixel (collapsed proposals at the image border do);
-//   5. the grad maps are zero-filled (memset, full bandwidth) and the touched
-//      pixels (compact list from step 3) are summed by waves striding over
-//      that list, lanes over channels (float4): each sums its contributions
-//      (or its segments' partials) in order and stores the pixel once.
+//   3. runs (one kernel): the touched-pixel list, each run's bounds, and for
+//      runs with more than kSeg contributions a block of kSeg-long segments
+//      (slots from a counter) summed by one wave each into a partial row —
+//      bounded work per wave however many ROIs pile onto one pixel (collapsed
+//      proposals at the image border do);
+//   4. the grad maps are zero-filled (one clear launch, full bandwidth) and
+//      the touched pixels are summed by waves striding over that list, four
+//      pixels per wave at C = 256 (16 lanes x 16 channels each): each sums its
+//      contributions (or its segments' partials) in order and stores the
+//      pixel once.
+// Two ROI sets of the same maps (the box and mask poolers, d2mi_roi_align_bwd2)
+// share one pass: keys carry (pixel, set), each set's run is summed apart and
+// the two sums added.
 // Summation order per pixel is (box, y, x, corner), the TF kernel's loop order
 // (partials regroup it for pixels past kSeg): deterministic run to run, and
 // bit-identical to the TF scatter for pixels with at most kSeg contributions
@@ -389,12 +393,21 @@ __global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, int set,
 // run_start[p] = first sorted index of pixel p (-1 untouched), run_end[p] = one past its last.
 // Every touched pixel is also appended to touched[] (*n_touched entries; the
 // list order varies run to run, the per-pixel sums do not).
-// With set_bits = 1 the runs are per (pixel, set) pair (run_start / run_end
-// indexed by pixel * 2 + set) and touched[] lists each pixel once.
+// One thread per sorted key.  The first key of a pixel appends the pixel to
+// touched[] (workgroup-aggregated counter); the first key of a (pixel, set)
+// run (set_bits = 1: runs per pair, indexed pixel * 2 + set) records the run:
+// start, end (found by walking the sorted keys: runs are a handful of keys),
+// and for a run longer than kSeg its segment count, a block of segment slots
+// taken from *n_segs and the slots' owner -- the split-run bookkeeping that
+// took a per-pixel pass, a scan and a fill pass before.  Slot order varies run
+// to run; each run's partials are summed in segment order (deterministic).
 __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
                                     int set_bits, long long total_pixels,
                                     int32_t* __restrict__ run_start,
-                                    int32_t* __restrict__ run_end, int32_t* __restrict__ touched,
+                                    int32_t* __restrict__ run_end, int32_t* __restrict__ nseg,
+                                    int32_t* __restrict__ seg_first,
+                                    int32_t* __restrict__ seg_pixel, int32_t* __restrict__ n_segs,
+                                    int32_t* __restrict__ touched,
                                     int32_t* __restrict__ n_touched) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t q = i < n ? keys[i] >> low_bits : ~0ull;  // pair
@@ -419,33 +432,21 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __re
   __syncthreads();
   base += wg_base;
   if (first) touched[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
-  if (first_pair) run_start[q] = (int32_t)i;
-  if (live && (i == n - 1 || (keys[i + 1] >> low_bits) != q)) run_end[q] = (int32_t)(i + 1);
-}
-
-// nseg[p] = number of kSeg segments of pixel p when it has more than kSeg
-// contributions, else 0; nseg[total_pixels] = 0 (scan sentinel).
-__global__ void roi_bwd_nseg_kernel(const int32_t* __restrict__ run_start,
-                                    const int32_t* __restrict__ run_end, long long total_pixels,
-                                    int32_t* __restrict__ nseg) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p > total_pixels) return;
-  int v = 0;
-  if (p < total_pixels && run_start[p] >= 0) {
-    const int len = run_end[p] - run_start[p];
-    v = len > kSeg ? (len + kSeg - 1) / kSeg : 0;
+  if (first_pair) {
+    long long j = i + 1;
+    while (j < n && (keys[j] >> low_bits) == q) ++j;
+    const int len = (int)(j - i);
+    run_start[q] = (int32_t)i;
+    run_end[q] = (int32_t)j;
+    int ns = 0;
+    if (len > kSeg) {
+      ns = (len + kSeg - 1) / kSeg;
+      const int f = atomicAdd(n_segs, ns);
+      seg_first[q] = f;
+      for (int k = 0; k < ns; ++k) seg_pixel[f + k] = (int32_t)q;
+    }
+    nseg[q] = ns;
   }
-  nseg[p] = v;
-}
-
-__global__ void roi_bwd_segpix_kernel(const int32_t* __restrict__ nseg,
-                                      const int32_t* __restrict__ seg_first, long long total_pixels,
-                                      int32_t* __restrict__ seg_pixel) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= total_pixels) return;
-  const int k = nseg[p];
-  const int f = seg_first[p];
-  for (int j = 0; j < k; ++j) seg_pixel[f + j] = (int32_t)p;
 }
 
 // TF order of operations: dtop = (1 - y_lerp) * g, dbot = y_lerp * g, then
@@ -511,23 +512,24 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
     const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
     const int32_t* __restrict__ seg_first, const int32_t* __restrict__ seg_pixel,
     const int32_t* __restrict__ total_segs, float* __restrict__ partial) {
-  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (seg >= *total_segs) return;
-  const int p = seg_pixel[seg];
-  const int k = seg - seg_first[p];
-  const int i0 = run_start[p] + k * kSeg;
-  const int i1 = min(i0 + kSeg, run_end[p]);
+  const int nsegs = *total_segs;
   const uint64_t low_mask = (1ull << low_bits) - 1ull;
   const int step = VEC4 ? 256 : 64;
-  for (int c0 = 0; c0 < a.C; c0 += step) {
-    const int c = c0 + (VEC4 ? lane * 4 : lane);
-    const bool live = c < a.C;
-    const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
-    if (live) {
-      float* dst = partial + (size_t)seg * a.C + c;
-      if (VEC4) *reinterpret_cast<float4*>(dst) = acc;
-      else *dst = acc.x;
+  for (int seg = blockIdx.x * 4 + (threadIdx.x >> 6); seg < nsegs; seg += gridDim.x * 4) {
+    const int p = seg_pixel[seg];
+    const int k = seg - seg_first[p];
+    const int i0 = run_start[p] + k * kSeg;
+    const int i1 = min(i0 + kSeg, run_end[p]);
+    for (int c0 = 0; c0 < a.C; c0 += step) {
+      const int c = c0 + (VEC4 ? lane * 4 : lane);
+      const bool live = c < a.C;
+      const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
+      if (live) {
+        float* dst = partial + (size_t)seg * a.C + c;
+        if (VEC4) *reinterpret_cast<float4*>(dst) = acc;
+        else *dst = acc.x;
+      }
     }
   }
 }
@@ -609,6 +611,101 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
           dst[c] = acc_lv ? dst[c] + res.x : res.x;
         }
       }
+    }
+  }
+}
+
+// C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
+// once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
+// independent load chains (run bounds -> keys -> records -> grad_out rows)
+// in flight per wave instead of one, the same per-pixel order and rounding.
+__global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
+    RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
+    int low_bits, int set_bits, const int32_t* __restrict__ run_start,
+    const int32_t* __restrict__ run_end, const int32_t* __restrict__ nseg,
+    const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
+    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched) {
+  constexpr int C = 256;
+  const int lane = threadIdx.x & 63;
+  const int grp = lane >> 4, sub = lane & 15;
+  const int c = sub * 16;  // this lane's 16 channels
+  const uint64_t low_mask = (1ull << low_bits) - 1ull;
+  const int nt = *n_touched;
+  const int nsets = 1 << set_bits;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (int tb = wave * 4; tb < nt; tb += gridDim.x * 16) {
+    const int t = tb + grp;
+    if (t >= nt) continue;
+    const long long pix = touched[t];
+    int l = 0;
+    while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
+    float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
+    float4 res[4];
+    bool any = false;
+    for (int sidx = 0; sidx < nsets; ++sidx) {
+      const long long q = (pix << set_bits) | sidx;
+      const int i0 = run_start[q];
+      if (i0 < 0) continue;
+      const int i1 = run_end[q];
+      const int ns = nseg[q];
+      float4 acc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ns == 0) {
+        for (int i = i0; i < i1; ++i) {
+          const uint64_t slot = keys[i] & low_mask;
+          const int corner = (int)(slot & 3u);
+          const Contrib e = rec[slot >> 2];
+          const float4* src =
+              reinterpret_cast<const float4*>(a.gout_s[e.set] + (size_t)e.row * C + c);
+          float4 v[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = src[k];
+          const int sr = a.sr_s[e.set];
+          const float inv = (float)(sr * sr);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float4 g = v[k];
+            if (sr > 0) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
+            acc[k].x += weigh(corner, e.yl, e.xl, g.x);
+            acc[k].y += weigh(corner, e.yl, e.xl, g.y);
+            acc[k].z += weigh(corner, e.yl, e.xl, g.z);
+            acc[k].w += weigh(corner, e.yl, e.xl, g.w);
+          }
+        }
+      } else {
+        const int f = seg_first[q];
+        for (int j = 0; j < ns; ++j) {
+          const float4* src = reinterpret_cast<const float4*>(partial + (size_t)(f + j) * C + c);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float4 v = src[k];
+            acc[k].x += v.x; acc[k].y += v.y; acc[k].z += v.z; acc[k].w += v.w;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (any) {
+          res[k].x = res[k].x + acc[k].x; res[k].y = res[k].y + acc[k].y;
+          res[k].z = res[k].z + acc[k].z; res[k].w = res[k].w + acc[k].w;
+        } else {
+          res[k] = acc[k];
+        }
+      }
+      any = true;
+    }
+    if (!any) continue;
+    const bool acc_lv = (a.acc_mask >> l) & 1;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (acc_lv) {
+        const float4 o = d4[k];
+        res[k].x = o.x + res[k].x; res[k].y = o.y + res[k].y;
+        res[k].z = o.z + res[k].z; res[k].w = o.w + res[k].w;
+      }
+      d4[k] = res[k];
     }
   }
 }
@@ -752,9 +849,8 @@ void bwd_layout(WS& w, int C, const BwdPlan& p) {
   w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
   w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
-  w.template take<int32_t>(1);                              // their count
-  w.template take<char>(max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
-                            exclusive_scan_i32_workspace_size((size_t)p.pairs + 1)));
+  w.template take<int32_t>(2);                              // their count, segment count
+  w.template take<char>(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit));
 }
 
 // The backward over nsets (1 or 2) ROI sets of the same maps; sets[k] holds
@@ -791,9 +887,9 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
   float* partial = w.take<float>((size_t)p.max_segs * C);
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
-  int32_t* n_touched = w.take<int32_t>(1);
-  const size_t tmp_bytes = max(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit),
-                               exclusive_scan_i32_workspace_size((size_t)p.pairs + 1));
+  int32_t* n_touched = w.take<int32_t>(2);  // [0] touched pixels, [1] segment slots
+  int32_t* n_segs = n_touched + 1;
+  const size_t tmp_bytes = radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit);
   void* tmp = w.take<char>(tmp_bytes);
   const long long TQ = p.pairs;
   ClearList cl = {};
@@ -809,7 +905,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     if (!((acc_mask >> l) & 1))
       clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
   clear(run_start, TQ, 0xffffffffu);
-  clear(n_touched, 1, 0u);
+  clear(n_touched, 2, 0u);
   hipLaunchKernelGGL(roi_bwd_clear_kernel,
                      dim3((unsigned)std::max(1LL, std::min((clear_words / 4 + 255) / 256, 8192LL))),
                      dim3(256), 0, st, cl);
@@ -831,27 +927,19 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     if (rc) return rc;
     hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
                        0, st, sorted, p.n_keys, p.low_bits, sb, p.total_pixels, run_start, run_end,
-                       touched, n_touched);
+                       nseg, seg_first, seg_pixel, n_segs, touched, n_touched);
     D2MI_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(roi_bwd_nseg_kernel, dim3((unsigned)((TQ + 1 + 255) / 256)), dim3(256), 0, st,
-                     run_start, run_end, TQ, nseg);
-  D2MI_LAUNCH_CHECK();
-  rc = exclusive_scan_i32(nseg, seg_first, (size_t)TQ + 1, tmp, tmp_bytes, st);
-  if (rc) return rc;
   if (p.n_keys == 0) return 0;
-  hipLaunchKernelGGL(roi_bwd_segpix_kernel, dim3((unsigned)((TQ + 255) / 256)), dim3(256), 0, st,
-                     nseg, seg_first, TQ, seg_pixel);
-  D2MI_LAUNCH_CHECK();
-  const dim3 sgrid((unsigned)((p.max_segs + 3) / 4));
+  // segment partials of the split runs: a grid-stride loop over *n_segs
+  // (usually a handful; bounded by max_segs)
+  const dim3 sgrid((unsigned)std::max(1LL, std::min<long long>((p.max_segs + 3) / 4, 1024LL)));
   if (vec4)
     hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                       p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TQ,
-                       partial);
+                       p.low_bits, run_start, run_end, seg_first, seg_pixel, n_segs, partial);
   else
     hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                       p.low_bits, run_start, run_end, seg_first, seg_pixel, seg_first + TQ,
-                       partial);
+                       p.low_bits, run_start, run_end, seg_first, seg_pixel, n_segs, partial);
   D2MI_LAUNCH_CHECK();
   // fixed grid (the touched count stays on the device): at most 8192
   // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
@@ -861,8 +949,16 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   hipLaunchKernelGGL((roi_bwd_pixel_kernel<V>), grid, dim3(256), 0, st, a, p.pm, sorted, rec, \
                      p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,  \
                      n_touched)
-  if (vec4) PIX(true);
-  else PIX(false);
+  if (vec4 && C == 256) {
+    hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel,
+                       dim3((unsigned)std::max(1LL, std::min((p.max_touched + 15) / 16, 8192LL))),
+                       dim3(256), 0, st, a, p.pm, sorted, rec, p.low_bits, sb, run_start, run_end,
+                       nseg, seg_first, partial, touched, n_touched);
+  } else if (vec4) {
+    PIX(true);
+  } else {
+    PIX(false);
+  }
 #undef PIX
   D2MI_LAUNCH_CHECK();
   return 0;
