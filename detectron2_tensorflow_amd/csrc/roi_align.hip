@@ -619,6 +619,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
 // once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
 // independent load chains (run bounds -> keys -> records -> grad_out rows)
 // in flight per wave instead of one, the same per-pixel order and rounding.
+template <int PPW>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
     int low_bits, int set_bits, const int32_t* __restrict__ run_start,
@@ -626,21 +627,23 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
     const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched) {
   constexpr int C = 256;
+  constexpr int LPP = 64 / PPW;     // lanes per pixel
+  constexpr int F = C / LPP / 4;    // float4 per lane
   const int lane = threadIdx.x & 63;
-  const int grp = lane >> 4, sub = lane & 15;
-  const int c = sub * 16;  // this lane's 16 channels
+  const int grp = lane / LPP, sub = lane % LPP;
+  const int c = sub * 4 * F;  // this lane's channels
   const uint64_t low_mask = (1ull << low_bits) - 1ull;
   const int nt = *n_touched;
   const int nsets = 1 << set_bits;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  for (int tb = wave * 4; tb < nt; tb += gridDim.x * 16) {
+  for (int tb = wave * PPW; tb < nt; tb += gridDim.x * 4 * PPW) {
     const int t = tb + grp;
     if (t >= nt) continue;
     const long long pix = touched[t];
     int l = 0;
     while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
-    float4 res[4];
+    float4 res[F];
     bool any = false;
     for (int sidx = 0; sidx < nsets; ++sidx) {
       const long long q = (pix << set_bits) | sidx;
@@ -648,9 +651,9 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
       if (i0 < 0) continue;
       const int i1 = run_end[q];
       const int ns = nseg[q];
-      float4 acc[4];
+      float4 acc[F];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < F; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (ns == 0) {
         for (int i = i0; i < i1; ++i) {
           const uint64_t slot = keys[i] & low_mask;
@@ -658,13 +661,13 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
           const Contrib e = rec[slot >> 2];
           const float4* src =
               reinterpret_cast<const float4*>(a.gout_s[e.set] + (size_t)e.row * C + c);
-          float4 v[4];
+          float4 v[F];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = src[k];
+          for (int k = 0; k < F; ++k) v[k] = src[k];
           const int sr = a.sr_s[e.set];
           const float inv = (float)(sr * sr);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < F; ++k) {
             float4 g = v[k];
             if (sr > 0) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
             acc[k].x += weigh(corner, e.yl, e.xl, g.x);
@@ -678,14 +681,14 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
         for (int j = 0; j < ns; ++j) {
           const float4* src = reinterpret_cast<const float4*>(partial + (size_t)(f + j) * C + c);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < F; ++k) {
             const float4 v = src[k];
             acc[k].x += v.x; acc[k].y += v.y; acc[k].z += v.z; acc[k].w += v.w;
           }
         }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < F; ++k) {
         if (any) {
           res[k].x = res[k].x + acc[k].x; res[k].y = res[k].y + acc[k].y;
           res[k].z = res[k].z + acc[k].z; res[k].w = res[k].w + acc[k].w;
@@ -699,7 +702,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     const bool acc_lv = (a.acc_mask >> l) & 1;
     float4* d4 = reinterpret_cast<float4*>(dst);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < F; ++k) {
       if (acc_lv) {
         const float4 o = d4[k];
         res[k].x = o.x + res[k].x; res[k].y = o.y + res[k].y;
@@ -950,10 +953,19 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                      p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,  \
                      n_touched)
   if (vec4 && C == 256) {
-    hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel,
-                       dim3((unsigned)std::max(1LL, std::min((p.max_touched + 15) / 16, 8192LL))),
-                       dim3(256), 0, st, a, p.pm, sorted, rec, p.low_bits, sb, run_start, run_end,
-                       nseg, seg_first, partial, touched, n_touched);
+    static const int ppw = [] {
+      const char* e = getenv("D2MI_ROI_BWD_PPW");
+      return e && e[0] == '8' ? 8 : 4;
+    }();
+    const dim3 g4((unsigned)std::max(1LL, std::min((p.max_touched + 4 * ppw - 1) / (4 * ppw), 8192LL)));
+    if (ppw == 8)
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, sorted, rec,
+                         p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,
+                         n_touched);
+    else
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, sorted, rec,
+                         p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,
+                         n_touched);
   } else if (vec4) {
     PIX(true);
   } else {
