@@ -51,9 +51,11 @@ int topk_core(const float* values, const int64_t* seg_start, const int32_t* seg_
               int max_len, int k, int key_mode, float* vals_out, int32_t* idx_out,
               int32_t* count_out, void* ws, size_t ws_bytes, hipStream_t stream);
 // seg_k (device, nullable): per-segment k limit (effective k = min(k, seg_k[s], len)).
+// sampled_floor (key_mode 1 only): try the one-pass sampled-floor select first
+// (topk.hip module comment); the output is the same top-k either way.
 int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* seg_len,
                  const int32_t* seg_k, int S, int max_len, int k, int key_mode, float* vals_out,
                  int32_t* idx_out, int32_t* count_out, void* ws, size_t ws_bytes,
-                 hipStream_t stream);
+                 hipStream_t stream, bool sampled_floor = false);
 
 }  // namespace d2mi

@@ -805,8 +805,9 @@ extern "C" int d2mi_retinanet_inference(const float* const* cls, const float* co
   hipLaunchKernelGGL(seg_setup_kernel, dim3((S + 63) / 64), dim3(64), 0, st, lv, N, K, k,
                      o.seg_start, o.seg_len, o.seg_k);
   D2MI_LAUNCH_CHECK();
+  // sampled floor: exact, and the decode below keeps j < tcount only
   rc = topk_core_ex(cls[0], o.seg_start, o.seg_len, o.seg_k, S, (int)maxlen, k, 1, o.tvals, o.tidx,
-                    o.tcount, o.topk_ws, o.topk_bytes, st);
+                    o.tcount, o.topk_ws, o.topk_bytes, st, /*sampled_floor=*/true);
   if (rc) return rc;
   hipLaunchKernelGGL(fill_u32_kernel, dim3((N + 255) / 256), dim3(256), 0, st, o.maxc, N,
                      0x007fffffu /* orderable(-inf) */);

@@ -33,6 +33,25 @@
 //            workgroups; rank < k scatters straight to the sorted output.
 // Every kernel is launched unconditionally and reads the per-segment state,
 // so the select is a fixed launch sequence (no host synchronisation).
+//
+// Sampled floor (key_mode 1, segments longer than the candidate buffer; the
+// RetinaNet levels: top-1000 of up to 12.1 M scores).  The three histogram
+// passes above cost far more than their reads: every element is an LDS atomic,
+// and detection logits pile into a few 12-bit bins (same-address conflicts).
+// The floor path replaces them with ONE read in the common case:
+//   sample   12-bit histogram of 1/16 of the segment (1,024 contiguous keys out
+//            of every 16,384)
+//   floor    one workgroup per segment: the highest bin whose sampled suffix
+//            count reaches 2 k scaled by the sampling rate; its lowest key,
+//            lowered to the lowest key with the same sigmoid (nothing below
+//            the floor ties with anything above it)
+//   fcollect one pass: every key >= floor -> one of 16 spread slots (block-
+//            aggregated; workgroup b appends to slot b % 16)
+//   decide   k <= |A| <= 8192 (A = the slots compacted): A holds the whole top-k (at least k keys at or
+//            above the floor, all strictly above everything below it in
+//            sigmoid) -> straight to rank; otherwise back to the radix passes,
+//            which then run exactly as without the floor.
+// Exact either way; the sample only decides how often the fallback runs.
 #include "internal.h"
 
 namespace d2mi {
@@ -55,6 +74,9 @@ struct SegState {
   float s_edge;      // sigmoid of the edge value (key_mode 1)
   int32_t nA, nB;    // candidates appended to A / B
   int32_t ncand;     // candidates after resolve (ranked)
+  int32_t pre;       // sampled floor: 2 floor chosen, 1 A is final (skip collect), 0 off
+  uint32_t floor_key;
+  int32_t nF[16];    // sampled floor: candidates per spread slot (fcollect)
 };
 
 __device__ __forceinline__ float sigmoidf_tf(float v) { return 1.f / (1.f + expf(-v)); }
@@ -331,7 +353,7 @@ __global__ __launch_bounds__(kThreads) void topk_collect_kernel(
     uint64_t* __restrict__ candA, uint64_t* __restrict__ candB, int key_mode) {
   const int s = blockIdx.y;
   const SegState x = st[s];
-  if (x.mode == 0 || x.mode == 4) return;
+  if (x.mode == 0 || x.mode == 4 || x.pre == 1) return;
   const int len = seg_len[s];
   const int b = blockIdx.x;
   const float* p = values + seg_start[s];
@@ -456,20 +478,20 @@ __global__ __launch_bounds__(1024) void topk_resolve_kernel(
 }
 
 // Counting rank on the final key (~orderable(score) << 32 | index): a block
-// ranks 64 candidates against all of its segment's, each wave a quarter of them.
-constexpr int kRankI = 64;
-__global__ __launch_bounds__(kThreads) void topk_rank_kernel(
+// ranks 64 candidates against all of its segment's, each of its 16 waves a sixteenth of them.
+constexpr int kRankI = 64, kRankT = 1024, kRankW = kRankT / 64;  // 16 waves split the keys
+__global__ __launch_bounds__(kRankT) void topk_rank_kernel(
     const uint64_t* __restrict__ candA, const SegState* __restrict__ st, int kmax, int key_mode,
     float* __restrict__ vals_out, int32_t* __restrict__ idx_out, int32_t* __restrict__ count_out) {
   extern __shared__ uint64_t sk[];
-  __shared__ uint32_t part[kThreads];
+  __shared__ uint32_t part[kRankT];
   const int s = blockIdx.y;
   const SegState x = st[s];
   const int n = x.mode == 4 ? 0 : x.ncand;
   const int kk = min(x.k, n);
   const int i0 = blockIdx.x * kRankI;
   if (blockIdx.x == 0) {
-    for (int i = kk + threadIdx.x; i < kmax; i += kThreads) {
+    for (int i = kk + threadIdx.x; i < kmax; i += kRankT) {
       vals_out[(size_t)s * kmax + i] = 0.f;
       idx_out[(size_t)s * kmax + i] = -1;
     }
@@ -477,23 +499,43 @@ __global__ __launch_bounds__(kThreads) void topk_rank_kernel(
   }
   if (i0 >= n) return;
   const uint64_t* A = candA + (size_t)s * kCap;
-  for (int j = threadIdx.x; j < n; j += kThreads) {
-    const uint64_t e = A[j];
-    const float sc = key_value(__uint_as_float((uint32_t)(e >> 32)), key_mode);
-    sk[j] = ((uint64_t)(~orderable(sc)) << 32) | (uint32_t)e;
+  // 8 loads in flight per thread (a dependent load per entry was the cost)
+  for (int j0 = 0; j0 < n; j0 += 8 * kRankT) {
+    uint64_t e[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * kRankT + threadIdx.x;
+      e[u] = j < n ? A[j] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * kRankT + threadIdx.x;
+      const float sc = key_value(__uint_as_float((uint32_t)(e[u] >> 32)), key_mode);
+      if (j < n) sk[j] = ((uint64_t)(~orderable(sc)) << 32) | (uint32_t)e[u];
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = i0 + lane;
   const uint64_t mine = i < n ? sk[i] : ~0ull;
-  const int q = (n + 3) >> 2;
+  const int q = (n + kRankW - 1) / kRankW;
   const int j0 = w * q, j1 = min(n, j0 + q);
   uint32_t r = 0;
-  for (int j = j0; j < j1; ++j) r += sk[j] < mine ? 1u : 0u;
+  int j = j0;
+  for (; j + 8 <= j1; j += 8) {  // 8 broadcast reads in flight
+    uint64_t c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c[u] = sk[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r += c[u] < mine ? 1u : 0u;
+  }
+  for (; j < j1; ++j) r += sk[j] < mine ? 1u : 0u;
   part[threadIdx.x] = r;
   __syncthreads();
   if (w == 0 && i < n) {
-    const uint32_t rank = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane];
+    uint32_t rank = 0;
+#pragma unroll
+    for (int v = 0; v < kRankW; ++v) rank += part[v * 64 + lane];
     if ((int)rank < kk) {
       vals_out[(size_t)s * kmax + rank] = from_orderable(~(uint32_t)(mine >> 32));
       idx_out[(size_t)s * kmax + rank] = (int32_t)(uint32_t)mine;
@@ -501,6 +543,189 @@ __global__ __launch_bounds__(kThreads) void topk_rank_kernel(
   }
 }
 
+
+// ------------------------------------------------------------ sampled floor
+constexpr int kSampleStride = 16384, kSampleRun = 1024, kSampleRunsPerWg = 16;
+// fcollect appends into 16 slots per segment (workgroup b -> slot b % 16), each
+// with its own counter: one counter per segment took every workgroup's atomic
+// on one address (measured 39 us for the pass vs 14 us for a histogram pass)
+constexpr int kFloorSlots = 16, kFloorSlotCap = 2048;
+
+// 12-bit histogram of the sampled keys (1,024 contiguous out of every 16,384).
+__global__ __launch_bounds__(kThreads) void topk_sample_kernel(
+    const float* __restrict__ values, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_len, const SegState* __restrict__ st,
+    uint32_t* __restrict__ hist) {
+  const int s = blockIdx.y;
+  const SegState x = st[s];
+  if (x.mode != 0) return;
+  const int len = seg_len[s];
+  const int64_t run0 = (int64_t)blockIdx.x * kSampleRunsPerWg;
+  if (run0 * kSampleStride >= len) return;
+  const float* p = values + seg_start[s];
+  constexpr int U = kSampleRun / kThreads;
+  float v[kSampleRunsPerWg][U];
+  bool ok[kSampleRunsPerWg][U];
+#pragma unroll
+  for (int r = 0; r < kSampleRunsPerWg; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = (run0 + r) * kSampleStride + u * kThreads + threadIdx.x;
+      ok[r][u] = i < len;
+      v[r][u] = ok[r][u] ? p[i] : 0.f;
+    }
+  __shared__ uint32_t h[kBins];
+  for (int i = threadIdx.x; i < kBins; i += kThreads) h[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSampleRunsPerWg; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (ok[r][u]) atomicAdd(&h[orderable(v[r][u]) >> 20], 1u);
+  __syncthreads();
+  uint32_t* g = hist + ((size_t)s * kRep + (blockIdx.x & (kRep - 1))) * kBins;
+  for (int i = threadIdx.x; i < kBins; i += kThreads)
+    if (h[i]) atomicAdd(&g[i], h[i]);
+}
+
+// Floor from the sampled histogram (module comment); clears the replicas.
+__global__ __launch_bounds__(kThreads) void topk_floor_kernel(SegState* st, uint32_t* hist,
+                                                              const int32_t* seg_len) {
+  const int s = blockIdx.x;
+  const SegState x = st[s];
+  if (x.mode != 0) return;
+  uint32_t* g = hist + (size_t)s * kRep * kBins;
+  __shared__ uint32_t part[kThreads];
+  __shared__ uint32_t cnt[kBins];
+  constexpr int per = kBins / kThreads;
+  const int t = threadIdx.x;
+  uint32_t loc = 0;
+  for (int j = 0; j < per; ++j) {  // thread t owns bins from the top, as topk_select_kernel
+    const int bin = kBins - 1 - (t * per + j);
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kRep; ++r) c += g[(size_t)r * kBins + bin];
+    cnt[bin] = c;
+    loc += c;
+  }
+  part[t] = loc;
+  __syncthreads();
+  for (int o = 1; o < kThreads; o <<= 1) {
+    const uint32_t add = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += add;
+    __syncthreads();
+  }
+  const uint32_t total = part[kThreads - 1];
+  const uint32_t before = part[t] - loc;
+  // sampled suffix count that stands for 2 k keys of the whole segment
+  const int len = seg_len[s];
+  const uint32_t target =
+      (uint32_t)max(1.0, ceil(2.0 * (double)x.k * (double)total / (double)max(len, 1)));
+  __shared__ int found_bin;
+  if (t == 0) found_bin = -1;
+  __syncthreads();
+  if (target > before && target <= part[t]) {
+    uint32_t acc = before;
+    for (int j = 0; j < per; ++j) {
+      const int bin = kBins - 1 - (t * per + j);
+      acc += cnt[bin];
+      if (acc >= target) {
+        found_bin = bin;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < kRep * kBins; i += kThreads) g[i] = 0;  // clean for the fallback passes
+  if (t == 0) {
+    SegState y = x;
+    if (found_bin < 0) {
+      y.pre = 0;
+    } else {
+      uint32_t f = (uint32_t)found_bin << 20;
+      if (f > kKeyNegInf && f <= kKeyPosInf) {  // no sigmoid tie across the floor
+        f = lower_bound_sig(kKeyNegInf, f, sigmoidf_tf(from_orderable(f)));
+        f = f > kKeyNegInf + kWindowMargin ? f - kWindowMargin : kKeyNegInf;  // as finish_state
+      }
+      y.floor_key = f;
+      y.pre = 2;
+    }
+    st[s] = y;
+  }
+}
+
+// Every key >= the floor -> its workgroup's spread slot (counted past the
+// slot's end: decide reads the counts).
+template <int V>
+__global__ __launch_bounds__(kThreads) void topk_floor_collect_kernel(
+    const float* __restrict__ values, const int64_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_len, SegState* __restrict__ st,
+    uint64_t* __restrict__ fbuf) {
+  const int s = blockIdx.y;
+  const SegState x = st[s];
+  if (x.mode != 0 || x.pre != 2) return;
+  const int len = seg_len[s];
+  const float* p = values + seg_start[s];
+  ChunkRegs<V> cr;
+  cr.load(p, len, blockIdx.x);
+  if (cr.empty) return;
+  const uint32_t f = x.floor_key;
+  int na = 0;
+  cr.visit([&](int, float v) { na += orderable(v) >= f ? 1 : 0; });
+  const int slot = blockIdx.x & (kFloorSlots - 1);
+  int oa = block_reserve(na, &st[s].nF[slot]);
+  uint64_t* A = fbuf + ((size_t)s * kFloorSlots + slot) * kFloorSlotCap;
+  cr.visit([&](int i, float v) {
+    if (orderable(v) >= f) {
+      if (oa < kFloorSlotCap) A[oa] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)i;
+      ++oa;
+    }
+  });
+}
+
+// One workgroup per segment: every slot fits and k <= total <= 8192 -> the
+// slots compacted into A (order is irrelevant: ranked), mode 1; otherwise the
+// radix passes run as without the floor.
+__global__ __launch_bounds__(kThreads) void topk_floor_decide_kernel(
+    SegState* st, const uint64_t* __restrict__ fbuf, uint64_t* __restrict__ candA) {
+  const int s = blockIdx.x;
+  const SegState x = st[s];
+  if (x.mode != 0 || x.pre != 2) return;
+  int off[kFloorSlots + 1];
+  bool fits = true;
+  off[0] = 0;
+#pragma unroll
+  for (int j = 0; j < kFloorSlots; ++j) {
+    fits = fits && x.nF[j] <= kFloorSlotCap;
+    off[j + 1] = off[j] + x.nF[j];
+  }
+  const int total = off[kFloorSlots];
+  const bool take = fits && total >= x.k && total <= kCap;
+  if (take) {
+    uint64_t* A = candA + (size_t)s * kCap;
+    for (int j = 0; j < kFloorSlots; ++j) {
+      const uint64_t* src = fbuf + ((size_t)s * kFloorSlots + j) * kFloorSlotCap;
+      for (int i = threadIdx.x; i < x.nF[j]; i += kThreads) A[off[j] + i] = src[i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    SegState y = x;
+    if (take) {
+      y.mode = 1;
+      y.edge = y.floor_key;
+      y.win_lo = y.floor_key;  // no tie window: nothing below the floor ties (floor kernel)
+      y.tie_hi = y.floor_key;
+      y.s_edge = 0.f;
+      y.nA = total;
+      y.nB = 0;
+      y.pre = 1;
+    } else {
+      y.pre = 0;  // the radix passes run as without the floor
+    }
+    st[s] = y;
+  }
+}
 }  // namespace
 
 size_t topk_workspace_size(int S, int k) {
@@ -510,13 +735,14 @@ size_t topk_workspace_size(int S, int k) {
   z.take<uint32_t>((size_t)S * kRep * kBins);
   z.take<uint64_t>((size_t)S * kCap);
   z.take<uint64_t>((size_t)S * kCap);
+  z.take<uint64_t>((size_t)S * kFloorSlots * kFloorSlotCap);
   return z.off;
 }
 
 int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* seg_len,
                  const int32_t* seg_k, int S, int max_len, int k, int key_mode, float* vals_out,
                  int32_t* idx_out, int32_t* count_out, void* ws, size_t ws_bytes,
-                 hipStream_t stream) {
+                 hipStream_t stream, bool sampled_floor) {
   D2MI_REQUIRE(k >= 0 && k <= kCap, "top-k k=%d must be in [0, %d]", k, kCap);
   D2MI_REQUIRE(key_mode == 0 || key_mode == 1, "key_mode must be 0 or 1");
   if (S == 0) return 0;
@@ -525,6 +751,7 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
   uint32_t* hist = w.take<uint32_t>((size_t)S * kRep * kBins);
   uint64_t* candA = w.take<uint64_t>((size_t)S * kCap);
   uint64_t* candB = w.take<uint64_t>((size_t)S * kCap);
+  uint64_t* fbuf = w.take<uint64_t>((size_t)S * kFloorSlots * kFloorSlotCap);
   D2MI_REQUIRE(w.ok(), "top-k workspace too small (%zu < %zu)", ws_bytes, w.off);
   // chunk per workgroup: 16 K elements for the dense RetinaNet levels, 4 K
   // for RPN-sized segments (more workgroups over a smaller scan)
@@ -534,6 +761,25 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
   hipLaunchKernelGGL(topk_init_kernel, dim3(kRep, S), dim3(256), 0, stream, st, hist, seg_len,
                      seg_k, k);
   D2MI_LAUNCH_CHECK();
+  static const char* floor_env = getenv("D2MI_TOPK_FLOOR");  // "0": radix passes only (A/B)
+  if (sampled_floor && key_mode == 1 && max_len > kCap && !(floor_env && floor_env[0] == '0')) {
+    const int runs = (max_len + kSampleStride - 1) / kSampleStride;
+    hipLaunchKernelGGL(topk_sample_kernel, dim3((runs + kSampleRunsPerWg - 1) / kSampleRunsPerWg, S),
+                       dim3(kThreads), 0, stream, values, seg_start, seg_len, st, hist);
+    D2MI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(topk_floor_kernel, dim3(S), dim3(kThreads), 0, stream, st, hist, seg_len);
+    D2MI_LAUNCH_CHECK();
+    if (big)
+      hipLaunchKernelGGL(topk_floor_collect_kernel<16>, dim3(gx, S), dim3(kThreads), 0, stream,
+                         values, seg_start, seg_len, st, fbuf);
+    else
+      hipLaunchKernelGGL(topk_floor_collect_kernel<4>, dim3(gx, S), dim3(kThreads), 0, stream,
+                         values, seg_start, seg_len, st, fbuf);
+    D2MI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(topk_floor_decide_kernel, dim3(S), dim3(kThreads), 0, stream, st, fbuf,
+                       candA);
+    D2MI_LAUNCH_CHECK();
+  }
   for (int pass = 0; pass < 3; ++pass) {
     if (big)
       hipLaunchKernelGGL(topk_hist_kernel<16>, dim3(gx, S), dim3(kThreads), 0, stream, values,
@@ -556,7 +802,7 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
   hipLaunchKernelGGL(topk_resolve_kernel, dim3(S), dim3(1024), 0, stream, values, seg_start,
                      seg_len, st, candA, candB, key_mode);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(topk_rank_kernel, dim3(kCap / kRankI, S), dim3(kThreads),
+  hipLaunchKernelGGL(topk_rank_kernel, dim3(kCap / kRankI, S), dim3(kRankT),
                      kCap * sizeof(uint64_t), stream, candA, st, k, key_mode, vals_out, idx_out,
                      count_out);
   D2MI_LAUNCH_CHECK();

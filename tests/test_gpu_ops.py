@@ -441,14 +441,30 @@ def test_fast_rcnn_inference_dense_layout_ignores_negative_slots(dev):
 
 
 # -------------------------------------------------------------- RetinaNet
-def test_retinanet_inference_vs_oracle(dev):
+def _retina_logits(rng, shape, dist):
+    x = rng.normal(-3, 1, size=shape)
+    if dist == "quantized":  # big tie groups at every value, some on the sampled floor
+        x = np.round(x * 4) / 4
+    elif dist == "saturated":  # >8192 keys with sigmoid == 1.0: floor overflows -> radix passes
+        x = np.where(rng.uniform(size=shape) < 0.2, rng.uniform(20, 40, size=shape), x)
+    elif dist == "sparse":  # few scores above 0.05: top-k mostly filtered
+        x = x - 3
+    return x.astype(F32)
+
+
+@pytest.mark.parametrize("dist", ["normal", "quantized", "saturated", "sparse"])
+def test_retinanet_inference_vs_oracle(dev, dist):
+    """Dense top-k + decode + NMS vs the oracle.  The distributions drive the
+    top-k down both of its paths: the sampled floor (normal, quantized, sparse)
+    and the radix passes it falls back to (saturated: the tie group of
+    sigmoid == 1 overflows the candidate buffer)."""
     rng = np.random.default_rng(41)
     N, IH, IW, A, K = 2, 320, 320, 9, 80
     strides = [8, 16, 32, 64, 128]
     hw = [(int(math.ceil(IH / s)), int(math.ceil(IW / s))) for s in strides]
     cells = [oracle.generate_cell_anchors([x, x * 2 ** (1 / 3), x * 2 ** (2 / 3)], [0.5, 1.0, 2.0])
              for x in [32, 64, 128, 256, 512]]
-    cls = [rng.normal(-3, 1, size=(N, h, w, A * K)).astype(F32) for h, w in hw]
+    cls = [_retina_logits(rng, (N, h, w, A * K), dist) for h, w in hw]
     box = [rng.normal(0, 0.3, size=(N, h, w, A * 4)).astype(F32) for h, w in hw]
     anchors = [oracle.grid_anchors(h, w, s, c) for (h, w), s, c in zip(hw, strides, cells)]
     want = oracle.retinanet_inference([c.reshape(N, -1, K) for c in cls],

@@ -19,37 +19,60 @@ import sys
 
 # (kernels of the group, the group's one-per-op kernel).  The split-K /
 # partial reductions are counted with their group; per-launch figures divide
-# by the op's main kernel count.  ROIAlign backward: its own roi_bwd_* kernels,
-# including roi_bwd_clear_kernel (the grad-map / run-start / counter clear,
-# 183 MB of writes at 1333x800).  The rocPRIM onesweep sort it launches (about
-# 40 us of the ~170 us per backward) is not attributable by name and is left
-# out, so `traffic` covers fewer kernels than the HIP-event time does
-# (DESIGN.md section 5 says so).
+# by the op's main kernel count.  conv_mfma_kernel<WM, WN, TM, TN, DB, SPLIT,
+# OCC, ML>: SPLIT (the sixth argument) tells the split-bf16 kernels from the
+# f32 ones.  ROIAlign backward: its own roi_bwd_* kernels (the clear kernel, one
+# per backward, is the main one: it writes the 183 MB of grad maps at
+# 1333x800) PLUS the rocPRIM onesweep sort it launches, attributed by dispatch
+# order (every dispatch between a roi_bwd_emit kernel and the next
+# roi_bwd_runs kernel), so `traffic` covers the same kernels as the HIP-event
+# time of the backward.
+SPLIT_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), true"
+F32_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), false"
 GROUPS = {
-    "conv2d_split": (re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel|splitk_reduce4?_kernel"),
-                     re.compile(r"conv_mfma_kernel<[^>]*, true>|conv_x3_kernel")),
-    "conv2d_mfma": (re.compile(r"conv_mfma_kernel<[^>]*, false>"), None),
+    "conv2d_split": (re.compile(SPLIT_CONV + r"|conv_x3_kernel|splitk_reduce\w*_kernel"),
+                     re.compile(SPLIT_CONV + r"|conv_x3_kernel")),
+    "conv2d_mfma": (re.compile(F32_CONV), None),
     "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),  # split below
-    "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_pixel_kernel")),
+    "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_clear_kernel")),
     "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce4?_kernel"),
                          re.compile(r"conv_wgrad_split_kernel")),
     "conv_wgrad": (re.compile(r"conv_wgrad_kernel<"), None),
 }
+ROI_BWD_OPEN = re.compile(r"roi_bwd_emit_kernel")
+ROI_BWD_CLOSE = re.compile(r"roi_bwd_runs_kernel")
 
 
 def load(d, counter):
+    """-> [(dispatch id, kernel name, grid size, value)] in dispatch order."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    per = collections.defaultdict(lambda: [0, 0.0])
-    disp = []  # (name, grid size, value) per dispatch
+    disp = []
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            name = r.get("Kernel_Name", "")
-            per[name][0] += 1
-            per[name][1] += float(r["Counter_Value"])
-            disp.append((name, int(float(r.get("Grid_Size", 0) or 0)), float(r["Counter_Value"])))
-    return per, disp
+            disp.append((int(r.get("Dispatch_Id", 0) or 0), r.get("Kernel_Name", ""),
+                         int(float(r.get("Grid_Size", 0) or 0)), float(r["Counter_Value"])))
+    disp.sort(key=lambda x: x[0])
+    return disp
+
+
+def members(disp, g, rx):
+    """Dispatches of group g (the ROIAlign backward also takes its sort)."""
+    out = []
+    inside = False
+    for d in disp:
+        name = d[1]
+        if g == "roi_align_bwd":
+            if ROI_BWD_OPEN.search(name):
+                inside = True
+            elif ROI_BWD_CLOSE.search(name):
+                inside = False
+            if rx.search(name) or inside:
+                out.append(d)
+        elif rx.search(name):
+            out.append(d)
+    return out
 
 
 def split_roi_fwd(disp):
@@ -58,7 +81,7 @@ def split_roi_fwd(disp):
     launches have the largest grids.  -> {"roi_align_fwd": [values],
     "roi_align_fwd_mask": [values]}"""
     rx = re.compile(r"roi_align_fwd_kernel<true>")
-    xs = [(g, v) for n, g, v in disp if rx.search(n)]
+    xs = [(g, v) for _, n, g, v in disp if rx.search(n)]
     if not xs:
         return {}
     gmax = max(g for g, _ in xs)
@@ -68,22 +91,20 @@ def split_roi_fwd(disp):
 
 def main():
     fd, wd, out = sys.argv[1:4]
-    fetch, fdisp = load(fd, "FETCH_SIZE")
-    write, wdisp = load(wd, "WRITE_SIZE")
+    fdisp = load(fd, "FETCH_SIZE")
+    wdisp = load(wd, "WRITE_SIZE")
     res = {"units": "bytes per dispatch", "fetch_correction": 2.0,
            "note": "FETCH_SIZE x2 (gfx950 16 B/lane reads); WRITE_SIZE as reported",
            "groups": {}}
     for g, (rx, main_rx) in GROUPS.items():
         main_rx = main_rx or rx
-        fn = sum(v[0] for k, v in fetch.items() if rx.search(k))
-        fb = sum(v[1] for k, v in fetch.items() if rx.search(k))
-        wn = sum(v[0] for k, v in write.items() if rx.search(k))
-        wb = sum(v[1] for k, v in write.items() if rx.search(k))
-        if fn == 0 and wn == 0:
+        fm, wm = members(fdisp, g, rx), members(wdisp, g, rx)
+        if not fm and not wm:
             continue
-        main_n = sum(v[0] for k, v in fetch.items() if main_rx.search(k))
+        main_n = sum(1 for d in fm if main_rx.search(d[1]))
+        fb, wb = sum(d[3] for d in fm), sum(d[3] for d in wm)
         res["groups"][g] = {
-            "dispatches": fn, "main_kernel_dispatches": main_n,
+            "dispatches": len(fm), "main_kernel_dispatches": main_n,
             "fetch_bytes_per_launch": 2.0 * fb * 1024 / max(main_n, 1),
             "write_bytes_per_launch": wb * 1024 / max(main_n, 1),
         }
