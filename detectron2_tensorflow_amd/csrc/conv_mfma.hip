@@ -978,7 +978,10 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
     const char* e = getenv("D2MI_CONV_SPLIT_SLOTS");
     return e ? atoi(e) : 0;
   }();
-  const int gs = GS > 0 ? GS : G;
+  // target: two workgroups per CU even for the 3-per-CU kernel (A/B over
+  // 384..1024 slots on the training step: 512 fastest, +2.5 % over 768 -- fewer
+  // splits, less partial-slab traffic for the reduce)
+  const int gs = GS > 0 ? GS : wg_slots(1);
   if (4 * p.ntiles < 3 * gs && p.nk >= 16) {
     p.splits = std::min(std::max(1, gs / p.ntiles), std::min(p.nk / 8, 16));
   }
