@@ -79,7 +79,14 @@ class StandardRPNHead(Layer):
             # a level the ROI poolers also read hands its input gradient over
             # (GeneralizedRCNN tags them; the pair_grad protocol)
             share = self.conv(x, pair_grad=getattr(x, "_d2mi_grad_pair", None))
-            rpn_features.append(share)
+            if fuse:
+                # the fused 1x1 is the declared SOLE consumer of the 3x3's ReLU
+                # output (its dgrad applies the ReLU mask, _RPNHead1x1Fn): the
+                # features handed back are detached, so nothing else adds an
+                # ungated gradient to it
+                rpn_features.append(share.detach())
+            else:
+                rpn_features.append(share)
             if fuse:
                 w16, wp, b16 = self._fused_1x1()
                 lg, dl = _RPNHead1x1Fn.apply(share, self.objectness_logits.weights,
@@ -99,13 +106,18 @@ class _RPNHead1x1Fn(torch.autograd.Function):
     kernel.  Backward: the two output gradients are concatenated (+ the zero
     pad column) into one [.., 16] gradient; the input gradient is ONE dgrad
     conv (instead of a dgrad per head + their sum), the weight and bias
-    gradients one skinny X^T G pass (d2mi_wgrad_skinny) sliced per head."""
+    gradients one skinny X^T G pass (d2mi_wgrad_skinny) sliced per head.  The
+    input gradient leaves through the dgrad's ReLU gate (share > 0) when share
+    is a fused-ReLU conv output, which then skips its threshold_backward (the
+    sole-consumer protocol of layers/convolutional.py:_ConvMFMAFn)."""
+    GATE = True  # False: leave the ReLU backward to the 3x3 conv (tests)
 
     @staticmethod
     def forward(ctx, share, wo, bo, wd, bd, w16, wp, b16):
         y = ops.conv2d_nhwc(share, wp, b16)
         A, D = wo.shape[3], wd.shape[3]
         ctx.save_for_backward(share, w16)
+        ctx.relu_info = getattr(share, "_d2mi_relu_info", None) if _RPNHead1x1Fn.GATE else None
         ctx.set_materialize_grads(False)  # a missing head gradient is zero-filled below
         ctx.dims = (A, D, y.shape[-1])
         return y[..., :A].contiguous(), y[..., A:A + D].contiguous()
@@ -124,7 +136,12 @@ class _RPNHead1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # 1x1 stride-1 dgrad: the forward weights' HWIO [1, 1, C, 16] is
             # the packed layout of the transposed conv
-            gx = ops.conv2d_nhwc(g16, w16, None, 1, (0, 0))
+            info = ctx.relu_info
+            if info is not None and share.shape[-1] % 4 == 0:
+                gx = ops.conv2d_nhwc(g16, w16, None, 1, (0, 0), relu_gate=share)
+                info["masked"] = True
+            else:
+                gx = ops.conv2d_nhwc(g16, w16, None, 1, (0, 0))
         gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)
         return (gx, gw[..., :A].contiguous(), gb[:A], gw[..., A:A + D].contiguous(), gb[A:A + D],
                 None, None, None)

@@ -207,6 +207,35 @@ def test_rpn_head_fused_1x1_matches_separate_convs(dev):
     assert all(torch.isfinite(x.grad).all() for x in xs)
 
 
+def test_rpn_head_relu_gate_in_1x1_dgrad_is_exact(dev):
+    """The 3x3 share conv's ReLU backward applied in the fused 1x1 head's dgrad
+    epilogue (share > 0 gate) gives bit-identical input and 3x3 weight / bias
+    gradients to the unfused threshold_backward."""
+    from detectron2_tensorflow_amd.layers import ShapeSpec
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead, _RPNHead1x1Fn
+    cfg = _cfg(True)
+    torch.manual_seed(1)
+    head = StandardRPNHead(cfg, [ShapeSpec(channels=256, stride=s) for s in (4, 8, 16, 32, 64)]).to(dev)
+    xs0 = [torch.randn(2, h, w, 256, device=dev) for h, w in ((40, 52), (20, 26))]
+    grads = []
+    for gate in (False, True):
+        _RPNHead1x1Fn.GATE = gate
+        try:
+            xs = [x.clone().requires_grad_(True) for x in xs0]
+            for prm in head.parameters():
+                prm.grad = None
+            _, logits, deltas = head(xs)
+            g = torch.Generator(device=dev).manual_seed(3)
+            outs = logits + deltas
+            torch.autograd.backward(outs, [torch.randn(t.shape, device=dev, generator=g) for t in outs])
+            grads.append([x.grad.clone() for x in xs] +
+                         [head.conv.weights.grad.clone(), head.conv.bias.grad.clone()])
+        finally:
+            _RPNHead1x1Fn.GATE = True
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 def test_fused_momentum_sgd_matches_foreach_reference(dev):
     """d2mi_momentum_sgd (L2 gradient + per-tensor clip_by_norm + momentum in
     two launches) against the torch._foreach restatement on CPU: weight-decay

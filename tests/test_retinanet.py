@@ -115,12 +115,12 @@ def _assert_post_matches_oracle(ref, cls, box, got):
     """Post-processing parity on identical head outputs: valid flags and class
     ids bit-exact, scores to 2e-7 relative (the sigmoid's expf), boxes within
     max(1e-4, 2 ulp)."""
-    from test_gpu_ops import assert_boxes_close
+    from test_gpu_ops import assert_boxes_close, assert_sigmoid_scores_close
     want = ref.postprocess([c.cpu().numpy() for c in cls], [b.cpu().numpy() for b in box])
     g = {k: v.cpu().numpy() for k, v in got.items()}
     np.testing.assert_array_equal(g["is_valid"], want["is_valid"])
     np.testing.assert_array_equal(g["classes"], want["classes"])
-    np.testing.assert_allclose(g["scores"], want["scores"], rtol=2e-7, atol=0)
+    assert_sigmoid_scores_close(g["scores"], want["scores"])
     for n in range(g["boxes"].shape[0]):
         assert_boxes_close(g["boxes"][n], want["boxes"][n])
     return want
