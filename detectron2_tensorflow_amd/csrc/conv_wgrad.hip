@@ -473,9 +473,19 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
   // about one round of resident workgroups (2 or 3 per CU), each walking
   // >= 16 chunks
   p.occ3 = p.TM == 2 && p.TN == 2 && P >= 65536 && wgrad_occ3();
-  const int G = p.occ3 ? 768 : 512;
+  // D2MI_WGRAD_SLOTS / D2MI_WGRAD_MINCH: the split target and the minimum
+  // chunks per split (A/B knobs)
+  static const int slots_env = [] {
+    const char* e = getenv("D2MI_WGRAD_SLOTS");
+    return e ? atoi(e) : 0;
+  }();
+  static const int minch = [] {
+    const char* e = getenv("D2MI_WGRAD_MINCH");
+    return e && atoi(e) > 0 ? atoi(e) : 16;
+  }();
+  const int G = slots_env > 0 ? slots_env : (p.occ3 ? 768 : 512);
   int splits = std::max(1, G / p.ntiles);
-  splits = std::min(splits, std::max(1, p.nchunks / 16));
+  splits = std::min(splits, std::max(1, p.nchunks / minch));
   splits = std::min(splits, 64);
   p.chunks_per_split = (p.nchunks + splits - 1) / splits;
   p.splits = (p.nchunks + p.chunks_per_split - 1) / p.chunks_per_split;
