@@ -507,18 +507,28 @@ __device__ __forceinline__ float mask_bit(const uint64_t* m, size_t p) {
   return (float)((m[p >> 6] >> (p & 63)) & 1ull);
 }
 
-constexpr int kPasteRows = 8;  // output rows per workgroup
+constexpr int kPasteRows = 16;   // output rows per workgroup
+constexpr int kPasteWords = 512; // mask words staged in LDS per workgroup
 
 // Masks of the kept detections resized from [Hm, Wm] to the padded image
 // [OH, OW] (TF bilinear, half-pixel centres), > thr, uint8.  A workgroup
 // owns kPasteRows output rows of one detection, four pixels per thread per
-// step; its box statistics (integers: exact in any order) — mask count,
-// coordinate sums, min / max of the coordinates > 0 — go to its own partial
-// slot (no atomics), reduced per detection by solo_boxes_kernel.
+// step.  The column interpolation (lo, hi, lerp: the same for every row) is
+// tabled in LDS once per workgroup, and the mask words under its source rows
+// (about 3 rows x Wm bits) are staged in LDS; a pixel whose four source bits
+// agree is that bit (tf_lerp of four equal 0 / 1 values is exact), the rest
+// run tf_lerp.  Box statistics (integers: exact in any order) — mask count,
+// coordinate sums, min / max of the coordinates > 0 — go to the workgroup's
+// own partial slot (no atomics), reduced per detection by solo_boxes_kernel.
+// Dynamic LDS: kPasteWords * 8 + OW * 8 bytes.
 __global__ __launch_bounds__(256) void solo_paste_kernel(
     const uint64_t* __restrict__ bits, const int32_t* __restrict__ det_src, int k, int W64, int Hm,
     int Wm, int OH, int OW, float sh, float sw, float thr, int max_det, uint8_t* __restrict__ out,
     BoxAcc* __restrict__ part) {
+  extern __shared__ uint64_t psm[];
+  uint64_t* wbuf = psm;
+  uint32_t* xidx = reinterpret_cast<uint32_t*>(psm + kPasteWords);  // lo | hi << 16
+  float* xlr = reinterpret_cast<float*>(xidx + OW);
   const int d = blockIdx.y, n = blockIdx.z;
   const int src = det_src[(size_t)n * max_det + d];
   const int r0 = blockIdx.x * kPasteRows, r1 = min(OH, r0 + kPasteRows);
@@ -531,36 +541,102 @@ __global__ __launch_bounds__(256) void solo_paste_kernel(
     return;
   }
   const uint64_t* m = bits + ((size_t)n * k + src) * W64;
+  const uint32_t* m32 = reinterpret_cast<const uint32_t*>(m);  // little-endian halves
+  for (int ox = threadIdx.x; ox < OW; ox += blockDim.x) {
+    const Interp ix = interp_at(ox, sw, Wm, 1);
+    xidx[ox] = (uint32_t)ix.lo | ((uint32_t)ix.hi << 16);
+    xlr[ox] = ix.lerp;
+  }
+  const int ylo = interp_at(r0, sh, Hm, 1).lo, yhi = interp_at(r1 - 1, sh, Hm, 1).hi;
+  const uint32_t w0 = (uint32_t)(((size_t)ylo * Wm) >> 5);
+  const uint32_t w1 = (uint32_t)((((size_t)yhi + 1) * Wm - 1) >> 5);
+  const bool staged = w1 - w0 + 1 <= 2u * kPasteWords;  // workgroup-uniform
+  uint32_t* wb32 = reinterpret_cast<uint32_t*>(wbuf);
+  if (staged)
+    for (int i = threadIdx.x; i <= (int)(w1 - w0); i += blockDim.x) wb32[i] = m32[w0 + i];
+  __syncthreads();
+  auto bit = [&](uint32_t p) -> uint32_t {
+    const uint32_t wd = staged ? wb32[(p >> 5) - w0] : m32[p >> 5];
+    return (wd >> (p & 31u)) & 1u;
+  };
   int cnt = 0, miny = INT_MAX, maxy = INT_MIN, minx = INT_MAX, maxx = INT_MIN;
   unsigned long long sy = 0, sx = 0;
+  // (row, quad) of q stepped incrementally (no per-step division), the row's
+  // interpolation recomputed only when the row changes
+  int qr = (int)threadIdx.x / qrow, qc = (int)threadIdx.x - qr * qrow;
+  int cur_row = -1;
+  Interp iy = {0, 0, 0.f};
+  uint32_t a0 = 0, a1 = 0;
   for (int q = threadIdx.x; q < nq; q += blockDim.x) {
-    const int oy = r0 + q / qrow, ox0 = (q % qrow) * 4;
-    const Interp iy = interp_at(oy, sh, Hm, 1);
-    const size_t a0 = (size_t)iy.lo * Wm, a1 = (size_t)iy.hi * Wm;
-    uint8_t b[4];
+    const int oy = r0 + qr, ox0 = qc * 4;
+    qc += blockDim.x;
+    while (qc >= qrow) {
+      qc -= qrow;
+      ++qr;
+    }
+    if (oy != cur_row) {
+      cur_row = oy;
+      iy = interp_at(oy, sh, Hm, 1);
+      a0 = (uint32_t)iy.lo * (uint32_t)Wm;
+      a1 = (uint32_t)iy.hi * (uint32_t)Wm;
+    }
+    const uint4 xi4 = *reinterpret_cast<const uint4*>(&xidx[ox0]);
+    const float4 xl4 = *reinterpret_cast<const float4*>(&xlr[ox0]);
+    const uint32_t xi[4] = {xi4.x, xi4.y, xi4.z, xi4.w};
+    const float xl[4] = {xl4.x, xl4.y, xl4.z, xl4.w};
+    uint32_t on4 = 0;  // bit e: pixel ox0 + e is on
+    // the four pixels' source bits of each row sit in one 64-bit window
+    // (two words) when the columns span < 32 (upsampling: a few bits)
+    const uint32_t lo0 = xi[0] & 0xffffu, hi3 = xi[3] >> 16;
+    const bool win = hi3 - lo0 < 32u;  // columns are monotone in ox
+    const uint32_t b0 = (a0 + lo0) & ~31u, b1 = (a1 + lo0) & ~31u;
+    uint64_t r0w = 0, r1w = 0;
+    if (win) {
+      r0w = (uint64_t)(staged ? wb32[(b0 >> 5) - w0] : m32[b0 >> 5]);
+      r1w = (uint64_t)(staged ? wb32[(b1 >> 5) - w0] : m32[b1 >> 5]);
+      if (((a0 + hi3) >> 5) != (b0 >> 5))
+        r0w |= (uint64_t)(staged ? wb32[(b0 >> 5) + 1 - w0] : m32[(b0 >> 5) + 1]) << 32;
+      if (((a1 + hi3) >> 5) != (b1 >> 5))
+        r1w |= (uint64_t)(staged ? wb32[(b1 >> 5) + 1 - w0] : m32[(b1 >> 5) + 1]) << 32;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int ox = ox0 + e;
-      const Interp ix = interp_at(ox, sw, Wm, 1);
-      const float v = tf_lerp(mask_bit(m, a0 + ix.lo), mask_bit(m, a0 + ix.hi),
-                              mask_bit(m, a1 + ix.lo), mask_bit(m, a1 + ix.hi), ix.lerp, iy.lerp);
-      const bool on = v > thr;
-      b[e] = on ? 1 : 0;
-      if (on) {
-        ++cnt;
-        sy += (unsigned long long)oy;
-        sx += (unsigned long long)ox;
-        if (oy > 0) {
-          miny = min(miny, oy);
-          maxy = max(maxy, oy);
-        }
-        if (ox > 0) {
-          minx = min(minx, ox);
-          maxx = max(maxx, ox);
-        }
+      const uint32_t lo = xi[e] & 0xffffu, hi = xi[e] >> 16;
+      uint32_t tl, tr, bl, br;
+      if (win) {
+        tl = (uint32_t)(r0w >> (a0 + lo - b0)) & 1u;
+        tr = (uint32_t)(r0w >> (a0 + hi - b0)) & 1u;
+        bl = (uint32_t)(r1w >> (a1 + lo - b1)) & 1u;
+        br = (uint32_t)(r1w >> (a1 + hi - b1)) & 1u;
+      } else {
+        tl = bit(a0 + lo);
+        tr = bit(a0 + hi);
+        bl = bit(a1 + lo);
+        br = bit(a1 + hi);
       }
+      const uint32_t all = tl & tr & bl & br, any = tl | tr | bl | br;
+      const float v = (all | (any ^ 1u)) ? (float)tl
+                                         : tf_lerp((float)tl, (float)tr, (float)bl, (float)br,
+                                                   xl[e], iy.lerp);
+      on4 |= (v > thr ? 1u : 0u) << e;
     }
-    *(uchar4*)(dst + (size_t)q * 4) = make_uchar4(b[0], b[1], b[2], b[3]);
+    // the four pixels' bytes, and their statistics from the 4-bit mask
+    *(uint32_t*)(dst + (size_t)q * 4) =
+        (on4 & 1u) | ((on4 & 2u) << 7) | ((on4 & 4u) << 14) | ((on4 & 8u) << 21);
+    const int c4 = __popc(on4);
+    cnt += c4;
+    sy += (unsigned long long)c4 * (unsigned long long)oy;
+    sx += (unsigned long long)c4 * (unsigned long long)ox0 + (unsigned)__popc(on4 & 0xAu) +
+          2u * (unsigned)__popc(on4 & 0xCu);
+    if (on4 && oy > 0) {
+      miny = min(miny, oy);
+      maxy = max(maxy, oy);
+    }
+    const uint32_t onx = ox0 == 0 ? on4 & ~1u : on4;  // coordinates > 0 only
+    if (onx) {
+      minx = min(minx, ox0 + __ffs((int)onx) - 1);
+      maxx = max(maxx, ox0 + 31 - __clz((int)onx));
+    }
   }
   __shared__ int s_i[4][5];
   __shared__ unsigned long long s_l[4][2];
@@ -849,7 +925,10 @@ extern "C" int d2mi_solo_finalize(const float* nms_scores, const int64_t* top_cl
                      out_valid);
   D2MI_LAUNCH_CHECK();
   const float sh = resize_scale(Hm, OH, 0), sw = resize_scale(Wm, OW, 0);
-  hipLaunchKernelGGL(solo_paste_kernel, dim3(nparts, max_det, N), dim3(256), 0, st, mask_bits,
+  D2MI_REQUIRE(Wm <= 65535, "SOLO mask width %d exceeds the 16-bit column table", Wm);
+  const size_t paste_lds = (size_t)kPasteWords * 8 + (size_t)OW * 8;
+  D2MI_REQUIRE(paste_lds <= 160 * 1024, "SOLO output width %d too large for the paste table", OW);
+  hipLaunchKernelGGL(solo_paste_kernel, dim3(nparts, max_det, N), dim3(256), paste_lds, st, mask_bits,
                      det_src, k, W64, Hm, Wm, OH, OW, sh, sw, mask_thr, max_det, out_masks, part);
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(solo_boxes_kernel, dim3(N * max_det), dim3(64), 0, st, part, det_src, nparts,
