@@ -385,6 +385,11 @@ class Conv2D(Layer):
         pads = same_pads(self.kernel_size, self.rate) if self.padding == "SAME" else (0, 0)
         fuse_relu = norm is None and is_relu(self.act_fn)
         ys = ops.conv2d_nhwc_levels(inputs, packed, b, self.stride, pads, relu=fuse_relu)
+        if (norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok")
+                and all(norm.fused_ok(y) for y in ys)):
+            # GroupNorm + ReLU over every level in one set of launches
+            return ops.group_norm_levels(ys, norm.num_groups, norm.gamma, norm.beta, norm.epsilon,
+                                         relu=True)
         out = []
         for y in ys:
             if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \

@@ -1058,6 +1058,35 @@ def group_norm(x, num_groups, gamma, beta, eps, relu=False, up2=False, accumulat
     return y
 
 
+def group_norm_levels(xs, num_groups, gamma, beta, eps, relu=False):
+    """The same GroupNorm (+ ReLU) over up to 6 feature levels in one set of
+    launches (d2mi_group_norm_nhwc_levels): per level ops.group_norm's
+    arithmetic.  Inference only (no grad)."""
+    xs = [_f32c(x) for x in xs]
+    gamma, beta = _f32c(gamma), _f32c(beta)
+    _C.require_device(gamma, beta, *xs)
+    if not 1 <= len(xs) <= 6:
+        raise ValueError(f"group_norm_levels takes 1..6 levels, got {len(xs)}")
+    C = xs[0].shape[-1]
+    dims, ys = [], []
+    for x in xs:
+        if x.dim() != 4 or x.shape[-1] != C:
+            raise ValueError(f"every level must be [N, H, W, {C}], got {tuple(x.shape)}")
+        dims += [x.shape[0], x.shape[1], x.shape[2]]
+        ys.append(torch.empty_like(x))
+    dm = _C.host_array(_C.ctypes.c_int32, dims)
+    lib = _C.lib()
+    wsb = lib.d2mi_group_norm_levels_workspace_size(dm, len(xs), C, int(num_groups))
+    ws = _C.scratch(wsb, xs[0].device) if wsb else None
+    xp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in xs])
+    yp = _C.host_array(_C.c_void_p, [y.data_ptr() for y in ys])
+    rc = lib.d2mi_group_norm_nhwc_levels(xp, dm, len(xs), C, int(num_groups), _C.ptr(gamma),
+                                         _C.ptr(beta), float(eps), int(bool(relu)), yp,
+                                         _C.ptr(ws), wsb, _C.stream_of(xs[0].device))
+    _C.check(rc, "d2mi_group_norm_nhwc_levels")
+    return ys
+
+
 # ------------------------------------------------------------ resize / SOLOv2
 def resize_bilinear(x, size, align_corners=False, half_pixel_centers=True):
     """TF ResizeBilinear on NHWC f32 (d2mi_resize_bilinear): x [N,H,W,C] ->

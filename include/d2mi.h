@@ -320,6 +320,16 @@ size_t d2mi_group_norm_workspace_size(int N, int H, int W, int C, int G);
 int d2mi_group_norm_nhwc(const float* x, int N, int H, int W, int C, int G, const float* gamma,
                          const float* beta, float eps, int relu, int up2, int accumulate,
                          float* y, void* workspace, size_t workspace_bytes, void* stream);
+/* The same GroupNorm (+ relu) applied to up to 6 feature levels sharing the
+ * layer — the SOLOv2 towers' per-level GroupNorm calls (solo_v2.py:173-183,
+ * one layer per level) — in five launches for all levels.  xs[l] / ys[l]
+ * [dims[3l], dims[3l+1], dims[3l+2], C]; per level identical arithmetic to
+ * d2mi_group_norm_nhwc; workspace from d2mi_group_norm_levels_workspace_size. */
+size_t d2mi_group_norm_levels_workspace_size(const int32_t* dims, int nlev, int C, int G);
+int d2mi_group_norm_nhwc_levels(const float* const* xs, const int32_t* dims, int nlev, int C,
+                                int G, const float* gamma, const float* beta, float eps, int relu,
+                                float* const* ys, void* workspace, size_t workspace_bytes,
+                                void* stream);
 
 /* --------------------------------------------------------------- conv2d
  * NHWC implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32),

@@ -336,6 +336,23 @@ def test_solo_r50_1333x800_geometry(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("relu", [False, True])
+def test_group_norm_levels_equals_per_level(dev, relu):
+    """d2mi_group_norm_nhwc_levels (one set of launches over the SOLOv2 grid
+    levels) is bit-identical to d2mi_group_norm_nhwc per level."""
+    from detectron2_tensorflow_amd.layers import ops
+    rng = np.random.default_rng(7)
+    C, G = 256, 32
+    xs = [torch.from_numpy((rng.normal(size=(2, S, S, C)) * 2 + 0.5).astype(F32)).to(dev)
+          for S in (40, 36, 24, 16, 12)]
+    gamma = torch.from_numpy(rng.uniform(0.5, 1.5, size=C).astype(F32)).to(dev)
+    beta = torch.from_numpy(rng.normal(size=C).astype(F32)).to(dev)
+    got = ops.group_norm_levels(xs, G, gamma, beta, 1e-5, relu)
+    for x, y in zip(xs, got):
+        assert torch.equal(y, ops.group_norm(x, G, gamma, beta, 1e-5, relu))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("C,G,relu,up2,acc", [(128, 32, True, False, False), (512, 32, True, False, False),
                                               (128, 32, True, True, True), (256, 32, False, True, False),
                                               (128, 32, True, False, True)])
