@@ -209,15 +209,27 @@ __global__ __launch_bounds__(256) void solo_mask_stats_kernel(const float* __res
   int cnt = 0;
   float acc = 0.f;
   if ((P & 3) == 0) {
-    for (int p = threadIdx.x * 4; p < P; p += blockDim.x * 4) {
-      const float4 v = *(const float4*)(row + p);
-      const float s[4] = {sigmoidf_tf(v.x), sigmoidf_tf(v.y), sigmoidf_tf(v.z), sigmoidf_tf(v.w)};
+    // four float4 loads in flight per thread, consumed in the same order
+    const int step = blockDim.x * 4;
+    for (int p0 = threadIdx.x * 4; p0 < P; p0 += 4 * step) {
+      float4 v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (s[q] > thr) {
-          ++cnt;
-          acc += s[q];
-        }
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + u * step;
+        v[u] = p < P ? *(const float4*)(row + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (p0 + u * step >= P) break;
+        const float s[4] = {sigmoidf_tf(v[u].x), sigmoidf_tf(v[u].y), sigmoidf_tf(v[u].z),
+                            sigmoidf_tf(v[u].w)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (s[q] > thr) {
+            ++cnt;
+            acc += s[q];
+          }
+      }
     }
   } else {
     for (int p = threadIdx.x; p < P; p += blockDim.x) {
@@ -311,11 +323,23 @@ __global__ __launch_bounds__(256) void solo_gather_kernel(
   const int cell = idx / K, cls = idx % K;
   const int gr = row_off[n] + live_row[(size_t)n * T + cell];
   const float* src = logits + (size_t)gr * P;
-  for (int w = wv; w < W64; w += blockDim.x >> 6) {
-    const int p = w * 64 + lane;
-    const bool on = p < P && sigmoidf_tf(src[p]) > thr;
-    const uint64_t b = __ballot(on);
-    if (lane == 0) dst[w] = b;
+  // 8 words per wave per step, all loads in flight before the sigmoids (one
+  // dependent load per word made this latency-bound)
+  const int nw = blockDim.x >> 6;
+  for (int w0 = wv * 8; w0 < W64; w0 += nw * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = (w0 + u) * 64 + lane;
+      v[u] = (w0 + u < W64 && p < P) ? src[p] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = (w0 + u) * 64 + lane;
+      const bool on = w0 + u < W64 && p < P && sigmoidf_tf(v[u]) > thr;
+      const uint64_t b = __ballot(on);
+      if (lane == 0 && w0 + u < W64) dst[w0 + u] = b;
+    }
   }
   if (threadIdx.x == 0) {
     classes[(size_t)n * k + t] = cls;
