@@ -397,6 +397,13 @@ def split_bf16x3(x):
 _CONV_WS, _WGRAD_WS = {}, {}
 
 
+# Narrow-Cout convs (<= 64: the 128x64 / 128x32 tiles) run the split-product
+# kernel too (r2 A/B, tools/conv_ab.py: res2 3x3 64->64 125 -> 103 us, 1x1
+# 256->64 71 -> 61 us, 512->64 46 -> 34 us vs the native f32 MFMA);
+# D2MI_NARROW_SPLIT=0 puts them back on the f32 kernel.
+_NARROW_SPLIT = os.environ.get("D2MI_NARROW_SPLIT", "1") != "0"
+
+
 def _presplit_ok(x, Cin):
     return Cin % 8 == 0 and 6 * x.numel() < 2 ** 31
 
@@ -446,9 +453,7 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
             raise ValueError(f"relu_gate {tuple(relu_gate.shape)} != output {tuple(y.shape)}")
     if residual is not None and residual.shape != y.shape:
         raise ValueError(f"residual {tuple(residual.shape)} != output {tuple(y.shape)}")
-    # measured policy (tools/bench_kernels.py --only conv): narrow Cout (the
-    # 128x64 / 128x32 tiles) gains nothing from the split products.
-    if math_mode == "split" and Cout <= 64:
+    if math_mode == "split" and Cout <= 64 and not _NARROW_SPLIT:
         math_mode = "f32"
     presplit = (math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps
                 and relu_gate is None) and (
@@ -516,7 +521,7 @@ def conv2d_nhwc_levels(xs, w_packed, bias=None, stride=1, pad=(0, 0), relu=False
         OW = (W + pb + pe - KW) // stride + 1
         ys.append(torch.empty((N, OH, OW, Cout), dtype=torch.float32, device=x.device))
         dims += [N, H, W]
-    if math_mode == "split" and Cout <= 64:
+    if math_mode == "split" and Cout <= 64 and not _NARROW_SPLIT:
         math_mode = "f32"
     flags = (1 if relu else 0) | (4 if math_mode == "split" else 0)
     xp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in xs])
