@@ -98,64 +98,96 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// One wave per segment.  removed[] lives in LDS (T words).
-__global__ __launch_bounds__(64) void nms_scan_kernel(const uint64_t* __restrict__ mask,
-                                                      const int32_t* __restrict__ idx,
-                                                      const int32_t* __restrict__ count, int cap,
-                                                      int T, int max_out,
-                                                      int32_t* __restrict__ keep,
-                                                      int32_t* __restrict__ num_keep) {
+// One workgroup of four waves per segment; removed[] lives in LDS (T words).
+// Wave 0 resolves each 64-row tile serially (the diagonal words in scalar
+// registers via v_readlane); then all four waves propagate the kept rows
+// into the removal words of the later tiles, each wave a quarter of the rows
+// (16 mask loads in flight per lane: one round of load latency per tile
+// instead of four), combined with an LDS atomic OR (order-free: exact).
+constexpr int kScanWaves = 4;
+__global__ __launch_bounds__(64 * kScanWaves) void nms_scan_kernel(
+    const uint64_t* __restrict__ mask, const int32_t* __restrict__ idx,
+    const int32_t* __restrict__ count, int cap, int T, int max_out, int32_t* __restrict__ keep,
+    int32_t* __restrict__ num_keep) {
   extern __shared__ uint64_t removed[];
+  __shared__ uint64_t s_keptm;
+  __shared__ int s_kept;
   const int s = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = count[s];
   const int nt = (n + 63) / 64;
-  for (int t = lane; t < nt; t += 64) removed[t] = 0;
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) removed[t] = 0;
   __syncthreads();
   const size_t base = (size_t)s * cap;
   int32_t* out = keep + (size_t)s * max_out;
   int kept = 0;
+  constexpr int RW = 64 / kScanWaves;  // propagation rows per wave
+  const int r0 = wave * RW;
+  // wave 0 holds the next tile's diagonal words and output indices in flight
+  // while the current tile resolves and propagates (neither depends on
+  // removed[]).  (Issuing the propagation loads before the resolve too
+  // measured slower: 157 vs 144 us per RPN scan.)
+  uint64_t diag_next = 0;
+  int32_t idx_next = 0;
+  if (wave == 0 && nt > 0) {
+    diag_next = lane < n ? mask[(base + lane) * T] : 0ull;
+    idx_next = lane < n ? idx[base + lane] : 0;
+  }
   for (int t = 0; t < nt && kept < max_out; ++t) {
-    const int row = t * 64 + lane;
-    const uint64_t diag = row < n ? mask[(base + row) * T + t] : 0ull;
-    const int rem = n - t * 64;
-    uint64_t w = removed[t];
-    if (rem < 64) w |= ~((1ull << rem) - 1ull);
-    uint64_t keptm = 0;
-    for (int r = 0; r < 64; ++r) {
-      if (kept >= max_out) break;
-      if (!((w >> r) & 1ull)) {
-        keptm |= 1ull << r;
-        ++kept;
-        w |= readlane64(diag, r);
+    const int t2a = t + 1 + lane;  // this lane's first later tile
+    if (wave == 0) {
+      const int row = t * 64 + lane;
+      const uint64_t diag = diag_next;
+      const int32_t my_idx = idx_next;
+      if (t + 1 < nt) {
+        const int nrow = row + 64;
+        diag_next = nrow < n ? mask[(base + nrow) * T + t + 1] : 0ull;
+        idx_next = nrow < n ? idx[base + nrow] : 0;
+      }
+      const int rem = n - t * 64;
+      uint64_t w = removed[t];
+      if (rem < 64) w |= ~((1ull << rem) - 1ull);
+      uint64_t keptm = 0;
+      for (int r = 0; r < 64; ++r) {
+        if (kept >= max_out) break;
+        if (!((w >> r) & 1ull)) {
+          keptm |= 1ull << r;
+          ++kept;
+          w |= readlane64(diag, r);
+        }
+      }
+      if ((keptm >> lane) & 1ull) {
+        const int pos = (kept - __popcll(keptm)) + __popcll(keptm & ((1ull << lane) - 1ull));
+        out[pos] = my_idx;
+      }
+      if (lane == 0) {
+        s_keptm = keptm;
+        s_kept = kept;
       }
     }
-    if ((keptm >> lane) & 1ull) {
-      const int pos = (kept - __popcll(keptm)) + __popcll(keptm & ((1ull << lane) - 1ull));
-      out[pos] = idx[base + row];
-    }
-    if (kept >= max_out) break;
-    // propagate kept rows of tile t into the removal words of later tiles.
-    // Tile t is not the last, so all its 64 rows exist: their words are
-    // loaded unconditionally, 16 in flight at a time, and masked by keptm
-    // (a loop over the kept rows only would wait on one load per row).
-    for (int t2 = t + 1 + lane; t2 < nt; t2 += 64) {
-      uint64_t acc = 0;
-      const uint64_t* col = mask + (base + (size_t)t * 64) * T + t2;
+    __syncthreads();
+    const uint64_t keptm = s_keptm;
+    kept = s_kept;
+    if (kept >= max_out) break;  // uniform: every wave read the same s_kept
+    // propagate the kept rows of tile t (not the last, so all 64 rows exist)
+    // into the removal words of the later tiles: wave v takes rows 16v..16v+15
+    if ((keptm >> r0) & ((1ull << RW) - 1ull)) {
+      for (int t2 = t2a; t2 < nt; t2 += 64) {
+        const uint64_t* col = mask + (base + (size_t)t * 64 + r0) * T + t2;
+        uint64_t v[RW];
 #pragma unroll
-      for (int r0 = 0; r0 < 64; r0 += 16) {
-        uint64_t v[16];
+        for (int r = 0; r < RW; ++r) v[r] = col[(size_t)r * T];
+        uint64_t acc = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = col[(size_t)(r0 + r) * T];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc |= ((keptm >> (r0 + r)) & 1ull) ? v[r] : 0ull;
+        for (int r = 0; r < RW; ++r) acc |= ((keptm >> (r0 + r)) & 1ull) ? v[r] : 0ull;
+        if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&removed[t2]),
+                          (unsigned long long)acc);
       }
-      removed[t2] |= acc;
     }
     __syncthreads();
   }
-  for (int i = kept + lane; i < max_out; i += 64) out[i] = -1;
-  if (lane == 0) num_keep[s] = kept;
+  for (int i = kept + (int)threadIdx.x; i < max_out; i += blockDim.x) out[i] = -1;
+  if (threadIdx.x == 0) num_keep[s] = kept;
 }
 
 }  // namespace
@@ -184,7 +216,8 @@ int nms_sorted(const float4* sboxes, const int32_t* sidx, const int32_t* count, 
   hipLaunchKernelGGL(nms_mask_kernel, dim3(T, T, S), dim3(64), 0, stream, sboxes, count, cap, T,
                      iou_thr, mask);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(64), T * sizeof(uint64_t), stream, mask, sidx,
+  hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(64 * kScanWaves), T * sizeof(uint64_t), stream,
+                     mask, sidx,
                      count, cap, T, max_out, keep, num_keep);
   D2MI_LAUNCH_CHECK();
   return 0;
