@@ -472,7 +472,12 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
   p.nchunks = (int)((P + KP - 1) / KP);
   // about one round of resident workgroups (2 or 3 per CU), each walking
   // >= 16 chunks
-  p.occ3 = p.TM == 2 && p.TN == 2 && P >= 65536 && wgrad_occ3();
+  // D2MI_WGRAD_OCC3_MIN_P: the pixel count from which the 3-per-CU kernel runs (A/B)
+  static const long long occ3_min_p = [] {
+    const char* e = getenv("D2MI_WGRAD_OCC3_MIN_P");
+    return e ? atoll(e) : 65536LL;
+  }();
+  p.occ3 = p.TM == 2 && p.TN == 2 && P >= occ3_min_p && wgrad_occ3();
   // D2MI_WGRAD_SLOTS / D2MI_WGRAD_MINCH: the split target and the minimum
   // chunks per split (A/B knobs)
   static const int slots_env = [] {
