@@ -196,7 +196,7 @@ def kernel_report(summary, mode="infer"):
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                      "traffic": pmc_traffic(pmc_group, mode), "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
-    for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_topk",
+    for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_postprocess",
                  "solo_mask_stats",
                  "solo_matrix_nms", "solo_paste"):
         if name not in summary:

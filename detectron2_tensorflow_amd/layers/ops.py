@@ -1322,7 +1322,7 @@ def retinanet_inference(box_cls, box_delta, strides, cell_anchors, num_classes, 
         _C.ptr(os_), _C.ptr(oc), _C.ptr(ov), _C.ptr(ws), wsb, _C.stream_of(dev))
     # algorithmic bytes: the dense logit scan, 4 B per (anchor, class) score
     # (64.5 MB per image at 1333x800)
-    KernelTimer.stop(ev, "retinanet_topk", 4 * sum(t.numel() for t in box_cls))
+    KernelTimer.stop(ev, "retinanet_postprocess", 4 * sum(t.numel() for t in box_cls))
     _C.check(rc, "d2mi_retinanet_inference")
     return ob, os_, oc, ov.bool()
 
