@@ -144,9 +144,14 @@ class StandardROIHeads(ROIHeads):
             # the box and mask poolers read the same p2..p5: one gradient map
             # set for both backwards (ops._RoIAlignFn grad_share)
             share = {} if self.mask_on else None
+            # the mask branch's foreground count is read while the box branch
+            # is enqueued (the device never idles at the read)
+            pending = None
+            if self.mask_on and self.mask_compact_rows:
+                pending = host_sync.start_read(self._mask_fg(sampled).sum())
             losses = self._box_losses(feats, sampled, share)
             if self.mask_on:
-                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share)
+                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending)
             return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
         pred = self.forward_with_given_boxes(features, pred)
@@ -185,7 +190,13 @@ class StandardROIHeads(ROIHeads):
                                 sampled["gt_boxes"].reshape(-1, 4), sampled["is_valid"].reshape(-1),
                                 self.box2box_transform, self.smooth_l1_beta)
 
-    def _mask_loss(self, feats, sampled, targets, grad_share=None):
+    def _mask_fg(self, sampled):
+        """Foreground flags of the first int(S * POSITIVE_FRACTION) slots per image."""
+        F_ = int(self.batch_size_per_image * self.positive_sample_fraction)
+        return (sampled["is_valid"][:, :F_] & (sampled["gt_classes"][:, :F_] >= 0)
+                & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
+
+    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None):
         """_forward_mask training branch (roi_heads.py:594-600) over the first
         int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
         foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
@@ -194,8 +205,7 @@ class StandardROIHeads(ROIHeads):
         N = sampled["boxes"].shape[0]
         dev = boxes.device
         cls = sampled["gt_classes"][:, :F_].reshape(-1)
-        fg = (sampled["is_valid"][:, :F_] & (sampled["gt_classes"][:, :F_] >= 0)
-              & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
+        fg = self._mask_fg(sampled)
         img = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(F_)
         gm = targets["gt_masks"]
         G = gm.shape[1]
@@ -207,7 +217,8 @@ class StandardROIHeads(ROIHeads):
             # host read of the foreground count; the rows are gathered fg-first
             # (image order kept) and padded to a multiple of MASK_ROW_BUCKET
             # with masked-out rows, which bounds the number of distinct shapes.
-            nfg = host_sync.read_ints(fg.sum())[0]
+            nfg = (host_sync.finish_read(pending) if pending is not None
+                   else host_sync.read_ints(fg.sum()))[0]
             B = fg.numel()
             R = min(B, max(self.MASK_ROW_BUCKET, -(-nfg // self.MASK_ROW_BUCKET) * self.MASK_ROW_BUCKET))
             key = (~fg).to(torch.int64) * B + torch.arange(B, device=dev)

@@ -25,6 +25,36 @@ def read_ints(t):
     return [int(v) for v in t.reshape(-1).cpu().tolist()]
 
 
+class PendingRead:
+    """A device-to-host read started early: the values are copied into pinned
+    host memory behind the work already queued, an event marks them ready,
+    and the host keeps enqueueing until it actually needs them."""
+
+    def __init__(self, t):
+        self.host = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+        self.host.copy_(t.reshape(-1), non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(t.device))
+
+
+def start_read(t):
+    """Begin reading a small device tensor without blocking (finish_read)."""
+    if not t.is_cuda:
+        return [int(v) for v in t.reshape(-1).tolist()]
+    return PendingRead(t)
+
+
+def finish_read(p):
+    """int values of a start_read, blocking (and timed) only if not yet there."""
+    global blocked_s
+    if not isinstance(p, PendingRead):
+        return p
+    t0 = time.perf_counter()
+    p.event.synchronize()
+    blocked_s += time.perf_counter() - t0
+    return [int(v) for v in p.host.tolist()]
+
+
 def reset():
     global blocked_s
     blocked_s = 0.0
