@@ -22,7 +22,10 @@ its slice of the reduced bucket.
 Bucket size: the ~44 M trainable fp32 gradients (~177 MB) of Mask R-CNN R50-FPN
 split into 32 MB buckets give 6 collectives per step — large enough that each
 ring all-reduce runs at xGMI link bandwidth, small enough that the first
-launches early in backward.
+launches early in backward.  The LAST bucket (the earliest-registered
+parameters, whose gradients backward produces last) is capped at
+``tail_bytes`` (4 MB, or bucket_bytes if smaller): its all-reduce is the one that cannot overlap the
+backward, so it is kept short.
 """
 import torch
 import torch.distributed as dist
@@ -37,23 +40,33 @@ class _Bucket:
 
 
 class BucketedAllReduce:
-    def __init__(self, params, bucket_bytes=32 << 20, group=None):
+    def __init__(self, params, bucket_bytes=32 << 20, group=None, tail_bytes=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.params = [p for p in params if p.requires_grad]
+        # partition in registration order starting from the tail bucket (at
+        # most tail_bytes), then launch order = reverse registration order
+        if tail_bytes is None:
+            tail_bytes = min(4 << 20, bucket_bytes)
+        groups, cur, cap, nbytes = [], [], tail_bytes, 0
+        for p in self.params:
+            if cur and nbytes + p.numel() * 4 > cap:
+                groups.append(cur)
+                cur, cap, nbytes = [], bucket_bytes, 0
+            cur.append(p)
+            nbytes += p.numel() * 4
+        if cur:
+            groups.append(cur)
         self.buckets = []
         self.where = {}
-        cur = _Bucket()
-        for p in reversed(self.params):
-            if cur.params and (cur.numel + p.numel()) * 4 > bucket_bytes:
-                self.buckets.append(cur)
-                cur = _Bucket()
-            self.where[p] = (len(self.buckets), len(cur.params))
-            cur.params.append(p)
-            cur.offsets.append(cur.numel)
-            cur.numel += p.numel()
-        if cur.params:
-            self.buckets.append(cur)
+        for g in reversed(groups):
+            b = _Bucket()
+            for p in reversed(g):
+                self.where[p] = (len(self.buckets), len(b.params))
+                b.params.append(p)
+                b.offsets.append(b.numel)
+                b.numel += p.numel()
+            self.buckets.append(b)
         self._next = 0
         self._hooks = []
         if self.world > 1:
