@@ -108,6 +108,7 @@ _SIGS = {
     "d2mi_column_sum": (c_int, [P, ctypes.c_longlong, c_int, P, P, c_size_t, P]),
     "d2mi_upsample2x_grad": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_stride_scatter": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_stride_scatter_ex": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_match_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_match_boxes": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_float,
                                  c_float, P, P, P, c_size_t, P]),

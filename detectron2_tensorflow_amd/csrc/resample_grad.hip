@@ -11,6 +11,8 @@
 //    GEMM on its strided grid: out[n,h,w,c] = (h%s == 0 && w%s == 0 ?
 //    g[n,h/s,w/s,c] : 0) (+ add[n,h,w,c]).  Replaces zeros + a strided copy
 //    (+ autograd's add of the other consumer's gradient).
+//    d2mi_stride_scatter_ex adds a second operand and a ReLU gate: the last
+//    of three consumers of a ReLU output forms its whole gradient in one pass.
 //
 // NHWC f32, C % 4 == 0: one float4 of channels per thread, grid-stride.
 #include "common.h"
@@ -50,8 +52,9 @@ __global__ void upsample2x_grad_kernel(const float4* __restrict__ gy, int N, int
 }
 
 __global__ void stride_scatter_kernel(const float4* __restrict__ g, const float4* __restrict__ add,
-                                      int N, int H, int W, int C4, int stride, int GH, int GW,
-                                      float4* __restrict__ out) {
+                                      const float4* __restrict__ add2,
+                                      const float4* __restrict__ gate, int N, int H, int W, int C4,
+                                      int stride, int GH, int GW, float4* __restrict__ out) {
   const int64_t total = (int64_t)N * H * W * C4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -67,6 +70,17 @@ __global__ void stride_scatter_kernel(const float4* __restrict__ g, const float4
     if (add) {
       const float4 a = add[i];
       v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (add2) {  // (scatter + add) + add2: autograd's order for a third consumer
+      const float4 a = add2[i];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (gate) {  // threshold_backward(v, gate, 0): kept where gate > 0
+      const float4 q = gate[i];
+      v.x = q.x > 0.f ? v.x : 0.f;
+      v.y = q.y > 0.f ? v.y : 0.f;
+      v.z = q.z > 0.f ? v.z : 0.f;
+      v.w = q.w > 0.f ? v.w : 0.f;
     }
     out[i] = v;
   }
@@ -93,19 +107,27 @@ extern "C" int d2mi_upsample2x_grad(const float* gy, int N, int OH, int OW, int 
   return 0;
 }
 
-extern "C" int d2mi_stride_scatter(const float* g, const float* add, int N, int H, int W, int C,
-                                   int stride, float* out, void* stream) {
+extern "C" int d2mi_stride_scatter_ex(const float* g, const float* add, const float* add2,
+                                      const float* gate, int N, int H, int W, int C, int stride,
+                                      float* out, void* stream) {
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0 && stride > 0,
                "bad stride-scatter shape");
   D2MI_REQUIRE(g && out && ((uintptr_t)g & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
-                   ((uintptr_t)add & 15) == 0,
-               "g / add / out must be 16-byte aligned");
+                   ((uintptr_t)add & 15) == 0 && ((uintptr_t)add2 & 15) == 0 &&
+                   ((uintptr_t)gate & 15) == 0,
+               "g / add / add2 / gate / out must be 16-byte aligned");
   const int GH = (H - 1) / stride + 1, GW = (W - 1) / stride + 1;
   const int64_t total = (int64_t)N * H * W * (C / 4);
   hipLaunchKernelGGL(stride_scatter_kernel, dim3(grid_for(total)), dim3(256), 0,
                      as_stream(stream), reinterpret_cast<const float4*>(g),
-                     reinterpret_cast<const float4*>(add), N, H, W, C / 4, stride, GH, GW,
+                     reinterpret_cast<const float4*>(add), reinterpret_cast<const float4*>(add2),
+                     reinterpret_cast<const float4*>(gate), N, H, W, C / 4, stride, GH, GW,
                      reinterpret_cast<float4*>(out));
   D2MI_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int d2mi_stride_scatter(const float* g, const float* add, int N, int H, int W, int C,
+                                   int stride, float* out, void* stream) {
+  return d2mi_stride_scatter_ex(g, add, nullptr, nullptr, N, H, W, C, stride, out, stream);
 }

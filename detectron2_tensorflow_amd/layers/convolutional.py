@@ -44,7 +44,7 @@ def same_pads(kernel_size, rate=1):
     return pb, pad_total - pb
 
 
-def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
+def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None, add2=None):
     """Input gradient (+ add, then the relu_gate mask, when given).  Stride 1:
     a forward conv of gy with the spatially flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
     of the transposed conv, flipped by the kernel's tap indexing (kFlipTaps) —
@@ -53,6 +53,13 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
     zeros.  Anything else: torch.nn.grad (MIOpen)."""
     KH, KW, Cin, Cout = w.shape
     gy = gy.contiguous()
+    if add2 is not None:  # (dgrad + add) + add2, gated: the strided 1x1 scatter only
+        if not (KH == 1 and KW == 1 and pb == 0 and pe == 0 and stride > 1 and Cin % 4 == 0
+                and Cout % 4 == 0):
+            gx = _dgrad(gy, w, x_shape, stride, pb, pe, add=add).add_(add2)
+            return gx if relu_gate is None else torch.ops.aten.threshold_backward(gx, relu_gate, 0.0)
+        g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
+        return ops.stride_scatter(g, x_shape, stride, add, add2, relu_gate)
     if KH == KW and Cout % 4 == 0:
         if stride == 1 and max(pb, pe) <= KH - 1:
             # the flip is an index flip inside the kernel (no flipped copy)
@@ -61,13 +68,14 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None):
                                    residual=add, relu_gate=relu_gate)
         if KH == 1 and pb == 0 and pe == 0:
             g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
-            if Cin % 4 == 0:  # zero holes + scatter (+ add) in one pass
-                return ops.stride_scatter(g, x_shape, stride, add)
+            if Cin % 4 == 0:  # zero holes + scatter (+ add) (+ gate) in one pass
+                return ops.stride_scatter(g, x_shape, stride, add, gate=relu_gate)
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
             gx[:, ::stride, ::stride] = g
-            return gx if add is None else gx.add_(add)
+            gx = gx if add is None else gx.add_(add)
+            return gx if relu_gate is None else torch.ops.aten.threshold_backward(gx, relu_gate, 0.0)
     if relu_gate is not None:
-        raise ValueError("relu_gate is fused into the stride-1 MFMA dgrad only")
+        raise ValueError("relu_gate is fused into the stride-1 MFMA dgrad / the 1x1 scatter only")
     xin_shape = (x_shape[0], x_shape[3], x_shape[1] + pb + pe, x_shape[2] + pb + pe)
     gx = torch.nn.grad.conv2d_input(xin_shape, w.permute(3, 2, 0, 1), gy.permute(0, 3, 1, 2),
                                     stride, 0)
@@ -142,7 +150,7 @@ class _ConvMFMAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
                 relu_after=False, gate_input=False, res_grad_to=None, grad_from=None,
-                pair_grad=None):
+                pair_grad=None, join=None):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
@@ -154,6 +162,9 @@ class _ConvMFMAFn(torch.autograd.Function):
         ctx.res_grad_to = res_grad_to if residual is not None else None
         ctx.grad_from = grad_from
         ctx.pair_grad = pair_grad
+        ctx.join = join
+        # the producer's ReLU tag, used if a join is registered by backward time
+        ctx.relu_cand = getattr(x, "_d2mi_relu_info", None)
         ctx.out_info = None
         if relu:  # (forward runs with grad mode off: tag unconditionally)
             ctx.out_info = {"masked": False}
@@ -179,7 +190,9 @@ class _ConvMFMAFn(torch.autograd.Function):
             ctx.res_grad_to["g"] = gres  # taken by the conv reading the same tensor
             gres = None
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and _join_active(ctx):
+            gx = _join_backward(ctx, gy, x, w, stride, pb, pe)
+        elif ctx.needs_input_grad[0]:
             add = ctx.grad_from.pop("g", None) if ctx.grad_from is not None else None
             pair = ctx.pair_grad
             deposit = False
@@ -205,7 +218,58 @@ class _ConvMFMAFn(torch.autograd.Function):
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
             gb = ops.column_sum(gy)
-        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None
+        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None
+
+
+def _join_active(ctx):
+    p = ctx.join if ctx.join is not None else ctx.pair_grad
+    return p is not None and p.get("join", False) and ctx.grad_from is None
+
+
+def _join_backward(ctx, gy, x, w, stride, pb, pe):
+    """Input gradient of a conv in a three-consumer join: a ReLU output x (a
+    ResNet stage output) read by the next stage's conv1 / projection-shortcut
+    pair AND by the FPN lateral (``join``, registered by the FPN forward in
+    the pair's dict).  Autograd would form  lat + (pair2 + pair1)  and then
+    the producer's threshold_backward; here
+      * the first pair member deposits its gradient ("g", as without a join);
+      * the second pair member forms  s = dgrad + g ; if the lateral's
+        gradient is already there it returns  gate((s) + lat)  (one scatter
+        pass for a strided 1x1), else it deposits s ("sum");
+      * the lateral returns  gate(dgrad + s)  if s is there, else it deposits
+        its own dgrad ("lat").
+    The last one applies the producer's ReLU mask in the same pass and flags
+    it (the producer then skips its threshold_backward), so the sum and the
+    gate are bit-identical to the autograd formulation.  Members that
+    deposit return None for x."""
+    info = ctx.relu_cand
+    if ctx.join is not None:  # the lateral
+        p = ctx.join
+        s = p.pop("sum", None)
+        if s is None:
+            p["lat"] = _dgrad(gy, w, x.shape, stride, pb, pe)
+            return None
+        p["last"] = "lateral"  # (tests: which member completed the join)
+        if info is not None and _gate_eligible(w.shape, stride, pb, pe):
+            gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=s)
+            info["masked"] = True
+            return gx
+        return _dgrad(gy, w, x.shape, stride, pb, pe, add=s)
+    p = ctx.pair_grad
+    other = p.pop("g", None)
+    if other is None:  # first of the pair
+        p["g"] = _dgrad(gy, w, x.shape, stride, pb, pe)
+        return None
+    lat = p.pop("lat", None)
+    if lat is None:
+        p["sum"] = _dgrad(gy, w, x.shape, stride, pb, pe, add=other)
+        return None
+    p["last"] = "pair"
+    gate = x if info is not None else None
+    gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=gate, add=other, add2=lat)
+    if info is not None:
+        info["masked"] = True
+    return gx
 
 
 class FoldGroup:
@@ -405,7 +469,7 @@ class Conv2D(Layer):
 
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
              relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None,
-             raw=False):
+             raw=False, join=None):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -430,6 +494,11 @@ class Conv2D(Layer):
             if (topdown is not None or residual is not None) and fuse_relu and not relu_after_add:
                 raise ValueError("relu(conv) + add cannot be fused; use relu_after_add")
             padc = (-self.in_channels) % 4
+            if join is not None:
+                if padc or not torch.is_grad_enabled():
+                    join = None  # (a padded input is another tensor: no join)
+                else:
+                    join["join"] = True  # the pair members now leave their sum to this layer
             if padc:
                 inputs = F.pad(inputs, (0, padc))
                 w = F.pad(w, (0, 0, 0, padc))
@@ -439,7 +508,7 @@ class Conv2D(Layer):
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add,
                                     bool(relu_input_sole_consumer), res_grad_to, grad_from,
-                                    pair_grad)
+                                    pair_grad, join)
             if raw:  # the conv (+ bias) alone: the caller applies the normalizer / activation
                 return ret
             if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \

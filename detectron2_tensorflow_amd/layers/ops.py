@@ -847,20 +847,27 @@ def upsample2x_grad(gy):
     return out
 
 
-def stride_scatter(g, out_shape, stride, add=None):
+def stride_scatter(g, out_shape, stride, add=None, add2=None, gate=None):
     """Input gradient of a 1x1 stride-s conv from its GEMM on the strided grid
-    (d2mi_stride_scatter): zeros off the grid, plus add (nullable)."""
+    (d2mi_stride_scatter_ex): zeros off the grid, + add, + add2 (nullable, in
+    that order), then zeroed where gate <= 0 (gate nullable: the ReLU backward
+    of the ReLU output ``gate``)."""
     g = _f32c(g)
     add = _f32c(add) if add is not None else None
+    add2 = _f32c(add2) if add2 is not None else None
+    gate = _f32c(gate) if gate is not None else None
     _C.require_device(g)
     N, H, W, C = out_shape
     if g.shape != (N, (H - 1) // stride + 1, (W - 1) // stride + 1, C):
         raise ValueError(f"stride_scatter: {tuple(g.shape)} is not the stride-{stride} grid of "
                          f"{tuple(out_shape)}")
+    for t in (add, add2, gate):
+        if t is not None and tuple(t.shape) != tuple(out_shape):
+            raise ValueError(f"stride_scatter: operand {tuple(t.shape)} != {tuple(out_shape)}")
     out = torch.empty(tuple(out_shape), dtype=torch.float32, device=g.device)
-    rc = _C.lib().d2mi_stride_scatter(_C.ptr(g), _C.ptr(add), N, H, W, C, int(stride),
-                                      _C.ptr(out), _C.stream_of(g.device))
-    _C.check(rc, "d2mi_stride_scatter")
+    rc = _C.lib().d2mi_stride_scatter_ex(_C.ptr(g), _C.ptr(add), _C.ptr(add2), _C.ptr(gate), N, H,
+                                         W, C, int(stride), _C.ptr(out), _C.stream_of(g.device))
+    _C.check(rc, "d2mi_stride_scatter_ex")
     return out
 
 

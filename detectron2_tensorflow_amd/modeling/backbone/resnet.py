@@ -59,6 +59,10 @@ class BottleneckBlock(Layer):
         # meet in the second one's epilogue instead of an autograd add
         pair = ({} if self.grad_pair and self.shortcut is not None and torch.is_grad_enabled()
                 else None)
+        if pair is not None:
+            # a later reader of x (the FPN lateral) may join the pair: see
+            # layers/convolutional.py:_join_backward
+            x._d2mi_pair = pair
         sc = self.shortcut(x, pair_grad=pair) if self.shortcut is not None else x
         # relu(conv3(...) + shortcut) in one kernel.  conv1 -> conv2 -> conv3 is
         # a chain of sole consumers: each one's dgrad applies the previous

@@ -8,6 +8,7 @@ LastLevelMaxPool is max_pool k1/s2 = p5[:, ::2, ::2] (fpn.py:171-183);
 LastLevelP6P7 returns post-ReLU p6 and p7 = conv3x3/2(p6) (fpn.py:186-217).
 """
 import math
+import os
 
 import torch
 
@@ -94,14 +95,31 @@ class FPN(Layer):
     def size_divisibility(self):
         return self._size_divisibility
 
+    # A bottom-up feature that is also the input of the next ResNet stage (its
+    # conv1 / projection-shortcut pair) and read by nothing else: the lateral
+    # joins that pair's gradient hand-off, so the last of the three backwards
+    # forms the feature's whole gradient with its ReLU mask (no autograd add,
+    # no threshold pass; layers/convolutional.py:_join_backward).
+    JOIN_GRAD = os.environ.get("D2MI_FPN_JOIN", "1") != "0"
+
+    def _join_of(self, name, feats):
+        if not self.JOIN_GRAD:
+            return None
+        if self.top_block is not None and getattr(self.top_block, "in_feature", None) == name:
+            return None  # a third reader (P6 from C5)
+        return getattr(feats, "_d2mi_pair", None)
+
     def call(self, bottom_up_features):
-        x = [bottom_up_features[f] for f in self.in_features[::-1]]
-        prev = self.lateral_convs[0](x[0])
+        names = self.in_features[::-1]
+        x = [bottom_up_features[f] for f in names]
+        prev = self.lateral_convs[0](x[0], join=self._join_of(names[0], x[0]))
         results = [self.output_convs[0](prev)]
         fused = self.fuse_type == "sum" and self.norm == ""
-        for feats, lat, out in zip(x[1:], self.lateral_convs[1:], self.output_convs[1:]):
+        for name, feats, lat, out in zip(names[1:], x[1:], self.lateral_convs[1:],
+                                         self.output_convs[1:]):
             if fused:
-                prev = lat(feats, topdown=prev)           # lateral + up2(prev) in one kernel
+                # lateral + up2(prev) in one kernel
+                prev = lat(feats, topdown=prev, join=self._join_of(name, feats))
             else:
                 prev = lat(feats) + upsample(prev, 2)
                 if self.fuse_type == "avg":

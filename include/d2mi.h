@@ -619,6 +619,14 @@ int d2mi_stem_pool(const float* y, const float* shift, int N, int H, int W, int 
 int d2mi_upsample2x_grad(const float* gy, int N, int OH, int OW, int C, float* gtd, void* stream);
 int d2mi_stride_scatter(const float* g, const float* add, int N, int H, int W, int C, int stride,
                         float* out, void* stream);
+/* d2mi_stride_scatter_ex: the same, then + add2 (nullable), then the ReLU
+ * backward of the producer (gate nullable: out = gate > 0 ? v : 0, the
+ * threshold_backward(v, gate, 0) of the ReLU output `gate`).  Used when a
+ * ResNet stage output feeds the next stage's strided conv1 / shortcut pair
+ * AND the FPN lateral (fpn.py:121-149, resnet.py:52-253): the last of the
+ * three backwards forms the whole gated gradient. */
+int d2mi_stride_scatter_ex(const float* g, const float* add, const float* add2, const float* gate,
+                           int N, int H, int W, int C, int stride, float* out, void* stream);
 
 /* ------------------------------------------------------ Momentum-SGD step
  * Replaces the update of lib/engine/trainer.py:116-139 for every trainable

@@ -1037,6 +1037,71 @@ def test_upsample2x_grad_and_stride_scatter(dev, shape):
                            ref + add)
 
 
+def test_stride_scatter_two_adds_and_gate(dev):
+    """d2mi_stride_scatter_ex: ((scatter + add) + add2) then the ReLU backward
+    of the gate tensor, exactly as torch forms it (threshold_backward)."""
+    g = torch.Generator().manual_seed(11)
+    N, H, W, C, s = 2, 13, 10, 12, 2
+    gs = torch.randn(N, (H - 1) // s + 1, (W - 1) // s + 1, C, generator=g)
+    add, add2 = torch.randn(N, H, W, C, generator=g), torch.randn(N, H, W, C, generator=g)
+    gate = torch.relu(torch.randn(N, H, W, C, generator=g))
+    ref = torch.zeros(N, H, W, C)
+    ref[:, ::s, ::s] = gs
+    want = torch.ops.aten.threshold_backward((ref + add) + add2, gate, 0.0)
+    got = ops().stride_scatter(gs.to(dev), (N, H, W, C), s, add.to(dev), add2.to(dev), gate.to(dev))
+    assert torch.equal(got.cpu(), want)
+    got = ops().stride_scatter(gs.to(dev), (N, H, W, C), s, gate=gate.to(dev))
+    assert torch.equal(got.cpu(), torch.ops.aten.threshold_backward(ref, gate, 0.0))
+
+
+@pytest.mark.parametrize("lateral_first", [False, True])
+def test_stage_output_join_with_fpn_lateral_is_exact(dev, lateral_first):
+    """A ReLU output (a stage output) read by the next stage's strided conv1 /
+    projection-shortcut pair and by an FPN lateral (with its fused top-down
+    add): the three-consumer join (the last backward adds the others'
+    gradients and applies the producer's ReLU mask) gives exactly the
+    gradients of the autograd formulation (adds + threshold_backward).  The
+    lateral created first runs its backward last (autograd runs ready nodes
+    by creation order, newest first): both completion orders are exercised."""
+    from detectron2_tensorflow_amd.layers import Conv2D
+    torch.manual_seed(5)
+    prod = Conv2D(64, 128, 3, activation="relu", impl="mfma", scope="prod").to(dev)
+    conv1 = Conv2D(128, 32, 1, stride=2, impl="mfma", scope="conv1").to(dev)
+    short = Conv2D(128, 256, 1, stride=2, activation=None, impl="mfma", scope="shortcut").to(dev)
+    lat = Conv2D(128, 64, 1, activation=None, impl="mfma", scope="lat").to(dev)
+    mods = (prod, conv1, short, lat)
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 20, 24, 64, generator=g).to(dev)
+    td = torch.randn(2, 10, 12, 64, generator=g).to(dev)
+    gh = torch.randn(2, 10, 12, 32, generator=g).to(dev)
+    gs = torch.randn(2, 10, 12, 256, generator=g).to(dev)
+    gl = torch.randn(2, 20, 24, 64, generator=g).to(dev)
+    res = {}
+    for join in (True, False):
+        for m in mods:
+            m.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        c = prod(xi)
+        pair = {}
+        if lateral_first:
+            lo = lat(c, topdown=td, join=pair if join else None)
+        sc = short(c, pair_grad=pair)
+        h = conv1(c, pair_grad=pair)
+        if not lateral_first:
+            lo = lat(c, topdown=td, join=pair if join else None)
+        torch.autograd.backward([h, sc, lo], [gh, gs, gl])
+        if join:
+            assert pair.get("last") == ("lateral" if lateral_first else "pair")
+            assert not ({"g", "sum", "lat"} & pair.keys())  # nothing left behind
+        res[join] = (xi.grad, {n: q.grad.clone() for m in mods for n, q in m.named_parameters()})
+    gxa, gpa = res[True]
+    gxb, gpb = res[False]
+    assert torch.equal(gxa, gxb)
+    assert gpa.keys() == gpb.keys() and gpa
+    for n in gpa:
+        assert torch.equal(gpa[n], gpb[n]), n
+
+
 @pytest.mark.parametrize("allow_low,per_image", [(True, False), (False, True)])
 def test_fused_match_equals_tensor_matcher(dev, allow_low, per_image):
     """d2mi_match_boxes (IoU + Matcher in one pass) gives the tensor

@@ -1,0 +1,69 @@
+#!/usr/bin/env python
+"""In-process A/B of a Python-level switch on the training step: one trainer,
+blocks of steps alternating between the arms (A B B A ...), each block timed
+with a synchronize on both sides, so box-to-box and run-to-run drift cancels.
+
+usage: python tools/ab_inproc.py --switch fpn_join [--blocks 8 --steps 10]
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _fpn_join(on):
+    from detectron2_tensorflow_amd.modeling.necks.fpn import FPN
+    FPN.JOIN_GRAD = on
+
+
+SWITCHES = {"fpn_join": _fpn_join}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--switch", default="fpn_join", choices=sorted(SWITCHES))
+    ap.add_argument("--blocks", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    import bench
+    sys.argv = [sys.argv[0]]
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    from detectron2_tensorflow_amd import _C
+    from detectron2_tensorflow_amd.engine import Trainer
+    _C.load()
+    cfg, model = bench.build(args, dev)
+    batch = bench.synthetic_batch(args, dev, 0)
+    bench.calibrate_scores(model, batch)
+    tr = Trainer(cfg, model)
+    sw = SWITCHES[a.switch]
+    for on in (True, False, True):
+        sw(on)
+        for _ in range(2):
+            tr.step(batch)
+    torch.cuda.synchronize()
+    times = {True: [], False: []}
+    for b in range(a.blocks):
+        for on in ((True, False) if b % 2 == 0 else (False, True)):
+            sw(on)
+            tr.step(batch)  # one untimed step after the switch
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                tr.step(batch)
+            torch.cuda.synchronize()
+            times[on].append((time.perf_counter() - t0) * 1e3 / a.steps)
+        print(f"block {b}: on {times[True][-1]:.3f} ms  off {times[False][-1]:.3f} ms", flush=True)
+    mon, moff = statistics.median(times[True]), statistics.median(times[False])
+    print(f"{a.switch}: on {mon:.3f} ms/step, off {moff:.3f} ms/step, on/off {mon / moff:.4f} "
+          f"(medians over {a.blocks} blocks of {a.steps} steps)")
+
+
+if __name__ == "__main__":
+    main()
