@@ -119,9 +119,12 @@ struct ConvArgs {
   // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
   // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
   // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
-  // default) MFMA phase, 2 the load-issue phase instead, 0 off.  Measured
-  // (tools/ab_prio.sh, 16 Mask R-CNN shapes): 1 is 1.3 % faster in total, 2-5 %
-  // on the res3-res5 3x3s and 1x1s; 2 is 0.2 %.
+  // default, with bit 4) MFMA phase, 2 the load-issue phase instead, 0 off;
+  // bit 4: the MFMA phase of the double-buffered narrow-Cout kernels too
+  // (default 5 = 1 | 4).  Measured (tools/ab_prio.sh, 16 Mask R-CNN shapes):
+  // 1 is 1.3 % faster in total, 2-5 % on the res3-res5 3x3s and 1x1s; 2 is
+  // 0.2 %; bit 4 (tools/ab_prio_narrow.sh) 2-4 % on the Cout <= 64 shapes,
+  // training bench +1 % in alternating pairs.
   int prio;
   // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
   // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
@@ -590,7 +593,9 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
           load_a(kt + 1, ra[0]);
           load_b(kt + 1);
         }
+        if (a.prio & 4) __builtin_amdgcn_s_setprio(1);
         compute(buf);
+        if (a.prio & 4) __builtin_amdgcn_s_setprio(0);
         if (more) store_tile(buf ^ 1, ra[0], rb);
         __syncthreads();
         buf ^= 1;
@@ -604,15 +609,15 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
       const int prio = a.prio;
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (prio == 2) __builtin_amdgcn_s_setprio(1);
+        if (prio & 2) __builtin_amdgcn_s_setprio(1);
         if (more && !(dbg & 1)) {
           load_b(kt + 1);
           load_a(kt + 1, ra[0]);
         }
-        if (prio == 2) __builtin_amdgcn_s_setprio(0);
-        if (prio == 1) __builtin_amdgcn_s_setprio(1);
+        if (prio & 2) __builtin_amdgcn_s_setprio(0);
+        if (prio & 1) __builtin_amdgcn_s_setprio(1);
         if (!(dbg & 4)) compute(0);
-        if (prio == 1) __builtin_amdgcn_s_setprio(0);
+        if (prio & 1) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         if (more) {
           if (!(dbg & 2)) store_tile(0, ra[0], rb);
@@ -1161,7 +1166,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     static const char* dbg = getenv("D2MI_CONV_DBG");
     a.dbg = dbg ? atoi(dbg) : 0;
     static const char* prio = getenv("D2MI_CONV_PRIO");
-    a.prio = prio ? atoi(prio) : 1;
+    a.prio = prio ? atoi(prio) : 5;
   }
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
