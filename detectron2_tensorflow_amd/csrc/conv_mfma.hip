@@ -124,7 +124,10 @@ struct ConvArgs {
   // (default 5 = 1 | 4).  Measured (tools/ab_prio.sh, 16 Mask R-CNN shapes):
   // 1 is 1.3 % faster in total, 2-5 % on the res3-res5 3x3s and 1x1s; 2 is
   // 0.2 %; bit 4 (tools/ab_prio_narrow.sh) 2-4 % on the Cout <= 64 shapes,
-  // training bench +1 % in alternating pairs.
+  // training bench +1 % in alternating pairs.  A/B-only bits: 8 = loads
+  // issued at priority 1 and the MFMA phase at 2; 16 = the activation loads
+  // issued before the weight loads (tools/ab_prio2.sh: 13 / 21 / 29 within
+  // 0.45 % of 5 on the 16 shapes, below the run-to-run spread; 5 kept).
   int prio;
   // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
   // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
@@ -609,15 +612,21 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
       const int prio = a.prio;
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (prio & 2) __builtin_amdgcn_s_setprio(1);
+        if (prio & (2 | 8)) __builtin_amdgcn_s_setprio(1);
         if (more && !(dbg & 1)) {
-          load_b(kt + 1);
-          load_a(kt + 1, ra[0]);
+          if (prio & 16) {
+            load_a(kt + 1, ra[0]);
+            load_b(kt + 1);
+          } else {
+            load_b(kt + 1);
+            load_a(kt + 1, ra[0]);
+          }
         }
         if (prio & 2) __builtin_amdgcn_s_setprio(0);
-        if (prio & 1) __builtin_amdgcn_s_setprio(1);
+        if (prio & 8) __builtin_amdgcn_s_setprio(2);
+        else if (prio & 1) __builtin_amdgcn_s_setprio(1);
         if (!(dbg & 4)) compute(0);
-        if (prio & 1) __builtin_amdgcn_s_setprio(0);
+        if (prio & (1 | 8)) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         if (more) {
           if (!(dbg & 2)) store_tile(0, ra[0], rb);
