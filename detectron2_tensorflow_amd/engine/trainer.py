@@ -47,7 +47,8 @@ class Trainer:
     def step(self, batched_inputs):
         """One iteration: forward + losses, backward with the overlapped
         all-reduce, clip + momentum update.  Returns the loss dict (device)."""
-        self.model.train()
+        if not self.model.training:  # (train() walks every module: host time per step)
+            self.model.train()
         self.optimizer.zero_grad()
         self.reducer.reset()
         losses = self.model(batched_inputs)

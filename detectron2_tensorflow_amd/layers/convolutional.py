@@ -393,14 +393,14 @@ class Conv2D(Layer):
         # constant while autograd is off or nothing in the fold trains (the
         # layers below FREEZE_AT): cached per parameter version
         cacheable = not (torch.is_grad_enabled() and self.fold_trainable())
-        key = self._param_key()
-        if cacheable and getattr(self, "_fold_key", None) == key:
-            return self._fold_w, self._fold_b, None, self._fold_p
-        group = getattr(self, "_fold_group", None)
-        if not cacheable and group is not None:
+        group = self.__dict__.get("_fold_group")
+        if not cacheable and group is not None:  # (the group checks the versions itself)
             got = group.fetch(self)
             if got is not None:
                 return got[0], got[1], None, got[2]
+        key = self._param_key()
+        if cacheable and getattr(self, "_fold_key", None) == key:
+            return self._fold_w, self._fold_b, None, self._fold_p
         w, b, packed = ops.fold_frozen_bn(self.weights, self.bias, norm.gamma, norm.beta,
                                           norm.moving_mean, norm.moving_variance, norm.epsilon,
                                           want_packed)
