@@ -487,3 +487,45 @@ def test_fused_mask_loss_matches_tensor_formulation(dev, C):
             mh.FUSED_LOSSES = True
     assert res[True][0] == pytest.approx(res[False][0], rel=2e-6)
     torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-9)
+
+
+def test_fpn_join_engages_and_matches_plain_step(dev, monkeypatch):
+    """In a real Mask R-CNN training step the stage-output join engages for
+    C3 and C4 (the next stage's conv1 / shortcut pair + the FPN lateral: three
+    members each; C2 is frozen) and the step's gradients equal those with the
+    join off (FPN.JOIN_GRAD = False: autograd add + threshold_backward)."""
+    from detectron2_tensorflow_amd.layers import convolutional as conv_mod
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.modeling.necks.fpn import FPN
+    from detectron2_tensorflow_amd.utils.synthetic import (calibrate_rcnn_scores,
+                                                           synthetic_train_batch)
+    cfg = _cfg(True)
+    torch.manual_seed(0)
+    model = build_model(cfg).to(dev).train()
+    batch = synthetic_train_batch(2, 256, 320, 5, dev)
+    calibrate_rcnn_scores(model, batch)
+    calls = []
+    real = conv_mod._join_backward
+
+    def counted(ctx, *args):
+        calls.append("lateral" if ctx.join is not None else "pair")
+        return real(ctx, *args)
+
+    monkeypatch.setattr(conv_mod, "_join_backward", counted)
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)  # (MIOpen stem)
+    grads = {}
+    for join in (True, False):
+        monkeypatch.setattr(FPN, "JOIN_GRAD", join)
+        model.zero_grad(set_to_none=True)
+        calls.clear()
+        torch.manual_seed(1)  # the same subsampling draws in both passes
+        losses = model(batch)
+        sum(losses.values()).backward()
+        if join:
+            assert sorted(calls) == ["lateral"] * 2 + ["pair"] * 4, calls
+        else:
+            assert calls == []
+        grads[join] = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    assert grads[True].keys() == grads[False].keys() and grads[True]
+    for n in grads[True]:
+        assert torch.equal(grads[True][n], grads[False][n]), n
