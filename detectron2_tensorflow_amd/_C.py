@@ -79,6 +79,7 @@ _SIGS = {
     "d2mi_group_norm_nhwc_levels": (c_int, [P, P, c_int, c_int, c_int, P, P, c_float, c_int, P, P,
                                             c_size_t, P]),
     "d2mi_conv_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_conv_pack_weights_many": (c_int, [c_int, P, P, P, P]),
     "d2mi_conv2d_nhwc": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_int, P]),
     "d2mi_conv2d_workspace_size": (c_size_t, [c_int] * 10),

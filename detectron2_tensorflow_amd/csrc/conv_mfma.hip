@@ -950,6 +950,40 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
     if (co0 + j < Cout) out[((size_t)tap * Cout + co0 + j) * Cin + ci0 + lane] = tile[lane][j];
 }
 
+// Many weight tensors packed by ONE launch (d2mi_conv_pack_weights_many): the
+// tiled transpose above over a table of up to kMaxPack tensors with
+// Cin % 64 == 0, a workgroup's tensor found from the per-tensor first-block
+// table (block-uniform, so the table reads are scalar).
+constexpr int kMaxPack = 32;
+struct PackMany {
+  const float* w[kMaxPack];
+  float* out[kMaxPack];
+  int Cin[kMaxPack], Cout[kMaxPack];
+  int block0[kMaxPack + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void pack_weights_many_kernel(PackMany p) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < p.n && b >= p.block0[e + 1]) ++e;
+  const int Cin = p.Cin[e], Cout = p.Cout[e];
+  const int nco = (Cout + 63) / 64, nci = Cin / 64;
+  const int local = b - p.block0[e];
+  const int tap = local / (nco * nci);
+  const int rem = local - tap * nco * nci;
+  const int ci0 = (rem / nco) * 64, co0 = (rem % nco) * 64;
+  const float* __restrict__ w = p.w[e];
+  float* __restrict__ out = p.out[e];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = wv; i < 64; i += 4)
+    tile[i][lane] = co0 + lane < Cout ? w[((size_t)tap * Cin + ci0 + i) * Cout + co0 + lane] : 0.f;
+  __syncthreads();
+  for (int j = wv; j < 64; j += 4)
+    if (co0 + j < Cout) out[((size_t)tap * Cout + co0 + j) * Cin + ci0 + lane] = tile[lane][j];
+}
+
 struct Plan {
   int cfg;  // 0: 128x128, 1: 128x64, 2: 128x32
   int BM, BN, splits, kt_per_split, nk, ntiles;
@@ -1049,6 +1083,41 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
 }  // namespace d2mi
 
 using namespace d2mi;
+
+extern "C" int d2mi_conv_pack_weights_many(int n, const float* const* w_hwio, const int32_t* dims,
+                                           float* const* w_packed, void* stream) {
+  D2MI_REQUIRE(n >= 0 && (n == 0 || (w_hwio && dims && w_packed)), "bad pack table");
+  PackMany p = {};
+  auto flush = [&]() -> int {
+    if (p.n == 0) return 0;
+    hipLaunchKernelGGL(pack_weights_many_kernel, dim3(p.block0[p.n]), dim3(256), 0,
+                       as_stream(stream), p);
+    D2MI_LAUNCH_CHECK();
+    p = PackMany{};
+    return 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    const int KH = dims[4 * i], KW = dims[4 * i + 1], Cin = dims[4 * i + 2], Cout = dims[4 * i + 3];
+    D2MI_REQUIRE(KH > 0 && KW > 0 && Cin > 0 && Cout > 0, "bad conv weight shape (entry %d)", i);
+    if (Cin % 64 != 0) {  // the generic kernel, alone
+      const int rc = d2mi_conv_pack_weights(w_hwio[i], KH, KW, Cin, Cout, w_packed[i], stream);
+      if (rc) return rc;
+      continue;
+    }
+    const long long blocks = (long long)KH * KW * ((Cout + 63) / 64) * (Cin / 64);
+    if (p.n == kMaxPack || (long long)p.block0[p.n] + blocks > (1LL << 30)) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    p.w[p.n] = w_hwio[i];
+    p.out[p.n] = w_packed[i];
+    p.Cin[p.n] = Cin;
+    p.Cout[p.n] = Cout;
+    p.block0[p.n + 1] = p.block0[p.n] + (int)blocks;
+    ++p.n;
+  }
+  return flush();
+}
 
 extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout,
                                       float* w_packed, void* stream) {

@@ -316,6 +316,47 @@ class FoldGroup:
         self.slots = {id(m): [w, b, p, False, m._param_key()] for m, (w, b, p) in zip(members, outs)}
 
 
+class PackGroup:
+    """The un-normalised MFMA convs of one model (FPN, RPN head, ROI heads):
+    their packed weight copies are refreshed together.  A layer joins on its
+    first packed_weights() call; the first fetch that finds its layer's
+    parameters changed (the optimizer stepped) repacks EVERY member whose
+    parameters changed in one launch (ops.pack_conv_weights_many) instead of
+    one launch per layer."""
+    ENABLED = True
+
+    def __init__(self):
+        self.members = []
+
+    @classmethod
+    def attach(cls, module):
+        layers = [m for m in module.modules()
+                  if isinstance(m, Conv2D) and not isinstance(m.normalizer_fn, BatchNorm)]
+        if not layers:
+            return None
+        g = cls()
+        for m in layers:
+            m._pack_group = g
+        return g
+
+    def fetch(self, layer):
+        if not any(m is layer for m in self.members):
+            self.members.append(layer)
+        key = layer._param_key()
+        if layer._packed is not None and layer._packed_key == key:
+            return layer._packed
+        stale, keys = [], []
+        for m in self.members:
+            k = key if m is layer else m._param_key()
+            if m._packed is None or m._packed_key != k:
+                stale.append(m)
+                keys.append(k)
+        outs = ops.pack_conv_weights_many([m.weights.detach() for m in stale])
+        for m, k, o in zip(stale, keys, outs):
+            m._packed, m._packed_key = o, k
+        return layer._packed
+
+
 @add_arg_scope
 class Conv2D(Layer):
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding="SAME", rate=1,
@@ -419,6 +460,10 @@ class Conv2D(Layer):
                 and self.in_channels % 4 == 0)
 
     def packed_weights(self, w_eff=None):
+        group = self.__dict__.get("_pack_group")
+        if (group is not None and PackGroup.ENABLED
+                and (w_eff is None or w_eff is self.weights)):
+            return group.fetch(self)
         key = self._param_key()
         if self._packed is None or self._packed_key != key:
             w = self.weights if w_eff is None else w_eff

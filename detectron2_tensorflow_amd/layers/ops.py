@@ -364,6 +364,23 @@ def pack_conv_weights(w_hwio):
     return out
 
 
+def pack_conv_weights_many(ws):
+    """pack_conv_weights of every HWIO tensor in ``ws`` (d2mi_conv_pack_weights_many:
+    one launch for all Cin % 64 == 0 tensors); bit-identical copies."""
+    ws = [_f32c(w) for w in ws]
+    if not ws:
+        return []
+    _C.require_device(*ws)
+    outs = [torch.empty((w.shape[0], w.shape[1], w.shape[3], w.shape[2]), dtype=torch.float32,
+                        device=w.device) for w in ws]
+    wp = _C.host_array(_C.c_void_p, [w.data_ptr() for w in ws])
+    op = _C.host_array(_C.c_void_p, [o.data_ptr() for o in outs])
+    dims = _C.host_array(_C.ctypes.c_int32, [int(v) for w in ws for v in w.shape])
+    rc = _C.lib().d2mi_conv_pack_weights_many(len(ws), wp, dims, op, _C.stream_of(ws[0].device))
+    _C.check(rc, "d2mi_conv_pack_weights_many")
+    return outs
+
+
 # Conv MFMA product form: "f32" = v_mfma_f32_32x32x2_f32 (exact f32 products);
 # "split" = the same f32 operands split exactly into three bf16 terms
 # (h + m + l == x) and multiplied with six v_mfma_f32_32x32x16_bf16 products

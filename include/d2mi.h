@@ -347,6 +347,13 @@ int d2mi_group_norm_nhwc_levels(const float* const* xs, const int32_t* dims, int
  */
 int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout,
                            float* w_packed, void* stream);
+/* d2mi_conv_pack_weights_many: n weight tensors (w_hwio[i], dims[4i..4i+3] =
+ * KH, KW, Cin, Cout) packed as d2mi_conv_pack_weights does, the Cin % 64 == 0
+ * ones by one launch per 32 tensors (the per-step repack of every
+ * un-normalised conv after the optimizer update: FPN, RPN, ROI heads,
+ * convolutional.py:198-263's weights).  Host arrays of device pointers. */
+int d2mi_conv_pack_weights_many(int n, const float* const* w_hwio, const int32_t* dims,
+                                float* const* w_packed, void* stream);
 int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const float* bias,
                      const float* topdown, const float* residual, float* y, int N, int H, int W,
                      int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,

@@ -1245,3 +1245,42 @@ def test_conv_levels_matches_per_level_convs(dev, cout, relu):
     if relu:
         r64 = r64.clamp_min(0)
     torch.testing.assert_close(ys[0].double(), r64, rtol=1e-4, atol=1e-4)
+
+
+def test_pack_weights_many_and_pack_group(dev):
+    """d2mi_conv_pack_weights_many equals d2mi_conv_pack_weights tensor by
+    tensor (tiled Cin % 64 == 0 entries batched, > 32 of them split over
+    launches; other Cin alone), and a PackGroup repacks every member whose
+    parameters changed in one call, leaving the fresh ones untouched."""
+    from detectron2_tensorflow_amd.layers import Conv2D
+    from detectron2_tensorflow_amd.layers.convolutional import PackGroup
+    g = torch.Generator().manual_seed(21)
+    shapes = [(3, 3, 256, 256), (1, 1, 512, 256), (1, 1, 24, 16), (3, 3, 64, 100)] * 9
+    ws = [torch.randn(*s, generator=g).to(dev) for s in shapes]
+    got = ops().pack_conv_weights_many(ws)
+    for w, p in zip(ws, got):
+        assert torch.equal(p, ops().pack_conv_weights(w))
+    convs = [Conv2D(64, 64, 3, impl="mfma", scope=f"c{i}").to(dev) for i in range(3)]
+    grp = PackGroup()
+    for c in convs:
+        c._pack_group = grp
+    x = torch.randn(1, 8, 8, 64, generator=g).to(dev)
+    for c in convs:
+        c(x)
+    assert len(grp.members) == 3
+    kept = convs[2]._packed
+    with torch.no_grad():
+        convs[0].weights.add_(1.0)
+        convs[1].weights.mul_(0.5)
+    calls = []
+    real = ops().pack_conv_weights_many
+    try:
+        ops().pack_conv_weights_many = lambda ws: calls.append(len(ws)) or real(ws)
+        for c in convs:
+            c(x)
+    finally:
+        ops().pack_conv_weights_many = real
+    assert calls == [2]
+    assert convs[2]._packed is kept
+    for c in convs:
+        assert torch.equal(c._packed, ops().pack_conv_weights(c.weights.detach()))

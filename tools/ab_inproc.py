@@ -22,7 +22,12 @@ def _fpn_join(on):
     FPN.JOIN_GRAD = on
 
 
-SWITCHES = {"fpn_join": _fpn_join}
+def _pack_group(on):
+    from detectron2_tensorflow_amd.layers.convolutional import PackGroup
+    PackGroup.ENABLED = on
+
+
+SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group}
 
 
 def main():
