@@ -172,7 +172,7 @@ constexpr int kRedOut = 16, kRedSeg = 16;
 
 __global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
     const float* __restrict__ partial, int chunks, int Cin, int Cout, float* __restrict__ gw,
-    float* __restrict__ gb) {
+    float* __restrict__ gb, int accumulate) {
   __shared__ float red[kRedSeg][kRedOut];
   const int n = (Cin + 1) * Cout;
   const int ol = threadIdx.x % kRedOut, sg = threadIdx.x / kRedOut;
@@ -188,8 +188,9 @@ __global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
     float t = 0.f;
 #pragma unroll
     for (int j = 0; j < kRedSeg; ++j) t += red[j][ol];
-    if (o < Cin * Cout) gw[o] = t;
-    else if (gb) gb[o - Cin * Cout] = t;
+    // accumulate: old + new, the rounding of autograd's sum of two gradients
+    if (o < Cin * Cout) gw[o] = accumulate ? gw[o] + t : t;
+    else if (gb) gb[o - Cin * Cout] = accumulate ? gb[o - Cin * Cout] + t : t;
   }
 }
 
@@ -243,7 +244,7 @@ extern "C" int d2mi_column_sum(const float* x, long long rows, int cols, float* 
   D2MI_LAUNCH_CHECK();
   // reduce: rows of the partial = chunks, "Cin" = 0, Cout = cols -> gb = out
   hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((cols + kRedOut - 1) / kRedOut), dim3(256),
-                     0, st, partial, (int)chunks, 0, cols, nullptr, out);
+                     0, st, partial, (int)chunks, 0, cols, nullptr, out, 0);
   D2MI_LAUNCH_CHECK();
   return 0;
 }
@@ -257,6 +258,12 @@ extern "C" size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout) {
 extern "C" int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout,
                                  float* gw, float* gb, void* workspace, size_t workspace_bytes,
                                  void* stream) {
+  return d2mi_wgrad_skinny_ex(x, g, P, Cin, Cout, gw, gb, 0, workspace, workspace_bytes, stream);
+}
+
+extern "C" int d2mi_wgrad_skinny_ex(const float* x, const float* g, int P, int Cin, int Cout,
+                                    float* gw, float* gb, int accumulate, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
   D2MI_REQUIRE(P > 0 && Cin > 0 && Cout > 0 && Cout <= kMaxCout,
                "wgrad_skinny: P=%d Cin=%d Cout=%d (Cout must be 1..%d)", P, Cin, Cout, kMaxCout);
   const size_t need = d2mi_wgrad_skinny_workspace_size(P, Cin, Cout);
@@ -275,7 +282,7 @@ extern "C" int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin,
   D2MI_LAUNCH_CHECK();
   const int n = (Cin + 1) * Cout;
   hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((n + kRedOut - 1) / kRedOut), dim3(256), 0,
-                     st, partial, chunks, Cin, Cout, gw, gb);
+                     st, partial, chunks, Cin, Cout, gw, gb, accumulate);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

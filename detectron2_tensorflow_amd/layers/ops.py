@@ -1382,22 +1382,31 @@ def paste_masks(box_masks, boxes, out_shape, valid=None, yx_scale=None, threshol
     return out
 
 
-def wgrad_skinny(x, g, with_bias=True):
+def wgrad_skinny(x, g, with_bias=True, accumulate_into=None):
     """1x1-conv weight (+ bias) gradient for Cout <= 16 over all pixels:
-    x [..., Cin], g [..., Cout] -> (gw [1, 1, Cin, Cout] HWIO, gb [Cout] or None)."""
+    x [..., Cin], g [..., Cout] -> (gw [1, 1, Cin, Cout] HWIO, gb [Cout] or None).
+    accumulate_into: a (gw, gb) pair of an earlier call to add this one into
+    (old + new, in place; returned)."""
     x, g = _f32c(x), _f32c(g)
     _C.require_device(x, g)
     Cin, Cout = x.shape[-1], g.shape[-1]
     P = x.numel() // Cin
     if g.numel() != P * Cout:
         raise ValueError(f"wgrad_skinny: {tuple(x.shape)} vs {tuple(g.shape)}")
-    gw = torch.empty((1, 1, Cin, Cout), dtype=torch.float32, device=x.device)
-    gb = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
+    if accumulate_into is not None:
+        gw, gb = accumulate_into
+        if (tuple(gw.shape) != (1, 1, Cin, Cout) or not gw.is_contiguous()
+                or (gb is None) == with_bias):
+            raise ValueError("wgrad_skinny: accumulate_into does not match this gradient")
+    else:
+        gw = torch.empty((1, 1, Cin, Cout), dtype=torch.float32, device=x.device)
+        gb = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
     wsb = _C.lib().d2mi_wgrad_skinny_workspace_size(P, Cin, Cout)
     ws = _C.workspace(wsb, x.device)
     ev = KernelTimer.start()
-    rc = _C.lib().d2mi_wgrad_skinny(_C.ptr(x), _C.ptr(g), P, Cin, Cout, _C.ptr(gw), _C.ptr(gb),
-                                    _C.ptr(ws), wsb, _C.stream_of(x.device))
+    rc = _C.lib().d2mi_wgrad_skinny_ex(_C.ptr(x), _C.ptr(g), P, Cin, Cout, _C.ptr(gw), _C.ptr(gb),
+                                       int(accumulate_into is not None), _C.ptr(ws), wsb,
+                                       _C.stream_of(x.device))
     # algorithmic bytes: x and g read once
     KernelTimer.stop(ev, "wgrad_skinny", 4 * P * (Cin + Cout))
     _C.check(rc, "d2mi_wgrad_skinny")

@@ -75,6 +75,11 @@ class StandardRPNHead(Layer):
                 logits.append(y[..., :A].contiguous())
                 deltas.append(y[..., A:A + D].contiguous())
             return shares, logits, deltas
+        # the fused 1x1's weight / bias gradient accumulates over the levels in
+        # one buffer (each level's skinny wgrad adds into it; the last level
+        # returns the sum): autograd's per-level adds and slices go away
+        wacc = ({"n": len(features), "k": 0}
+                if fuse and torch.is_grad_enabled() and _RPNHead1x1Fn.ACC_LEVELS else None)
         for x in features:
             # a level the ROI poolers also read hands its input gradient over
             # (GeneralizedRCNN tags them; the pair_grad protocol)
@@ -92,7 +97,7 @@ class StandardRPNHead(Layer):
                 lg, dl = _RPNHead1x1Fn.apply(share, self.objectness_logits.weights,
                                              self.objectness_logits.bias,
                                              self.anchor_deltas.weights, self.anchor_deltas.bias,
-                                             w16, wp, b16)
+                                             w16, wp, b16, wacc)
                 logits.append(lg)
                 deltas.append(dl)
             else:
@@ -111,15 +116,21 @@ class _RPNHead1x1Fn(torch.autograd.Function):
     is a fused-ReLU conv output, which then skips its threshold_backward (the
     sole-consumer protocol of layers/convolutional.py:_ConvMFMAFn)."""
     GATE = True  # False: leave the ReLU backward to the 3x3 conv (tests)
+    # True: the levels of one forward share a weight-gradient accumulator
+    # (wacc: {"n": levels, "k": done}); every level but the last returns no
+    # weight gradient, the last one the in-order sum -- autograd's
+    # ((g1 + g2) + g3) ... of the per-level gradients, without its adds
+    ACC_LEVELS = True
 
     @staticmethod
-    def forward(ctx, share, wo, bo, wd, bd, w16, wp, b16):
+    def forward(ctx, share, wo, bo, wd, bd, w16, wp, b16, wacc=None):
         y = ops.conv2d_nhwc(share, wp, b16)
         A, D = wo.shape[3], wd.shape[3]
         ctx.save_for_backward(share, w16)
         ctx.relu_info = getattr(share, "_d2mi_relu_info", None) if _RPNHead1x1Fn.GATE else None
         ctx.set_materialize_grads(False)  # a missing head gradient is zero-filled below
         ctx.dims = (A, D, y.shape[-1])
+        ctx.wacc = wacc
         return y[..., :A].contiguous(), y[..., A:A + D].contiguous()
 
     @staticmethod
@@ -142,9 +153,18 @@ class _RPNHead1x1Fn(torch.autograd.Function):
                 info["masked"] = True
             else:
                 gx = ops.conv2d_nhwc(g16, w16, None, 1, (0, 0))
-        gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)
+        acc = ctx.wacc
+        if acc is not None:
+            acc["k"] += 1
+            acc["buf"] = ops.wgrad_skinny(share, g16, with_bias=True,
+                                          accumulate_into=acc.get("buf"))
+            if acc["k"] < acc["n"]:
+                return gx, None, None, None, None, None, None, None, None
+            gw, gb = acc.pop("buf")
+        else:
+            gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)
         return (gx, gw[..., :A].contiguous(), gb[:A], gw[..., A:A + D].contiguous(), gb[A:A + D],
-                None, None, None)
+                None, None, None, None)
 
 
 @PROPOSAL_GENERATOR_REGISTRY.register()

@@ -524,6 +524,12 @@ int d2mi_paste_masks(const float* box_masks, const float* boxes, const float* yx
 size_t d2mi_wgrad_skinny_workspace_size(int P, int Cin, int Cout);
 int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
                       float* gb, void* workspace, size_t workspace_bytes, void* stream);
+/* d2mi_wgrad_skinny_ex: accumulate != 0 adds the result into gw / gb (old +
+ * new: autograd's accumulation of a weight shared by several calls -- the RPN
+ * head's fused 1x1 over the FPN levels, rpn.py:83-96). */
+int d2mi_wgrad_skinny_ex(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
+                         float* gb, int accumulate, void* workspace, size_t workspace_bytes,
+                         void* stream);
 /* Column sums of a row-major [rows, cols] f32 matrix (a conv's bias gradient,
  * TF BiasAddGrad, when its weight gradient runs as a library GEMM): out[cols],
  * fixed-order two-level reduction; workspace from
