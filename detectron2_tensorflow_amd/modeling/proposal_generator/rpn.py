@@ -161,6 +161,7 @@ class _RPNHead1x1Fn(torch.autograd.Function):
             if acc["k"] < acc["n"]:
                 return gx, None, None, None, None, None, None, None, None
             gw, gb = acc.pop("buf")
+            acc["k"] = 0  # (a second backward of the same graph starts over)
         else:
             gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)
         return (gx, gw[..., :A].contiguous(), gb[:A], gw[..., A:A + D].contiguous(), gb[A:A + D],
