@@ -71,7 +71,8 @@ def parse():
     p.add_argument("--width", type=int, default=1333)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
     p.add_argument("--cpu-images", type=int, default=2, help="images per CPU iteration (<= batch)")
-    p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations")
+    p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations (median)")
+    p.add_argument("--cpu-one-core", type=int, default=1, help="also time 1 image on 1 core")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--timed-step-sample", type=int, default=-1,
                    help="timed step whose kernel launches carry HIP events (-1: the last)")
@@ -79,6 +80,11 @@ def parse():
     p.add_argument("--mask-format", default="conventional", choices=["conventional", "raw", "fixed"],
                    help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
+    p.add_argument("--mask-fixed-rows", action="store_true",
+                   help="train: the mask head on the fixed BATCH_SIZE_PER_IMAGE x "
+                        "POSITIVE_FRACTION rows per image (128 at the defaults, "
+                        "defaults.py:413-415; the steady-state load of a trained model) "
+                        "instead of the step's foreground rows")
     return p.parse_args()
 
 
@@ -177,11 +183,21 @@ def pmc_traffic(group, mode):
         return None
 
 
-def kernel_report(summary, mode="infer"):
+def kernel_report(summary, mode="infer", extras=None):
     """Roofline objects from the live HIP-event timings of the timed region.
     Convs are reported per product form: "conv2d_split" (f32 operands split
     into 3 bf16 terms, 6 bf16 MFMA products; peak = BF16 dense / 6) and
-    "conv2d_mfma" (f32 MFMA products; peak = FP32 matrix)."""
+    "conv2d_mfma" (f32 MFMA products; peak = FP32 matrix).
+
+    HBM-bound kernels: ``achieved`` / ``frac`` use the launch's UNIQUE bytes
+    where a model exists (ROIAlign: the distinct feature rows the samples
+    read + the output written, forward; grad_out read + the dense gradient
+    maps written, backward) -- the least traffic that can serve the launch,
+    so frac <= 1 -- with the SURVEY 8d D4 figure (4 corner reads per sample,
+    which neighbouring bins share in cache) beside it as ``achieved_d4`` and
+    the rocprofv3 PMC bytes of the same kernel (``traffic``, training only)
+    as ``achieved_counter`` / ``frac_counter``."""
+    extras = extras or {}
     rep = {}
     convs = (("conv2d_split", MFMA_SPLIT_PEAK_TFLOPS, "conv2d_split"),
              ("conv2d_mfma", MFMA_F32_PEAK_TFLOPS, "conv2d_mfma"),
@@ -202,20 +218,118 @@ def kernel_report(summary, mode="infer"):
         if name not in summary:
             continue
         n, ms, byts = summary[name]
-        ach = byts / (ms * 1e-3) / 1e9
-        rep[name] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(name, mode), "launches": n, "avg_us": round(ms * 1e3 / n, 2),
-                     "algorithmic_per_launch": byts / n}
+        sec = ms * 1e-3
+        uniq = extras.get(name, {}).get("unique_bytes")
+        model = uniq if uniq is not None else byts
+        ach = model / sec / 1e9
+        traffic = pmc_traffic(name, mode)
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+             "bytes_model": "unique" if uniq is not None else "algorithmic",
+             "traffic": traffic, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+             "algorithmic_per_launch": model / n}
+        if uniq is not None:
+            r["achieved_d4"] = round(byts / sec / 1e9, 1)
+            r["d4_per_launch"] = byts / n
+        if traffic:
+            ac = traffic * n / sec / 1e9
+            r["achieved_counter"] = round(ac, 1)
+            r["frac_counter"] = round(ac / HBM_PEAK_GBPS, 4)
+        rep[name] = r
     return rep
 
 
+def cpu_model_name():
+    """The host CPU's model name (lscpu's "Model name", from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _median_time(fn, iters, warm=0):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts
+
+
+def cpu_per_op_c2(batch, cores, reps=20):
+    """the hot-path ops of the CPU
+    restatement on one 1333x800 image (seeded synthetic inputs of the
+    bench geometry), each 3 warm-ups + the median of ``reps`` runs, in ms:
+    ROIAlign 7x7 over p2..p5 with 1,000 ROIs (SURVEY D2 boxes), the RPN
+    proposals (anchors + decode + per-level top-k 1000 + NMS over 5 levels,
+    post 1000), class-offset Fast R-CNN NMS (1,000 ROIs x 80 classes), and
+    anchor generation + delta decode of all 268,569 anchors."""
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(0)
+    H, W, TH, TW = 800, 1344, 800, 1333
+    strides = [4, 8, 16, 32]
+    feats = [rng.normal(size=(1, H // s, W // s, 256)).astype(np.float32) for s in strides]
+    c = rng.uniform([0, 0], [TH, TW], size=(1000, 2))
+    sz = np.exp(rng.uniform(np.log(16), np.log(800), size=1000))
+    ar = np.exp(rng.uniform(np.log(0.5), np.log(2.0), size=1000))
+    h, w = sz * np.sqrt(ar), sz / np.sqrt(ar)
+    boxes = np.stack([c[:, 0] - h / 2, c[:, 1] - w / 2, c[:, 0] + h / 2, c[:, 1] + w / 2],
+                     1).astype(np.float32)
+    bimg = np.zeros(1000, np.int32)
+    out = {}
+    t, _ = _median_time(lambda: oracle.roi_pooler(feats, boxes, bimg, (7, 7),
+                                                  [1.0 / s for s in strides], 0, True), reps, 3)
+    out["roi_align_7x7_1000rois_ms"] = round(t * 1e3, 3)
+    rs = [4, 8, 16, 32, 64]
+    hw = [(-(-H // s), -(-W // s)) for s in rs]
+    cells = [oracle.generate_cell_anchors([z], [0.5, 1.0, 2.0]) for z in [32, 64, 128, 256, 512]]
+    logits = [rng.normal(size=(1, a * b * 3)).astype(np.float32) for a, b in hw]
+    deltas = [rng.normal(0, 0.1, size=(a * b * 3, 4)).astype(np.float32) for a, b in hw]
+    ihw = np.array([[TH, TW]], np.int32)
+
+    def anchors_decode():
+        return [oracle.apply_deltas(d, oracle.grid_anchors(a, b, s, cl), (1, 1, 1, 1))
+                for (a, b), s, cl, d in zip(hw, rs, cells, deltas)]
+
+    t, _ = _median_time(anchors_decode, reps, 3)
+    out["anchors_decode_268569_ms"] = round(t * 1e3, 3)
+    props = [p[None] for p in anchors_decode()]
+    t, _ = _median_time(lambda: oracle.find_top_rpn_proposals(props, logits, ihw, 0.7, 1000, 1000,
+                                                              0.0), reps, 3)
+    out["rpn_proposals_5lvl_pre1000_ms"] = round(t * 1e3, 3)
+    K, P = 80, 1000
+    lg = rng.normal(0, 3, size=(P, K + 1)).astype(np.float32)
+    probs = oracle.softmax(lg)
+    bx = oracle.apply_deltas(rng.normal(0, 0.5, size=(P, K * 4)).astype(np.float32),
+                             oracle.clip_to_window(boxes, [0, 0, TH, TW]), (10, 10, 5, 5))
+    t, _ = _median_time(lambda: oracle.fast_rcnn_inference(bx, probs, np.zeros(P, np.int64),
+                                                           np.arange(P), P, ihw, 0.05, 0.5, 100),
+                        reps, 3)
+    out["fast_rcnn_class_offset_nms_1000x80_ms"] = round(t * 1e3, 3)
+    out["protocol"] = f"3 warm-ups + median of {reps}, {cores} threads, 1 image 1333x800"
+    return out
+
+
 def cpu_baseline(args, model, batch, cfg=None):
-    """The oracle's CPU restatement timed on this host (rank 0, N=1): for
-    --mode train --cpu-iters training iterations (oracle/cpu_train.py: forward
-    with autograd, losses, backward, update) of min(--cpu-images, --batch)
-    images of the same size (default 3 x 2) — the bounded sample; for --mode
-    infer the inference forward of the model (cpu_pipeline.py)."""
+    """The oracle's CPU restatement timed on this host (rank 0, N=1), per
+    BASELINE.md section 2: the bench workload on every core the job may use
+    (``cores``: the median of --cpu-iters iterations of min(--cpu-images,
+    --batch) images after a small warm-up), the same on ONE core
+    (threadpoolctl + torch.set_num_threads(1): 1 iteration of 1 image, the
+    bounded sample), the host CPU model, and for the (Mask / Faster) R-CNN
+    inference workload the C2 per-op timings (cpu_per_op_c2).  --mode train:
+    oracle/cpu_train.py training iterations (forward with autograd, losses,
+    backward, update); --mode infer: the inference forward (cpu_pipeline.py)."""
+    from threadpoolctl import threadpool_limits
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cpu_pipeline import CPUReference, cpu_cores
     cores = cpu_cores()
@@ -223,35 +337,28 @@ def cpu_baseline(args, model, batch, cfg=None):
     iters = max(1, args.cpu_iters)
     imgs = batch["image"][:n].cpu().numpy()
     shapes = batch["image_shape"][:n].cpu().numpy()
+    extra = {}
     if args.mode == "train":
         import cpu_train
         step = cpu_train.CPUTrainStep(model, cfg)
         inst = {k: v[:n].cpu() for k, v in batch["instances"].items()}
         small = {k: v[:1] for k, v in inst.items()}
         step.step(imgs[:1, :256, :320], [[256, 320]], small, threads=cores)  # warm the libraries
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            step.step(imgs, shapes, inst, threads=cores)
-        dt = time.perf_counter() - t0
+        run = lambda k, th: step.step(imgs[:k], shapes[:k], {a: v[:k] for a, v in inst.items()},
+                                      threads=th)
         what = "training iteration(s) (forward + losses + backward + Momentum-SGD update)"
     elif is_solo(model):
         from cpu_pipeline import CPUSOLOv2
         ref = CPUSOLOv2(model.eval())
         ref(imgs[:1, :256, :320], threads=cores)  # warm the libraries
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            ref(imgs, threads=cores)
-        dt = time.perf_counter() - t0
+        run = lambda k, th: ref(imgs[:k], threads=th)
         what = ("inference forward(s) (backbone + FPN + SOLOv2 kernel / feature branches + "
                 "dynamic conv, Matrix NMS, masks to the image)")
     elif is_single_stage(model):
         from cpu_pipeline import CPURetinaNet
         ref = CPURetinaNet(model.eval())
         ref(imgs[:1, :256, :320], threads=cores)  # warm the libraries
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            ref(imgs, threads=cores)
-        dt = time.perf_counter() - t0
+        run = lambda k, th: ref(imgs[:k], threads=th)
         what = "inference forward(s) (backbone + FPN P6P7 + box tower + dense top-k/decode/NMS)"
     else:
         ref = CPUReference(model.eval())
@@ -262,15 +369,26 @@ def cpu_baseline(args, model, batch, cfg=None):
         if args.mask_format == "conventional":
             d = model.neck.size_divisibility or 1
             canvas = tuple(-(-int(v) // d) * d for v in imgs.shape[1:3])
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            ref(imgs, shapes, threads=cores, paste_to=canvas)
-        dt = time.perf_counter() - t0
+        run = lambda k, th: ref(imgs[:k], shapes[:k], threads=th, paste_to=canvas)
         what = "inference forward(s)" + (" + mask pasting" if canvas else "")
-    return {"value": round(n * iters / dt, 4), "unit": "img/s", "cores": cores, "kind": "port",
-            "sample": f"{iters} x {n} image(s) {args.height}x{args.width}, {args.model} {what}, "
-                      f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU "
-                      f"convs/autograd), {dt:.1f} s on {cores} threads"}
+        with threadpool_limits(cores):
+            extra["per_op_c2"] = cpu_per_op_c2(batch, cores)
+    with threadpool_limits(cores):
+        med, ts = _median_time(lambda: run(n, cores), iters)
+    out = {"value": round(n / med, 4), "unit": "img/s", "cores": cores, "kind": "port",
+           "cpu_model": cpu_model_name(),
+           "sample": f"median of {iters} x {n} image(s) {args.height}x{args.width} "
+                     f"({', '.join(f'{t:.2f}' for t in ts)} s), {args.model} {what}, "
+                     f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU "
+                     f"convs/autograd), {cores} threads"}
+    if args.cpu_one_core:
+        with threadpool_limits(1):
+            t1, _ = _median_time(lambda: run(1, 1), 1)
+        torch.set_num_threads(cores)
+        out["value_1core"] = round(1.0 / t1, 4)
+        out["sample_1core"] = f"1 x 1 image, 1 thread (threadpoolctl + torch), {t1:.1f} s"
+    out.update(extra)
+    return out
 
 
 def main():
@@ -305,6 +423,8 @@ def main():
     calibrate_scores(model, batch)
     if args.mode == "train":
         from detectron2_tensorflow_amd.engine import Trainer
+        if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
+            model.roi_heads.mask_compact_rows = False
         trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
         grad_ctx = torch.enable_grad
@@ -338,6 +458,7 @@ def main():
         torch.cuda.nvtx.range_pop()
         KernelTimer.enabled = False
     summary = KernelTimer.summary()
+    extras = KernelTimer.extras()
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -363,7 +484,7 @@ def main():
         extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 
     if rank == 0:
-        kernels = kernel_report(summary, args.mode)
+        kernels = kernel_report(summary, args.mode, extras)
         result = {
             "metric": METRICS[args.model],
             "value": round(world * args.batch * args.steps / elapsed, 3),
@@ -383,6 +504,8 @@ def main():
                             "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                             "parallelism": (f"dp{world}" if args.mode == "train" else f"replicas{world}"),
                             "mode": args.mode,
+                            **({"mask_rows": "fixed" if args.mask_fixed_rows else "foreground"}
+                               if args.mode == "train" else {}),
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
                             else f"{sample + 1}/{args.steps}",
                             **({"mask_format": args.mask_format} if args.mode == "infer" else {})},

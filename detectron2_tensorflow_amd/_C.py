@@ -25,6 +25,7 @@ P = c_void_p  # device or host pointer
 # name -> (restype, argtypes)
 _SIGS = {
     "d2mi_version": (c_int, []),
+    "d2mi_source_hash": (c_char_p, []),
     "d2mi_last_error": (c_char_p, []),
     "d2mi_error_word_dev": (c_void_p, []),
     "d2mi_clear_errors": (c_int, [P]),
@@ -154,6 +155,15 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)  # AttributeError if the export is missing
         fn.restype = res
         fn.argtypes = args
+    # the library must be built from the sources next to it (a stale prebuilt
+    # .so would silently run other kernels than the tree's)
+    from . import _build
+    if os.path.isdir(_build.CSRC) and os.environ.get("D2MI_LIB") is None:
+        want, got = _build.source_hash(), lib.d2mi_source_hash().decode()
+        if got != want:
+            _load_error = (f"{path} was built from other sources (hash {got}, tree {want}); "
+                           "rebuild with detectron2_tensorflow_amd._build.build()")
+            raise D2MIError(_load_error)
     _lib = lib
     return lib
 

@@ -30,6 +30,14 @@ extern "C" {
 
 int d2mi_version(void) { return 1; }
 
+// Hash of the sources this library was built from (csrc/*.hip, csrc/*.h,
+// include/d2mi.h; _build.source_hash), passed in by the build: _C.load
+// refuses a library whose hash differs from the tree it is loaded from.
+#ifndef D2MI_SOURCE_HASH
+#define D2MI_SOURCE_HASH "unknown"
+#endif
+const char* d2mi_source_hash(void) { return D2MI_SOURCE_HASH; }
+
 const char* d2mi_last_error(void) { return g_msg; }
 
 int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }

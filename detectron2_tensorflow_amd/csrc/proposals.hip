@@ -269,12 +269,13 @@ __global__ void frcnn_gather_kernel(const uint64_t* __restrict__ sorted,
                                     const int32_t* __restrict__ flat2pos,
                                     const float4* __restrict__ cbox,
                                     const uint32_t* __restrict__ maxc, int cap, int P, int K,
-                                    float4* __restrict__ sboxes, int32_t* __restrict__ sidx,
-                                    int32_t* __restrict__ count) {
+                                    int agnostic_nms, float4* __restrict__ sboxes,
+                                    int32_t* __restrict__ sidx, int32_t* __restrict__ count) {
   const int n = blockIdx.y;
   const int len = lens[n];
   if (blockIdx.x == 0 && threadIdx.x == 0) count[n] = len;
-  const float off1 = from_orderable(maxc[n]) + 1.f;
+  // nms_cls_agnostic (fast_rcnn.py:138-139): the filtered boxes as they are
+  const float off1 = agnostic_nms ? 0.f : from_orderable(maxc[n]) + 1.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
     const size_t o = (size_t)n * cap + i;
     const uint32_t flat = (uint32_t)(sorted[o] & 0xffffffffu);
@@ -282,7 +283,7 @@ __global__ void frcnn_gather_kernel(const uint64_t* __restrict__ sorted,
     const int pos = flat2pos[(size_t)n * P * K + flat];
     const float4 b = cbox[(size_t)n * cap + pos];
     const float off = (float)c * off1;  // tf.cast(cls, f32) * (max_coord + 1)
-    sboxes[o] = make_float4(b.x + off, b.y + off, b.z + off, b.w + off);
+    sboxes[o] = agnostic_nms ? b : make_float4(b.x + off, b.y + off, b.z + off, b.w + off);
     sidx[o] = pos;
   }
 }
@@ -661,6 +662,10 @@ extern "C" int d2mi_fast_rcnn_inference(const float* logits, const float* deltas
                "bad fast_rcnn_inference sizes");
   D2MI_REQUIRE(((uintptr_t)deltas & 15) == 0 && ((uintptr_t)proposals & 15) == 0,
                "deltas/proposals must be 16B aligned");
+  // cls_agnostic: bit 0 = one class-agnostic box per ROI (deltas [R, 4]),
+  // bit 1 = class-agnostic NMS (NMS_CLS_AGNOSTIC: no class offsets)
+  D2MI_REQUIRE((cls_agnostic & ~3) == 0, "bad cls_agnostic flags %d", cls_agnostic);
+  const int agnostic_box = cls_agnostic & 1, agnostic_nms = (cls_agnostic >> 1) & 1;
   const int cap = frcnn_cap(P, K, score_thresh);
   Workspace w(workspace, workspace_bytes);
   FrcnnWs o;
@@ -679,7 +684,7 @@ extern "C" int d2mi_fast_rcnn_inference(const float* logits, const float* deltas
     hipLaunchKernelGGL(frcnn_score_kernel, dim3((R + 3) / 4), dim3(256), 0, st, logits,
                        reinterpret_cast<const float4*>(deltas),
                        reinterpret_cast<const float4*>(proposals), roi_img, roi_slot, R, N, P, K,
-                       cls_agnostic, image_hw, make_dc(weights4_host, scale_clamp), score_thresh,
+                       agnostic_box, image_hw, make_dc(weights4_host, scale_clamp), score_thresh,
                        cap, o.maxc, o.cnt, o.keys, o.cbox, o.cscore, err);
     D2MI_LAUNCH_CHECK();
   }
@@ -691,7 +696,8 @@ extern "C" int d2mi_fast_rcnn_inference(const float* logits, const float* deltas
   int rc = sort_keys_segmented(o.keys, o.sorted, o.cnt, N, cap, o.sort_ws, o.sort_bytes, st);
   if (rc) return rc;
   hipLaunchKernelGGL(frcnn_gather_kernel, dim3(grid1(cap, 256, 64), N), dim3(256), 0, st, o.sorted,
-                     o.cnt, o.flat2pos, o.cbox, o.maxc, cap, P, K, o.sboxes, o.sidx, o.count);
+                     o.cnt, o.flat2pos, o.cbox, o.maxc, cap, P, K, agnostic_nms, o.sboxes, o.sidx,
+                     o.count);
   D2MI_LAUNCH_CHECK();
   rc = nms_sorted(o.sboxes, o.sidx, o.count, N, cap, max_det, nms_thresh, o.keep, o.num_keep,
                   o.nms_ws, o.nms_bytes, st);

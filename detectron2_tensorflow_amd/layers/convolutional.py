@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ..utils.arg_scope import add_arg_scope
+from . import handoff
 from . import initializers as init
 from . import ops
 from .activation import get_activation, is_relu
@@ -187,7 +188,7 @@ class _ConvMFMAFn(torch.autograd.Function):
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
         gres = gy if has_res and ctx.needs_input_grad[8] else None
         if gres is not None and ctx.res_grad_to is not None:
-            ctx.res_grad_to["g"] = gres  # taken by the conv reading the same tensor
+            handoff.deposit(ctx.res_grad_to, "g", gres, "residual")  # taken by the conv reading it
             gres = None
         gx = gw = gb = None
         if ctx.needs_input_grad[0] and _join_active(ctx):
@@ -211,7 +212,7 @@ class _ConvMFMAFn(torch.autograd.Function):
             else:
                 gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add)
             if deposit:
-                pair["g"] = gx
+                handoff.deposit(pair, "g", gx, "pair")
                 gx = None
         want_b = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
@@ -247,7 +248,7 @@ def _join_backward(ctx, gy, x, w, stride, pb, pe):
         p = ctx.join
         s = p.pop("sum", None)
         if s is None:
-            p["lat"] = _dgrad(gy, w, x.shape, stride, pb, pe)
+            handoff.deposit(p, "lat", _dgrad(gy, w, x.shape, stride, pb, pe), "join (lateral)")
             return None
         p["last"] = "lateral"  # (tests: which member completed the join)
         if info is not None and _gate_eligible(w.shape, stride, pb, pe):
@@ -258,11 +259,11 @@ def _join_backward(ctx, gy, x, w, stride, pb, pe):
     p = ctx.pair_grad
     other = p.pop("g", None)
     if other is None:  # first of the pair
-        p["g"] = _dgrad(gy, w, x.shape, stride, pb, pe)
+        handoff.deposit(p, "g", _dgrad(gy, w, x.shape, stride, pb, pe), "join (pair)")
         return None
     lat = p.pop("lat", None)
     if lat is None:
-        p["sum"] = _dgrad(gy, w, x.shape, stride, pb, pe, add=other)
+        handoff.deposit(p, "sum", _dgrad(gy, w, x.shape, stride, pb, pe, add=other), "join (sum)")
         return None
     p["last"] = "pair"
     gate = x if info is not None else None
@@ -342,12 +343,12 @@ class PackGroup:
     def fetch(self, layer):
         if not any(m is layer for m in self.members):
             self.members.append(layer)
-        key = layer._param_key()
+        key = layer._pack_key(layer.weights)
         if layer._packed is not None and layer._packed_key == key:
             return layer._packed
         stale, keys = [], []
         for m in self.members:
-            k = key if m is layer else m._param_key()
+            k = key if m is layer else m._pack_key(m.weights)
             if m._packed is None or m._packed_key != k:
                 stale.append(m)
                 keys.append(k)
@@ -421,6 +422,9 @@ class Conv2D(Layer):
                     if t is not None]
         return tuple(key)
 
+    def _pack_key(self, w):
+        return self._param_key() + (tuple(w.shape),)
+
     def effective_params(self, want_packed=False):
         """(weights HWIO, bias, normalizer still to apply, packed-or-None) with a
         frozen BatchNorm folded in by one fused HIP kernel (d2mi_fold_frozen_bn,
@@ -464,9 +468,12 @@ class Conv2D(Layer):
         if (group is not None and PackGroup.ENABLED
                 and (w_eff is None or w_eff is self.weights)):
             return group.fetch(self)
-        key = self._param_key()
+        w = self.weights if w_eff is None else w_eff
+        # the packed tensor's own shape is part of the key: a Cin-padded w_eff
+        # (Cin % 4 != 0) packs to [.., Cout, Cin + pad], never to be returned
+        # for the layer's own weights (or the other way round)
+        key = self._pack_key(w)
         if self._packed is None or self._packed_key != key:
-            w = self.weights if w_eff is None else w_eff
             self._packed = ops.pack_conv_weights(w.detach())
             self._packed_key = key
         return self._packed

@@ -48,9 +48,14 @@ class GroupNorm(Layer):
         self.beta = torch.nn.Parameter(torch.zeros(channels), requires_grad=trainable)
 
     def fused_ok(self, x):
-        """The HIP GroupNorm (d2mi_group_norm_nhwc) takes inference on the GPU."""
+        """The HIP GroupNorm (d2mi_group_norm_nhwc, no autograd) takes the call
+        only when no gradient is needed at all: neither the input nor the
+        affine parameters require one (a frozen GN in a trainable branch must
+        still pass the input gradient through torch's group_norm)."""
         C = self.channels
-        return (x.is_cuda and not (torch.is_grad_enabled() and self.gamma.requires_grad)
+        needs_grad = torch.is_grad_enabled() and (
+            x.requires_grad or self.gamma.requires_grad or self.beta.requires_grad)
+        return (x.is_cuda and not needs_grad
                 and C % self.num_groups == 0 and (C // self.num_groups) % 4 == 0 and C <= 1024
                 and self.num_groups <= 64)
 

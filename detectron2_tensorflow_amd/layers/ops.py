@@ -13,6 +13,7 @@ import torch
 
 from .. import _C
 from ..utils import host_sync
+from . import handoff
 
 _DEFAULT_SCALE_CLAMP = math.log(1000.0 / 16)  # lib/modeling/box_regression.py:10
 
@@ -43,22 +44,102 @@ class KernelTimer:
         return ev
 
     @classmethod
-    def stop(cls, ev0, name, work):
+    def stop(cls, ev0, name, work, extra=None):
+        """extra: None or a zero-argument callable returning {key: amount} of
+        further work models for this launch (evaluated after the timed region,
+        by extras())."""
         if ev0 is None:
             return
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record(torch.cuda.current_stream())
-        cls.records.append((name, ev0, ev1, float(work)))
+        cls.records.append((name, ev0, ev1, float(work), extra))
 
     @classmethod
     def summary(cls):
         """{name: (launches, total_ms, total_work)} (synchronises)."""
         torch.cuda.synchronize()
         out = {}
-        for name, e0, e1, w in cls.records:
+        for name, e0, e1, w, _ in cls.records:
             n, t, tw = out.get(name, (0, 0.0, 0.0))
             out[name] = (n + 1, t + e0.elapsed_time(e1), tw + w)
         return out
+
+    @classmethod
+    def extras(cls):
+        """{name: {key: total}} of the launches' extra work models."""
+        out = {}
+        for name, _, _, _, ex in cls.records:
+            if ex is None:
+                continue
+            d = out.setdefault(name, {})
+            for k, v in ex().items():
+                d[k] = d.get(k, 0.0) + float(v)
+        return out
+
+
+def roi_touched_rows(boxes, box_ind, params, shapes):
+    """Distinct feature rows (level, image, y, x) that one ROIAlign forward
+    reads (the 4 bilinear corners of every in-range sample): the unique-bytes
+    model of bench.py's roofline (rows x C x 4 bytes is the least HBM
+    traffic that can deliver the launch's inputs, however many samples share
+    a row).  A float32 torch restatement of roi_geom / make_tap in
+    csrc/roi_align.hip, for the byte count only (a log-boundary box may land
+    on the other level here: immaterial for a traffic model)."""
+    (oh, ow, scales, sr, mode, pad, assign, min_l, max_l, canon_s, canon_l, _) = params
+    dev = boxes.device
+    b = boxes.detach().float().reshape(-1, 4)
+    R = b.shape[0]
+    if R == 0:
+        return 0
+    if assign and len(shapes) > 1:
+        area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+        v = canon_l + torch.log(torch.sqrt(area) / canon_s + 2.220446049250313e-16) / math.log(2)
+        lv = torch.nan_to_num(torch.floor(v), nan=min_l).clamp(min_l, max_l).long() - min_l
+    else:
+        lv = torch.zeros(R, dtype=torch.long, device=dev)
+    Hs = torch.tensor([s[1] for s in shapes], device=dev)[lv]
+    Ws = torch.tensor([s[2] for s in shapes], device=dev)[lv]
+    sc = torch.tensor(list(scales), dtype=torch.float32, device=dev)[lv]
+    S = max(sr, 1)
+    ch, cw = oh * S, ow * S
+    y1, x1, y2, x2 = b.unbind(1)
+    if mode != BOX_MODE_RAW:
+        y1, x1, y2, x2 = y1 * sc, x1 * sc, y2 * sc, x2 * sc
+    Hp, Wp = (Hs + 2, Ws + 2) if pad else (Hs, Ws)
+    if pad:
+        y1, x1, y2, x2 = y1 + 1, x1 + 1, y2 + 1, x2 + 1
+    i0, i1 = (Hp - 1).float(), (Wp - 1).float()
+    if mode == BOX_MODE_ALIGNED:
+        sh, sw = (y2 - y1) / ch, (x2 - x1) / cw
+        ny, nx = (y1 + sh / 2 - 0.5) / i0, (x1 + sw / 2 - 0.5) / i1
+        y1, x1, y2, x2 = ny, nx, ny + sh * (ch - 1) / i0, nx + sw * (cw - 1) / i1
+    elif mode == BOX_MODE_UNALIGNED:
+        y1, y2, x1, x2 = y1 / Hp.float(), y2 / Hp.float(), x1 / Wp.float(), x2 / Wp.float()
+
+    def taps(c1, c2, img_p, img, crop):
+        i = torch.arange(crop, device=dev, dtype=torch.float32)
+        if crop > 1:
+            pos = c1[:, None] * (img_p - 1).float()[:, None] + i * (
+                (c2 - c1) * (img_p - 1).float() / (crop - 1))[:, None]
+        else:
+            pos = (0.5 * (c1 + c2) * (img_p - 1).float())[:, None]
+        ok = (pos >= 0) & (pos <= (img_p - 1).float()[:, None])
+        lo, hi = torch.floor(pos).long(), torch.ceil(pos).long()
+        d = 1 if pad else 0
+        top = img[:, None] - 1
+        return ok, (lo - d).clamp(min=0).minimum(top), (hi - d).clamp(min=0).minimum(top)
+
+    oky, ylo, yhi = taps(y1, y2, Hp, Hs, ch)
+    okx, xlo, xhi = taps(x1, x2, Wp, Ws, cw)
+    n = box_ind.detach().long().reshape(-1)
+    base = torch.tensor([0] + [s[0] * s[1] * s[2] for s in shapes], device=dev).cumsum(0)
+    img0 = (base[lv] + n * Hs * Ws)[:, None, None]
+    ok = (oky[:, :, None] & okx[:, None, :]).reshape(-1)
+    ids = []
+    for yy in (ylo, yhi):
+        for xx in (xlo, xhi):
+            ids.append((img0 + yy[:, :, None] * Ws[:, None, None] + xx[:, None, :]).reshape(-1)[ok])
+    return int(torch.unique(torch.cat(ids)).numel())
 
 
 def _f32c(t):
@@ -116,7 +197,10 @@ class _RoIAlignFn(torch.autograd.Function):
         # dozen ROIs per step: latency-bound)
         name = ("crop_and_resize_fwd_narrow" if C < 64 else
                 "roi_align_fwd" if out_h * out_w <= 49 else "roi_align_fwd_mask")
-        KernelTimer.stop(ev, name, R * out_h * out_w * C * (16 * S + 4))
+        shapes = [tuple(f.shape) for f in feats]
+        KernelTimer.stop(ev, name, R * out_h * out_w * C * (16 * S + 4),
+                         extra=lambda: {"unique_bytes": C * 4 * (
+                             roi_touched_rows(boxes, box_ind, params, shapes) + R * out_h * out_w)})
         _C.check(rc, "d2mi_roi_align_fwd")
         ctx.params = params
         ctx.share = grad_share
@@ -146,7 +230,7 @@ class _RoIAlignFn(torch.autograd.Function):
             first = share.pop("set0", None)
             g = _f32c(grad_out)
             if first is None:
-                share["set0"] = (boxes, box_ind, g, ctx.params)
+                handoff.deposit(share, "set0", (boxes, box_ind, g, ctx.params), "box/mask poolers")
                 return (None,) * (4 + len(ctx.shapes))
             # levels whose other consumer already left its input gradient:
             # accumulate into it; the others: written here and left for it
@@ -155,7 +239,8 @@ class _RoIAlignFn(torch.autograd.Function):
             out = []
             for pr, gv, gr in zip(ctx.pairs, given, grads):
                 if pr is not None and gv is None:
-                    pr["g"] = gr  # the other consumer adds it in its dgrad epilogue
+                    # the other consumer adds it in its dgrad epilogue
+                    handoff.deposit(pr, "g", gr, "RPN head / ROI pooler level")
                     out.append(None)
                 else:
                     out.append(gr)
@@ -182,11 +267,13 @@ class _RoIAlignFn(torch.autograd.Function):
         # algorithmic bytes: R*oh*ow*C*(4 + 32*S) = the grad_out read
         # + 4 corner read-modify-writes per sample of the reference's scatter
         S = max(sr, 1) ** 2
+        maps = sum(int(np.prod(s)) for s in ctx.shapes) * 4
         KernelTimer.stop(ev, "roi_align_bwd" if C >= 64 else "crop_and_resize_bwd_narrow",
-                         R * out_h * out_w * C * (4 + 32 * S))
+                         R * out_h * out_w * C * (4 + 32 * S),
+                         extra=lambda: {"unique_bytes": R * out_h * out_w * C * 4 + maps})
         _C.check(rc, "d2mi_roi_align_bwd")
         if share is not None and prior is None:  # first of a pair: hand the maps over
-            share["maps"] = grads
+            handoff.deposit(share, "maps", grads, "box/mask poolers")
             return (None,) * (4 + len(grads))
         return (None, None, None, None, *grads)
 
@@ -234,8 +321,12 @@ def _roi_align_bwd2(set0, set1, shapes, given=None):
                                  _C.ptr(g0), _C.ptr(b1), _C.ptr(i1), R1, oh1, ow1, sr1, _C.ptr(g1),
                                  acc_mask, _C.ptr(ws), wsb, _C.stream_of(dev))
     S0, S1 = max(sr0, 1) ** 2, max(sr1, 1) ** 2
+    # unique-bytes model: both grad_out sets read once + every element of the
+    # dense gradient maps written once
+    maps = sum(int(np.prod(s)) for s in shapes) * 4
     KernelTimer.stop(ev, "roi_align_bwd", R0 * oh0 * ow0 * C * (4 + 32 * S0) +
-                     R1 * oh1 * ow1 * C * (4 + 32 * S1))
+                     R1 * oh1 * ow1 * C * (4 + 32 * S1),
+                     extra=lambda: {"unique_bytes": (R0 * oh0 * ow0 + R1 * oh1 * ow1) * C * 4 + maps})
     _C.check(rc, "d2mi_roi_align_bwd2")
     return grads
 
@@ -1289,9 +1380,11 @@ def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk,
 
 def fast_rcnn_inference(logits, deltas, proposals, roi_img, roi_slot, num_images, P, image_hw,
                         weights, score_thresh, nms_thresh, topk_per_image,
-                        cls_agnostic=False, scale_clamp=_DEFAULT_SCALE_CLAMP):
+                        cls_agnostic=False, scale_clamp=_DEFAULT_SCALE_CLAMP, nms_cls_agnostic=False):
     """FastRCNNOutputs.inference + fast_rcnn_inference (fast_rcnn.py:28-187,
-    :359-395): softmax, decode, clip, threshold, class-offset NMS, pad."""
+    :359-395): softmax, decode, clip, threshold, class-offset NMS (plain NMS
+    with nms_cls_agnostic, fast_rcnn.py:138-139), pad.  cls_agnostic: one
+    class-agnostic box per ROI (deltas [R, 4])."""
     logits, deltas, proposals = _f32c(logits), _f32c(deltas), _f32c(proposals)
     roi_img, roi_slot, image_hw = _i32c(roi_img), _i32c(roi_slot), _i32c(image_hw)
     _C.require_device(logits, deltas, proposals, roi_img, roi_slot, image_hw)
@@ -1309,7 +1402,7 @@ def fast_rcnn_inference(logits, deltas, proposals, roi_img, roi_slot, num_images
     ws = _C.workspace(wsb, dev)
     rc = _C.lib().d2mi_fast_rcnn_inference(
         _C.ptr(logits), _C.ptr(deltas), _C.ptr(proposals), _C.ptr(roi_img), _C.ptr(roi_slot), R,
-        N, int(P), K, int(bool(cls_agnostic)), _C.ptr(image_hw),
+        N, int(P), K, int(bool(cls_agnostic)) | (int(bool(nms_cls_agnostic)) << 1), _C.ptr(image_hw),
         _C.host_array(_C.c_float, [float(w) for w in weights]), float(scale_clamp),
         float(score_thresh), float(nms_thresh), int(topk_per_image), _C.ptr(ob), _C.ptr(os_),
         _C.ptr(oc), _C.ptr(ov), _C.ptr(oroi), _C.ptr(ws), wsb, _C.stream_of(dev))

@@ -126,8 +126,11 @@ def _smallest(keys, mask, k, limit):
         take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals > -2.0)
         return sel.scatter_(1, idx.long(), take)
     # beyond the HIP select's capacity (batch sizes above 8192 per image, e.g.
-    # every anchor sampled) or off the GPU: torch's top-k, same selection
+    # every anchor sampled) or off the GPU: a STABLE ascending sort, so tied
+    # keys go to the lowest index first — the HIP select's tie rule (topk's
+    # order among ties is unspecified)
     kk = torch.where(mask, keys, torch.full_like(keys, 2.0))
-    vals, idx = kk.topk(k, dim=1, largest=False, sorted=True)
+    vals, idx = torch.sort(kk, dim=1, stable=True)
+    vals, idx = vals[:, :k], idx[:, :k]
     take = (torch.arange(k, device=keys.device)[None, :] < limit) & (vals < 2.0)
     return sel.scatter_(1, idx, take)

@@ -10,7 +10,7 @@ import torch
 
 from ...layers import Conv2D, Layer
 from ...layers import initializers as init
-from ...layers import ops
+from ...layers import handoff, ops
 from ...layers.loss import smooth_l1_loss
 from ..matcher import Matcher, match_boxes, subsample_labels
 from ...structures import BoxList
@@ -156,6 +156,13 @@ class _RPNHead1x1Fn(torch.autograd.Function):
         acc = ctx.wacc
         if acc is not None:
             acc["k"] += 1
+            if acc["k"] == 1:
+                # every level's backward must run in this pass: otherwise the
+                # weight gradient (returned by the last level) never leaves
+                # and a stale buffer would poison a later backward
+                handoff.expect_complete(acc, lambda a: a["k"] == 0,
+                                        lambda a: (a.pop("buf", None), a.__setitem__("k", 0)),
+                                        "RPN head 1x1 weight-gradient levels")
             acc["buf"] = ops.wgrad_skinny(share, g16, with_bias=True,
                                           accumulate_into=acc.get("buf"))
             if acc["k"] < acc["n"]:

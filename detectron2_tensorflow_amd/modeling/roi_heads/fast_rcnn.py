@@ -38,16 +38,17 @@ def fast_rcnn_inference(pred_class_logits, pred_proposal_deltas, proposal_boxes,
                         num_images, num_slots, image_shapes, box2box_transform, score_thresh,
                         nms_thresh, topk_per_image, nms_cls_agnostic=False):
     """Returns (boxes [N,k,4], scores [N,k], classes int64 [N,k], is_valid [N,k],
-    kept ROI row [N,k] (-1 pad)); rows with roi_slot < 0 are ignored."""
-    if nms_cls_agnostic:
-        raise NotImplementedError("class-agnostic NMS is not on the hot path")
+    kept ROI row [N,k] (-1 pad)); rows with roi_slot < 0 are ignored.
+    nms_cls_agnostic: one plain NMS over every class's filtered boxes
+    (fast_rcnn.py:138-139) instead of the class-offset NMS."""
     K = pred_class_logits.shape[1] - 1
     agnostic = pred_proposal_deltas.shape[1] == 4 and K != 1
     return ops.fast_rcnn_inference(pred_class_logits, pred_proposal_deltas, proposal_boxes, roi_img,
                                    roi_slot, num_images, num_slots, image_shapes,
                                    box2box_transform.weights, score_thresh, nms_thresh,
                                    topk_per_image, cls_agnostic=agnostic,
-                                   scale_clamp=box2box_transform.scale_clamp)
+                                   scale_clamp=box2box_transform.scale_clamp,
+                                   nms_cls_agnostic=nms_cls_agnostic)
 
 
 def fast_rcnn_losses(pred_class_logits, pred_proposal_deltas, proposal_boxes, gt_classes,

@@ -225,6 +225,8 @@ class StandardROIHeads(ROIHeads):
             rows = key.sort().values[:R] % B
             boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))
             self.last_mask_rows = R
+        else:
+            self.last_mask_rows = int(boxes.shape[0])
         x = self.mask_pooler.pool(feats, boxes.contiguous(), img, grad_share=grad_share)
         _, logits = self.mask_head(x)
         return mask_rcnn_loss(logits, boxes, gt_boxes, cls, gm.reshape(N * G, *gm.shape[2:]), mind,

@@ -53,10 +53,13 @@ def calibrate_rcnn_scores(model, batch):
     """BASELINE.md score injection for a random-init (Mask / Faster) R-CNN:
     rescale the box-head class logits to ~ N(0, 3^2), the RPN objectness to
     ~ N(0, 1) and the RPN anchor deltas to N(0, 0.1^2) on this batch's
-    features.  The unnormalised features of a random-init ResNet otherwise
-    give class logits in the hundreds (a Fast R-CNN CE loss of ~750) and
-    deltas of O(10), which collapse most proposals onto the image border (a
-    random-init artefact, not a training distribution)."""
+    features; also the box-head deltas to ~ N(0, 0.5^2) and the mask logits
+    to ~ N(0, 1).  The unnormalised features of a random-init ResNet otherwise
+    give class logits in the hundreds (a Fast R-CNN CE loss of ~750), deltas
+    of O(10), which collapse most proposals onto the image border, and mask
+    logits of O(10) (a saturated BCE of ~13 whose size depends on the image
+    size) -- random-init artefacts, not a training distribution.  The
+    rescaling changes weights only, never the work a step does."""
     import math
     stats = {}
 
@@ -72,17 +75,24 @@ def calibrate_rcnn_scores(model, batch):
     # the shared conv's output on the last level (the head returns them all)
     h2 = rpn_head.register_forward_hook(lambda m, i, o: stats.__setitem__(
         "rpn", float((o[0][-1].reshape(-1, o[0][-1].shape[-1]) ** 2).sum(-1).mean())))
+    mask_pred = getattr(getattr(rh, "mask_head", None), "predictor", None)
+    h3 = mask_pred.register_forward_hook(grab("mask")) if mask_pred is not None else None
     was = model.training
     model.eval()
     model.inference({"image": batch["image"], "image_shape": batch["image_shape"]})
     model.train(was)
     h1.remove()
     h2.remove()
+    if h3 is not None:
+        h3.remove()
     cls = rh.box_predictor.cls_score
     cls.weights.normal_(0.0, 3.0 / math.sqrt(max(stats["box"], 1e-12)))
     obj = rpn_head.objectness_logits
     obj.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["rpn"], 1e-12)))
     rpn_head.anchor_deltas.weights.normal_(0.0, 0.1 / math.sqrt(max(stats["rpn"], 1e-12)))
+    rh.box_predictor.bbox_pred.weights.normal_(0.0, 0.5 / math.sqrt(max(stats["box"], 1e-12)))
+    if "mask" in stats:
+        mask_pred.weights.normal_(0.0, 1.0 / math.sqrt(max(stats["mask"], 1e-12)))
 
 
 @torch.no_grad()

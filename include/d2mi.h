@@ -39,6 +39,9 @@ extern "C" {
 
 /* ------------------------------------------------------------------ misc */
 int d2mi_version(void);
+/* sha256 prefix of the sources the library was built from (csrc/*.hip,
+ * csrc/*.h, this header): the loader checks it against its tree. */
+const char* d2mi_source_hash(void);
 const char* d2mi_last_error(void);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
@@ -195,7 +198,8 @@ int d2mi_rpn_proposals(const float* const* logits, const float* const* deltas,
  * true image shape, score > thresh in class-major order, class-offset NMS
  * (offset = cls * (max clipped coord of the image + 1)), top-k, pad.
  * logits [R, K+1] (background last), deltas [R, K*4] (or [R,4] when
- * cls_agnostic), proposals [R,4]; roi_img/roi_slot int32 [R] = (image, dense
+ * bit 0 of cls_agnostic is set), proposals [R,4]; bit 1 of cls_agnostic =
+ * NMS_CLS_AGNOSTIC (fast_rcnn.py:138-139: plain NMS, no class offsets); roi_img/roi_slot int32 [R] = (image, dense
  * slot) of each ROI (SparseBoxList.indices); P = dense slots per image.
  * Outputs [N, max_det] boxes/scores/classes(int64)/valid(uint8) and
  * out_roi int32 [N, max_det] (kept ROI row, -1 pad).

@@ -289,8 +289,9 @@ def find_top_rpn_proposals(proposals, logits, image_shapes, nms_thresh, pre_nms_
 
 
 def fast_rcnn_inference(boxes, probs, roi_img, roi_slot, P, image_shapes, score_thresh,
-                        nms_thresh, topk_per_image):
-    """fast_rcnn.py:28-187 (class-specific boxes).  boxes [R, K*4] decoded,
+                        nms_thresh, topk_per_image, nms_cls_agnostic=False):
+    """fast_rcnn.py:28-187 (class-specific boxes; nms_cls_agnostic: plain NMS
+    over the filtered boxes, fast_rcnn.py:138-139).  boxes [R, K*4] decoded,
     probs [R, K+1], (roi_img, roi_slot) the SparseBoxList indices, P dense
     slots per image.  Returns per image (boxes, scores, classes, valid, roi)."""
     boxes, probs = _f32(boxes), _f32(probs)
@@ -315,7 +316,7 @@ def fast_rcnn_inference(boxes, probs, roi_img, roi_slot, P, image_shapes, score_
         fs = sc[filt[:, 0], filt[:, 1]]
         max_coord = bx.max() if bx.size else F32(0)
         offsets = filt[:, 0].astype(F32)[:, None] * (max_coord + F32(1))
-        keep = nms(fb + offsets, fs, topk_per_image, nms_thresh)
+        keep = nms(fb if nms_cls_agnostic else fb + offsets, fs, topk_per_image, nms_thresh)
         ob = np.zeros((topk_per_image, 4), F32)
         osc = np.zeros(topk_per_image, F32)
         oc = np.zeros(topk_per_image, np.int64)

@@ -26,6 +26,19 @@ box_ops_golden.npz (same loader):
     ymax = ymin + h) -> decoded boxes, |dh|, |dw| below Box2BoxTransform's
     clamp log(1000/16) so the two formulas differ only by rounding.
 
+multiclass_nms_golden.npz (same loader):
+  * np_box_list_ops.multi_class_non_max_suppression (np_box_list_ops.py:220-290:
+    per class, score > thresh, NMS, then every class's survivors sorted by
+    score) on 300 clustered boxes x 12 classes whose scores are the softmax
+    (float32, TF's exp(x - max) * (1 / sum)) of seeded logits; the class-offset
+    NMS of fast_rcnn_inference (fast_rcnn.py:141-145) makes the same per-class
+    decisions on these inputs: boxes inside [0, 900) with max_coord + 1
+    offsets separate the classes, every pairwise IoU is 1e-4 away from the
+    threshold, candidate scores are 2e-6 apart and 1e-5 away from score_thresh, and
+    the survivors (< 100) fit topk_per_image.  Stored: boxes, logits, the
+    selected boxes / scores / classes and each one's ROI row (matched back by
+    exact box equality: the reference's BoxList drops extra fields).
+
     python tests/golden/make_golden.py [/root/reference]
 """
 import importlib.util
@@ -36,6 +49,7 @@ import types
 import numpy as np
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "nms_golden.npz")
+OUT_MC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "multiclass_nms_golden.npz")
 OUT_BOX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "box_ops_golden.npz")
 
 
@@ -134,6 +148,44 @@ def box_ops_cases(mods, rng):
     return data
 
 
+def softmax_tf32(logits):
+    """float32 softmax in TF's CPU order: e = exp(x - max), e * (1 / sum(e))."""
+    x = logits.astype(np.float32)
+    e = np.exp(x - x.max(axis=1, keepdims=True)).astype(np.float32)
+    return (e * (np.float32(1) / e.sum(axis=1, keepdims=True, dtype=np.float32))).astype(np.float32)
+
+
+def multiclass_case(mods, rng, R=120, K=6, thr=0.5, score_thresh=0.3):
+    lops, bl = mods["np_box_list_ops"], mods["np_box_list"]
+    for _ in range(500):
+        boxes = np.clip(random_boxes(rng, R, extent=800.0, min_side=40.0, max_side=70.0,
+                                     clusters=6), 1.0, 899.0).astype(np.float32)
+        boxes[:, 2:] = np.maximum(boxes[:, 2:], boxes[:, :2] + 4.0)
+        iou = iou64(boxes)
+        np.fill_diagonal(iou, 0)
+        if np.any(np.abs(iou - thr) < 1e-4):
+            continue
+        logits = rng.normal(0, 2.0, size=(R, K + 1)).astype(np.float32)
+        probs = softmax_tf32(logits)
+        sc = probs[:, :K]
+        cand = np.sort(sc[sc > score_thresh])
+        if len(cand) == 0 or np.any(np.diff(cand) < 2e-6) or \
+                np.any(np.abs(sc - score_thresh) < 1e-5):
+            continue
+        blist = bl.BoxList(boxes.copy())
+        blist.add_field("scores", sc.copy())
+        res = lops.multi_class_non_max_suppression(blist, score_thresh, thr, 100)
+        sel = res.get()
+        if not 20 <= len(sel) < 100 or len(sel) >= len(cand):
+            continue  # want suppression to happen and every survivor to fit
+        rows = np.array([np.nonzero((boxes == b).all(1))[0][0] for b in sel], np.int32)
+        return dict(mc_boxes=boxes, mc_logits=logits, mc_sel_boxes=sel.astype(np.float32),
+                    mc_sel_scores=res.get_field("scores").astype(np.float32),
+                    mc_sel_classes=res.get_field("classes").astype(np.int64),
+                    mc_sel_rows=rows, mc_params=np.array([thr, score_thresh], np.float64))
+    raise RuntimeError("could not draw a threshold-safe multi-class case")
+
+
 def main(ref_root="/root/reference"):
     mods = load_reference_np_ops(ref_root)
     rng = np.random.default_rng(20261015)
@@ -154,6 +206,9 @@ def main(ref_root="/root/reference"):
     box = box_ops_cases(mods, np.random.default_rng(20261016))
     np.savez_compressed(OUT_BOX, **box)
     print("wrote", OUT_BOX, {k: v.shape for k, v in box.items()})
+    mc = multiclass_case(mods, np.random.default_rng(20261017))
+    np.savez_compressed(OUT_MC, **mc)
+    print("wrote", OUT_MC, {k: v.shape for k, v in mc.items()})
 
 
 if __name__ == "__main__":

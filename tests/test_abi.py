@@ -28,9 +28,12 @@ def test_library_exports_every_declared_symbol():
 
 def test_loader_sets_signatures_and_version():
     from detectron2_tensorflow_amd import _C
+    from detectron2_tensorflow_amd import _build
     lib = _C.load()
     assert lib.d2mi_version() == 1
     assert _C.last_error() == ""
+    # built from exactly this tree's sources (the loader refuses otherwise)
+    assert lib.d2mi_source_hash().decode() == _build.source_hash()
 
 
 def test_host_side_argument_errors_raise_without_gpu():

@@ -110,7 +110,10 @@ def test_rpn_proposals_baseline_geometry(dev, pre, post):
 
 
 # ------------------------------------------------------------- Fast R-CNN
-def test_fast_rcnn_inference_baseline_geometry(dev):
+@pytest.mark.parametrize("nms_cls_agnostic", [False, True])
+def test_fast_rcnn_inference_baseline_geometry(dev, nms_cls_agnostic):
+    """nms_cls_agnostic=True: ROI_HEADS.NMS_CLS_AGNOSTIC (fast_rcnn.py:138-139),
+    one plain NMS over every class's filtered boxes."""
     rng = np.random.default_rng(303)
     N, P, K = 2, 1000, 80
     image_hw = np.array([[TH, TW], [TH, TW]], np.int32)
@@ -123,12 +126,13 @@ def test_fast_rcnn_inference_baseline_geometry(dev):
     w = (10.0, 10.0, 5.0, 5.0)
     probs = oracle.softmax(logits)
     boxes = oracle.apply_deltas(deltas, props, w)
-    want = oracle.fast_rcnn_inference(boxes, probs, roi_img, roi_slot, P, image_hw, 0.05, 0.5, 100)
+    want = oracle.fast_rcnn_inference(boxes, probs, roi_img, roi_slot, P, image_hw, 0.05, 0.5, 100,
+                                      nms_cls_agnostic)
     gb, gs, gc, gv, groi = _ops().fast_rcnn_inference(
         torch.from_numpy(logits).to(dev), torch.from_numpy(deltas).to(dev),
         torch.from_numpy(props).to(dev), torch.from_numpy(roi_img).to(dev),
         torch.from_numpy(roi_slot).to(dev), N, P, torch.from_numpy(image_hw).to(dev), w, 0.05,
-        0.5, 100)
+        0.5, 100, nms_cls_agnostic=nms_cls_agnostic)
     assert int((probs[:, :-1] > 0.05).sum()) > 5000  # ~3.8 (box, class) survivors per ROI
     for n in range(N):
         wb, wsc, wc, wv, wroi = want[n]
@@ -188,3 +192,27 @@ def test_apply_deltas_vs_reference_numpy_decode(dev):
     want = g["dec_out"]
     tol = np.maximum(F32(1e-4), 4 * np.spacing(np.abs(want).max(axis=1, keepdims=True)))
     assert (np.abs(got - want) <= tol).all()
+
+
+def test_fast_rcnn_inference_vs_reference_multiclass_nms(dev):
+    """The HIP fast_rcnn_inference (softmax + decode + clip + threshold +
+    class-offset NMS) on one class-agnostic box per ROI (zero deltas, boxes
+    inside the image) == the reference's numpy multi_class_non_max_suppression
+    (np_box_list_ops.py:220-290) of the same boxes and softmax scores
+    (tests/golden/multiclass_nms_golden.npz, offset-safe inputs): the same
+    ROIs, classes and order; scores within the softmax's expf ulps."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "multiclass_nms_golden.npz"))
+    boxes, logits = g["mc_boxes"], g["mc_logits"]
+    thr, score_thresh = g["mc_params"]
+    R = boxes.shape[0]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    gb, gs, gc, gv, groi = _ops().fast_rcnn_inference(
+        t(logits), t(np.zeros((R, 4), F32)), t(boxes), t(np.zeros(R, np.int32)),
+        t(np.arange(R, dtype=np.int32)), 1, R, t(np.array([[1000, 1000]], np.int32)),
+        (10.0, 10.0, 5.0, 5.0), float(score_thresh), float(thr), 100, cls_agnostic=True)
+    n = int(gv[0].sum())
+    assert n == len(g["mc_sel_rows"])
+    np.testing.assert_array_equal(groi[0, :n].cpu().numpy(), g["mc_sel_rows"])
+    np.testing.assert_array_equal(gc[0, :n].cpu().numpy(), g["mc_sel_classes"])
+    np.testing.assert_allclose(gs[0, :n].cpu().numpy(), g["mc_sel_scores"], rtol=2e-6, atol=1e-7)
+    assert_boxes_close(gb[0, :n].cpu().numpy(), g["mc_sel_boxes"])

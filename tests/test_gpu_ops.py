@@ -492,9 +492,11 @@ def test_retinanet_inference_vs_oracle(dev, dist):
 
 
 # ------------------------------------------------------------ Matrix NMS
-def test_matrix_nms_vs_oracle(dev):
+@pytest.mark.parametrize("M,H,W", [(150, 50, 84), (500, 200, 336)])
+def test_matrix_nms_vs_oracle(dev, M, H, W):
+    """(500, 200, 336): the C5 geometry -- TOPK_CANDIDATES_TEST = 500 masks of
+    the 1333x800 SOLOv2 mask features."""
     rng = np.random.default_rng(51)
-    M, H, W = 150, 50, 84
     masks = (rng.uniform(size=(M, H, W)) > 0.7).astype(F32)
     for i in range(0, M, 3):  # overlapping pairs
         masks[i + 1] = np.maximum(masks[i], masks[i + 1] * (rng.uniform() > 0.5))

@@ -208,3 +208,30 @@ def test_apply_deltas_matches_reference_numpy_decode():
     want = g["dec_out"]
     tol = np.maximum(np.float32(1e-4), 4 * np.spacing(np.abs(want).max(axis=1, keepdims=True)))
     assert (np.abs(got - want) <= tol).all()
+
+
+MC_GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "multiclass_nms_golden.npz")
+
+
+def test_fast_rcnn_inference_matches_reference_multiclass_nms():
+    """oracle.fast_rcnn_inference (class-offset NMS, fast_rcnn.py:141-145) on
+    one class-agnostic box per ROI == the reference's numpy
+    multi_class_non_max_suppression (np_box_list_ops.py:220-290) on the same
+    boxes and softmax scores (tests/golden/multiclass_nms_golden.npz: inputs
+    where the offset trick cannot change an IoU decision)."""
+    g = np.load(MC_GOLDEN)
+    boxes, logits = g["mc_boxes"], g["mc_logits"]
+    thr, score_thresh = g["mc_params"]
+    R, K = logits.shape[0], logits.shape[1] - 1
+    probs = oracle.softmax(logits)
+    np.testing.assert_array_equal(probs[:, :K][probs[:, :K] > score_thresh].size,
+                                  (probs[:, :K] > score_thresh).sum())
+    res = oracle.fast_rcnn_inference(np.tile(boxes, (1, K)), probs, np.zeros(R, np.int64),
+                                     np.arange(R), R, [(1000, 1000)], score_thresh, thr, 100)
+    ob, osc, oc, ov, oroi = res[0]
+    n = int(ov.sum())
+    assert n == len(g["mc_sel_rows"])
+    np.testing.assert_array_equal(oroi[:n], g["mc_sel_rows"])
+    np.testing.assert_array_equal(oc[:n], g["mc_sel_classes"])
+    np.testing.assert_array_equal(osc[:n], g["mc_sel_scores"])
+    np.testing.assert_array_equal(ob[:n], g["mc_sel_boxes"])
