@@ -9,9 +9,11 @@ synthetic COCO-shaped images + GT already resident in HBM.  value = all
 ranks' images / (max-over-ranks time of K steps), weak scaling.
 
 --mode infer: one step = one batched forward of the whole model over
-synthetic images already resident in HBM: ResNet-50 (PyTorch-ROCm convs) -> FPN (MFMA
+synthetic images already resident in HBM: ResNet-50 (every conv but the frozen
+7x7 stem on the HIP split-product MFMA kernels, FrozenBN folded) -> FPN (MFMA
 kernels, fused top-down add) -> RPN head (MFMA) + fused top-k/decode/NMS
-proposals -> multi-level ROIAlign 7x7 -> box head (hipBLASLt GEMMs) -> fused
+proposals -> multi-level ROIAlign 7x7 -> box head (fc1 on the MFMA kernel,
+fc2 / predictors hipBLASLt) -> fused
 Fast R-CNN post-processing (softmax/decode/clip/class-offset NMS) -> ROIAlign
 14x14 on the detections -> mask head (MFMA) -> per-class mask sigmoid.
 
@@ -169,11 +171,16 @@ def _latest_pmc():
 PMC_FILE = _latest_pmc()
 
 
+# kernels whose PMC-counted bytes belong to the default (foreground-row)
+# training workload only: --mask-fixed-rows changes their work
+PMC_SKIP = set()
+
+
 def pmc_traffic(group, mode):
     """HBM bytes per launch of a kernel group from the committed rocprofv3 PMC
     passes (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)
     of this same bench command in training mode; None when not available."""
-    if mode != "train" or not os.path.exists(PMC_FILE):
+    if mode != "train" or not os.path.exists(PMC_FILE) or group in PMC_SKIP:
         return None
     try:
         with open(PMC_FILE) as f:
@@ -366,7 +373,7 @@ def cpu_baseline(args, model, batch, cfg=None):
         # the same output format as the timed GPU step: "conventional" pastes
         # onto the padded canvas (size divisibility 32)
         canvas = None
-        if args.mask_format == "conventional":
+        if args.mask_format == "conventional" and getattr(model.roi_heads, "mask_on", False):
             d = model.neck.size_divisibility or 1
             canvas = tuple(-(-int(v) // d) * d for v in imgs.shape[1:3])
         run = lambda k, th: ref(imgs[:k], shapes[:k], threads=th, paste_to=canvas)
@@ -425,6 +432,7 @@ def main():
         from detectron2_tensorflow_amd.engine import Trainer
         if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
             model.roi_heads.mask_compact_rows = False
+            PMC_SKIP.update({"roi_align_fwd_mask", "roi_align_bwd"})
         trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
         grad_ctx = torch.enable_grad

@@ -42,6 +42,7 @@
 // f32-class error (tests: error vs float64 within a small factor of the
 // native f32 path's).
 #include "common.h"
+#include "internal.h"
 
 namespace d2mi {
 namespace {
@@ -666,6 +667,233 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
 }
 
+// Warp-specialised split-product conv: a 256x128 tile, 16 waves (1024
+// threads), one workgroup per CU.  Waves 0-7 only compute: each owns a
+// 64x64 block (2x2 tiles of 32x32) and issues ds_read + MFMA.  Waves 8-15
+// only stage: global loads LD k-steps ahead into registers, the exact bf16x3
+// split, the LDS writes.  Two LDS stages of the split planes (72 KiB each):
+// at iteration u the stagers write k-step u + 1 while the compute waves
+// multiply k-step u -- one barrier per 32-deep k-step, and no compute wave
+// waits for a global load.  Waves w, w + 4, w + 8, w + 12 share a SIMD
+// (dispatch order 0 2 1 3): two MFMA streams (which hide each other's LDS
+// latency) beside two staging streams on every SIMD.  The 256-row tile reads
+// 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
+// Same K order, product order and accumulation sequence as
+// conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
+template <bool ML, int LD>
+__global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
+  constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
+  constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
+  constexpr int A_WORDS = 3 * BM * LDSB / 2, B_WORDS = 3 * BN * LDSB / 2;
+  constexpr int STAGE = A_WORDS + B_WORDS;  // 18432 words = 72 KiB
+  __shared__ __attribute__((aligned(16))) float smem[S * STAGE];
+  static_assert(S * STAGE >= 32 * (BN + 4), "LDS epilogue slab does not fit");
+
+  const int orig = blockIdx.x;
+  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
+  int tile =
+      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const Geo g = ML ? select_level(a, tile) : geo_of(a);
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.y;
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
+  const int nks = max(kt1 - kt0, 0);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;  // (stagers: wr >= 4, never an acc slab)
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (wave >= 8) {
+    // ------------------------------------------------------------ stagers
+    const int st = tid - 512;
+    const int srow = st >> 3, schunk = (st & 7) * 4;  // rows srow + 64 p
+    int ih0[RA], iw0[RA], base[RA];
+#pragma unroll
+    for (int p = 0; p < RA; ++p) {
+      const int m = m0 + srow + 64 * p;
+      const int mm = m < g.M ? m : 0;
+      const int n = mm / (g.OH * g.OW);
+      const int rem = mm - n * g.OH * g.OW;
+      const int oh = rem / g.OW, ow = rem - oh * g.OW;
+      const int ihv = oh * a.stride - a.pad;
+      ih0[p] = m < g.M ? ihv : -(1 << 29);
+      iw0[p] = ow * a.stride - a.pad;
+      base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + schunk;
+    }
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
+    constexpr uint32_t kOOB = 0x80000000u;
+    const int taps = a.KH * a.KW;
+    // ablation bits (D2MI_CONV_DBG, timing experiments only): 1 = no global
+    // loads, 2 = no split / LDS writes (the loaded values kept live)
+    const int dbg = a.dbg;
+    auto load = [&](int kt, float4 (&la)[RA], float4 (&lb)[RB]) {
+      if (dbg & 1) return;
+      const int chunk = kt / taps;
+      const int tap = kt - chunk * taps;
+      const int cc = chunk * BK;
+      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+      const bool cok = cc + schunk < a.Cin;
+      const int toff = (kh * g.W + kw) * a.Cin + cc;
+      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
+#pragma unroll
+      for (int p = 0; p < RB; ++p) {
+        const int co = n0 + srow + 64 * p;
+        const uint32_t off = (cok & (co < a.Cout))
+                                 ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
+                                 : kOOB;
+        lb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+      }
+#pragma unroll
+      for (int p = 0; p < RA; ++p) {
+        const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
+                        ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
+        const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
+        la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+      }
+    };
+    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
+      if (dbg & 2) {
+#pragma unroll
+        for (int p = 0; p < RA; ++p) asm volatile("" ::"v"(la[p].x));
+#pragma unroll
+        for (int p = 0; p < RB; ++p) asm volatile("" ::"v"(lb[p].x));
+        return;
+      }
+      uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
+      uint16_t* B16 = A16 + 3 * BM * LDSB;
+#pragma unroll
+      for (int p = 0; p < RA; ++p) {
+        uint2 h, m, l;
+        split3(la[p], h, m, l);
+        const int o = swz(srow + 64 * p, schunk);
+        *reinterpret_cast<uint2*>(&A16[o]) = h;
+        *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&A16[2 * BM * LDSB + o]) = l;
+      }
+#pragma unroll
+      for (int p = 0; p < RB; ++p) {
+        uint2 h, m, l;
+        split3(lb[p], h, m, l);
+        const int o = swz(srow + 64 * p, schunk);
+        *reinterpret_cast<uint2*>(&B16[o]) = h;
+        *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&B16[2 * BN * LDSB + o]) = l;
+      }
+    };
+    // Register ring of LD k-steps (static indices: the loops are unrolled by
+    // LD).  Every load is UNCONDITIONAL (k-steps past the end re-load the last
+    // one): with a data-dependent load count hipcc cannot count the loads in
+    // flight and drains them all (vmcnt(0)) before each write.
+    float4 ra[LD][RA], rb[LD][RB];
+    if (dbg & 1) {
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+#pragma unroll
+        for (int p = 0; p < RA; ++p) ra[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
+#pragma unroll
+        for (int p = 0; p < RB; ++p) rb[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
+      }
+    }
+    const int klast = kt0 + max(nks, 1) - 1;
+    auto kclamp = [&](int v) { return min(kt0 + v, klast); };
+#pragma unroll
+    for (int j = 0; j < LD; ++j) load(kclamp(j), ra[j], rb[j]);
+    if (nks > 0) write(0, ra[0], rb[0]);  // prologue: k-step 0 into buffer 0
+    load(kclamp(LD), ra[0], rb[0]);
+    __syncthreads();  // B_{-1}
+    // iteration u: k-step v = u + 1 -> buffer v % 2 from register set v % LD,
+    // that set re-filled with k-step v + LD; then B_u
+    int u0 = 0;
+    for (; u0 + LD <= nks; u0 += LD) {
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        const int v = u0 + j + 1;
+        const int set = (j + 1) % LD;  // (unrolled: a constant index)
+        if (v < nks) write(v & 1, ra[set], rb[set]);
+        load(kclamp(v + LD), ra[set], rb[set]);
+        __syncthreads();  // B_u
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LD - 1; ++j) {  // the remaining nks % LD iterations
+      if (u0 + j < nks) {
+        const int v = u0 + j + 1;
+        const int set = (j + 1) % LD;
+        if (v < nks) write(v & 1, ra[set], rb[set]);
+        __syncthreads();
+      }
+    }
+  } else {
+    // ------------------------------------------------------------ compute
+    const int li = lane & 31, lh = lane >> 5;
+    const int cdbg = a.dbg;
+    bf16x8 fa[3][TM], fb[3][TN];
+    auto ldf = [&](int buf, int ks) {
+      const uint16_t* A16 = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
+      const uint16_t* B16 = A16 + 3 * BM * LDSB;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[pl][i] = *reinterpret_cast<const bf16x8*>(
+              &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[pl][j] = *reinterpret_cast<const bf16x8*>(
+              &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+      }
+    };
+    auto mma = [&]() {
+      if (cdbg & 4) {  // ablation: no MFMAs (the fragments kept live)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          asm volatile("" ::"v"(fa[pl][0]), "v"(fa[pl][1]), "v"(fb[pl][0]), "v"(fb[pl][1]));
+        return;
+      }
+      constexpr int PA[6] = {1, 2, 0, 0, 1, 0};
+      constexpr int PB[6] = {1, 0, 2, 1, 0, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
+                                                                 acc[i][j], 0, 0, 0);
+    };
+    const int prio = a.prio;
+    __syncthreads();  // B_{-1}
+    for (int u = 0; u < nks; ++u) {
+      const int buf = u & 1;
+      if (prio & 1) __builtin_amdgcn_s_setprio(1);
+      ldf(buf, 0);
+      mma();
+      ldf(buf, 1);
+      mma();
+      if (prio & 1) __builtin_amdgcn_s_setprio(0);
+      // keep the MFMAs ahead of the barrier: moved past it, they would wait
+      // for the stagers instead of overlapping them
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();  // B_u
+    }
+  }
+  store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, smem);
+}
+
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
 // exact split, d2mi_split_bf16x3 / a producer that wrote them), so staging is
 // a plain copy global -> LDS (no VALU split per tap and per Cout tile) and the
@@ -1016,16 +1244,25 @@ static int wg_slots(int cfg) {
       c = 256;  // MI355X
     cus = c;
   }
+  if (cfg == 3) return cus;  // the warp-specialised kernel: one per CU
   return (cfg == 0 && occ3_enabled() ? 3 : 2) * cus;
 }
 
 // wide_ok: the 128x128 tile may be used -- its kernels only carry the LDS
 // epilogue (Cout % 4 == 0 and 16-B aligned operands); otherwise 128x64.
-Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
+// split: the split-product math (kSplit3); cfg 3 (the warp-specialised
+// 256x128 kernel, tuning "conv_ws") exists only in that form, and takes the
+// long-K convs (>= 16 k-steps: every 3x3 with Cin >= 64, the 1x1s with
+// Cin >= 512), where its deeper staging pipeline pays; the short-K 1x1s
+// (2-8 k-steps) stay on the 3-per-CU kernel, whose prologue / epilogue
+// overlap across workgroups (tools/ws_ab.py, 16 Mask R-CNN shapes).
+Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool split = true) {
   Plan p;
   p.cfg = Cout <= 32 ? 2 : (Cout <= 64 || !wide_ok ? 1 : 0);
-  p.BM = 128;
-  p.BN = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
+  if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 && KH * KW * ((Cin + BK - 1) / BK) >= 16)
+    p.cfg = 3;
+  p.BM = p.cfg == 3 ? 256 : 128;
+  p.BN = (p.cfg == 0 || p.cfg == 3) ? 128 : (p.cfg == 1 ? 64 : 32);
   const int nM = (M + p.BM - 1) / p.BM, nN = (Cout + p.BN - 1) / p.BN;
   p.ntiles = nM * nN;
   p.nk = KH * KW * ((Cin + BK - 1) / BK);
@@ -1041,7 +1278,7 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok) {
   // target: two workgroups per CU even for the 3-per-CU kernel (A/B over
   // 384..1024 slots on the training step: 512 fastest, +2.5 % over 768 -- fewer
   // splits, less partial-slab traffic for the reduce)
-  const int gs = GS > 0 ? GS : wg_slots(1);
+  const int gs = GS > 0 ? GS : (p.cfg == 3 ? wg_slots(3) : wg_slots(1));
   if (4 * p.ntiles < 3 * gs && p.nk >= 16) {
     p.splits = std::min(std::max(1, gs / p.ntiles), std::min(p.nk / 8, 16));
   }
@@ -1136,8 +1373,18 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
   return 0;
 }
 
+// D2MI_CONV_WS / d2mi_set_tuning("conv_ws", d): the warp-specialised
+// 256x128 split kernel (conv_ws_kernel, plan cfg 3): 0 off, 2 / 3 the
+// stagers' register prefetch depth (k-steps).
+static int ws_depth() { return tuning(kTuneConvWS); }
+
 template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
+    // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
+    hipLaunchKernelGGL((conv_ws_kernel<false, 2>), grid, dim3(1024), 0, st, a);
+    return;
+  }
   if (cfg == 0 && !db && occ3_enabled()) {
     hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3>), grid, dim3(256), 0, st, a);
     return;
@@ -1246,7 +1493,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     static const char* prio = getenv("D2MI_CONV_PRIO");
     a.prio = prio ? atoi(prio) : 5;
   }
-  Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0);
+  Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0 && !x3);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
     p.splits = 1;
     p.kt_per_split = p.nk;
@@ -1400,7 +1647,7 @@ extern "C" int d2mi_conv2d_nhwc(const float* x, const float* w_packed, const flo
 // tile count (Cout % 4 == 0 for the level-aware reduce).
 static int levels_splits(const int32_t* dims, int nlev, int Cin, int Cout, int KH, int KW,
                          int stride, int pad_beg, int pad_end, int64_t* rows, int* ntiles) {
-  const Plan p0 = make_plan(1, Cout, KH, KW, Cin, Cout % 4 == 0);
+  const Plan p0 = make_plan(1, Cout, KH, KW, Cin, Cout % 4 == 0, false);  // (no cfg 3)
   const int nN = (Cout + p0.BN - 1) / p0.BN;
   int64_t r = 0;
   int t = 0;
@@ -1479,7 +1726,8 @@ extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* di
     Mtot += (int64_t)N * OH * OW;
   }
   a.lds_epi = al;
-  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al);
+  // multi-level launches keep the 128-row kernels (no cfg 3)
+  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al, false);
   a.nN = (Cout + p.BN - 1) / p.BN;
   int t = 0;
   for (int l = 0; l < nlev; ++l) {

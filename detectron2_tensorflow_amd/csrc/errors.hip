@@ -1,8 +1,11 @@
 // Thread-local host error string + the device error word (see include/d2mi.h).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
+#include "internal.h"
 
 namespace {
 thread_local char g_msg[1024] = "";
@@ -10,6 +13,23 @@ __device__ int32_t g_error_word = 0;
 }  // namespace
 
 namespace d2mi {
+
+namespace {
+const char* const kTuneNames[kTuneCount] = {"conv_ws", "roi_fwd"};
+const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS", "D2MI_ROI_FWD"};
+const int kTuneDefault[kTuneCount] = {2, 0};
+int g_tune[kTuneCount];
+bool g_tune_set[kTuneCount];
+}  // namespace
+
+int tuning(TuneKey k) {
+  if (!g_tune_set[k]) {
+    const char* e = getenv(kTuneEnv[k]);
+    g_tune[k] = e ? atoi(e) : kTuneDefault[k];
+    g_tune_set[k] = true;
+  }
+  return g_tune[k];
+}
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -39,6 +59,19 @@ int d2mi_version(void) { return 1; }
 const char* d2mi_source_hash(void) { return D2MI_SOURCE_HASH; }
 
 const char* d2mi_last_error(void) { return g_msg; }
+
+int d2mi_set_tuning(const char* key, int value) {
+  D2MI_REQUIRE(key != nullptr, "null tuning key");
+  for (int k = 0; k < d2mi::kTuneCount; ++k) {
+    if (strcmp(key, d2mi::kTuneNames[k]) == 0) {
+      d2mi::g_tune[k] = value;
+      d2mi::g_tune_set[k] = true;
+      return 0;
+    }
+  }
+  D2MI_REQUIRE(false, "unknown tuning key '%s'", key);
+  return -1;
+}
 
 int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }
 

@@ -58,4 +58,9 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
                  int32_t* idx_out, int32_t* count_out, void* ws, size_t ws_bytes,
                  hipStream_t stream, bool sampled_floor = false);
 
+// Process-wide kernel-selection knobs (d2mi_set_tuning; initial values from
+// the environment): in-process A/B timing of kernel variants (tools/).
+enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneCount };
+int tuning(TuneKey k);
+
 }  // namespace d2mi

@@ -37,6 +37,7 @@ struct RoiArgs {
   const float* gout;
   int32_t* err;
   int bpb;  // forward: output bins per workgroup (16, 32 or 64)
+  int xcd_remap;  // forward: ROIs spread XCD-contiguously (roi_fwd tuning bit 8)
   // backward over one or two ROI sets of the same maps (Contrib::set picks):
   // each set's grad_out and its sampling ratio (the avg-pool divisor)
   const float* gout_s[2];
@@ -151,9 +152,18 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float t) {
 // few-ROI launches (the mask pooler's foreground ROIs) still fill 256 CUs.
 constexpr int kMaxBinsPerBlock = 64, kMinBinsPerBlock = 16, kFwdMinBlocks = 2048;
 
-template <bool VEC4>
+// U: bins per wave iteration in the C = 256 path (their 4U corner loads are
+// in flight together); NT: output rows stored non-temporally (streamed past
+// the L2 the feature maps are being gathered through); XCD: ROI r taken from
+// a bijective XCD-contiguous remap of blockIdx.x (ROIs that neighbour in the
+// sampled layout -- foreground proposals of one GT -- share an XCD's L2).
+template <bool VEC4, int U = 4, bool NT = false>
 __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
-  const int r = blockIdx.x;
+  int r = blockIdx.x;
+  if (a.xcd_remap) {
+    const int nwg = gridDim.x, q = nwg / 8, r8 = nwg % 8, xcd = r % 8;
+    r = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + r / 8;
+  }
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const RoiGeom g = roi_geom(a, r);
@@ -173,7 +183,6 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
     // all 4U corner loads issued before any is consumed (the taps are clamped
     // to valid rows, so the loads are unconditional; invalid samples are zeroed
     // after) — memory-level parallelism instead of one latency per bin.
-    constexpr int U = 4;
     const float4* p = reinterpret_cast<const float4*>(base);
     for (int bb = blockIdx.y * a.bpb + wave; bb < b_end; bb += 4 * U) {
       float4 c00[U], c01[U], c10[U], c11[U];
@@ -200,7 +209,12 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
         const float4 top = lerp4(c00[u], c01[u], lx[u]);
         const float4 bot = lerp4(c10[u], c11[u], lx[u]);
         const float4 v = ok[u] ? lerp4(top, bot, ly[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        reinterpret_cast<float4*>(a.out + ((size_t)r * nbins + bin) * C)[lane] = v;
+        float4* dst = reinterpret_cast<float4*>(a.out + ((size_t)r * nbins + bin) * C) + lane;
+        if (NT) {
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(dst));
+        } else
+          *dst = v;
       }
     }
     return;
@@ -785,11 +799,26 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   while (a.bpb > kMinBinsPerBlock &&
          (long long)R * ((nbins + a.bpb - 1) / a.bpb) < kFwdMinBlocks)
     a.bpb /= 2;
-  dim3 grid(R, (nbins + a.bpb - 1) / a.bpb);
-  if (vec4)
-    hipLaunchKernelGGL(roi_align_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), a);
+  // tuning "roi_fwd" (A/B, tools/roi_ab.py): bit 1 = 2 bins per wave
+  // iteration (fewer VGPRs, more resident waves), bit 2 = the blocks of a ROI
+  // split its bins evenly, bit 4 = non-temporal output stores, bit 8 = XCD-
+  // contiguous ROI order
+  const int tv = tuning(kTuneRoiFwd);
+  const int nby = (nbins + a.bpb - 1) / a.bpb;
+  if (tv & 2) a.bpb = (nbins + nby - 1) / nby;
+  a.xcd_remap = (tv & 8) ? 1 : 0;
+  dim3 grid(R, nby);
+  hipStream_t st = as_stream(stream);
+  if (!vec4)
+    hipLaunchKernelGGL((roi_align_fwd_kernel<false>), grid, dim3(256), 0, st, a);
+  else if ((tv & 5) == 0)
+    hipLaunchKernelGGL((roi_align_fwd_kernel<true, 4, false>), grid, dim3(256), 0, st, a);
+  else if ((tv & 5) == 1)
+    hipLaunchKernelGGL((roi_align_fwd_kernel<true, 2, false>), grid, dim3(256), 0, st, a);
+  else if ((tv & 5) == 4)
+    hipLaunchKernelGGL((roi_align_fwd_kernel<true, 4, true>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(roi_align_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL((roi_align_fwd_kernel<true, 2, true>), grid, dim3(256), 0, st, a);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

@@ -142,6 +142,14 @@ def roi_touched_rows(boxes, box_ind, params, shapes):
     return int(torch.unique(torch.cat(ids)).numel())
 
 
+def set_tuning(key, value):
+    """d2mi_set_tuning (in-process A/B of kernel variants, tools/); clears the
+    conv workspace-size cache, whose plans may depend on the knob."""
+    _C.check(_C.lib().d2mi_set_tuning(key.encode(), int(value)), "d2mi_set_tuning")
+    _CONV_WS.clear()
+    _WGRAD_WS.clear()
+
+
 def _f32c(t):
     if t.dtype is torch.float32 and t.is_contiguous():
         return t

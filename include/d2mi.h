@@ -39,10 +39,17 @@ extern "C" {
 
 /* ------------------------------------------------------------------ misc */
 int d2mi_version(void);
-/* sha256 prefix of the sources the library was built from (csrc/*.hip,
- * csrc/*.h, this header): the loader checks it against its tree. */
+/* sha256 prefix of the sources the library was built from (the csrc .hip
+ * and .h files and this header): the loader checks it against its tree. */
 const char* d2mi_source_hash(void);
 const char* d2mi_last_error(void);
+/* Process-wide kernel-selection knobs for in-process A/B timing (tools/);
+ * each starts from its environment variable.  No reference counterpart (a
+ * tuning hook of this implementation).  Keys:
+ *   "conv_ws"  D2MI_CONV_WS  warp-specialised 256x128 split conv kernel for
+ *                            the long-K convs: 0 off, else on (default 2);
+ *   "roi_fwd"  D2MI_ROI_FWD  ROIAlign forward variant bits. */
+int d2mi_set_tuning(const char* key, int value);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
 int32_t* d2mi_error_word_dev(void);
@@ -351,6 +358,7 @@ int d2mi_group_norm_nhwc_levels(const float* const* xs, const int32_t* dims, int
  */
 int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int Cin, int Cout,
                            float* w_packed, void* stream);
+
 /* d2mi_conv_pack_weights_many: n weight tensors (w_hwio[i], dims[4i..4i+3] =
  * KH, KW, Cin, Cout) packed as d2mi_conv_pack_weights does, the Cin % 64 == 0
  * ones by one launch per 32 tensors (the per-step repack of every

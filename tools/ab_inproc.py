@@ -32,7 +32,13 @@ def _rpn_acc(on):
     _RPNHead1x1Fn.ACC_LEVELS = on
 
 
-SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc}
+def _conv_ws(on):
+    from detectron2_tensorflow_amd.layers import ops
+    ops.set_tuning("conv_ws", 2 if on else 0)
+
+
+SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+            "conv_ws": _conv_ws}
 
 
 def main():
