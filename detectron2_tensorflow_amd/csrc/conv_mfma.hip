@@ -680,7 +680,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <bool ML, int LD>
+template <bool ML, int LD, bool BATCH = true>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -875,15 +875,63 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
                                                                  acc[i][j], 0, 0, 0);
     };
+    // One 16-deep step with its LDS reads in three plane batches, each
+    // issued one MFMA group ahead of its first use (products in the PA / PB
+    // order): after a barrier all eight compute waves read at once, and 4
+    // reads per wave before the first MFMA (not 12) shorten that burst.
+    auto ld1 = [&](const uint16_t* A16, const uint16_t* B16, int pa, int pb, int ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[pa][i] = *reinterpret_cast<const bf16x8*>(
+            &A16[pa * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[pb][j] = *reinterpret_cast<const bf16x8*>(
+            &B16[pb * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+    };
+    auto mm1 = [&](int pa, int pb) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
+    };
+    auto step16 = [&](int buf, int ks) {
+      if (cdbg & 4) {
+        ldf(buf, ks);
+        mma();
+        return;
+      }
+      const uint16_t* A16 = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
+      const uint16_t* B16 = A16 + 3 * BM * LDSB;
+      ld1(A16, B16, 1, 1, ks);
+      __builtin_amdgcn_sched_barrier(0);
+      ld1(A16, B16, 2, 0, ks);
+      mm1(1, 1);  // m*m
+      __builtin_amdgcn_sched_barrier(0);
+      ld1(A16, B16, 0, 2, ks);
+      mm1(2, 0);  // l*h
+      __builtin_amdgcn_sched_barrier(0);
+      mm1(0, 2);  // h*l
+      mm1(0, 1);  // h*m
+      mm1(1, 0);  // m*h
+      mm1(0, 0);  // h*h
+    };
     const int prio = a.prio;
     __syncthreads();  // B_{-1}
     for (int u = 0; u < nks; ++u) {
       const int buf = u & 1;
       if (prio & 1) __builtin_amdgcn_s_setprio(1);
-      ldf(buf, 0);
-      mma();
-      ldf(buf, 1);
-      mma();
+      if constexpr (BATCH) {
+        step16(buf, 0);
+        step16(buf, 1);
+      } else {  // (A/B, tuning conv_ws = 1: all 12 reads of a step up front)
+        ldf(buf, 0);
+        mma();
+        ldf(buf, 1);
+        mma();
+      }
       if (prio & 1) __builtin_amdgcn_s_setprio(0);
       // keep the MFMAs ahead of the barrier: moved past it, they would wait
       // for the stagers instead of overlapping them
@@ -1382,7 +1430,10 @@ template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
   if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
-    hipLaunchKernelGGL((conv_ws_kernel<false, 2>), grid, dim3(1024), 0, st, a);
+    if (ws_depth() == 1)
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true>), grid, dim3(1024), 0, st, a);
     return;
   }
   if (cfg == 0 && !db && occ3_enabled()) {

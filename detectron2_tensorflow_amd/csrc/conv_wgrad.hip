@@ -18,6 +18,7 @@
 // FIXED split order (deterministic).  Global loads of the next chunk are issued
 // before the current chunk's MFMAs (register double buffering).
 #include "common.h"
+#include "internal.h"
 
 namespace d2mi {
 namespace {
@@ -439,6 +440,228 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_split_kernel(WgradArgs a,
   }
 }
 
+
+// Warp-specialised split wgrad (the conv_ws_kernel structure of
+// conv_mfma.hip for the weight gradient): a 256 (ci) x 128 (co) tile of one
+// tap, 16 waves, one workgroup per CU.  Waves 0-7 compute (4 x 2 blocks of
+// 64 x 64, ds_read + MFMA only); waves 8-15 stage: the 32-pixel chunks of X
+// (shifted by the tap) and dY into registers two chunks ahead, transposed to
+// [channel][pixel], split exactly into bf16 planes and written to one of two
+// LDS stages; one barrier per chunk.  Stager threads 0-511 each own one
+// (4-channel, 4-pixel) item of X; threads 256-511 also one item of dY (and
+// its bias-gradient partial sums, reduced in the fixed order of the 128 x 128
+// kernel).  Same pixel order, product order and accumulation sequence as
+// conv_wgrad_split_kernel: bit-identical for equal pixel splits.
+template <int LD>
+__global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, FastDiv fd_hw,
+                                                                FastDiv fd_w) {
+  constexpr int TM = 2, TN = 2, BM = 256, BN = 128, S = 2;
+  constexpr int GA = BM / 4, GB = BN / 4;  // 4-channel groups
+  constexpr int A_H = 3 * BM * LDW, B_H = 3 * BN * LDW;  // halfwords per stage
+  constexpr int STAGE = A_H + B_H;                      // 36864 halfwords = 72 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t smem[S * STAGE];
+  __shared__ float bred[8][BN];
+
+  const int tile = blockIdx.x;
+  const int per_tap = a.nCi * a.nCo;
+  const int tap = tile / per_tap;
+  const int rem = tile - tap * per_tap;
+  const int cit = rem / a.nCo, cot = rem - cit * a.nCo;
+  const int kh = tap / a.KW, kw = tap - kh * a.KW;
+  const int ci0 = cit * BM, co0 = cot * BN;
+  const int split = blockIdx.y;
+  const int c_begin = split * a.chunks_per_split;
+  const int c_end = min(a.nchunks, c_begin + a.chunks_per_split);
+  const int nks = max(c_end - c_begin, 0);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;  // compute waves 0-7: 4 x 2
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_bias = a.dbias != nullptr && tap == 0 && cit == 0;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (wave >= 8) {
+    // ------------------------------------------------------------ stagers
+    const int st = tid - 512;
+    const int cga = st % GA, pga = st / GA;             // X item (all 512)
+    const bool b_on = st >= 256;                        // dY item (threads 256-511)
+    const int sb = st - 256;
+    const int cgb = (b_on ? sb : 0) % GB, pgb = (b_on ? sb : 0) / GB;
+    const int ci = ci0 + 4 * cga, co = co0 + 4 * cgb;
+    const bool ci_ok = ci < a.Cin, co_ok = b_on && co < a.Cout;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x), 0, a.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.dy), 0, a.dy_bytes, 0x00020000);
+    constexpr uint32_t kOOB = 0x80000000u;
+    float4 ra[LD][4], rb[LD][4];
+    auto load = [&](int ch, float4 (&la)[4], float4 (&lb)[4]) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = ch * KP + 4 * pga + q;
+        const uint32_t n = fdiv((uint32_t)p, fd_hw);
+        const int r2 = p - (int)n * (a.OH * a.OW);
+        const int oy = (int)fdiv((uint32_t)r2, fd_w), ox = r2 - oy * a.OW;
+        const int iy = oy * a.stride - a.pad + kh, ix = ox * a.stride - a.pad + kw;
+        const bool ok = ci_ok & (p < a.P) & ((unsigned)iy < (unsigned)a.H) &
+                        ((unsigned)ix < (unsigned)a.W);
+        const uint32_t off =
+            ok ? (uint32_t)(((((int)n * a.H + iy) * a.W + ix) * a.Cin + ci) * 4) : kOOB;
+        la[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        const int pb = ch * KP + 4 * pgb + q;
+        const uint32_t offb = (co_ok & (pb < a.P)) ? (uint32_t)((pb * a.Cout + co) * 4) : kOOB;
+        lb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, offb, 0, 0));
+      }
+    };
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto write = [&](int buf, const float4 (&la)[4], const float4 (&lb)[4]) {
+      uint16_t* As = smem + buf * STAGE;
+      uint16_t* Bs = As + A_H;
+      const float* f = reinterpret_cast<const float*>(la);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 h, m, l;
+        split3w(make_float4(f[j], f[4 + j], f[8 + j], f[12 + j]), h, m, l);
+        const int o = wswz(4 * cga + j, 4 * pga);
+        *reinterpret_cast<uint2*>(&As[o]) = h;
+        *reinterpret_cast<uint2*>(&As[BM * LDW + o]) = m;
+        *reinterpret_cast<uint2*>(&As[2 * BM * LDW + o]) = l;
+      }
+      if (b_on) {
+        const float* g = reinterpret_cast<const float*>(lb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 v = make_float4(g[j], g[4 + j], g[8 + j], g[12 + j]);
+          if (do_bias) bsum[j] += ((v.x + v.y) + v.z) + v.w;
+          uint2 h, m, l;
+          split3w(v, h, m, l);
+          const int o = wswz(4 * cgb + j, 4 * pgb);
+          *reinterpret_cast<uint2*>(&Bs[o]) = h;
+          *reinterpret_cast<uint2*>(&Bs[BN * LDW + o]) = m;
+          *reinterpret_cast<uint2*>(&Bs[2 * BN * LDW + o]) = l;
+        }
+      }
+    };
+    // unconditional loads (chunks past the end re-load the last one): hipcc
+    // then counts the loads in flight instead of draining them
+    const int clast = c_begin + max(nks, 1) - 1;
+    auto cclamp = [&](int v) { return min(c_begin + v, clast); };
+#pragma unroll
+    for (int j = 0; j < LD; ++j) load(cclamp(j), ra[j], rb[j]);
+    if (nks > 0) write(0, ra[0], rb[0]);
+    load(cclamp(LD), ra[0], rb[0]);
+    __syncthreads();  // B_{-1}
+    int u0 = 0;
+    for (; u0 + LD <= nks; u0 += LD) {
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        const int v = u0 + j + 1;
+        const int set = (j + 1) % LD;
+        if (v < nks) write(v & 1, ra[set], rb[set]);
+        load(cclamp(v + LD), ra[set], rb[set]);
+        __syncthreads();  // B_u
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LD - 1; ++j) {
+      if (u0 + j < nks) {
+        const int v = u0 + j + 1;
+        const int set = (j + 1) % LD;
+        if (v < nks) write(v & 1, ra[set], rb[set]);
+        __syncthreads();
+      }
+    }
+    if (do_bias && b_on) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bred[pgb][4 * cgb + j] = bsum[j];
+    }
+  } else {
+    // ------------------------------------------------------------ compute
+    bf16x8 fa[3][TM], fb[3][TN];
+    auto ld1 = [&](const uint16_t* As, const uint16_t* Bs, int pa, int pb, int ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[pa][i] = *reinterpret_cast<const bf16x8*>(
+            &As[pa * BM * LDW + wswz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[pb][j] = *reinterpret_cast<const bf16x8*>(
+            &Bs[pb * BN * LDW + wswz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
+    };
+    auto mm1 = [&](int pa, int pb) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
+    };
+    // products in the split kernel's order {mm, lh, hl, hm, mh, hh}, reads in
+    // three plane batches one MFMA group ahead of their first use
+    auto step16 = [&](const uint16_t* As, const uint16_t* Bs, int ks) {
+      ld1(As, Bs, 1, 1, ks);
+      __builtin_amdgcn_sched_barrier(0);
+      ld1(As, Bs, 2, 0, ks);
+      mm1(1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      ld1(As, Bs, 0, 2, ks);
+      mm1(2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm1(0, 2);
+      mm1(0, 1);
+      mm1(1, 0);
+      mm1(0, 0);
+    };
+    __syncthreads();  // B_{-1}
+    for (int u = 0; u < nks; ++u) {
+      const uint16_t* As = smem + (u & 1) * STAGE;
+      const uint16_t* Bs = As + A_H;
+      if (a.prio) __builtin_amdgcn_s_setprio(1);
+      step16(As, Bs, 0);
+      step16(As, Bs, 1);
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();  // B_u
+    }
+  }
+  if (do_bias) {  // fixed-order reduction over the 8 pixel groups
+    __syncthreads();
+    if (tid < BN && co0 + tid < a.Cout) {
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s += bred[g][tid];
+      if (a.splits > 1) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
+      else a.dbias[co0 + tid] = s;
+    }
+  }
+  if (wave >= 8) return;
+  const size_t wsz = (size_t)a.KH * a.KW * a.Cin * a.Cout;
+  float* out = a.splits > 1 ? a.partial + (size_t)split * wsz : a.dw;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int oc = co0 + (wc * TN + j) * 32 + li;
+    if (oc >= a.Cout) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cb = ci0 + (wr * TM + i) * 32 + 4 * lh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = cb + (r & 3) + 8 * (r >> 2);
+        if (c < a.Cin) out[((size_t)tap * a.Cin + c) * a.Cout + oc] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
   f.d = d;
@@ -452,6 +675,7 @@ FastDiv make_fastdiv(uint32_t d) {
 struct WPlan {
   int TM, TN, BM, BN, ntiles, splits, chunks_per_split, nchunks;
   bool occ3;
+  bool ws;  // conv_wgrad_ws_kernel (256 x 128 tiles, one workgroup per CU)
 };
 
 // The 128x128 split wgrad can run three workgroups per CU (168 VGPRs, 52 KiB
@@ -467,12 +691,15 @@ static bool wgrad_occ3() {
   return on;
 }
 
-WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
+// split3: the split-product math (the warp-specialised kernel exists only in
+// that form).  It takes Cin % 256 == 0, Cout % 128 == 0 (tuning "wgrad_ws").
+WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW, bool split3 = true) {
   WPlan p;
   // 128 x 128 tiles for 256-wide channels; 64-wide when a dimension is small
   p.TM = Cin > 64 ? 2 : 1;
   p.TN = Cout > 64 ? 2 : 1;
-  p.BM = 64 * p.TM;
+  p.ws = split3 && tuning(kTuneWgradWS) > 0 && Cin % 256 == 0 && Cout % 128 == 0;
+  p.BM = p.ws ? 256 : 64 * p.TM;
   p.BN = 64 * p.TN;
   p.ntiles = KH * KW * ((Cin + p.BM - 1) / p.BM) * ((Cout + p.BN - 1) / p.BN);
   const long long P = (long long)N * OH * OW;
@@ -484,7 +711,7 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
     const char* e = getenv("D2MI_WGRAD_OCC3_MIN_P");
     return e ? atoll(e) : 65536LL;
   }();
-  p.occ3 = p.TM == 2 && p.TN == 2 && P >= occ3_min_p && wgrad_occ3();
+  p.occ3 = !p.ws && p.TM == 2 && p.TN == 2 && P >= occ3_min_p && wgrad_occ3();
   // D2MI_WGRAD_SLOTS / D2MI_WGRAD_MINCH: the split target and the minimum
   // chunks per split (A/B knobs)
   static const int slots_env = [] {
@@ -495,7 +722,7 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW) {
     const char* e = getenv("D2MI_WGRAD_MINCH");
     return e && atoi(e) > 0 ? atoi(e) : 16;
   }();
-  const int G = slots_env > 0 ? slots_env : (p.occ3 ? 768 : 512);
+  const int G = slots_env > 0 ? slots_env : (p.ws ? 256 : (p.occ3 ? 768 : 512));
   int splits = std::max(1, G / p.ntiles);
   splits = std::min(splits, std::max(1, p.nchunks / minch));
   splits = std::min(splits, 64);
@@ -516,9 +743,10 @@ extern "C" size_t d2mi_conv2d_wgrad_workspace_size(int N, int H, int W, int Cin,
   const int OH = (H + pad_beg + pad_end - KH) / stride + 1;
   const int OW = (W + pad_beg + pad_end - KW) / stride + 1;
   if (OH <= 0 || OW <= 0) return 0;
-  const WPlan p = wplan(N, OH, OW, Cin, Cout, KH, KW);
-  return p.splits > 1 ? (size_t)p.splits * ((size_t)KH * KW * Cin * Cout + Cout) * sizeof(float)
-                      : 0;
+  // the larger of the split-product and the f32 plans (either math mode fits)
+  const int s = std::max(wplan(N, OH, OW, Cin, Cout, KH, KW, true).splits,
+                         wplan(N, OH, OW, Cin, Cout, KH, KW, false).splits);
+  return s > 1 ? (size_t)s * ((size_t)KH * KW * Cin * Cout + Cout) * sizeof(float) : 0;
 }
 
 extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_hwio,
@@ -555,9 +783,10 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
   D2MI_REQUIRE(a.OH > 0 && a.OW > 0, "conv output is empty");
   D2MI_REQUIRE((long long)N * a.OH * a.OW < (1LL << 31), "too many pixels");
   a.P = N * a.OH * a.OW;
-  WPlan p = wplan(N, a.OH, a.OW, Cin, Cout, KH, KW);
-  const size_t need = d2mi_conv2d_wgrad_workspace_size(N, H, W, Cin, Cout, KH, KW, stride,
-                                                       pad_beg, pad_end);
+  const bool split3 = (flags & 4) != 0;
+  WPlan p = wplan(N, a.OH, a.OW, Cin, Cout, KH, KW, split3);
+  const size_t need =
+      p.splits > 1 ? (size_t)p.splits * ((size_t)KH * KW * Cin * Cout + Cout) * sizeof(float) : 0;
   if (need > workspace_bytes || workspace == nullptr) {  // no workspace: one split
     p.splits = 1;
     p.chunks_per_split = p.nchunks;
@@ -572,7 +801,6 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
   a.pbias = p.splits > 1 ? (float*)workspace + (size_t)p.splits * KH * KW * Cin * Cout : nullptr;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
-  const bool split3 = (flags & 4) != 0;
   if (split3) {
     D2MI_REQUIRE((int64_t)N * H * W * Cin * 4 < (1ll << 31) &&
                      (int64_t)a.P * Cout * 4 < (1ll << 31),
@@ -580,7 +808,13 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
     a.x_bytes = (int)((int64_t)N * H * W * Cin * 4);
     a.dy_bytes = (int)((int64_t)a.P * Cout * 4);
     const FastDiv fhw = make_fastdiv((uint32_t)(a.OH * a.OW)), fw = make_fastdiv((uint32_t)a.OW);
-    if (p.occ3)
+    // tuning wgrad_ws: 1 = loads one chunk ahead (no spills), 2 = two chunks
+    // ahead (10 VGPRs of the stagers' ring spill at the 128-VGPR budget)
+    if (p.ws && tuning(kTuneWgradWS) >= 2)
+      hipLaunchKernelGGL((conv_wgrad_ws_kernel<2>), grid, dim3(1024), 0, st, a, fhw, fw);
+    else if (p.ws)
+      hipLaunchKernelGGL((conv_wgrad_ws_kernel<1>), grid, dim3(1024), 0, st, a, fhw, fw);
+    else if (p.occ3)
       hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 2, 3>), grid, dim3(256), 0, st, a, fhw, fw);
     else if (p.TM == 2 && p.TN == 2)
       hipLaunchKernelGGL((conv_wgrad_split_kernel<2, 2>), grid, dim3(256), 0, st, a, fhw, fw);

@@ -15,9 +15,9 @@ __device__ int32_t g_error_word = 0;
 namespace d2mi {
 
 namespace {
-const char* const kTuneNames[kTuneCount] = {"conv_ws", "roi_fwd"};
-const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS", "D2MI_ROI_FWD"};
-const int kTuneDefault[kTuneCount] = {2, 0};
+const char* const kTuneNames[kTuneCount] = {"conv_ws", "roi_fwd", "wgrad_ws"};
+const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS", "D2MI_ROI_FWD", "D2MI_WGRAD_WS"};
+const int kTuneDefault[kTuneCount] = {2, 0, 0};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

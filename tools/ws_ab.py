@@ -30,7 +30,8 @@ def main():
     a = ap.parse_args()
     arms = [int(v) for v in a.arms.split(",")]
     names = list(SETS) if a.set == "all" else a.set.split(",")
-    shapes = ([s for n in names for s in SETS[n] if not s.endswith(",w")] if a.shapes is None
+    wg = a.key.startswith("wgrad")
+    shapes = ([s for n in names for s in SETS[n] if s.endswith(",w") == wg] if a.shapes is None
               else a.shapes.split(";"))
     lib = _C.load()
     dev = torch.device("cuda:0")
@@ -46,10 +47,15 @@ def main():
         wp = ops.pack_conv_weights(w)
         p = (k - 1) // 2
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-        res = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "r" in form else None
-        gate = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "g" in form else None
-        kw = dict(residual=res, relu_gate=gate, relu_after_add=(form == "r"), relu=(form == "r"))
-        run = lambda: ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode="split", **kw)
+        if form == "w":
+            dy = torch.randn(N, OH, OW, Cout, generator=g).to(dev)
+            run = lambda: torch.cat([t.reshape(-1) for t in ops.conv2d_wgrad(
+                x, dy, k, s, (p, p), with_bias=True)])
+        else:
+            res = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "r" in form else None
+            gate = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "g" in form else None
+            kw = dict(residual=res, relu_gate=gate, relu_after_add=(form == "r"), relu=(form == "r"))
+            run = lambda: ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode="split", **kw)
         outs, times = {}, {v: [] for v in arms}
         for v in arms:
             ops.set_tuning(a.key, v)
