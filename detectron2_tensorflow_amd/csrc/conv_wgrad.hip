@@ -692,13 +692,17 @@ static bool wgrad_occ3() {
 }
 
 // split3: the split-product math (the warp-specialised kernel exists only in
-// that form).  It takes Cin % 256 == 0, Cout % 128 == 0 (tuning "wgrad_ws").
+// that form).  It takes the KxK convs with Cin % 256 == 0, Cout % 128 == 0
+// (tuning "wgrad_ws"; tools/ws_ab.py --key wgrad_ws: 3x3 shapes 10-20 %
+// faster, the 1x1s 9 % slower -- their 8 chunks of 32 pixels per split are
+// too short for its prologue).
 WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW, bool split3 = true) {
   WPlan p;
   // 128 x 128 tiles for 256-wide channels; 64-wide when a dimension is small
   p.TM = Cin > 64 ? 2 : 1;
   p.TN = Cout > 64 ? 2 : 1;
-  p.ws = split3 && tuning(kTuneWgradWS) > 0 && Cin % 256 == 0 && Cout % 128 == 0;
+  p.ws = split3 && tuning(kTuneWgradWS) > 0 && KH * KW > 1 && Cin % 256 == 0 &&
+         Cout % 128 == 0;
   p.BM = p.ws ? 256 : 64 * p.TM;
   p.BN = 64 * p.TN;
   p.ntiles = KH * KW * ((Cin + p.BM - 1) / p.BM) * ((Cout + p.BN - 1) / p.BN);

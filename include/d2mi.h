@@ -48,9 +48,10 @@ const char* d2mi_last_error(void);
  * tuning hook of this implementation).  Keys:
  *   "conv_ws"  D2MI_CONV_WS  warp-specialised 256x128 split conv kernel for
  *                            the long-K convs: 0 off, else on (default 2);
- *   "roi_fwd"  D2MI_ROI_FWD  ROIAlign forward variant bits;
+ *   "roi_fwd"  D2MI_ROI_FWD  ROIAlign forward variant bits (-1 = default);
  *   "wgrad_ws" D2MI_WGRAD_WS warp-specialised 256x128 split weight-gradient
- *                            kernel (Cin % 256 == 0, Cout % 128 == 0): 0 off. */
+ *                            kernel for KxK convs (Cin % 256 == 0,
+ *                            Cout % 128 == 0): 0 off, 1 (default) on. */
 int d2mi_set_tuning(const char* key, int value);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
