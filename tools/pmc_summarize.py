@@ -30,13 +30,13 @@ import sys
 SPLIT_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), true"
 F32_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), false"
 GROUPS = {
-    "conv2d_split": (re.compile(SPLIT_CONV + r"|conv_x3_kernel|splitk_reduce\w*_kernel"),
-                     re.compile(SPLIT_CONV + r"|conv_x3_kernel")),
+    "conv2d_split": (re.compile(SPLIT_CONV + r"|conv_x3_kernel|conv_ws_kernel|splitk_reduce\w*_kernel"),
+                     re.compile(SPLIT_CONV + r"|conv_x3_kernel|conv_ws_kernel")),
     "conv2d_mfma": (re.compile(F32_CONV), None),
-    "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true>"), None),  # split below
+    "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true"), None),  # split below
     "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_clear_kernel")),
-    "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|wgrad_reduce4?_kernel"),
-                         re.compile(r"conv_wgrad_split_kernel")),
+    "conv_wgrad_split": (re.compile(r"conv_wgrad_split_kernel|conv_wgrad_ws_kernel|wgrad_reduce4?_kernel"),
+                         re.compile(r"conv_wgrad_split_kernel|conv_wgrad_ws_kernel")),
     "conv_wgrad": (re.compile(r"conv_wgrad_kernel<"), None),
 }
 ROI_BWD_OPEN = re.compile(r"roi_bwd_emit_kernel")
@@ -80,7 +80,7 @@ def split_roi_fwd(disp):
     (14x14, a few dozen ROIs) launches, told apart by grid size: the box
     launches have the largest grids.  -> {"roi_align_fwd": [values],
     "roi_align_fwd_mask": [values]}"""
-    rx = re.compile(r"roi_align_fwd_kernel<true>")
+    rx = re.compile(r"roi_align_fwd_kernel<true")
     xs = [(g, v) for _, n, g, v in disp if rx.search(n)]
     if not xs:
         return {}
