@@ -117,6 +117,7 @@ struct ConvArgs {
   int x_plane_bytes, w_plane_bytes;
   int tdH, tdW;
   int dbg;  // ablation bits (D2MI_CONV_DBG, timing experiments only; 0 in production)
+  int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
   // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
   // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
   // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
@@ -661,7 +662,12 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   }
 
   if (a.dbg & 8) return;
-  if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
+  // split-K partial slabs leave straight from the accumulators (each store
+  // instruction writes two whole 128-B row segments; no LDS round trip and
+  // none of its barriers) unless tuning conv_epi = 0
+  if (a.splits > 1 && a.reg_partials)
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+  else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
     store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, &As[0][0]);
   else
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
@@ -938,6 +944,11 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // B_u
     }
+  }
+  if (a.dbg & 8) return;  // (ablation: no epilogue)
+  if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
+    if (wave < 8) store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    return;
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, smem);
 }
@@ -1543,6 +1554,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     a.dbg = dbg ? atoi(dbg) : 0;
     static const char* prio = getenv("D2MI_CONV_PRIO");
     a.prio = prio ? atoi(prio) : 5;
+    a.reg_partials = tuning(kTuneConvEpi) != 0;
   }
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0 && !x3);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
