@@ -13,19 +13,6 @@ size_t sort_workspace_size(int S, int cap);
 int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* lens, int S,
                         int cap, void* ws, size_t ws_bytes, hipStream_t stream);
 
-// Stable ascending radix sort of n 64-bit keys on bits [begin_bit, end_bit):
-// keys equal on that range keep their input order.  Always the onesweep LSD
-// path (rocPRIM's default switches to a merge sort below 1 M keys, whose cost
-// does not shrink with the bit range).
-size_t radix_sort_u64_workspace_size(size_t n, int begin_bit, int end_bit);
-int radix_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, size_t n, int begin_bit,
-                   int end_bit, void* ws, size_t ws_bytes, hipStream_t stream);
-
-// Exclusive prefix sum of n int32 (rocPRIM).
-size_t exclusive_scan_i32_workspace_size(size_t n);
-int exclusive_scan_i32(const int32_t* in, int32_t* out, size_t n, void* ws, size_t ws_bytes,
-                       hipStream_t stream);
-
 // Greedy NMS core over candidates already in capacity layout.
 //   keys   [S*cap] sort keys (desc_key(score, local idx)); lens [S]
 //   boxes  candidate boxes; candidate i of segment s is at

@@ -18,6 +18,8 @@
 #include "common.h"
 #include "internal.h"
 
+#include <climits>
+
 namespace d2mi {
 namespace {
 
@@ -289,25 +291,30 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 // TF CropAndResizeGradImage (+ AvgPoolGrad's 1/count and MirrorPadGrad folding
 // the pad rows onto the edge rows, implicit in the clamped taps) as a GATHER:
 // device-scope float atomics on gfx950 resolve beyond the XCD-private L2 and a
-// scatter of them ran at ~120 GB/s.  Instead:
-//   1. emit: for every (ROI, sample, corner) contribution a 64-bit key
-//      pixel << low_bits | slot, slot = (roi * samples + sample) * 4 + corner,
-//      and its (grad_out row, y_lerp, x_lerp) record at index slot (the ROI
-//      geometry is computed in place);
-//   2. stable onesweep radix sort on the pixel bits only: pixel-major, and
-//      within a pixel the emission (TF loop) order is kept;
-//   3. runs (one kernel): the touched-pixel list, each run's bounds, and for
-//      runs with more than kSeg contributions a block of kSeg-long segments
-//      (slots from a counter) summed by one wave each into a partial row —
-//      bounded work per wave however many ROIs pile onto one pixel (collapsed
-//      proposals at the image border do);
-//   4. the grad maps are zero-filled (one clear launch, full bandwidth) and
-//      the touched pixels are summed by waves striding over that list, four
-//      pixels per wave at C = 256 (16 lanes x 16 channels each): each sums its
-//      contributions (or its segments' partials) in order and stores the
-//      pixel once.
+// scatter of them ran at ~120 GB/s.  Instead, a hand-written counting sort of
+// the contributions by (pixel, set) -- r1/r2 ran a rocPRIM onesweep radix sort
+// here, ~87 us of its ~11 launches per step:
+//   1. emit: for every (ROI, sample, corner) contribution, slot = (roi *
+//      samples + sample) * 4 + corner, its (grad_out row, y_lerp, x_lerp)
+//      record at slot >> 2 and an integer atomic on its pair's counter, whose
+//      old value is the contribution's arrival rank in the pair (a wave whose
+//      live lanes all hit one pair -- collapsed boxes -- takes one atomic);
+//   2. runs (one thread per pixel): each touched pair gets a contiguous range
+//      of the arrival array (workgroup-aggregated cursor: ranges are
+//      independent, so their placement order does not matter), the pixel goes
+//      on the touched list, and a run longer than kSeg gets a block of
+//      kSeg-long segments plus the tasks of its long sort;
+//   3. place (one thread per contribution): arrival[start + rank] = slot;
+//   4. a run's arrival order is not deterministic, its slot order (the TF
+//      loop order) is: runs up to kSeg are ranked by slot inside the pixel
+//      pass (a few LDS / shuffle compares per lane); longer runs are ranked by
+//      `roi_bwd_long_sort_kernel` (1,024 elements per task, each ranked
+//      against the whole run through LDS tiles) into sorted_long;
+//   5. segment partials of the long runs (one wave per kSeg slots), then the
+//      grad maps -- zero-filled by the clear launch -- get their touched
+//      pixels summed by waves striding over the touched list.
 // Two ROI sets of the same maps (the box and mask poolers, d2mi_roi_align_bwd2)
-// share one pass: keys carry (pixel, set), each set's run is summed apart and
+// share one pass: pairs are (pixel, set), each set's run is summed apart and
 // the two sums added.
 // Summation order per pixel is (box, y, x, corner), the TF kernel's loop order
 // (partials regroup it for pixels past kSeg): deterministic run to run, and
@@ -315,6 +322,8 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 // and no folded pad row.
 constexpr int kSeg = 64;    // contributions per wave before a pixel is split
 constexpr int kBatch = 2;   // contributions in flight per wave (r1 sweep, pixel kernel avg: 16 -> 103 us, 8 -> 64, 4 -> 49.5, 2 -> 46.7: occupancy, not loads in flight, binds)
+constexpr int kLongTask = 1024;  // run elements ranked per long-sort task (one workgroup)
+constexpr int kLongTile = 4096;  // run elements per LDS tile of the long sort
 
 struct PixMap {
   long long base[D2MI_MAX_LEVELS + 1];  // first global pixel id per level
@@ -326,8 +335,13 @@ struct Contrib {
   int32_t set;  // ROI set (0 / 1) of a merged backward
 };
 
+// Device-side bookkeeping of one backward (cleared by the clear launch).
+struct BwdCounters {
+  int32_t touched, segs, tasks, cursor;
+};
+
 // One launch clears every buffer the backward starts from (the per-level grad
-// maps to 0, run_start to -1, the touched counter to 0) instead of a
+// maps to 0, the pair counters and the bookkeeping counters to 0) instead of a
 // hipMemsetAsync per buffer: each memset is its own ~5 us dispatch.
 constexpr int kMaxClear = D2MI_MAX_LEVELS + 2;
 struct ClearList {
@@ -356,25 +370,47 @@ __global__ __launch_bounds__(256) void roi_bwd_clear_kernel(ClearList cl) {
   }
 }
 
+// Arrival rank of this lane's contribution to pair q (live lanes only).  When
+// every live lane of the wave hits the same pair -- degenerate boxes collapsed
+// onto one point, where hundreds of ROIs pile onto a pixel -- one atomic takes
+// the whole wave's ranks: same-address device atomics serialise.
+__device__ __forceinline__ uint32_t arrival_rank(int32_t* __restrict__ count, uint32_t q, bool live) {
+  const unsigned long long lm = __ballot(live);
+  if (lm == 0) return 0u;
+  const int lane = threadIdx.x & 63;
+  const int lead = __ffsll((long long)lm) - 1;
+  const uint32_t q0 = (uint32_t)__shfl((int)q, lead);
+  const unsigned long long same = __ballot(live && q == q0);
+  if (same == lm) {
+    uint32_t base = 0;
+    if (lane == lead) base = (uint32_t)atomicAdd(&count[q0], __popcll(lm));
+    base = (uint32_t)__shfl((int)base, lead);
+    return base + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
+  }
+  return live ? (uint32_t)atomicAdd(&count[q], 1) : 0u;
+}
+
 // The ROI geometry is recomputed per sample (a few dozen flops against the
-// 40 B the thread stores) rather than staged by a separate launch.
+// 48 B the thread stores) rather than staged by a separate launch.
 // set / sample_base: a merged backward emits its second ROI set after the
-// first (samples from sample_base on) with pair keys pixel * 2 + set
+// first (samples from sample_base on) with pairs pixel * 2 + set
 // (set_bits = 1): each set's contributions of a pixel form their own run.
-__global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, int set, int set_bits,
-                                    long long sample_base, uint64_t* __restrict__ keys,
-                                    Contrib* __restrict__ rec) {
+// ent[slot] = pair << 32 | arrival rank, ~0 for a contribution outside the map.
+__global__ __launch_bounds__(256) void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int set,
+                                                           int set_bits, long long sample_base,
+                                                           int32_t* __restrict__ count,
+                                                           uint64_t* __restrict__ ent,
+                                                           Contrib* __restrict__ rec) {
   const int S = a.sr > 0 ? a.sr : 1;
   const long long nsamp = (long long)a.out_h * a.out_w * S * S;
   const long long tl = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tl >= (long long)a.R * nsamp) return;
-  const int r = (int)(tl / nsamp);
-  const int s = (int)(tl - (long long)r * nsamp);
-  const RoiGeom g = roi_geom(a, r);
+  const bool in_range = tl < (long long)a.R * nsamp;
+  const int r = in_range ? (int)(tl / nsamp) : 0;
+  const int s = in_range ? (int)(tl - (long long)r * nsamp) : 0;
+  const RoiGeom g = roi_geom(a, in_range ? r : 0);
   const long long t = sample_base + tl;
   const uint64_t slot = (uint64_t)t * 4u;
-  uint64_t* k = keys + slot;
-  bool ok = g.ok;
+  bool ok = in_range && g.ok;
   Tap ty = {}, tx = {};
   int iy = 0, ix = 0;
   if (ok) {
@@ -385,81 +421,156 @@ __global__ void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int low_bits, int set,
     tx = make_tap(in_coord(g.x1, g.x2, g.ws, ix, g.cw, g.Wp), g.Wp, g.W, pad);
     ok = ty.valid && tx.valid;
   }
-  if (!ok) {
-    k[0] = k[1] = k[2] = k[3] = ~0ull;
-    return;
+  uint32_t q[4] = {0u, 0u, 0u, 0u};
+  if (ok) {
+    Contrib c;
+    c.row = r * (a.out_h * a.out_w) + (iy / S) * a.out_w + ix / S;
+    c.yl = ty.lerp;
+    c.xl = tx.lerp;
+    c.set = set;
+    rec[t] = c;  // shared by the 4 corners: slot >> 2
+    const uint64_t img = (uint64_t)pm.base[g.lvl] + (uint64_t)g.n * g.H * g.W;
+    const uint32_t sb = (uint32_t)set;
+    q[0] = (uint32_t)((img + (uint64_t)ty.r0 * g.W + tx.r0) << set_bits) | sb;
+    q[1] = (uint32_t)((img + (uint64_t)ty.r0 * g.W + tx.r1) << set_bits) | sb;
+    q[2] = (uint32_t)((img + (uint64_t)ty.r1 * g.W + tx.r0) << set_bits) | sb;
+    q[3] = (uint32_t)((img + (uint64_t)ty.r1 * g.W + tx.r1) << set_bits) | sb;
   }
-  Contrib c;
-  c.row = r * (a.out_h * a.out_w) + (iy / S) * a.out_w + ix / S;
-  c.yl = ty.lerp;
-  c.xl = tx.lerp;
-  c.set = set;
-  rec[t] = c;  // shared by the 4 corners: slot >> 2
-  const uint64_t img = (uint64_t)pm.base[g.lvl] + (uint64_t)g.n * g.H * g.W;
-  const int sh = low_bits + set_bits;
-  const uint64_t sb = (uint64_t)set << low_bits;
-  k[0] = ((img + (uint64_t)ty.r0 * g.W + tx.r0) << sh) | sb | (slot + 0);
-  k[1] = ((img + (uint64_t)ty.r0 * g.W + tx.r1) << sh) | sb | (slot + 1);
-  k[2] = ((img + (uint64_t)ty.r1 * g.W + tx.r0) << sh) | sb | (slot + 2);
-  k[3] = ((img + (uint64_t)ty.r1 * g.W + tx.r1) << sh) | sb | (slot + 3);
+  uint64_t e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t rank = arrival_rank(count, q[k], ok);
+    e[k] = ok ? ((uint64_t)q[k] << 32) | rank : ~0ull;
+  }
+  if (in_range) {
+    uint64_t* d = ent + slot;
+    d[0] = e[0];
+    d[1] = e[1];
+    d[2] = e[2];
+    d[3] = e[3];
+  }
 }
 
-// run_start[p] = first sorted index of pixel p (-1 untouched), run_end[p] = one past its last.
-// Every touched pixel is also appended to touched[] (*n_touched entries; the
-// list order varies run to run, the per-pixel sums do not).
-// One thread per sorted key.  The first key of a pixel appends the pixel to
-// touched[] (workgroup-aggregated counter); the first key of a (pixel, set)
-// run (set_bits = 1: runs per pair, indexed pixel * 2 + set) records the run:
-// start, end (found by walking the sorted keys: runs are a handful of keys),
-// and for a run longer than kSeg its segment count, a block of segment slots
-// taken from *n_segs and the slots' owner -- the split-run bookkeeping that
-// took a per-pixel pass, a scan and a fill pass before.  Slot order varies run
-// to run; each run's partials are summed in segment order (deterministic).
-__global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(const uint64_t* __restrict__ keys, long long n, int low_bits,
-                                    int set_bits, long long total_pixels,
-                                    int32_t* __restrict__ run_start,
-                                    int32_t* __restrict__ run_end, int32_t* __restrict__ nseg,
-                                    int32_t* __restrict__ seg_first,
-                                    int32_t* __restrict__ seg_pixel, int32_t* __restrict__ n_segs,
-                                    int32_t* __restrict__ touched,
-                                    int32_t* __restrict__ n_touched) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t q = i < n ? keys[i] >> low_bits : ~0ull;  // pair
-  const uint64_t p = q >> set_bits;                         // pixel
-  const bool live = i < n && (long long)p < total_pixels;  // invalid contributions sort last
-  const uint64_t qprev = (live && i > 0) ? keys[i - 1] >> low_bits : ~0ull;
-  const bool first = live && (i == 0 || (qprev >> set_bits) != p);  // first of the pixel
-  const bool first_pair = live && (i == 0 || qprev != q);
-  // one global counter atomic per 1024-thread workgroup: same-address device
-  // atomics serialise (one per wave still cost ~20 us per launch); the waves'
-  // offsets come from an LDS counter
-  __shared__ int wg_count, wg_base;
-  if (threadIdx.x == 0) wg_count = 0;
+// Workgroup-aggregated allocation from a global counter: returns this
+// thread's offset for `want` items (one device atomic per workgroup --
+// same-address atomics serialise, one per wave cost ~20 us per launch).
+template <int NT>
+__device__ __forceinline__ int wg_alloc(int want, int32_t* __restrict__ counter, int* s_wave,
+                                        int* s_base) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // inclusive wave scan
+  int x = want;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_wave[w] = x;
   __syncthreads();
-  const uint64_t m = __ballot(first);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (m && lane == 0) base = atomicAdd(&wg_count, __popcll(m));
-  base = __shfl(base, 0);
-  __syncthreads();
-  if (threadIdx.x == 0) wg_base = wg_count ? atomicAdd(n_touched, wg_count) : 0;
-  __syncthreads();
-  base += wg_base;
-  if (first) touched[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
-  if (first_pair) {
-    long long j = i + 1;
-    while (j < n && (keys[j] >> low_bits) == q) ++j;
-    const int len = (int)(j - i);
-    run_start[q] = (int32_t)i;
-    run_end[q] = (int32_t)j;
-    int ns = 0;
-    if (len > kSeg) {
-      ns = (len + kSeg - 1) / kSeg;
-      const int f = atomicAdd(n_segs, ns);
-      seg_first[q] = f;
-      for (int k = 0; k < ns; ++k) seg_pixel[f + k] = (int32_t)q;
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int k = 0; k < NT / 64; ++k) {
+      const int v = s_wave[k];
+      s_wave[k] = tot;
+      tot += v;
     }
-    nseg[q] = ns;
+    *s_base = tot ? atomicAdd(counter, tot) : 0;
+  }
+  __syncthreads();
+  const int off = *s_base + s_wave[w] + x - want;
+  __syncthreads();  // s_wave / s_base reusable by the caller's next allocation
+  return off;
+}
+
+// One thread per pixel: each touched (pixel, set) pair gets its range of the
+// arrival array, the pixel goes on the touched list, and a pair with more
+// than kSeg contributions gets its segment slots (owner = pair) and the tasks
+// of its long sort.  The list / range orders vary run to run; every per-pixel
+// sum does not.
+__global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
+    const int32_t* __restrict__ count, long long total_pixels, int set_bits,
+    int32_t* __restrict__ run_start, int32_t* __restrict__ seg_first,
+    int32_t* __restrict__ seg_pixel, int2* __restrict__ tasks, int32_t* __restrict__ touched,
+    BwdCounters* __restrict__ ctr) {
+  __shared__ int s_wave[16], s_base;
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = p < total_pixels;
+  const int nsets = 1 << set_bits;
+  int c[2] = {0, 0};
+  for (int s = 0; s < nsets; ++s) c[s] = live ? count[(p << set_bits) | s] : 0;
+  const int tot = c[0] + c[1];
+  int nseg[2] = {0, 0}, ntask[2] = {0, 0};
+  for (int s = 0; s < nsets; ++s) {
+    if (c[s] > kSeg) {
+      nseg[s] = (c[s] + kSeg - 1) / kSeg;
+      ntask[s] = (c[s] + kLongTask - 1) / kLongTask;
+    }
+  }
+  const int pos = wg_alloc<1024>(tot, &ctr->cursor, s_wave, &s_base);
+  const int tix = wg_alloc<1024>(tot > 0 ? 1 : 0, &ctr->touched, s_wave, &s_base);
+  const int sf = wg_alloc<1024>(nseg[0] + nseg[1], &ctr->segs, s_wave, &s_base);
+  const int tf = wg_alloc<1024>(ntask[0] + ntask[1], &ctr->tasks, s_wave, &s_base);
+  if (tot == 0) return;
+  touched[tix] = (int32_t)p;
+  int o = pos, so = sf, to = tf;
+  for (int s = 0; s < nsets; ++s) {
+    const int q = (int)((p << set_bits) | s);
+    if (c[s] == 0) continue;
+    run_start[q] = o;
+    o += c[s];
+    if (nseg[s]) {
+      seg_first[q] = so;
+      for (int k = 0; k < nseg[s]; ++k) seg_pixel[so + k] = q;
+      so += nseg[s];
+      for (int k = 0; k < ntask[s]; ++k) tasks[to + k] = make_int2(q, k);
+      to += ntask[s];
+    }
+  }
+}
+
+// One thread per contribution: its slot at its arrival rank in its pair's range.
+__global__ __launch_bounds__(256) void roi_bwd_place_kernel(const uint64_t* __restrict__ ent,
+                                                            long long n,
+                                                            const int32_t* __restrict__ run_start,
+                                                            int32_t* __restrict__ arrival) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t e = ent[i];
+  if (e == ~0ull) return;
+  const int q = (int)(e >> 32);
+  arrival[run_start[q] + (int)(uint32_t)e] = (int32_t)i;
+}
+
+// Long runs (> kSeg contributions) in slot order: a task ranks kLongTask of a
+// run's elements against the whole run (slots are distinct), streamed through
+// LDS in kLongTile tiles.  O(len^2) compares per run, spread over len / 1024
+// workgroups; only degenerate piles of boxes make runs this long.
+__global__ __launch_bounds__(1024) void roi_bwd_long_sort_kernel(
+    const int32_t* __restrict__ arrival, const int32_t* __restrict__ count,
+    const int32_t* __restrict__ run_start, const int2* __restrict__ tasks,
+    const BwdCounters* __restrict__ ctr, int32_t* __restrict__ sorted_long) {
+  __shared__ int32_t tile[kLongTile];
+  const int ntasks = ctr->tasks;
+  for (int tk = blockIdx.x; tk < ntasks; tk += gridDim.x) {
+    const int2 task = tasks[tk];
+    const int i0 = run_start[task.x], len = count[task.x];
+    const int e = task.y * kLongTask + (int)threadIdx.x;
+    const int mine = e < len ? arrival[i0 + e] : INT_MAX;
+    int rank = 0;
+    for (int j0 = 0; j0 < len; j0 += kLongTile) {
+      const int m = min(kLongTile, len - j0);
+      __syncthreads();
+      for (int j = threadIdx.x; j < m; j += blockDim.x) tile[j] = arrival[i0 + j0 + j];
+      __syncthreads();
+      int j = 0;
+      for (; j + 8 <= m; j += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += tile[j + u] < mine ? 1 : 0;
+      }
+      for (; j < m; ++j) rank += tile[j] < mine ? 1 : 0;
+    }
+    if (e < len) sorted_long[i0 + rank] = mine;
+    __syncthreads();
   }
 }
 
@@ -470,22 +581,22 @@ __device__ __forceinline__ float weigh(int corner, float yl, float xl, float v) 
   return (corner & 1) ? xl * d : (1.f - xl) * d;
 }
 
-// Sum of sorted contributions [i0, i1) for the lane's channel(s) c.
+// Sum of the contributions slots[0, n) (slot order) for the lane's channel(s) c.
 template <bool VEC4>
-__device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __restrict__ keys,
-                                          const Contrib* __restrict__ rec, uint64_t low_mask,
-                                          int i0, int i1, int c, bool live) {
+__device__ __forceinline__ float4 sum_slots(const RoiArgs& a, const int32_t* slots,
+                                            const Contrib* __restrict__ rec, int n, int c,
+                                            bool live) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int C = a.C;
-  for (int i = i0; i < i1; i += kBatch) {
+  for (int i = 0; i < n; i += kBatch) {
     int corner[kBatch];
     Contrib e[kBatch];
-    const int m = min(kBatch, i1 - i);
+    const int m = min(kBatch, n - i);
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) {
       if (u < m) {
-        const uint64_t slot = keys[i + u] & low_mask;
-        corner[u] = (int)(slot & 3u);
+        const int slot = slots[i + u];
+        corner[u] = slot & 3;
         e[u] = rec[slot >> 2];
       }
     }
@@ -519,26 +630,55 @@ __device__ __forceinline__ float4 sum_run(const RoiArgs& a, const uint64_t* __re
   return acc;
 }
 
+// Slot order of a short run (n <= kSeg) by the G lanes of one group (G = 64
+// or 16, `sub` = the lane's index in it): each lane holds kSeg / G of the
+// run's arrival-ordered slots, ranks them against all n (slots are distinct)
+// and stores them at their ranks in the group's LDS row `out`; `in` is a
+// second row of scratch.  Wave-local: LDS operations of one wave complete in
+// order.
+template <int G>
+__device__ __forceinline__ void order_run(const int32_t* __restrict__ arrival, int i0, int n,
+                                          int sub, int32_t* in, int32_t* out) {
+  constexpr int K = kSeg / G;
+  int v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int idx = sub + k * G;
+    v[k] = idx < n ? arrival[i0 + idx] : INT_MAX;
+    if (idx < n) in[idx] = v[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  int rank[K] = {};
+  for (int j = 0; j < n; ++j) {
+    const int o = in[j];
+#pragma unroll
+    for (int k = 0; k < K; ++k) rank[k] += o < v[k] ? 1 : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (sub + k * G < n) out[rank[k]] = v[k];
+  __builtin_amdgcn_wave_barrier();
+}
+
 // One wave per split segment: partial[seg] (C floats).
 template <bool VEC4>
 __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
-    RoiArgs a, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec, int low_bits,
-    const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_end,
+    RoiArgs a, const int32_t* __restrict__ sorted_long, const Contrib* __restrict__ rec,
+    const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const int32_t* __restrict__ seg_pixel,
-    const int32_t* __restrict__ total_segs, float* __restrict__ partial) {
+    const BwdCounters* __restrict__ ctr, float* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
-  const int nsegs = *total_segs;
-  const uint64_t low_mask = (1ull << low_bits) - 1ull;
+  const int nsegs = ctr->segs;
   const int step = VEC4 ? 256 : 64;
   for (int seg = blockIdx.x * 4 + (threadIdx.x >> 6); seg < nsegs; seg += gridDim.x * 4) {
-    const int p = seg_pixel[seg];
-    const int k = seg - seg_first[p];
-    const int i0 = run_start[p] + k * kSeg;
-    const int i1 = min(i0 + kSeg, run_end[p]);
+    const int q = seg_pixel[seg];
+    const int k = seg - seg_first[q];
+    const int i0 = run_start[q] + k * kSeg;
+    const int n = min(kSeg, count[q] - k * kSeg);
     for (int c0 = 0; c0 < a.C; c0 += step) {
       const int c = c0 + (VEC4 ? lane * 4 : lane);
       const bool live = c < a.C;
-      const float4 acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
+      const float4 acc = sum_slots<VEC4>(a, sorted_long + i0, rec, n, c, live);
       if (live) {
         float* dst = partial + (size_t)seg * a.C + c;
         if (VEC4) *reinterpret_cast<float4*>(dst) = acc;
@@ -550,29 +690,29 @@ __global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
 
 // Touched pixels only (the grad maps were zero-filled at full bandwidth
 // first): waves stride over the compact touched-pixel list, one pixel per wave
-// iteration, so the dependent load chain of a pixel (run bounds -> sorted keys
-// -> records -> grad_out rows) overlaps across waves instead of a wave per
+// iteration, so the dependent load chain of a pixel (run bounds -> slots ->
+// records -> grad_out rows) overlaps across waves instead of a wave per
 // feature-map pixel (most of which only stored zeros) -- that launch was bound
 // by wave start-up and latency, at ~1/4 of its store bandwidth.
 template <bool VEC4>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
-    RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
-    int low_bits, int set_bits, const int32_t* __restrict__ run_start,
-    const int32_t* __restrict__ run_end, const int32_t* __restrict__ nseg,
+    RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
+    int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched) {
-  const int lane = threadIdx.x & 63;
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr) {
+  __shared__ int32_t lds[4][2][kSeg];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int C = a.C;
-  const uint64_t low_mask = (1ull << low_bits) - 1ull;
   const int step = VEC4 ? 256 : 64;
-  const int nt = *n_touched;
+  const int nt = ctr->touched;
   const int nsets = 1 << set_bits;
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += gridDim.x * 4) {
+  for (int t = blockIdx.x * 4 + w; t < nt; t += gridDim.x * 4) {
     const long long pix = touched[t];
     int l = 0;
     while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
     const bool acc_lv = (a.acc_mask >> l) & 1;
+    // each set's run in slot order once per pixel (the channel loop reuses it)
     for (int c0 = 0; c0 < C; c0 += step) {
       const int c = c0 + (VEC4 ? lane * 4 : lane);
       const bool live = c < C;
@@ -582,15 +722,16 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
       // set 0 + set 1: the rounding of the sum of two separate backwards
       for (int sidx = 0; sidx < nsets; ++sidx) {
         const long long q = (pix << set_bits) | sidx;
+        const int n = count[q];
+        if (n == 0) continue;
         const int i0 = run_start[q];
-        if (i0 < 0) continue;
-        const int i1 = run_end[q];
-        const int ns = nseg[q];
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ns == 0) {
-          acc = sum_run<VEC4>(a, keys, rec, low_mask, i0, i1, c, live);
+        if (n <= kSeg) {
+          order_run<64>(arrival, i0, n, lane, lds[w][0], lds[w][1]);
+          acc = sum_slots<VEC4>(a, lds[w][1], rec, n, c, live);
         } else if (live) {
           const int f = seg_first[q];
+          const int ns = (n + kSeg - 1) / kSeg;
           for (int j = 0; j < ns; ++j) {
             const float* src = partial + (size_t)(f + j) * C + c;
             if (VEC4) {
@@ -631,25 +772,26 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
 
 // C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
 // once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
-// independent load chains (run bounds -> keys -> records -> grad_out rows)
+// independent load chains (run bounds -> slots -> records -> grad_out rows)
 // in flight per wave instead of one, the same per-pixel order and rounding.
 template <int PPW>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
-    RoiArgs a, PixMap pm, const uint64_t* __restrict__ keys, const Contrib* __restrict__ rec,
-    int low_bits, int set_bits, const int32_t* __restrict__ run_start,
-    const int32_t* __restrict__ run_end, const int32_t* __restrict__ nseg,
+    RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
+    int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched) {
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr) {
   constexpr int C = 256;
   constexpr int LPP = 64 / PPW;     // lanes per pixel
   constexpr int F = C / LPP / 4;    // float4 per lane
-  const int lane = threadIdx.x & 63;
+  __shared__ int32_t lds[4][PPW][2][kSeg];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane / LPP, sub = lane % LPP;
   const int c = sub * 4 * F;  // this lane's channels
-  const uint64_t low_mask = (1ull << low_bits) - 1ull;
-  const int nt = *n_touched;
+  const int nt = ctr->touched;
   const int nsets = 1 << set_bits;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int32_t* lin = lds[w][grp][0];
+  int32_t* lout = lds[w][grp][1];
+  const int wave = blockIdx.x * 4 + w;
   for (int tb = wave * PPW; tb < nt; tb += gridDim.x * 4 * PPW) {
     const int t = tb + grp;
     if (t >= nt) continue;
@@ -661,17 +803,17 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     bool any = false;
     for (int sidx = 0; sidx < nsets; ++sidx) {
       const long long q = (pix << set_bits) | sidx;
+      const int n = count[q];
+      if (n == 0) continue;
       const int i0 = run_start[q];
-      if (i0 < 0) continue;
-      const int i1 = run_end[q];
-      const int ns = nseg[q];
       float4 acc[F];
 #pragma unroll
       for (int k = 0; k < F; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ns == 0) {
-        for (int i = i0; i < i1; ++i) {
-          const uint64_t slot = keys[i] & low_mask;
-          const int corner = (int)(slot & 3u);
+      if (n <= kSeg) {
+        order_run<LPP>(arrival, i0, n, sub, lin, lout);
+        for (int i = 0; i < n; ++i) {
+          const int slot = lout[i];
+          const int corner = slot & 3;
           const Contrib e = rec[slot >> 2];
           const float4* src =
               reinterpret_cast<const float4*>(a.gout_s[e.set] + (size_t)e.row * C + c);
@@ -692,6 +834,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
         }
       } else {
         const int f = seg_first[q];
+        const int ns = (n + kSeg - 1) / kSeg;
         for (int j = 0; j < ns; ++j) {
           const float4* src = reinterpret_cast<const float4*>(partial + (size_t)(f + j) * C + c);
 #pragma unroll
@@ -830,15 +973,9 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
 namespace d2mi {
 namespace {
 
-int bits_for(unsigned long long v) {  // smallest b with 2^b > v
-  int b = 0;
-  while (b < 64 && (v >> b) != 0) ++b;
-  return b;
-}
-
 struct BwdPlan {
-  long long total_pixels, pairs, n_keys, n_samples, max_segs, max_touched;
-  int low_bits, end_bit, set_bits;
+  long long total_pixels, pairs, n_keys, n_samples, max_segs, max_touched, max_tasks;
+  int set_bits;
   PixMap pm;
 };
 
@@ -857,12 +994,11 @@ int bwd_plan_n(const int32_t* dims, int num_levels, long long n_samples, int set
   p->pm.base[num_levels] = t;
   p->total_pixels = t;
   p->pairs = t << set_bits;
-  // every split run has > kSeg contributions: segments <= 2 * n / kSeg
+  // every split run has > kSeg contributions: segments <= 2 * n / kSeg, and
+  // long-sort tasks <= n / kLongTask + (number of long runs)
   p->max_segs = 2 * (p->n_keys / kSeg) + 1;
+  p->max_tasks = p->n_keys / kLongTask + p->n_keys / (kSeg + 1) + 2;
   p->max_touched = std::min(p->n_keys, t);
-  p->low_bits = max(1, bits_for(p->n_keys > 0 ? (unsigned long long)(p->n_keys - 1) : 0ull));
-  p->end_bit = p->low_bits + set_bits + bits_for((unsigned long long)t);
-  D2MI_REQUIRE(p->end_bit <= 64, "ROIAlign backward key space too large (%d bits)", p->end_bit);
   D2MI_REQUIRE(p->n_keys < (1LL << 31) && p->pairs < (1LL << 31), "ROIAlign backward too large");
   return 0;
 }
@@ -875,18 +1011,18 @@ int bwd_plan(const int32_t* dims, int num_levels, int R, int out_h, int out_w, i
 
 template <class WS>
 void bwd_layout(WS& w, int C, const BwdPlan& p) {
-  w.template take<uint64_t>((size_t)p.n_keys + 1);          // keys
-  w.template take<uint64_t>((size_t)p.n_keys + 1);          // sorted keys
+  w.template take<uint64_t>((size_t)p.n_keys + 1);          // ent: pair << 32 | arrival rank
+  w.template take<int32_t>((size_t)p.n_keys + 1);           // arrival-ordered slots
+  w.template take<int32_t>((size_t)p.n_keys + 1);           // long runs in slot order
   w.template take<Contrib>((size_t)p.n_samples + 1);        // records
+  w.template take<int32_t>((size_t)p.pairs + 1);            // count
   w.template take<int32_t>((size_t)p.pairs + 1);            // run_start
-  w.template take<int32_t>((size_t)p.pairs + 1);            // run_end
-  w.template take<int32_t>((size_t)p.pairs + 1);            // nseg
   w.template take<int32_t>((size_t)p.pairs + 1);            // seg_first
   w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
   w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
-  w.template take<int32_t>(2);                              // their count, segment count
-  w.template take<char>(radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit));
+  w.template take<int2>((size_t)p.max_tasks);               // long-sort tasks
+  w.template take<BwdCounters>(1);
 }
 
 // The backward over nsets (1 or 2) ROI sets of the same maps; sets[k] holds
@@ -913,21 +1049,18 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                "ROIAlign backward workspace too small: %zu < %zu", workspace_bytes, z.off);
   if (p.total_pixels == 0) return 0;
   Workspace w(workspace, workspace_bytes);
-  uint64_t* keys = w.take<uint64_t>((size_t)p.n_keys + 1);
-  uint64_t* sorted = w.take<uint64_t>((size_t)p.n_keys + 1);
+  uint64_t* ent = w.take<uint64_t>((size_t)p.n_keys + 1);
+  int32_t* arrival = w.take<int32_t>((size_t)p.n_keys + 1);
+  int32_t* sorted_long = w.take<int32_t>((size_t)p.n_keys + 1);
   Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
+  int32_t* count = w.take<int32_t>((size_t)p.pairs + 1);
   int32_t* run_start = w.take<int32_t>((size_t)p.pairs + 1);
-  int32_t* run_end = w.take<int32_t>((size_t)p.pairs + 1);
-  int32_t* nseg = w.take<int32_t>((size_t)p.pairs + 1);
   int32_t* seg_first = w.take<int32_t>((size_t)p.pairs + 1);
   int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
   float* partial = w.take<float>((size_t)p.max_segs * C);
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
-  int32_t* n_touched = w.take<int32_t>(2);  // [0] touched pixels, [1] segment slots
-  int32_t* n_segs = n_touched + 1;
-  const size_t tmp_bytes = radix_sort_u64_workspace_size((size_t)p.n_keys, p.low_bits, p.end_bit);
-  void* tmp = w.take<char>(tmp_bytes);
-  const long long TQ = p.pairs;
+  int2* tasks = w.take<int2>((size_t)p.max_tasks);
+  BwdCounters* ctr = w.take<BwdCounters>(1);
   ClearList cl = {};
   long long clear_words = 0;
   auto clear = [&](void* ptr, long long words, uint32_t value) {
@@ -940,51 +1073,48 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero (accumulated levels: kept)
     if (!((acc_mask >> l) & 1))
       clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
-  clear(run_start, TQ, 0xffffffffu);
-  clear(n_touched, 2, 0u);
+  clear(count, p.pairs, 0u);
+  clear(ctr, sizeof(BwdCounters) / 4, 0u);
   hipLaunchKernelGGL(roi_bwd_clear_kernel,
                      dim3((unsigned)std::max(1LL, std::min((clear_words / 4 + 255) / 256, 8192LL))),
                      dim3(256), 0, st, cl);
   D2MI_LAUNCH_CHECK();
-  if (p.n_keys > 0) {
-    long long base = 0;
-    for (int k = 0; k < nsets; ++k) {
-      if (ns[k] > 0) {
-        hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((ns[k] + 255) / 256)), dim3(256),
-                           0, st, sets[k], p.pm, p.low_bits, k, sb, base, keys, rec);
-        D2MI_LAUNCH_CHECK();
-      }
-      base += ns[k];
-    }
-    // pair bits only: the sort is stable and the keys are emitted in slot
-    // (TF loop) order, so each (pixel, set) run stays in that order
-    rc = radix_sort_u64(keys, sorted, (size_t)p.n_keys, p.low_bits, p.end_bit, tmp, tmp_bytes,
-                        st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.n_keys + 1023) / 1024)), dim3(1024),
-                       0, st, sorted, p.n_keys, p.low_bits, sb, p.total_pixels, run_start, run_end,
-                       nseg, seg_first, seg_pixel, n_segs, touched, n_touched);
-    D2MI_LAUNCH_CHECK();
-  }
   if (p.n_keys == 0) return 0;
-  // segment partials of the split runs: a grid-stride loop over *n_segs
-  // (usually a handful; bounded by max_segs)
+  long long base = 0;
+  for (int k = 0; k < nsets; ++k) {
+    if (ns[k] > 0) {
+      hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((ns[k] + 255) / 256)), dim3(256), 0,
+                         st, sets[k], p.pm, k, sb, base, count, ent, rec);
+      D2MI_LAUNCH_CHECK();
+    }
+    base += ns[k];
+  }
+  hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.total_pixels + 1023) / 1024)),
+                     dim3(1024), 0, st, count, p.total_pixels, sb, run_start, seg_first, seg_pixel,
+                     tasks, touched, ctr);
+  D2MI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
+                     st, ent, p.n_keys, run_start, arrival);
+  D2MI_LAUNCH_CHECK();
+  // long runs (degenerate piles of boxes) in slot order, then their segment
+  // partials: grid-stride loops over the device-side task / segment counts
+  // (zero in an ordinary step: the launches exit at once)
+  hipLaunchKernelGGL(roi_bwd_long_sort_kernel,
+                     dim3((unsigned)std::max(1LL, std::min<long long>(p.max_tasks, 512LL))),
+                     dim3(1024), 0, st, arrival, count, run_start, tasks, ctr, sorted_long);
+  D2MI_LAUNCH_CHECK();
   const dim3 sgrid((unsigned)std::max(1LL, std::min<long long>((p.max_segs + 3) / 4, 1024LL)));
   if (vec4)
-    hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                       p.low_bits, run_start, run_end, seg_first, seg_pixel, n_segs, partial);
+    hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
+                       count, run_start, seg_first, seg_pixel, ctr, partial);
   else
-    hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted, rec,
-                       p.low_bits, run_start, run_end, seg_first, seg_pixel, n_segs, partial);
+    hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
+                       count, run_start, seg_first, seg_pixel, ctr, partial);
   D2MI_LAUNCH_CHECK();
   // fixed grid (the touched count stays on the device): at most 8192
   // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
   // beyond residency start as earlier ones retire (the kBatch sweep above)
   const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
-#define PIX(V)                                                                            \
-  hipLaunchKernelGGL((roi_bwd_pixel_kernel<V>), grid, dim3(256), 0, st, a, p.pm, sorted, rec, \
-                     p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,  \
-                     n_touched)
   if (vec4 && C == 256) {
     static const int ppw = [] {
       const char* e = getenv("D2MI_ROI_BWD_PPW");
@@ -992,19 +1122,18 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     }();
     const dim3 g4((unsigned)std::max(1LL, std::min((p.max_touched + 4 * ppw - 1) / (4 * ppw), 8192LL)));
     if (ppw == 8)
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, sorted, rec,
-                         p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,
-                         n_touched);
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
+                         sb, count, run_start, seg_first, partial, touched, ctr);
     else
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, sorted, rec,
-                         p.low_bits, sb, run_start, run_end, nseg, seg_first, partial, touched,
-                         n_touched);
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
+                         sb, count, run_start, seg_first, partial, touched, ctr);
   } else if (vec4) {
-    PIX(true);
+    hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
+                       sb, count, run_start, seg_first, partial, touched, ctr);
   } else {
-    PIX(false);
+    hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
+                       sb, count, run_start, seg_first, partial, touched, ctr);
   }
-#undef PIX
   D2MI_LAUNCH_CHECK();
   return 0;
 }

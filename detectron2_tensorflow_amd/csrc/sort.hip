@@ -3,8 +3,6 @@
 // are sorted by a stable counting rank spread over len/64 workgroups per
 // segment (keys staged in LDS, 64 KiB at most); larger capacities fall back
 // to rocPRIM's segmented radix sort.
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "internal.h"
@@ -125,48 +123,6 @@ int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32
                                               (unsigned int)((size_t)S * cap), (unsigned int)S,
                                               (const int*)begin, (const int*)end, 0u, 64u, stream,
                                               false));
-  return 0;
-}
-
-// merge-sort limit 0: onesweep for everything above one block
-using OnesweepSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                      rocprim::default_config, 0>;
-
-size_t radix_sort_u64_workspace_size(size_t n, int begin_bit, int end_bit) {
-  size_t bytes = 0;
-  rocprim::radix_sort_keys<OnesweepSortConfig>((void*)nullptr, bytes, (const uint64_t*)nullptr,
-                                               (uint64_t*)nullptr, n, (unsigned)begin_bit,
-                                               (unsigned)end_bit, (hipStream_t)0, false);
-  return bytes;
-}
-
-int radix_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, size_t n, int begin_bit,
-                   int end_bit, void* ws, size_t ws_bytes, hipStream_t stream) {
-  if (n == 0) return 0;
-  D2MI_REQUIRE(0 <= begin_bit && begin_bit < end_bit && end_bit <= 64, "bad sort bit range [%d, %d)",
-               begin_bit, end_bit);
-  size_t need = radix_sort_u64_workspace_size(n, begin_bit, end_bit);
-  D2MI_REQUIRE(ws_bytes >= need, "radix sort workspace too small (%zu < %zu)", ws_bytes, need);
-  D2MI_HIP(rocprim::radix_sort_keys<OnesweepSortConfig>(ws, need, keys_in, keys_out, n,
-                                                        (unsigned)begin_bit, (unsigned)end_bit,
-                                                        stream, false));
-  return 0;
-}
-
-size_t exclusive_scan_i32_workspace_size(size_t n) {
-  size_t bytes = 0;
-  rocprim::exclusive_scan((void*)nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                          (int32_t)0, n, rocprim::plus<int32_t>(), (hipStream_t)0, false);
-  return bytes;
-}
-
-int exclusive_scan_i32(const int32_t* in, int32_t* out, size_t n, void* ws, size_t ws_bytes,
-                       hipStream_t stream) {
-  if (n == 0) return 0;
-  size_t need = exclusive_scan_i32_workspace_size(n);
-  D2MI_REQUIRE(ws_bytes >= need, "scan workspace too small (%zu < %zu)", ws_bytes, need);
-  D2MI_HIP(rocprim::exclusive_scan(ws, need, in, out, (int32_t)0, n, rocprim::plus<int32_t>(),
-                                   stream, false));
   return 0;
 }
 

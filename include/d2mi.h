@@ -53,7 +53,8 @@ const char* d2mi_last_error(void);
  *                            kernel for KxK convs (Cin % 256 == 0,
  *                            Cout % 128 == 0): 0 off, 1 (default) on;
  *   "conv_epi" D2MI_CONV_EPI split-K partial slabs stored from the MFMA
- *                            accumulators (1) or through the LDS epilogue (0). */
+ *                            accumulators (1, default) or through the LDS
+ *                            epilogue (0). */
 int d2mi_set_tuning(const char* key, int value);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */

@@ -2,14 +2,18 @@
 trace: for the last few sequences (from the grad-map clear to the pixel pass)
 print each kernel's start offset, duration and the gap before it.
 
-    python tools/roi_bwd_timeline.py gpurun_out/prof_roi/<...>_kernel_trace.csv
+    python tools/roi_bwd_timeline.py gpurun_out/prof_roi/<...>_kernel_trace.csv | <rocprofv3 -d dir>
 """
 import csv
+import glob
+import os
 import re
 import sys
 
 
 def main(path, last=4):
+    if os.path.isdir(path):  # a rocprofv3 -d directory: its (first) kernel trace
+        path = sorted(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True))[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     seqs, cur = [], None
     for r in rows:
