@@ -118,6 +118,9 @@ struct ConvArgs {
   int tdH, tdW;
   int dbg;  // ablation bits (D2MI_CONV_DBG, timing experiments only; 0 in production)
   int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
+  // stream-K launch of conv_ws_kernel (plan sk): sk_T = ntiles * nk k-steps
+  // over gridDim.x workgroups; partial slabs [piece][M][Cout]
+  int sk, sk_T, sk_P;
   // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
   // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
   // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
@@ -216,10 +219,11 @@ __device__ __forceinline__ float epilogue(const ConvArgs& a, const Geo& g, float
 template <int WN, int TM, int TN>
 __device__ __forceinline__ void store_outputs(const ConvArgs& a, const Geo& g,
                                               floatx16 (&acc)[TM][TN], int m0,
-                                              int n0, int wr, int wc, int lane, int split) {
+                                              int n0, int wr, int wc, int lane, int split,
+                                              bool part) {
   const int li = lane & 31, lh = lane >> 5;
   // C/D map for 32x32: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const bool simple = a.splits == 1 && !a.topdown && !a.residual && !g.gate;
+  const bool simple = !part && !a.topdown && !a.residual && !g.gate;
   const bool relu = (a.flags & kRelu) != 0;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -241,7 +245,7 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, const Geo& g,
         }
         continue;
       }
-      if (a.splits > 1) {
+      if (part) {
         float* pp =
             a.partial + ((size_t)split * g.pstride + (mb - g.prow0)) * a.Cout + co;
 #pragma unroll
@@ -305,6 +309,30 @@ __device__ __forceinline__ void store_outputs(const ConvArgs& a, const Geo& g,
   }
 }
 
+// Split-K / stream-K partial slab straight from the accumulators (raw sums:
+// the reduce applies the epilogue).  Slab `split`, rows mapped as store_outputs.
+template <int WN, int TM, int TN>
+__device__ __forceinline__ void store_partial(const ConvArgs& a, const Geo& g,
+                                              floatx16 (&acc)[TM][TN], int m0, int n0, int wr,
+                                              int wc, int lane, int split) {
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = n0 + (wc * TN + j) * 32 + li;
+    if (co >= a.Cout) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = m0 + (wr * TM + i) * 32 + 4 * lh;
+      float* pp = a.partial + ((size_t)split * g.pstride + (mb - g.prow0)) * a.Cout + co;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        if (mb + dm < g.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // LDS-staged epilogue (ConvArgs::lds_epi): the accumulators leave through
 // LDS one 32-row slab at a time as row-major float4s, so every store
 // instruction writes whole rows of the tile (BN * 4 bytes) instead of 32-float
@@ -316,14 +344,13 @@ template <int WM, int WN, int TM, int TN, int NT = 256>
 __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& g,
                                                   floatx16 (&acc)[TM][TN],
                                                   int m0, int n0, int wr, int wc, int lane,
-                                                  int split, float* smem) {
+                                                  int split, bool part, float* smem) {
   constexpr int BN = WN * TN * 32;
   constexpr int LS = BN + 4;        // slab row stride (floats)
   constexpr int F4 = BN / 4;        // float4 per tile row
   constexpr int Q = 32 * F4 / NT;   // float4 per thread per slab
   const int tid = threadIdx.x;
   const int li = lane & 31, lh = lane >> 5;
-  const bool part = a.splits > 1;
   float* const dst = part ? a.partial + (size_t)split * g.pstride * a.Cout : g.y;
   const int mrow0 = part ? g.prow0 : 0;
   const bool relu = (a.flags & kRelu) != 0, relu_after = (a.flags & kReluAfterResidual) != 0;
@@ -666,11 +693,22 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // instruction writes two whole 128-B row segments; no LDS round trip and
   // none of its barriers) unless tuning conv_epi = 0
   if (a.splits > 1 && a.reg_partials)
-    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, true);
   else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
-    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, &As[0][0]);
+    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
+                                      &As[0][0]);
   else
-    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1);
+}
+
+// Stream-K partition of T = ntiles * nk k-steps over P workgroups:
+// workgroup b owns [sk_lo(b), sk_lo(b + 1)); sk_wg_of(i) is the workgroup
+// owning iteration i.
+__host__ __device__ __forceinline__ long long sk_lo(long long b, long long P, long long T) {
+  return b * T / P;
+}
+__host__ __device__ __forceinline__ int sk_wg_of(long long i, long long P, long long T) {
+  return (int)(((i + 1) * P - 1) / T);
 }
 
 // Warp-specialised split-product conv: a 256x128 tile, 16 waves (1024
@@ -686,7 +724,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <bool ML, int LD, bool BATCH = true>
+template <bool ML, int LD, bool BATCH = true, bool SK = false>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -695,33 +733,54 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[S * STAGE];
   static_assert(S * STAGE >= 32 * (BN + 4), "LDS epilogue slab does not fit");
 
-  const int orig = blockIdx.x;
-  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  int tile =
-      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-  const Geo g = ML ? select_level(a, tile) : geo_of(a);
-  const int mt = tile / a.nN, nt = tile - mt * a.nN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int split = blockIdx.y;
-  const int kt0 = split * a.kt_per_split;
-  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
-  const int nks = max(kt1 - kt0, 0);
-
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;  // (stagers: wr >= 4, never an acc slab)
 
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // XCD-contiguous order of the workgroup index: consecutive tiles (or
+  // stream-K ranges), which share input halo rows and weight tiles, land on
+  // one XCD's L2.
+  const int orig = blockIdx.x, nwg = gridDim.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int lw = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  // Stream-K (SK, ConvArgs::sk): the workgroup runs iterations [it, it_end)
+  // of the tile-major, k-minor sequence of all ntiles * nk k-steps -- one
+  // piece per tile it touches, each stored raw from the accumulators to
+  // partial slab (its index among the tile's pieces); sk_reduce4_kernel sums
+  // every tile's pieces in k order and applies the epilogue.  Otherwise one
+  // piece: tile lw, split blockIdx.y.  The stagers and the compute waves walk
+  // the same pieces, so their barriers pair up.
+  int it = 0, it_end = 1;
+  if constexpr (SK) {
+    it = (int)sk_lo(lw, nwg, a.sk_T);
+    it_end = (int)sk_lo(lw + 1, nwg, a.sk_T);
+    if (it >= it_end) return;
+  }
+  auto piece = [&](int i, int& tile, int& kt0, int& kt1, int& split) {
+    if constexpr (SK) {
+      tile = i / a.nk;
+      kt0 = i - tile * a.nk;
+      kt1 = min(a.nk, kt0 + (it_end - i));
+      split = lw - sk_wg_of((long long)tile * a.nk, nwg, a.sk_T);
+    } else {
+      tile = a.tile_base + lw;
+      split = blockIdx.y;
+      kt0 = split * a.kt_per_split;
+      kt1 = min(a.nk, kt0 + a.kt_per_split);
+    }
+  };
 
+  floatx16 acc[TM][TN];
   if (wave >= 8) {
     // ------------------------------------------------------------ stagers
+    for (int pit = it;;) {
+    int tile, kt0, kt1, split;
+    piece(pit, tile, kt0, kt1, split);
+    const Geo g = ML ? select_level(a, tile) : geo_of(a);
+    const int mt = tile / a.nN, nt = tile - mt * a.nN;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int nks = max(kt1 - kt0, 0);
     const int st = tid - 512;
     const int srow = st >> 3, schunk = (st & 7) * 4;  // rows srow + 64 p
     int ih0[RA], iw0[RA], base[RA];
@@ -843,8 +902,21 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         __syncthreads();
       }
     }
+    pit += kt1 - kt0;
+    if (!SK || pit >= it_end) break;
+    }  // pieces
   } else {
     // ------------------------------------------------------------ compute
+    for (int pit = it;;) {
+    int tile, kt0, kt1, split;
+    piece(pit, tile, kt0, kt1, split);
+    const int nks = max(kt1 - kt0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int li = lane & 31, lh = lane >> 5;
     const int cdbg = a.dbg;
     bf16x8 fa[3][TM], fb[3][TN];
@@ -944,13 +1016,27 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // B_u
     }
+    if (SK && !(a.dbg & 8)) {
+      const Geo g = ML ? select_level(a, tile) : geo_of(a);
+      const int mt = tile / a.nN, nt = tile - mt * a.nN;
+      store_partial<WN, TM, TN>(a, g, acc, mt * BM, nt * BN, wr, wc, lane, split);
+    }
+    pit += kt1 - kt0;
+    if (!SK || pit >= it_end) break;
+    }  // pieces
   }
-  if (a.dbg & 8) return;  // (ablation: no epilogue)
+  if (SK || (a.dbg & 8)) return;  // (dbg 8: ablation, no epilogue)
+  int tile, kt0, kt1, split;
+  piece(it, tile, kt0, kt1, split);
+  const Geo g = ML ? select_level(a, tile) : geo_of(a);
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
   if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
-    if (wave < 8) store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
     return;
   }
-  store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, smem);
+  store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
+                                          smem);
 }
 
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
@@ -1114,10 +1200,10 @@ __global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
     }
   }
   if (WN * TN * 32 == 128 || a.lds_epi)
-    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split,
+    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                       reinterpret_cast<float*>(&As[0][0]));
   else
-    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1);
 }
 
 // x [n] f32 -> [3][n] bf16 planes (h, m, l of the exact truncation split).
@@ -1166,6 +1252,39 @@ __global__ void splitk_reduce4_kernel(ConvArgs a) {
     const int64_t e = 4 * i;
     const int ml = (int)(e / a.Cout), co = (int)(e - (int64_t)ml * a.Cout);
     const int m = a.m_base + ml;
+    float4 o;
+    o.x = epilogue(a, g, acc.x, m, co);
+    o.y = epilogue(a, g, acc.y, m, co + 1);
+    o.z = epilogue(a, g, acc.z, m, co + 2);
+    o.w = epilogue(a, g, acc.w, m, co + 3);
+    *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
+  }
+}
+
+// Stream-K fix-up (ConvArgs::sk): every output element of a tile that is
+// split over workgroups gets its pieces summed in k order (slab s = the
+// tile's s-th piece; a tile inside one workgroup's range has one), then the
+// epilogue.  float4 over channels (the WS kernel's plans have Cout % 4 == 0).
+__global__ void sk_reduce4_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 128;  // conv_ws_kernel's tile
+  const Geo g = geo_of(a);
+  const int C4 = a.Cout / 4;
+  const int64_t total4 = (int64_t)a.M * C4;
+  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / C4), co = (int)(i - (int64_t)m * C4) * 4;
+    const long long t0 = (long long)((m / BM) * a.nN + co / BN) * a.nk;
+    const int b0 = sk_wg_of(t0, a.sk_P, a.sk_T);
+    const int np = sk_wg_of(t0 + a.nk - 1, a.sk_P, a.sk_T) - b0 + 1;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < np; ++s) {
+      const float4 v = p4[(size_t)s * total4 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
     float4 o;
     o.x = epilogue(a, g, acc.x, m, co);
     o.y = epilogue(a, g, acc.y, m, co + 1);
@@ -1278,6 +1397,9 @@ struct Plan {
   // tail_tiles (whole pixel-row blocks) split K tail_splits ways
   int full_tiles, tail_tiles, tail_splits, tail_kt_per_split;
   int main_m_end;  // output rows of the main launch (its split-K partial rows)
+  // stream-K (cfg 3 only): sk_T = ntiles * nk k-steps over sk_P workgroups,
+  // at most sk_slabs pieces per tile
+  int sk, sk_T, sk_P, sk_slabs;
   size_t ws_bytes;
 };
 
@@ -1372,6 +1494,48 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool spli
       }
     }
   }
+  // Stream-K for the WS kernel (tuning "conv_sk"): when the tile grid leaves
+  // CUs idle -- 132 tiles of a 256-CU chip (res3 3x3, 33,600 pixels x 128) --
+  // every CU takes an equal contiguous range of the ntiles * nk k-steps; the
+  // pieces of every tile are summed in a fixed-order fix-up pass.  Cost model
+  // in microseconds, fitted to tools/ws_ab.py on MI355X: a WS k-step 2.4, the
+  // second piece's pipeline fill 2 k-steps, a reduce launch 3, and each M x
+  // Cout f32 slab written or read at 4 TB/s.  Stream-K only where it wins by
+  // 10 %: the partial traffic of the fix-up (every tile, 3-5 slabs) eats the
+  // balance gain on the short-K 1x1s (tools/sk_ab.sh).  Off by default: the
+  // three shapes it takes run 6-17 % faster alone (res3 3x3 84 -> 70 us), but
+  // the training step ran 0.9 % SLOWER with it (in-process A/B, 8 blocks; the
+  // fix-up's slab traffic displaces neighbouring layers' data from the MALL).
+  p.sk = 0;
+  p.sk_T = p.sk_P = p.sk_slabs = 0;
+  if (p.cfg == 3 && tuning(kTuneConvSK) > 0) {
+    const int P = wg_slots(3);
+    const long long T = (long long)p.ntiles * p.nk;
+    const long long per = T / P;
+    const double kstep = 2.4, slab = (double)M * Cout * 4.0 / 4.0e6;
+    double std_us;
+    if (p.tail_tiles > 0)
+      std_us = ((p.full_tiles / G) * p.nk + p.tail_kt_per_split) * kstep;
+    else
+      std_us = ((p.ntiles * p.splits + G - 1) / G) * p.kt_per_split * kstep;
+    if (p.splits > 1) std_us += 3.0 + (p.splits + 1) * slab;
+    if (per >= 6 && T < (1LL << 31)) {
+      const double pieces = (double)p.nk / (double)per + 1.0;  // per tile, about
+      const double sk_us = ((T + P - 1) / P + 2) * kstep + 3.0 + (pieces + 1.0) * slab;
+      if (sk_us < 0.9 * std_us) {
+        p.sk = 1;
+        p.sk_T = (int)T;
+        p.sk_P = P;
+        p.sk_slabs = (int)std::min<long long>(p.nk, (p.nk + per - 1) / per + 1);
+        p.splits = 1;
+        p.kt_per_split = p.nk;
+        p.full_tiles = p.ntiles;
+        p.tail_tiles = 0;
+        p.main_m_end = M;
+        p.ws_bytes = (size_t)p.sk_slabs * M * Cout * sizeof(float);
+      }
+    }
+  }
   return p;
 }
 
@@ -1441,7 +1605,9 @@ template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
   if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
-    if (ws_depth() == 1)
+    if (a.sk)
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true>), grid, dim3(1024), 0, st, a);
+    else if (ws_depth() == 1)
       hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
     else
       hipLaunchKernelGGL((conv_ws_kernel<false, 2, true>), grid, dim3(1024), 0, st, a);
@@ -1515,7 +1681,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
                      const float* residual, const float* gate, float* y, int N, int H, int W,
                      int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
                      int flags, void* workspace, size_t workspace_bytes, void* stream) {
-  ConvArgs a;
+  ConvArgs a = {};
   a.x = x;
   a.x3 = x3;
   a.w3 = w3;
@@ -1558,6 +1724,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   }
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0 && !x3);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
+    p.sk = 0;
     p.splits = 1;
     p.kt_per_split = p.nk;
     p.full_tiles = p.ntiles;
@@ -1579,6 +1746,10 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.tdW = (a.OW + 1) / 2;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
+  a.sk = p.sk;
+  a.sk_T = p.sk_T;
+  a.sk_P = p.sk_P;
+  if (p.sk) a.partial = (float*)workspace;
   ConvArgs t = a;  // the tail launch (when planned)
   if (p.tail_tiles > 0) {
     t.tile_base = p.full_tiles;
@@ -1598,7 +1769,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   bool db = false;
   if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
   auto launch = [&](const ConvArgs& c) {
-    const dim3 g(c.ntiles, c.splits);
+    const dim3 g(c.sk ? c.sk_P : c.ntiles, c.sk ? 1 : c.splits);
     if (x3)
       launch_x3(p.cfg, db, g, st, c);
     else if (flags & kSplit3)
@@ -1606,7 +1777,11 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     else
       launch_conv<false>(p.cfg, db, g, st, c);
     D2MI_LAUNCH_CHECK();
-    if (c.splits > 1) {
+    if (c.sk) {
+      const int gr = (int)std::min<int64_t>(((int64_t)c.M * Cout / 4 + 255) / 256, 8192);
+      hipLaunchKernelGGL(sk_reduce4_kernel, dim3(gr), dim3(256), 0, st, c);
+      D2MI_LAUNCH_CHECK();
+    } else if (c.splits > 1) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
       if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
         const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);

@@ -15,11 +15,12 @@ __device__ int32_t g_error_word = 0;
 namespace d2mi {
 
 namespace {
-const char* const kTuneNames[kTuneCount] = {"conv_ws", "roi_fwd", "wgrad_ws", "conv_epi"};
+const char* const kTuneNames[kTuneCount] = {"conv_ws", "roi_fwd", "wgrad_ws", "conv_epi",
+                                            "conv_sk"};
 const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS", "D2MI_ROI_FWD", "D2MI_WGRAD_WS",
-                                          "D2MI_CONV_EPI"};
+                                          "D2MI_CONV_EPI", "D2MI_CONV_SK"};
 // defaults: measured per shape and in the training step
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1};
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 0};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

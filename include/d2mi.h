@@ -54,7 +54,10 @@ const char* d2mi_last_error(void);
  *                            Cout % 128 == 0): 0 off, 1 (default) on;
  *   "conv_epi" D2MI_CONV_EPI split-K partial slabs stored from the MFMA
  *                            accumulators (1, default) or through the LDS
- *                            epilogue (0). */
+ *                            epilogue (0);
+ *   "conv_sk"  D2MI_CONV_SK  stream-K plans for the WS conv where its cost
+ *                            model wins (1) or never (0, default: faster per
+ *                            shape, +0.9 % on the training step). */
 int d2mi_set_tuning(const char* key, int value);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */

@@ -574,6 +574,45 @@ def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
         assert es <= 4 * ef + 1e-6, (es, ef)
 
 
+@pytest.mark.parametrize("shape", [
+    (2, 100, 168, 128, 128, 3),  # res3 3x3: 132 tiles of a 256-CU chip
+    (2, 50, 84, 1024, 512, 1),   # res4 -> res5 1x1: 132 tiles
+])
+def test_conv2d_stream_k_matches_split_k(dev, shape):
+    """The WS kernel's stream-K plan (tuning "conv_sk", chosen where the tile
+    grid would leave CUs idle) forms the same products in other K groups:
+    within f32 rounding of the tile-per-workgroup plan, within 1e-4 of float64
+    on a crop, deterministic, and through the fix-up's epilogue (bias,
+    residual, ReLU after the add)."""
+    N, H, W, Cin, Cout, k = shape
+    pad = (k - 1) // 2
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
+    b = torch.randn(Cout, generator=g)
+    res = torch.randn(N, H, W, Cout, generator=g)
+    wp = ops().pack_conv_weights(w.to(dev))
+    kw = dict(relu=True, residual=res.to(dev), relu_after_add=True)
+    run = lambda: ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), 1, (pad, pad), math_mode="split", **kw)
+    try:
+        ops().set_tuning("conv_sk", 0)
+        y0 = run()
+        ops().set_tuning("conv_sk", 1)
+        y1, y2 = run(), run()
+    finally:
+        ops().set_tuning("conv_sk", 0)  # the default
+    assert torch.equal(y1, y2)
+    np.testing.assert_allclose(y1.cpu().numpy(), y0.cpu().numpy(), rtol=2e-5, atol=2e-5)
+    # float64 on the first image's first 8 output rows (input rows 0..8 + pad)
+    rows = 8
+    xc = x[:1, :rows + k - 1 - pad].permute(0, 3, 1, 2).double()
+    ref = torch.nn.functional.conv2d(xc, w.permute(3, 2, 0, 1).double(), b.double(),
+                                     padding=pad).permute(0, 2, 3, 1)[:, :rows]
+    want = torch.relu(ref + res[:1, :rows].double())
+    np.testing.assert_allclose(y1[:1, :rows].cpu().double().numpy(), want.numpy(), rtol=1e-4,
+                               atol=1e-4)
+
+
 def test_split_bf16x3_is_exact(dev):
     """h + m + l == x bit for bit (evaluated in float64), each term a bf16.
     Exact wherever the residuals stay normal f32 (|x| >= 2^-110 or so); below
