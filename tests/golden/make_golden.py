@@ -39,6 +39,12 @@ multiclass_nms_golden.npz (same loader):
     selected boxes / scores / classes and each one's ROI row (matched back by
     exact box equality: the reference's BoxList drops extra fields).
 
+voc_metrics_golden.npz: the reference's lib/evaluation/metrics.py
+(compute_precision_recall / compute_average_precision, metrics.py:7-95) on
+seeded detections: tie-free scores, bool and weighted-float labels, a class
+with no detections; the file uses np.float / np.bool / np.NAN, which numpy 2
+removed, so those aliases (float, bool, nan) are restored before it loads.
+
     python tests/golden/make_golden.py [/root/reference]
 """
 import importlib.util
@@ -51,6 +57,38 @@ import numpy as np
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "nms_golden.npz")
 OUT_MC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "multiclass_nms_golden.npz")
 OUT_BOX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "box_ops_golden.npz")
+OUT_VOC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "voc_metrics_golden.npz")
+
+
+def load_reference_metrics(ref_root):
+    for name, v in (("float", float), ("bool", bool), ("NAN", np.nan)):
+        if name not in np.__dict__:
+            setattr(np, name, v)
+    spec = importlib.util.spec_from_file_location(
+        "_refmetrics", os.path.join(ref_root, "lib", "evaluation", "metrics.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def voc_metrics_cases(metrics, rng):
+    data, n = {}, 0
+    for size, frac, weighted, extra_gt in [(50, 0.4, False, 5), (400, 0.2, False, 30),
+                                           (1000, 0.6, True, 100), (7, 0.5, False, 0),
+                                           (0, 0.0, False, 12)]:
+        scores = (rng.permutation(size) + rng.uniform(0.1, 0.9, size)) / max(size, 1)
+        labels = rng.uniform(size=size) < frac
+        if weighted:
+            labels = labels * rng.uniform(0.5, 1.0, size)
+        num_gt = int(np.ceil(np.sum(labels))) + extra_gt
+        prec, rec = metrics.compute_precision_recall(scores, labels, num_gt)
+        ap = metrics.compute_average_precision(prec, rec)
+        data.update({f"v{n}_scores": scores, f"v{n}_labels": labels,
+                     f"v{n}_num_gt": np.array(num_gt), f"v{n}_precision": prec,
+                     f"v{n}_recall": rec, f"v{n}_ap": np.array(ap)})
+        n += 1
+    data["num_cases"] = np.array(n)
+    return data
 
 
 def load_reference_np_ops(ref_root):
@@ -209,6 +247,9 @@ def main(ref_root="/root/reference"):
     mc = multiclass_case(mods, np.random.default_rng(20261017))
     np.savez_compressed(OUT_MC, **mc)
     print("wrote", OUT_MC, {k: v.shape for k, v in mc.items()})
+    voc = voc_metrics_cases(load_reference_metrics(ref_root), np.random.default_rng(20261018))
+    np.savez_compressed(OUT_VOC, **voc)
+    print("wrote", OUT_VOC, {k: v.shape for k, v in voc.items()})
 
 
 if __name__ == "__main__":

@@ -235,3 +235,24 @@ def test_fast_rcnn_inference_matches_reference_multiclass_nms():
     np.testing.assert_array_equal(oc[:n], g["mc_sel_classes"])
     np.testing.assert_array_equal(osc[:n], g["mc_sel_scores"])
     np.testing.assert_array_equal(ob[:n], g["mc_sel_boxes"])
+
+
+# ------------------------------------------------ reference-held VOC metrics goldens
+VOC_GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "voc_metrics_golden.npz")
+
+
+def test_voc_metrics_match_reference_metrics():
+    """evaluation/voc_metrics == lib/evaluation/metrics.py:7-95 (the
+    reference's own compute_precision_recall / compute_average_precision,
+    tests/golden/voc_metrics_golden.npz) bit for bit, bool and weighted
+    labels, a class without detections; num_gt == 0 -> (None, None) -> NaN."""
+    from detectron2_tensorflow_amd.evaluation import voc_metrics
+    d = np.load(VOC_GOLDEN)
+    for i in range(int(d["num_cases"])):
+        p, r = voc_metrics.precision_recall(d[f"v{i}_scores"], d[f"v{i}_labels"],
+                                            int(d[f"v{i}_num_gt"]))
+        np.testing.assert_array_equal(p, d[f"v{i}_precision"])
+        np.testing.assert_array_equal(r, d[f"v{i}_recall"])
+        assert voc_metrics.average_precision(p, r) == float(d[f"v{i}_ap"])
+    p, r = voc_metrics.precision_recall(np.array([0.5]), np.array([False]), 0)
+    assert p is None and r is None and math.isnan(voc_metrics.average_precision(p, r))
