@@ -701,7 +701,13 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW, bool split
   // 128 x 128 tiles for 256-wide channels; 64-wide when a dimension is small
   p.TM = Cin > 64 ? 2 : 1;
   p.TN = Cout > 64 ? 2 : 1;
-  p.ws = split3 && tuning(kTuneWgradWS) > 0 && KH * KW > 1 && Cin % 256 == 0 &&
+  // 1x1s (tuning "wgrad_ws1"): only from ~6 GFLOP up -- the smaller ones have
+  // too few 256x128 tiles x 16-chunk splits to fill the chip (tools/wgrad_ws1_ab.sh:
+  // the FPN p2 lateral 165 -> 140 us, the strided shortcuts 8-13 % faster,
+  // the 4.4 GFLOP res4 1x1s 7 % slower)
+  const bool ws1 = KH * KW == 1 && tuning(kTuneWgradWS1) > 0 &&
+                   2.0 * N * OH * OW * (double)Cin * Cout >= 6e9;
+  p.ws = split3 && tuning(kTuneWgradWS) > 0 && (KH * KW > 1 || ws1) && Cin % 256 == 0 &&
          Cout % 128 == 0;
   p.BM = p.ws ? 256 : 64 * p.TM;
   p.BN = 64 * p.TN;
@@ -729,7 +735,12 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW, bool split
   const int G = slots_env > 0 ? slots_env : (p.ws ? 256 : (p.occ3 ? 768 : 512));
   int splits = std::max(1, G / p.ntiles);
   splits = std::min(splits, std::max(1, p.nchunks / minch));
-  splits = std::min(splits, 64);
+  // D2MI_WGRAD_MAXSPLIT: the cap on splits (A/B knob)
+  static const int maxsplit = [] {
+    const char* e = getenv("D2MI_WGRAD_MAXSPLIT");
+    return e && atoi(e) > 0 ? atoi(e) : 128;
+  }();
+  splits = std::min(splits, maxsplit);
   p.chunks_per_split = (p.nchunks + splits - 1) / splits;
   p.splits = (p.nchunks + p.chunks_per_split - 1) / p.chunks_per_split;
   return p;

@@ -57,7 +57,9 @@ const char* d2mi_last_error(void);
  *                            epilogue (0);
  *   "conv_sk"  D2MI_CONV_SK  stream-K plans for the WS conv where its cost
  *                            model wins (1) or never (0, default: faster per
- *                            shape, +0.9 % on the training step). */
+ *                            shape, +0.9 % on the training step);
+ *   "wgrad_ws1" D2MI_WGRAD_WS1 the warp-specialised weight-gradient kernel
+ *                            on 1x1 convs of >= 6 GFLOP too (1, default). */
 int d2mi_set_tuning(const char* key, int value);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */

@@ -784,6 +784,32 @@ def test_conv2d_wgrad_kernel_with_bias(dev, conf, mode):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("conf", [(2, 200, 336, 256, 256, 1, 1), (2, 100, 168, 512, 1024, 1, 2),
+                                  (2, 40, 52, 256, 256, 3, 1)])
+def test_conv2d_wgrad_ws_1x1_vs_float64(dev, conf):
+    """The warp-specialised wgrad kernel on the large 1x1 convs too (tuning
+    "wgrad_ws1", >= 6 GFLOP): vs float64, bias gradient included,
+    deterministic."""
+    N, H, W, Cin, Cout, k, s = conf
+    g = torch.Generator().manual_seed(7 + sum(conf))
+    p = (k - 1) // 2
+    x = torch.randn(N, H, W, Cin, generator=g)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, OH, OW, Cout, generator=g)
+    want = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (Cout, Cin, k, k),
+                                       dy.permute(0, 3, 1, 2).double(), s, p).permute(2, 3, 1, 0)
+    run = lambda: ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True,
+                                     math_mode="split")
+    ops().set_tuning("wgrad_ws1", 1)  # (the default)
+    dw, db = run()
+    dw2, db2 = run()
+    scale = float(want.abs().max())
+    np.testing.assert_allclose(dw.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=2e-5 * scale)
+    np.testing.assert_allclose(db.cpu().double().numpy(), dy.double().sum((0, 1, 2)).numpy(),
+                               rtol=1e-4, atol=1e-3)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_fold_frozen_bn_forward_backward(dev, with_bias):
     g = torch.Generator().manual_seed(5)

@@ -42,13 +42,19 @@ def _conv_sk(on):
     ops.set_tuning("conv_sk", 1 if on else 0)
 
 
+def _wgrad_ws1(on):
+    from detectron2_tensorflow_amd.layers import ops
+    ops.set_tuning("wgrad_ws1", 1 if on else 0)
+
+
 def _conv_epi(on):
     from detectron2_tensorflow_amd.layers import ops
     ops.set_tuning("conv_epi", 1 if on else 0)
 
 
 SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
-            "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk}
+            "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
+            "wgrad_ws1": _wgrad_ws1}
 
 
 def main():

@@ -59,6 +59,35 @@ def main():
     if a.stacks:
         shapes = prof.key_averages(group_by_stack_n=6).table(
             sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=40)
+    if a.stacks:
+        # self device time of the small aten ops (the glue between the d2mi
+        # kernels) by call site: the innermost package frame of the op's
+        # Python stack, else its nearest autograd-node / Python-function
+        # ancestor in the profiler's event tree
+        agg = {}
+        nstack = 0
+        for e in prof.events():
+            if not e.name.startswith("aten::") or e.self_device_time_total <= 0:
+                continue
+            site = None
+            frames = [f for f in (e.stack or []) if "detectron2_tensorflow_amd" in f]
+            if frames:
+                nstack += 1
+                site = frames[0].split("detectron2_tensorflow_amd/")[-1]
+            par = e.cpu_parent
+            while site is None and par is not None:
+                n = par.name
+                if ("Backward" in n or "evaluate_function" in n or ".py(" in n
+                        or n.startswith("_")):
+                    site = n[:90]
+                par = par.cpu_parent
+            k = (e.name, site or "?")
+            t, c = agg.get(k, (0.0, 0))
+            agg[k] = (t + e.self_device_time_total, c + 1)
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][0])[: a.rows]
+        shapes = f"(events with a package stack: {nstack})\n" + "\n".join(
+            f"{t / a.steps:9.1f} us/step {c / a.steps:6.1f} calls  {k[0]:28s} {k[1]}"
+            for k, (t, c) in rows)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"torch_prof_{a.mode}.txt"), "w") as f:
         f.write(table + "\n\n" + shapes)
