@@ -47,6 +47,9 @@ _SIGS = {
     "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
     "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_topk": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, c_size_t, P]),
+    "d2mi_subsample_workspace_size": (c_size_t, [c_int, c_int]),
+    "d2mi_subsample": (c_int, [P, c_int, c_int, ctypes.c_longlong, c_int, c_int, P, P, P, P, P,
+                               c_int, P, c_size_t, P]),
     "d2mi_grid_anchors": (c_int, [c_int, c_int, c_float, P, c_int, P, P]),
     "d2mi_apply_deltas": (c_int, [P, P, c_int, c_int, P, c_float, P, P]),
     "d2mi_rpn_proposals_workspace_size": (c_size_t, [c_int, c_int, P, c_int, c_int, c_int]),
@@ -117,6 +120,7 @@ _SIGS = {
     "d2mi_match_boxes": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_float,
                                  c_float, P, P, P, c_size_t, P]),
     "d2mi_stem_pool": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_stem_conv": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "d2mi_rpn_loss_blocks": (c_int, []),
     "d2mi_rpn_loss_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P]),
     "d2mi_rpn_loss_bwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P, P,

@@ -421,6 +421,34 @@ def topk_segments(values, seg_start, seg_len, k, max_seg_len, sigmoid=False):
     return vals[:, :k], idx[:, :k], cnt
 
 
+def subsample(labels, num_samples, num_pos, bg_label, seed, order_slots=0):
+    """d2mi_subsample: (pos, neg) [N, P] bool -- a uniformly random
+    min(num_pos, #pos) positives and min(num_samples - that, #neg) negatives
+    per row (labels int64: -1 ignore, bg_label negative, else positive);
+    with order_slots = S also (order [N, S] int64, valid [N, S] bool): the
+    selected indices positives first, each kind in index order.  seed: a
+    device int64 tensor [1]."""
+    labels = labels.to(torch.int64).contiguous()
+    _C.require_device(labels, seed)
+    N, P = labels.shape
+    dev = labels.device
+    pos = torch.empty((N, P), dtype=torch.uint8, device=dev)
+    neg = torch.empty((N, P), dtype=torch.uint8, device=dev)
+    S = int(order_slots)
+    order = torch.empty((N, S), dtype=torch.int64, device=dev) if S else None
+    valid = torch.empty((N, S), dtype=torch.uint8, device=dev) if S else None
+    wsb = _C.lib().d2mi_subsample_workspace_size(N, P)
+    ws = _C.workspace(wsb, dev)
+    rc = _C.lib().d2mi_subsample(_C.ptr(labels), N, P, int(bg_label), int(num_samples),
+                                 int(num_pos), _C.ptr(seed), _C.ptr(pos), _C.ptr(neg),
+                                 _C.ptr(order), _C.ptr(valid), S, _C.ptr(ws), wsb,
+                                 _C.stream_of(dev))
+    _C.check(rc, "d2mi_subsample")
+    if S:
+        return pos.bool(), neg.bool(), order, valid.bool()
+    return pos.bool(), neg.bool()
+
+
 # ------------------------------------------------------------ anchors/deltas
 def grid_anchors(H, W, stride, cell_anchors, device):
     """DefaultAnchorGenerator.grid_anchors for one level -> [H*W*A, 4]."""
@@ -935,6 +963,33 @@ def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, 
                             tuple(weights), float(beta))
 
 
+def stem_conv_weights(w):
+    """HWIO [7, 7, 3, Cout=64] -> the [3][64][160] bf16 planes d2mi_stem_conv
+    takes (K = (kh * 7 + kw) * 3 + c, zero-padded to 160)."""
+    if tuple(w.shape) != (7, 7, 3, 64):
+        raise ValueError(f"stem conv weights must be [7, 7, 3, 64], got {tuple(w.shape)}")
+    wt = torch.zeros((64, 160), dtype=torch.float32, device=w.device)
+    wt[:, :147] = _f32c(w).reshape(147, 64).t()
+    return split_bf16x3(wt.contiguous())
+
+
+def stem_conv(x, w3):
+    """d2mi_stem_conv: the 7x7 / stride-2 stem conv (Cin 3 -> 64, pad 3) on
+    the split-bf16 MFMA; x [N, H, W, 3] NHWC, w3 from stem_conv_weights.
+    Raw sums (the folded shift is stem_pool's); no gradient."""
+    x = _f32c(x)
+    _C.require_device(x, w3)
+    N, H, W, C = x.shape
+    if C != 3:
+        raise ValueError(f"stem conv takes 3 input channels, got {C}")
+    y = torch.empty((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64), dtype=torch.float32,
+                    device=x.device)
+    rc = _C.lib().d2mi_stem_conv(_C.ptr(x), _C.ptr(w3), N, H, W, _C.ptr(y),
+                                 _C.stream_of(x.device))
+    _C.check(rc, "d2mi_stem_conv")
+    return y
+
+
 def stem_pool(y, shift=None):
     """relu(y + shift) -> zero pad 1 -> 3x3 / 2 VALID max pool, NHWC
     (d2mi_stem_pool): the ResNet stem tail in one pass (no gradient)."""
@@ -1346,14 +1401,32 @@ def solo_inference(cate_logits, kernels, mask_features, strides, out_hw, score_t
 
 
 # ------------------------------------------------------- fused post-processing
+# host copies of the cell anchors (constant buffers, often on the GPU: one
+# read per element was ~60 device-to-host syncs per training step)
+_CELLS = {}
+
+
+def _cell_host_array(cell_anchors):
+    key = tuple((c.data_ptr(), c._version, tuple(c.shape), str(c.device)) if torch.is_tensor(c)
+                else tuple(np.asarray(c, np.float32).reshape(-1).tolist()) for c in cell_anchors)
+    got = _CELLS.get(key)
+    if got is None:
+        cells = torch.cat([torch.as_tensor(c, dtype=torch.float32).reshape(-1).cpu()
+                           for c in cell_anchors]).tolist()
+        got = (_C.host_array(_C.c_float, cells), len(cells))
+        if len(_CELLS) > 64:
+            _CELLS.clear()
+        _CELLS[key] = got
+    return got
+
+
 def _level_arrays(tensors, hw, strides, cell_anchors):
     L = len(tensors)
     ptrs = _C.host_array(_C.c_void_p, [t.data_ptr() for t in tensors])
     lhw = _C.host_array(_C.ctypes.c_int32, [v for h, w in hw for v in (int(h), int(w))])
     st = _C.host_array(_C.c_float, [float(s) for s in strides])
-    cells = [float(v) for c in cell_anchors for v in torch.as_tensor(c, dtype=torch.float32).reshape(-1)]
-    A = len(cells) // (4 * L)
-    return ptrs, lhw, st, _C.host_array(_C.c_float, cells), A
+    cells, n = _cell_host_array(cell_anchors)
+    return ptrs, lhw, st, cells, n // (4 * L)
 
 
 def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk, post_nms_topk,

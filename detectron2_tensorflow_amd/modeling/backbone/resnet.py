@@ -93,13 +93,24 @@ class Stem(Layer):
         return (x.is_cuda and not needs_grad and is_relu(c.act_fn) and c.padding == "SAME"
                 and c.rate == 1 and c.num_groups == 1 and c.out_channels % 4 == 0)
 
+    # the frozen stem's conv on the split-bf16 MFMA stem kernel (d2mi_stem_conv;
+    # False: MIOpen, the A/B arm)
+    MFMA_CONV = True
+
     def call(self, x):
         if self._fused_ok(x):
-            # frozen stem: MIOpen conv without its bias, then relu(+ shift),
+            # frozen stem: the 7x7 conv without its bias, then relu(+ shift),
             # the zero pad and the 3x3/2 pool in one HIP pass (ops.stem_pool)
             c = self.conv1
             w, b, norm, _ = c.effective_params()
             if norm is None:
+                if (self.MFMA_CONV and tuple(w.shape) == (7, 7, 3, 64) and c.stride == 2
+                        and x.shape[-1] == 3):
+                    key = c._param_key()  # (the fold is cached on the same versions)
+                    if getattr(self, "_w3_key", None) != key:
+                        self._w3 = ops.stem_conv_weights(w)
+                        self._w3_key = key
+                    return ops.stem_pool(ops.stem_conv(x, self._w3), b)
                 p = (c.kernel_size - 1) // 2
                 y = F.conv2d(x.permute(0, 3, 1, 2),
                              w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last),

@@ -24,6 +24,10 @@ from ...layers import Layer
 
 ROI_HEADS_REGISTRY = Registry("ROI_HEADS")
 
+# GPU: the sampled ROI batch in fg-first order straight from the fused
+# sampler (d2mi_subsample order output) instead of a key sort (A/B switch)
+FUSED_ORDER = True
+
 
 def build_roi_heads(cfg, input_shape, **kwargs):
     return ROI_HEADS_REGISTRY.get(cfg.MODEL.ROI_HEADS.NAME)(cfg, input_shape, **kwargs)
@@ -76,17 +80,21 @@ class ROIHeads(Layer):
                                  torch.where(labels == 0, torch.full_like(gcls, K),
                                              torch.full_like(gcls, -1)))
         gt_classes = torch.where(pvalid, gt_classes, torch.full_like(gt_classes, -1))
-        pos, neg = subsample_labels(gt_classes, self.batch_size_per_image,
-                                    self.positive_sample_fraction, K)
         S = self.batch_size_per_image
-        ar = torch.arange(M, device=boxes.device)
-        key = torch.where(pos, 0, torch.where(neg, 1, 2)) * M + ar
-        if M < S:
-            key = torch.cat([key, torch.full((N, S - M), 3 * M, dtype=key.dtype,
-                                             device=key.device)], dim=1)
-        key = key.sort(dim=1).values[:, :S]
-        valid = key < 2 * M
-        order = torch.where(valid, key % M, torch.zeros_like(key))
+        if boxes.is_cuda and FUSED_ORDER:
+            # fused: the sampled rows come back in fg-first, index order
+            _, _, order, valid = subsample_labels(gt_classes, S, self.positive_sample_fraction, K,
+                                                  order_slots=S)
+        else:
+            pos, neg = subsample_labels(gt_classes, S, self.positive_sample_fraction, K)
+            ar = torch.arange(M, device=boxes.device)
+            key = torch.where(pos, 0, torch.where(neg, 1, 2)) * M + ar
+            if M < S:
+                key = torch.cat([key, torch.full((N, S - M), 3 * M, dtype=key.dtype,
+                                                 device=key.device)], dim=1)
+            key = key.sort(dim=1).values[:, :S]
+            valid = key < 2 * M
+            order = torch.where(valid, key % M, torch.zeros_like(key))
         take = lambda t: torch.gather(t, 1, order)
         take4 = lambda t: torch.gather(t, 1, order[..., None].expand(-1, -1, 4))
         gidx = take(matches)

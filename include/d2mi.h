@@ -178,6 +178,23 @@ int d2mi_topk(const float* values, const int64_t* seg_start, const int32_t* seg_
               int32_t* idx_out, int32_t* count_out, void* workspace, size_t workspace_bytes,
               void* stream);
 
+/* ---------------------------------------------------------- subsampling
+ * subsample_labels (lib/modeling/sampling.py, called at rpn_outputs.py:278-283
+ * and roi_heads.py:160-216) over labels [N, P] int64: pos_out / neg_out [N, P]
+ * (uint8) mark a uniformly random min(num_pos, #positive) of the positives
+ * (label not -1 and not bg_label) and min(num_samples - that, #negative) of
+ * the negatives (label == bg_label).  The draw: each element's rank among its
+ * kind through a keyed pseudo-random bijection of [0, n), kept iff < k (the
+ * reference shuffles and takes the first k: the same distribution, another
+ * stream); seed [1] int64 on the device.  order_out [N, S] (nullable, with
+ * order_valid [N, S] uint8): the selected indices positives first, each kind
+ * in index order, then 0 / invalid -- the ROI heads' fg-first batch. */
+size_t d2mi_subsample_workspace_size(int N, int P);
+int d2mi_subsample(const int64_t* labels, int N, int P, long long bg_label, int num_samples,
+                   int num_pos, const int64_t* seed, uint8_t* pos_out, uint8_t* neg_out,
+                   int64_t* order_out, uint8_t* order_valid, int S, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
 /* -------------------------------------------------------- anchors/deltas
  * DefaultAnchorGenerator.grid_anchors for one level (anchor_generator.py:92-109):
  * out[(h*W + w)*A + a] = cell[a] + (h*stride, w*stride, h*stride, w*stride). */
@@ -642,6 +659,16 @@ int d2mi_mask_loss_bwd(const float* logits, const float* target, const long long
  * the stem conv (without its bias); out [N,(H-1)/2+1,(W-1)/2+1,C].  shift
  * [C] nullable; C % 4 == 0; 16-B aligned. */
 int d2mi_stem_pool(const float* y, const float* shift, int N, int H, int W, int C, float* out,
+                   void* stream);
+/* The stem conv feeding it: 7x7 / stride 2, Cin 3 -> Cout 64, the symmetric
+ * pad of 3 then VALID of lib/layers/convolutional.py:12-24 (fix_padding) and
+ * resnet.py Stem.conv1, on the split-bf16 MFMA (f32-class).  x [N,H,W,3]
+ * NHWC f32; w3 [3][64][160] bf16 planes (d2mi_split_bf16x3) of the weights
+ * transposed to [Cout][K] (K = (kh * 7 + kw) * 3 + c, HWIO order) and
+ * zero-padded to K = 160; y [N,(H-1)/2+1,(W-1)/2+1,64] the raw sums (no bias:
+ * d2mi_stem_pool adds the folded shift).  Replaces the MIOpen conv of the
+ * frozen stem. */
+int d2mi_stem_conv(const float* x, const uint16_t* w3, int N, int H, int W, float* y,
                    void* stream);
 
 /* ------------------------------------------------ resampling gradients

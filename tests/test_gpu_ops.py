@@ -1219,8 +1219,10 @@ def test_sampling_smallest_keys_on_hip_topk(dev):
 
 
 def test_fused_stem_pool_matches_unfused(dev):
-    """The frozen stem (MIOpen conv + d2mi_stem_pool: relu(+shift), zero pad,
-    3x3/2 VALID pool) equals conv + ReLU + F.pad + max_pool2d bit for bit."""
+    """The frozen stem's tail (d2mi_stem_pool: relu(+shift), zero pad, 3x3/2
+    VALID pool, here after its MIOpen-conv arm) equals conv + ReLU + F.pad +
+    max_pool2d bit for bit (the MFMA conv arm: test_stem_conv_mfma_vs_float64
+    and test_stem_mfma_conv_matches_miopen_stem)."""
     from detectron2_tensorflow_amd.layers import BatchNorm
     from detectron2_tensorflow_amd.modeling.backbone.resnet import Stem
     from detectron2_tensorflow_amd.utils.arg_scope import arg_scope
@@ -1238,6 +1240,7 @@ def test_fused_stem_pool_matches_unfused(dev):
     x = torch.randn(2, 101, 134, 3, device=dev) * 50
     with torch.no_grad():
         assert stem._fused_ok(x)
+        stem.MFMA_CONV = False  # the MIOpen arm: the same conv as the unfused path
         got = stem(x)
         stem._fused_ok = lambda x: False
         want = stem(x)
@@ -1351,3 +1354,98 @@ def test_pack_weights_many_and_pack_group(dev):
     assert convs[2]._packed is kept
     for c in convs:
         assert torch.equal(c._packed, ops().pack_conv_weights(c.weights.detach()))
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 37, 53), (2, 800, 1344)])
+def test_stem_conv_mfma_vs_float64(dev, shape):
+    """d2mi_stem_conv (the frozen stem's 7x7 / stride-2 conv, Cin 3 -> 64,
+    fix_padding's symmetric pad 3) on the split-bf16 MFMA vs float64, odd
+    sizes (partial 128-pixel tiles, bottom / right padding) and the bench
+    geometry; then the whole Stem (conv + shift + ReLU + pad + pool) against
+    its MIOpen arm."""
+    N, H, W = shape
+    g = torch.Generator().manual_seed(H + W)
+    x = torch.randn(N, H, W, 3, generator=g) * 50.0
+    w = torch.randn(7, 7, 3, 64, generator=g) / math.sqrt(147.0)
+    y = ops().stem_conv(x.to(dev), ops().stem_conv_weights(w.to(dev)))
+    if N * H * W <= 10000:
+        ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(),
+                                         w.permute(3, 2, 0, 1).double(), stride=2,
+                                         padding=3).permute(0, 2, 3, 1)
+    else:  # the first 4 output rows of image 0 (input rows 0..9 + the top pad)
+        ref = torch.nn.functional.conv2d(x[:1, :10].permute(0, 3, 1, 2).double(),
+                                         w.permute(3, 2, 0, 1).double(), stride=2,
+                                         padding=3).permute(0, 2, 3, 1)[:, :4]
+        y = y[:1, :4]
+    scale = float(ref.abs().max())
+    np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_stem_mfma_conv_matches_miopen_stem(dev):
+    from detectron2_tensorflow_amd.modeling.backbone.resnet import Stem, resnet_arg_scope
+    torch.manual_seed(0)
+    with resnet_arg_scope(True, "FrozenBN"):
+        stem = Stem(3, 64, scope="stem").to(dev)
+    norm = stem.conv1.normalizer_fn  # a non-trivial frozen BN fold
+    with torch.no_grad():
+        for t in (norm.gamma, norm.beta, norm.moving_mean, norm.moving_variance):
+            t.uniform_(0.5, 1.5)
+    for t in stem.parameters():
+        t.requires_grad_(False)
+    x = torch.randn(2, 160, 224, 3, device=dev) * 50.0
+    with torch.no_grad():
+        Stem.MFMA_CONV = True
+        a = stem(x)
+        Stem.MFMA_CONV = False
+        b = stem(x)
+        Stem.MFMA_CONV = True
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4,
+                               atol=1e-5 * float(b.abs().max()))
+
+
+def test_fused_subsample_counts_order_and_uniformity(dev):
+    """d2mi_subsample (the fused subsample_labels): exact counts
+    min(num_pos, #pos) / min(num_samples - that, #neg) inside the masks, the
+    fg-first index order, determinism per seed, every element drawn with
+    probability k / n (binomial bound over 400 seeds), and all kept when they
+    fit."""
+    g = torch.Generator().manual_seed(3)
+    N, P, S, num_pos, bg = 3, 5000, 512, 128, 80
+    lab = torch.randint(-1, 81, (N, P), generator=g)
+    lab[1] = torch.where(torch.rand(P, generator=g) < 0.995, torch.full((P,), bg), lab[1])
+    lab[2, :] = -1
+    lab[2, :40] = 3
+    lab[2, 40:100] = bg  # fewer than S candidates: everything kept
+    lab = lab.to(dev)
+    seed = torch.tensor([12345], dtype=torch.int64, device=dev)
+    pos, neg, order, valid = ops().subsample(lab, S, num_pos, bg, seed, order_slots=S)
+    pos2, neg2 = ops().subsample(lab, S, num_pos, bg, seed)
+    assert torch.equal(pos, pos2) and torch.equal(neg, neg2)
+    lc = lab.cpu()
+    for r in range(N):
+        ispos = (lc[r] != -1) & (lc[r] != bg)
+        isneg = lc[r] == bg
+        p, q = pos[r].cpu(), neg[r].cpu()
+        assert not (p & ~ispos).any() and not (q & ~isneg).any()
+        kp = min(num_pos, int(ispos.sum()))
+        assert int(p.sum()) == kp
+        assert int(q.sum()) == min(S - kp, int(isneg.sum()))
+        want = torch.cat([torch.nonzero(p).flatten(), torch.nonzero(q).flatten()])
+        nv = int(valid[r].sum())
+        assert nv == len(want) and bool(valid[r, :nv].all())
+        assert torch.equal(order[r, :nv].cpu(), want)
+        assert not order[r, nv:].any()
+    assert bool(pos[2, :40].all()) and bool(neg[2, 40:100].all())
+    # uniformity: row 0 positives (k = 128 of n) over 400 seeds
+    ispos0 = ((lc[0] != -1) & (lc[0] != bg)).to(dev)
+    n0 = int(ispos0.sum())
+    hits = torch.zeros(P, device=dev)
+    T = 400
+    for t in range(T):
+        p, _ = ops().subsample(lab[:1], S, num_pos, bg, torch.tensor([t * 7919 + 1], device=dev))
+        hits += p[0].float()
+    f = (hits[ispos0] / T).cpu().numpy()
+    pk = num_pos / n0
+    sd = math.sqrt(pk * (1 - pk) / T)
+    assert abs(f.mean() - pk) < 1e-6 + 1e-3  # exact k per draw
+    assert (np.abs(f - pk) < 6 * sd).mean() > 0.999, (pk, f.min(), f.max())

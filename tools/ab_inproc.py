@@ -47,6 +47,18 @@ def _wgrad_ws1(on):
     ops.set_tuning("wgrad_ws1", 1 if on else 0)
 
 
+def _stem_mfma(on):
+    from detectron2_tensorflow_amd.modeling.backbone.resnet import Stem
+    Stem.MFMA_CONV = on
+
+
+def _fused_sample(on):
+    from detectron2_tensorflow_amd.modeling import matcher
+    from detectron2_tensorflow_amd.modeling.roi_heads import roi_heads
+    matcher.FUSED_SUBSAMPLE = on
+    roi_heads.FUSED_ORDER = on
+
+
 def _conv_epi(on):
     from detectron2_tensorflow_amd.layers import ops
     ops.set_tuning("conv_epi", 1 if on else 0)
@@ -54,7 +66,7 @@ def _conv_epi(on):
 
 SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
-            "wgrad_ws1": _wgrad_ws1}
+            "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
 
 def main():
