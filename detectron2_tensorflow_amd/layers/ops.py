@@ -428,15 +428,17 @@ def subsample(labels, num_samples, num_pos, bg_label, seed, order_slots=0):
     with order_slots = S also (order [N, S] int64, valid [N, S] bool): the
     selected indices positives first, each kind in index order.  seed: a
     device int64 tensor [1]."""
-    labels = labels.to(torch.int64).contiguous()
+    if labels.dtype is not torch.int64 or not labels.is_contiguous():
+        labels = labels.to(torch.int64).contiguous()
     _C.require_device(labels, seed)
     N, P = labels.shape
     dev = labels.device
-    pos = torch.empty((N, P), dtype=torch.uint8, device=dev)
-    neg = torch.empty((N, P), dtype=torch.uint8, device=dev)
+    # bool outputs written directly (one byte, 0 / 1: the kernel's uint8)
+    pos = torch.empty((N, P), dtype=torch.bool, device=dev)
+    neg = torch.empty((N, P), dtype=torch.bool, device=dev)
     S = int(order_slots)
     order = torch.empty((N, S), dtype=torch.int64, device=dev) if S else None
-    valid = torch.empty((N, S), dtype=torch.uint8, device=dev) if S else None
+    valid = torch.empty((N, S), dtype=torch.bool, device=dev) if S else None
     wsb = _C.lib().d2mi_subsample_workspace_size(N, P)
     ws = _C.workspace(wsb, dev)
     rc = _C.lib().d2mi_subsample(_C.ptr(labels), N, P, int(bg_label), int(num_samples),
@@ -445,8 +447,8 @@ def subsample(labels, num_samples, num_pos, bg_label, seed, order_slots=0):
                                  _C.stream_of(dev))
     _C.check(rc, "d2mi_subsample")
     if S:
-        return pos.bool(), neg.bool(), order, valid.bool()
-    return pos.bool(), neg.bool()
+        return pos, neg, order, valid
+    return pos, neg
 
 
 # ------------------------------------------------------------ anchors/deltas
