@@ -23,10 +23,10 @@ import sys
 # OCC, ML>: SPLIT (the sixth argument) tells the split-bf16 kernels from the
 # f32 ones.  ROIAlign backward: its own roi_bwd_* kernels (the clear kernel, one
 # per backward, is the main one: it writes the 183 MB of grad maps at
-# 1333x800) PLUS the rocPRIM onesweep sort it launches, attributed by dispatch
-# order (every dispatch between a roi_bwd_emit kernel and the next
-# roi_bwd_runs kernel), so `traffic` covers the same kernels as the HIP-event
-# time of the backward.
+# 1333x800) PLUS anything dispatched between a roi_bwd_emit kernel and the
+# next roi_bwd_runs kernel (r1/r2: the rocPRIM sort; since the r3 counting
+# sort nothing), so `traffic` covers the same kernels as the HIP-event time of
+# the backward.
 SPLIT_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), true"
 F32_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), false"
 GROUPS = {
