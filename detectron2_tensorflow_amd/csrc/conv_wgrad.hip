@@ -44,7 +44,30 @@ struct WgradArgs {
   // set 1.9 % faster in total (FPN p2 3x3 1025 -> 1008 us, res5 3x3 97 -> 92),
   // the training bench +1.4 % (89.6 -> 90.9 img/s, two alternating pairs).
   int prio;
+  // tuning "wgrad_xcd" (default 1): the (tile, split) grid walked in an
+  // XCD-contiguous order -- the tiles of one pixel range (its taps and channel
+  // blocks, which read the same x rows and dY chunk) land on one XCD, so the
+  // re-reads meet in that XCD's L2 instead of eight.  Bit-identical (each
+  // workgroup's (tile, split) work is unchanged, only its placement).
+  int xcd;
 };
+
+// (tile, split) of this workgroup: blockIdx as launched, or its XCD-contiguous
+// remap (hardware dispatch puts linear workgroup L on XCD L % 8; logical index
+// l = the L-th of XCD L % 8's contiguous block, tile fastest).
+__device__ __forceinline__ void wgrad_tile_split(const WgradArgs& a, int& tile, int& split) {
+  if (!a.xcd) {
+    tile = blockIdx.x;
+    split = blockIdx.y;
+    return;
+  }
+  const int nwg = gridDim.x * gridDim.y;
+  const int L = blockIdx.x + blockIdx.y * gridDim.x;
+  const int q = nwg / 8, r8 = nwg % 8, x8 = L % 8;
+  const int l = (x8 < r8 ? x8 * (q + 1) : r8 * (q + 1) + (x8 - r8) * q) + L / 8;
+  split = l / gridDim.x;
+  tile = l - split * gridDim.x;
+}
 
 template <int TM, int TN>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
@@ -284,14 +307,14 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_split_kernel(WgradArgs a,
   __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * BN * LDW];
   __shared__ float bred[8][BN];
 
-  const int tile = blockIdx.x;
+  int tile, split;
+  wgrad_tile_split(a, tile, split);
   const int per_tap = a.nCi * a.nCo;
   const int tap = tile / per_tap;
   const int rem = tile - tap * per_tap;
   const int cit = rem / a.nCo, cot = rem - cit * a.nCo;
   const int kh = tap / a.KW, kw = tap - kh * a.KW;
   const int ci0 = cit * BM, co0 = cot * BN;
-  const int split = blockIdx.y;
   const int c_begin = split * a.chunks_per_split;
   const int c_end = min(a.nchunks, c_begin + a.chunks_per_split);
 
@@ -462,14 +485,14 @@ __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, Fas
   __shared__ __attribute__((aligned(16))) uint16_t smem[S * STAGE];
   __shared__ float bred[8][BN];
 
-  const int tile = blockIdx.x;
+  int tile, split;
+  wgrad_tile_split(a, tile, split);
   const int per_tap = a.nCi * a.nCo;
   const int tap = tile / per_tap;
   const int rem = tile - tap * per_tap;
   const int cit = rem / a.nCo, cot = rem - cit * a.nCo;
   const int kh = tap / a.KW, kw = tap - kh * a.KW;
   const int ci0 = cit * BM, co0 = cot * BN;
-  const int split = blockIdx.y;
   const int c_begin = split * a.chunks_per_split;
   const int c_end = min(a.nchunks, c_begin + a.chunks_per_split);
   const int nks = max(c_end - c_begin, 0);
@@ -780,6 +803,7 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
     static const char* e = getenv("D2MI_WGRAD_PRIO");
     a.prio = e ? atoi(e) : 1;
   }
+  a.xcd = tuning(kTuneWgradXCD) > 0 ? 1 : 0;
   a.x = x;
   a.dy = dy;
   a.dw = dw_hwio;

@@ -71,7 +71,9 @@ SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_ac
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--switch", default="fpn_join", choices=sorted(SWITCHES))
+    ap.add_argument("--switch", default="fpn_join",
+                    help="one of %s, or tune:<key>[=on,off] (d2mi_set_tuning values, default 1,0)"
+                    % ", ".join(sorted(SWITCHES)))
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
@@ -86,7 +88,13 @@ def main():
     batch = bench.synthetic_batch(args, dev, 0)
     bench.calibrate_scores(model, batch)
     tr = Trainer(cfg, model)
-    sw = SWITCHES[a.switch]
+    if a.switch.startswith("tune:"):
+        from detectron2_tensorflow_amd.layers import ops
+        key, _, vals = a.switch[5:].partition("=")
+        von, voff = (int(v) for v in (vals or "1,0").split(","))
+        sw = lambda on: ops.set_tuning(key, von if on else voff)  # noqa: E731
+    else:
+        sw = SWITCHES[a.switch]
     for on in (True, False, True):
         sw(on)
         for _ in range(2):
