@@ -121,6 +121,7 @@ struct ConvArgs {
   // stream-K launch of conv_ws_kernel (plan sk): sk_T = ntiles * nk k-steps
   // over gridDim.x workgroups; partial slabs [piece][M][Cout]
   int sk, sk_T, sk_P;
+  int xcd2;  // xcd_tile(): the 2-D XCD-contiguous remap (tuning conv_xcd, default 1)
   // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
   // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
   // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
@@ -417,6 +418,23 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& 
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
+// XCD-contiguous remap of a (tiles x splits) grid: hardware dispatch puts
+// linear workgroup L = x + y * gridDim.x on XCD L % 8; logical index l = the
+// (L / 8)-th of XCD L % 8's contiguous block, tile fastest, so consecutive
+// tiles of one split (which share input rows and the split's weight rows)
+// meet in one XCD's L2.  xcd2 = 0 (tuning conv_xcd = 0, A/B): the 1-D remap of
+// blockIdx.x alone with the split from blockIdx.y (exact XCD placement only
+// when gridDim.x % 8 == 0).  Placement only: outputs are bit-identical.
+__device__ __forceinline__ int xcd_tile(int xcd2, int& split) {
+  const int nx = gridDim.x;
+  const int nwg = xcd2 ? nx * gridDim.y : nx;
+  const int L = xcd2 ? blockIdx.x + blockIdx.y * nx : blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, x8 = L % 8;
+  const int l = (x8 < r8 ? x8 * (q + 1) : r8 * (q + 1) + (x8 - r8) * q) + L / 8;
+  split = xcd2 ? l / nx : blockIdx.y;
+  return xcd2 ? l - split * nx : l;
+}
+
 template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false>
 __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -431,14 +449,11 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 
   // XCD-aware tile order: consecutive tiles (the Cout tiles of one pixel tile
   // and neighbouring pixel tiles, which share input halo rows) land on one XCD.
-  const int orig = blockIdx.x;
-  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  int tile =
-      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  int split;
+  int tile = a.tile_base + xcd_tile(a.xcd2, split);
   const Geo g = ML ? select_level(a, tile) : geo_of(a);  // ML: a multi-level launch
   const int mt = tile / a.nN, nt = tile - mt * a.nN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int split = blockIdx.y;
   const int kt0 = split * a.kt_per_split;
   const int kt1 = min(a.nk, kt0 + a.kt_per_split);
 
@@ -741,9 +756,9 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   // XCD-contiguous order of the workgroup index: consecutive tiles (or
   // stream-K ranges), which share input halo rows and weight tiles, land on
   // one XCD's L2.
-  const int orig = blockIdx.x, nwg = gridDim.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int lw = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int nwg = gridDim.x;
+  int split_xy;
+  const int lw = xcd_tile(SK ? 0 : a.xcd2, split_xy);
   // Stream-K (SK, ConvArgs::sk): the workgroup runs iterations [it, it_end)
   // of the tile-major, k-minor sequence of all ntiles * nk k-steps -- one
   // piece per tile it touches, each stored raw from the accumulators to
@@ -765,7 +780,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       split = lw - sk_wg_of((long long)tile * a.nk, nwg, a.sk_T);
     } else {
       tile = a.tile_base + lw;
-      split = blockIdx.y;
+      split = split_xy;
       kt0 = split * a.kt_per_split;
       kt1 = min(a.nk, kt0 + a.kt_per_split);
     }
@@ -840,10 +855,18 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       }
       uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
       uint16_t* B16 = A16 + 3 * BM * LDSB;
+      // ablation bits 32 / 16: no split VALU for A / B (the high halves
+      // packed, m = l = 0: wrong sums, timing only)
+      auto hi_only = [](const float4 v, uint2& h, uint2& m, uint2& l) {
+        h.x = (__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u);
+        h.y = (__float_as_uint(v.z) >> 16) | (__float_as_uint(v.w) & 0xffff0000u);
+        m = l = make_uint2(0u, 0u);
+      };
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
         uint2 h, m, l;
-        split3(la[p], h, m, l);
+        if (dbg & 32) hi_only(la[p], h, m, l);
+        else split3(la[p], h, m, l);
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&A16[o]) = h;
         *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
@@ -852,7 +875,8 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        split3(lb[p], h, m, l);
+        if (dbg & 16) hi_only(lb[p], h, m, l);
+        else split3(lb[p], h, m, l);
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -1037,6 +1061,223 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                           smem);
+}
+
+// 16-deep LDS images (conv_ws16_kernel): 32-B rows (16 bf16), the two 16-B
+// chunks XOR-swizzled by (row >> 3) & 1.  The ds_read_b128 lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and their +32 twins: 16 rows of
+// one 32-row fragment) pair rows r, r' with r = r' mod 8 and r >> 3 of
+// opposite parity, so every group covers the 16 slots of the 256-B bank row
+// once; a ds_write_b64 group (16 lanes = 4 whole rows) covers 128 B.
+// Conflict-free reads and writes.
+__device__ __forceinline__ int swz16(int row, int elem) {
+  return row * 16 + ((((elem >> 3) ^ (row >> 3)) & 1) << 3) + (elem & 7);
+}
+
+// Warp-specialised split-product conv with a 16-deep, NS-stage LDS ring
+// (tuning conv_ws = 4 / 5 / 6; conv_ws_kernel is the 32-deep two-stage form).
+// Same tile (256 x 128, waves 0-7 compute 64 x 64 each, waves 8-15 stage),
+// same K order and product order -- bit-identical outputs -- but the compute
+// waves never wait for LDS after a barrier: during step u they issue the
+// ds_reads of step u + 1 between the MFMA groups of step u, each plane batch
+// as soon as the step-u MFMAs that read its registers have issued (fa[2] /
+// fb[2] after the l*h, h*l products, fa[1] / fb[1] after m*h, fa[0] / fb[0]
+// after h*h).  That needs step u + 1 complete in LDS one barrier earlier, so
+// the stagers run NS - 1 steps ahead: at iteration u they write step
+// u + NS - 1 into stage (u + NS - 1) % NS, which last held step u - 1 (read
+// during iteration u - 2, complete at barrier u - 2).  NS >= 3; one barrier
+// per 16-deep step.  Stagers: thread st owns rows st / 4 and st / 4 + 128 of
+// A and row st / 4 of B, 4 channels at (st % 4) * 4; a ring of LD steps of
+// global loads in registers.
+template <int NS, int LD>
+__global__ __launch_bounds__(1024, 1) void conv_ws16_kernel(ConvArgs a) {
+  static_assert(NS >= 3, "the read-ahead needs three stages");
+  constexpr int WN = 2, TM = 2, TN = 2;
+  constexpr int BM = 256, BN = 128, RA = 2, RB = 1;
+  constexpr int A_H = 3 * BM * 16, B_H = 3 * BN * 16;  // halfwords per stage
+  constexpr int STAGE = A_H + B_H;                      // 18432 halfwords = 36 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * STAGE];
+  static_assert(NS * STAGE / 2 >= 32 * (BN + 4), "LDS epilogue slab does not fit");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;  // (stagers: wr >= 4, never an acc slab)
+  int split;
+  const int tile = a.tile_base + xcd_tile(a.xcd2, split);
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
+  const int nst = 2 * max(kt1 - kt0, 0);  // 16-deep steps
+  const Geo g = geo_of(a);
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  floatx16 acc[TM][TN];
+  if (wave >= 8) {
+    // ------------------------------------------------------------ stagers
+    const int st = tid - 512;
+    const int srow = st >> 2, schunk = (st & 3) * 4;
+    int ih0[RA], iw0[RA], base[RA];
+#pragma unroll
+    for (int p = 0; p < RA; ++p) {
+      const int m = m0 + srow + 128 * p;
+      const int mm = m < g.M ? m : 0;
+      const int n = mm / (g.OH * g.OW);
+      const int rem = mm - n * g.OH * g.OW;
+      const int oh = rem / g.OW, ow = rem - oh * g.OW;
+      const int ihv = oh * a.stride - a.pad;
+      ih0[p] = m < g.M ? ihv : -(1 << 29);
+      iw0[p] = ow * a.stride - a.pad;
+      base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + schunk;
+    }
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
+    constexpr uint32_t kOOB = 0x80000000u;
+    const int taps = a.KH * a.KW;
+    const int co = n0 + srow;
+    auto load = [&](int v, float4 (&la)[RA], float4 (&lb)[RB]) {
+      const int kt = kt0 + (v >> 1);
+      const int chunk = kt / taps;
+      const int tap = kt - chunk * taps;
+      const int cc = chunk * BK + (v & 1) * 16;
+      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+      const bool cok = cc + schunk < a.Cin;
+      const int toff = (kh * g.W + kw) * a.Cin + cc;
+      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
+      const uint32_t offb = (cok & (co < a.Cout))
+                                ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
+                                : kOOB;
+      lb[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, offb, 0, 0));
+#pragma unroll
+      for (int p = 0; p < RA; ++p) {
+        const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
+                        ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
+        const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
+        la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+      }
+    };
+    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
+      uint16_t* A16 = smem + buf * STAGE;
+      uint16_t* B16 = A16 + A_H;
+#pragma unroll
+      for (int p = 0; p < RA; ++p) {
+        uint2 h, m, l;
+        split3(la[p], h, m, l);
+        const int o = swz16(srow + 128 * p, schunk);
+        *reinterpret_cast<uint2*>(&A16[o]) = h;
+        *reinterpret_cast<uint2*>(&A16[BM * 16 + o]) = m;
+        *reinterpret_cast<uint2*>(&A16[2 * BM * 16 + o]) = l;
+      }
+      uint2 h, m, l;
+      split3(lb[0], h, m, l);
+      const int o = swz16(srow, schunk);
+      *reinterpret_cast<uint2*>(&B16[o]) = h;
+      *reinterpret_cast<uint2*>(&B16[BN * 16 + o]) = m;
+      *reinterpret_cast<uint2*>(&B16[2 * BN * 16 + o]) = l;
+    };
+    // register ring: step v in set v % LD (static indices: loops unrolled by
+    // LD); every load unconditional (steps past the end re-load the last), so
+    // hipcc counts the loads in flight instead of draining them
+    float4 ra[LD][RA], rb[LD][RB];
+    const int vlast = max(nst, 1) - 1;
+    auto vclamp = [&](int v) { return min(v, vlast); };
+#pragma unroll
+    for (int j = 0; j < LD; ++j) load(vclamp(j), ra[j], rb[j]);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) {  // prologue: steps 0 .. NS - 2
+      const int set = s % LD;
+      if (s < nst) write(s, ra[set], rb[set]);
+      load(vclamp(s + LD), ra[set], rb[set]);
+    }
+    __syncthreads();  // B_init
+    int u0 = 0;
+    for (; u0 + LD <= nst; u0 += LD) {
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        const int v = u0 + j + NS - 1;
+        const int set = (j + NS - 1) % LD;
+        if (v < nst) write(v % NS, ra[set], rb[set]);
+        load(vclamp(v + LD), ra[set], rb[set]);
+        __syncthreads();  // B_u
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LD - 1; ++j) {  // the remaining nst % LD iterations
+      if (u0 + j < nst) {
+        const int v = u0 + j + NS - 1;
+        const int set = (j + NS - 1) % LD;
+        if (v < nst) write(v % NS, ra[set], rb[set]);
+        __syncthreads();
+      }
+    }
+  } else {
+    // ------------------------------------------------------------ compute
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int li = lane & 31, lh = lane >> 5;
+    bf16x8 fa[3][TM], fb[3][TN];
+    int ao[TM], bo[TN];  // fragment offsets inside a plane
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ao[i] = swz16((wr * TM + i) * 32 + li, lh * 8);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bo[j] = swz16((wc * TN + j) * 32 + li, lh * 8);
+    auto rd = [&](int buf, int pa, int pb) {
+      const uint16_t* A16 = smem + buf * STAGE;
+      const uint16_t* B16 = A16 + A_H;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[pa][i] = *reinterpret_cast<const bf16x8*>(&A16[pa * BM * 16 + ao[i]]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[pb][j] = *reinterpret_cast<const bf16x8*>(&B16[pb * BN * 16 + bo[j]]);
+    };
+    auto mm1 = [&](int pa, int pb) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
+    };
+    const int prio = a.prio;
+    __syncthreads();  // B_init
+    rd(0, 1, 1);
+    rd(0, 2, 0);
+    rd(0, 0, 2);
+    int nb = 1 % NS;  // the stage of step u + 1
+    for (int u = 0; u < nst; ++u) {
+      if (prio & 1) __builtin_amdgcn_s_setprio(1);
+      // products in the split kernel's order {mm, lh, hl, hm, mh, hh}
+      mm1(1, 1);
+      mm1(2, 0);
+      mm1(0, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(nb, 2, 2);  // fa[2] (last read by l*h) and fb[2] (h*l) are free
+      mm1(0, 1);
+      mm1(1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(nb, 1, 1);  // fb[1] (h*m), fa[1] (m*h)
+      mm1(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(nb, 0, 0);
+      if (prio & 1) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();  // B_u
+      nb = nb + 1 == NS ? 0 : nb + 1;
+    }
+  }
+  if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
+    if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    return;
+  }
+  store_outputs_lds<4, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
+                                         reinterpret_cast<float*>(smem));
 }
 
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
@@ -1607,6 +1848,12 @@ static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvA
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
     if (a.sk)
       hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true>), grid, dim3(1024), 0, st, a);
+    else if (ws_depth() == 4)
+      hipLaunchKernelGGL((conv_ws16_kernel<3, 4>), grid, dim3(1024), 0, st, a);
+    else if (ws_depth() == 5)
+      hipLaunchKernelGGL((conv_ws16_kernel<4, 4>), grid, dim3(1024), 0, st, a);
+    else if (ws_depth() == 6)
+      hipLaunchKernelGGL((conv_ws16_kernel<3, 2>), grid, dim3(1024), 0, st, a);
     else if (ws_depth() == 1)
       hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
     else
@@ -1721,6 +1968,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     static const char* prio = getenv("D2MI_CONV_PRIO");
     a.prio = prio ? atoi(prio) : 5;
     a.reg_partials = tuning(kTuneConvEpi) != 0;
+    a.xcd2 = tuning(kTuneConvXCD) != 0;
   }
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0 && !x3);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K

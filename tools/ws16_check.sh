@@ -15,3 +15,9 @@ grep -v amdgpu.ids gpurun_out/ws16_ab.log | tail -20
 timeout -k 10 300 python -u tools/ab_inproc.py --switch tune:conv_ws=${WS_ON:-4},2 --blocks 6 --steps 10 \
   > gpurun_out/ws16_inproc.log 2>&1 || { tail -20 gpurun_out/ws16_inproc.log; exit 1; }
 tail -1 gpurun_out/ws16_inproc.log
+timeout -k 10 400 python -u tools/ws_ab.py --key conv_xcd --arms 0,1 --set kxk,short_k --iters 20 --rounds 3 \
+  > gpurun_out/conv_xcd_ab.log 2>&1 || { tail -20 gpurun_out/conv_xcd_ab.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/conv_xcd_ab.log | tail -1
+timeout -k 10 300 python -u tools/ab_inproc.py --switch tune:conv_xcd --blocks 6 --steps 10 \
+  > gpurun_out/conv_xcd_inproc.log 2>&1 || { tail -20 gpurun_out/conv_xcd_inproc.log; exit 1; }
+tail -1 gpurun_out/conv_xcd_inproc.log
