@@ -418,6 +418,21 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& 
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
+// Staging registers of one weight-operand row chunk (4 K-elements): f32 to
+// be split, or (BP) its three bf16 planes as loaded.
+template <bool BP>
+struct BReg {
+  float4 v;
+  __device__ static BReg ones() { return BReg{make_float4(1.f, 2.f, 3.f, 4.f)}; }
+};
+template <>
+struct BReg<true> {
+  uint2 h, m, l;
+  __device__ static BReg ones() {
+    return BReg{make_uint2(0x3f80u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u)};
+  }
+};
+
 // XCD-contiguous remap of a (tiles x splits) grid: hardware dispatch puts
 // linear workgroup L = x + y * gridDim.x on XCD L % 8; logical index l = the
 // (L / 8)-th of XCD L % 8's contiguous block, tile fastest, so consecutive
@@ -435,7 +450,8 @@ __device__ __forceinline__ int xcd_tile(int xcd2, int& split) {
   return xcd2 ? l - split * nx : l;
 }
 
-template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false>
+template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false,
+          bool BP = false>
 __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
@@ -493,7 +509,10 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // L2-resident): an activation gather has two compute phases to return, one
   // phase (~0.6 us at 2 workgroups/CU) being below its loaded latency.
   // OCC 3 (three workgroups per CU): a 1-deep activation prefetch (fewer VGPRs)
-  float4 ra[OCC >= 3 ? 1 : 2][RA], rb[RB];
+  float4 ra[OCC >= 3 ? 1 : 2][RA];
+  BReg<BP> rb[RB];  // BP (SPLIT only): the weight tile's bf16 planes as loaded
+  const __amdgpu_buffer_rsrc_t w3rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w3), 0, BP ? 3 * a.w_plane_bytes : 0, 0x00020000);
   // channel-chunk-major, tap-minor K order: consecutive k-steps read the
   // same 32 channels at neighbouring pixels (the 3x3 taps), which are still
   // in L2 (tap-major order re-fetched them Cin/32 steps later)
@@ -524,13 +543,22 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < RB; ++p) {
       const int co = n0 + srow + 32 * p;
-      const uint32_t off = (cok & (co < a.Cout))
-                               ? (uint32_t)((tap * a.Cout + co) * a.Cin + cc + schunk) * 4u
-                               : kOOB;
-      rb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+      const bool bok = cok & (co < a.Cout);
+      const uint32_t e = (uint32_t)((tap * a.Cout + co) * a.Cin + cc + schunk);
+      if constexpr (BP) {
+        const uint32_t off = bok ? e * 2u : kOOB;
+        rb[p].h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 0, 0));
+        rb[p].m = __builtin_bit_cast(
+            uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, a.w_plane_bytes, 0));
+        rb[p].l = __builtin_bit_cast(
+            uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 2 * a.w_plane_bytes, 0));
+      } else {
+        const uint32_t off = bok ? e * 4u : kOOB;
+        rb[p].v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+      }
     }
   };
-  auto store_tile = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
+  auto store_tile = [&](int buf, const float4 (&la)[RA], const BReg<BP> (&lb)[RB]) {
     if constexpr (SPLIT) {
       uint16_t* A16 = reinterpret_cast<uint16_t*>(As[buf]);
       uint16_t* B16 = reinterpret_cast<uint16_t*>(Bs[buf]);
@@ -546,7 +574,13 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        split3(lb[p], h, m, l);
+        if constexpr (BP) {
+          h = lb[p].h;
+          m = lb[p].m;
+          l = lb[p].l;
+        } else {
+          split3(lb[p].v, h, m, l);
+        }
         const int o = swz(srow + 32 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -558,7 +592,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
         *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = la[p];
 #pragma unroll
       for (int p = 0; p < RB; ++p)
-        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = lb[p];
+        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = lb[p].v;
     }
   };
 
@@ -739,7 +773,7 @@ __host__ __device__ __forceinline__ int sk_wg_of(long long i, long long P, long 
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <bool ML, int LD, bool BATCH = true, bool SK = false>
+template <bool ML, int LD, bool BATCH = true, bool SK = false, bool BP = false>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -820,7 +854,13 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // ablation bits (D2MI_CONV_DBG, timing experiments only): 1 = no global
     // loads, 2 = no split / LDS writes (the loaded values kept live)
     const int dbg = a.dbg;
-    auto load = [&](int kt, float4 (&la)[RA], float4 (&lb)[RB]) {
+    // BP: the weight operand arrives as its three exact bf16 planes (a.w3,
+    // [3][taps][Cout][Cin], plane stride a.w_plane_bytes): the stagers copy
+    // them (three 8-B loads per row chunk) instead of loading f32 and
+    // splitting -- a third of their split VALU (tools/ws_ablate3.sh: bit 16)
+    const __amdgpu_buffer_rsrc_t w3rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.w3), 0, BP ? 3 * a.w_plane_bytes : 0, 0x00020000);
+    auto load = [&](int kt, float4 (&la)[RA], BReg<BP> (&lb)[RB]) {
       if (dbg & 1) return;
       const int chunk = kt / taps;
       const int tap = kt - chunk * taps;
@@ -832,10 +872,19 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         const int co = n0 + srow + 64 * p;
-        const uint32_t off = (cok & (co < a.Cout))
-                                 ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
-                                 : kOOB;
-        lb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+        const bool bok = cok & (co < a.Cout);
+        const uint32_t e = (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk);
+        if constexpr (BP) {
+          const uint32_t off = bok ? e * 2u : kOOB;
+          lb[p].h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 0, 0));
+          lb[p].m = __builtin_bit_cast(
+              uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, a.w_plane_bytes, 0));
+          lb[p].l = __builtin_bit_cast(
+              uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 2 * a.w_plane_bytes, 0));
+        } else {
+          const uint32_t off = bok ? e * 4u : kOOB;
+          lb[p].v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+        }
       }
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
@@ -845,12 +894,10 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
       }
     };
-    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
+    auto write = [&](int buf, const float4 (&la)[RA], const BReg<BP> (&lb)[RB]) {
       if (dbg & 2) {
 #pragma unroll
         for (int p = 0; p < RA; ++p) asm volatile("" ::"v"(la[p].x));
-#pragma unroll
-        for (int p = 0; p < RB; ++p) asm volatile("" ::"v"(lb[p].x));
         return;
       }
       uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
@@ -875,8 +922,15 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        if (dbg & 16) hi_only(lb[p], h, m, l);
-        else split3(lb[p], h, m, l);
+        if constexpr (BP) {
+          h = lb[p].h;
+          m = lb[p].m;
+          l = lb[p].l;
+        } else if (dbg & 16) {
+          hi_only(lb[p].v, h, m, l);
+        } else {
+          split3(lb[p].v, h, m, l);
+        }
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -887,14 +941,15 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // LD).  Every load is UNCONDITIONAL (k-steps past the end re-load the last
     // one): with a data-dependent load count hipcc cannot count the loads in
     // flight and drains them all (vmcnt(0)) before each write.
-    float4 ra[LD][RA], rb[LD][RB];
+    float4 ra[LD][RA];
+    BReg<BP> rb[LD][RB];
     if (dbg & 1) {
 #pragma unroll
       for (int j = 0; j < LD; ++j) {
 #pragma unroll
         for (int p = 0; p < RA; ++p) ra[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
 #pragma unroll
-        for (int p = 0; p < RB; ++p) rb[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
+        for (int p = 0; p < RB; ++p) rb[j][p] = BReg<BP>::ones();
       }
     }
     const int klast = kt0 + max(nks, 1) - 1;
@@ -1061,223 +1116,6 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                           smem);
-}
-
-// 16-deep LDS images (conv_ws16_kernel): 32-B rows (16 bf16), the two 16-B
-// chunks XOR-swizzled by (row >> 3) & 1.  The ds_read_b128 lane groups
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and their +32 twins: 16 rows of
-// one 32-row fragment) pair rows r, r' with r = r' mod 8 and r >> 3 of
-// opposite parity, so every group covers the 16 slots of the 256-B bank row
-// once; a ds_write_b64 group (16 lanes = 4 whole rows) covers 128 B.
-// Conflict-free reads and writes.
-__device__ __forceinline__ int swz16(int row, int elem) {
-  return row * 16 + ((((elem >> 3) ^ (row >> 3)) & 1) << 3) + (elem & 7);
-}
-
-// Warp-specialised split-product conv with a 16-deep, NS-stage LDS ring
-// (tuning conv_ws = 4 / 5 / 6; conv_ws_kernel is the 32-deep two-stage form).
-// Same tile (256 x 128, waves 0-7 compute 64 x 64 each, waves 8-15 stage),
-// same K order and product order -- bit-identical outputs -- but the compute
-// waves never wait for LDS after a barrier: during step u they issue the
-// ds_reads of step u + 1 between the MFMA groups of step u, each plane batch
-// as soon as the step-u MFMAs that read its registers have issued (fa[2] /
-// fb[2] after the l*h, h*l products, fa[1] / fb[1] after m*h, fa[0] / fb[0]
-// after h*h).  That needs step u + 1 complete in LDS one barrier earlier, so
-// the stagers run NS - 1 steps ahead: at iteration u they write step
-// u + NS - 1 into stage (u + NS - 1) % NS, which last held step u - 1 (read
-// during iteration u - 2, complete at barrier u - 2).  NS >= 3; one barrier
-// per 16-deep step.  Stagers: thread st owns rows st / 4 and st / 4 + 128 of
-// A and row st / 4 of B, 4 channels at (st % 4) * 4; a ring of LD steps of
-// global loads in registers.
-template <int NS, int LD>
-__global__ __launch_bounds__(1024, 1) void conv_ws16_kernel(ConvArgs a) {
-  static_assert(NS >= 3, "the read-ahead needs three stages");
-  constexpr int WN = 2, TM = 2, TN = 2;
-  constexpr int BM = 256, BN = 128, RA = 2, RB = 1;
-  constexpr int A_H = 3 * BM * 16, B_H = 3 * BN * 16;  // halfwords per stage
-  constexpr int STAGE = A_H + B_H;                      // 18432 halfwords = 36 KiB
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * STAGE];
-  static_assert(NS * STAGE / 2 >= 32 * (BN + 4), "LDS epilogue slab does not fit");
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WN, wc = wave % WN;  // (stagers: wr >= 4, never an acc slab)
-  int split;
-  const int tile = a.tile_base + xcd_tile(a.xcd2, split);
-  const int kt0 = split * a.kt_per_split;
-  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
-  const int nst = 2 * max(kt1 - kt0, 0);  // 16-deep steps
-  const Geo g = geo_of(a);
-  const int mt = tile / a.nN, nt = tile - mt * a.nN;
-  const int m0 = mt * BM, n0 = nt * BN;
-
-  floatx16 acc[TM][TN];
-  if (wave >= 8) {
-    // ------------------------------------------------------------ stagers
-    const int st = tid - 512;
-    const int srow = st >> 2, schunk = (st & 3) * 4;
-    int ih0[RA], iw0[RA], base[RA];
-#pragma unroll
-    for (int p = 0; p < RA; ++p) {
-      const int m = m0 + srow + 128 * p;
-      const int mm = m < g.M ? m : 0;
-      const int n = mm / (g.OH * g.OW);
-      const int rem = mm - n * g.OH * g.OW;
-      const int oh = rem / g.OW, ow = rem - oh * g.OW;
-      const int ihv = oh * a.stride - a.pad;
-      ih0[p] = m < g.M ? ihv : -(1 << 29);
-      iw0[p] = ow * a.stride - a.pad;
-      base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + schunk;
-    }
-    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
-    constexpr uint32_t kOOB = 0x80000000u;
-    const int taps = a.KH * a.KW;
-    const int co = n0 + srow;
-    auto load = [&](int v, float4 (&la)[RA], float4 (&lb)[RB]) {
-      const int kt = kt0 + (v >> 1);
-      const int chunk = kt / taps;
-      const int tap = kt - chunk * taps;
-      const int cc = chunk * BK + (v & 1) * 16;
-      const int kh = tap / a.KW, kw = tap - kh * a.KW;
-      const bool cok = cc + schunk < a.Cin;
-      const int toff = (kh * g.W + kw) * a.Cin + cc;
-      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
-      const uint32_t offb = (cok & (co < a.Cout))
-                                ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
-                                : kOOB;
-      lb[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, offb, 0, 0));
-#pragma unroll
-      for (int p = 0; p < RA; ++p) {
-        const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
-                        ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
-        const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
-        la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
-      }
-    };
-    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
-      uint16_t* A16 = smem + buf * STAGE;
-      uint16_t* B16 = A16 + A_H;
-#pragma unroll
-      for (int p = 0; p < RA; ++p) {
-        uint2 h, m, l;
-        split3(la[p], h, m, l);
-        const int o = swz16(srow + 128 * p, schunk);
-        *reinterpret_cast<uint2*>(&A16[o]) = h;
-        *reinterpret_cast<uint2*>(&A16[BM * 16 + o]) = m;
-        *reinterpret_cast<uint2*>(&A16[2 * BM * 16 + o]) = l;
-      }
-      uint2 h, m, l;
-      split3(lb[0], h, m, l);
-      const int o = swz16(srow, schunk);
-      *reinterpret_cast<uint2*>(&B16[o]) = h;
-      *reinterpret_cast<uint2*>(&B16[BN * 16 + o]) = m;
-      *reinterpret_cast<uint2*>(&B16[2 * BN * 16 + o]) = l;
-    };
-    // register ring: step v in set v % LD (static indices: loops unrolled by
-    // LD); every load unconditional (steps past the end re-load the last), so
-    // hipcc counts the loads in flight instead of draining them
-    float4 ra[LD][RA], rb[LD][RB];
-    const int vlast = max(nst, 1) - 1;
-    auto vclamp = [&](int v) { return min(v, vlast); };
-#pragma unroll
-    for (int j = 0; j < LD; ++j) load(vclamp(j), ra[j], rb[j]);
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s) {  // prologue: steps 0 .. NS - 2
-      const int set = s % LD;
-      if (s < nst) write(s, ra[set], rb[set]);
-      load(vclamp(s + LD), ra[set], rb[set]);
-    }
-    __syncthreads();  // B_init
-    int u0 = 0;
-    for (; u0 + LD <= nst; u0 += LD) {
-#pragma unroll
-      for (int j = 0; j < LD; ++j) {
-        const int v = u0 + j + NS - 1;
-        const int set = (j + NS - 1) % LD;
-        if (v < nst) write(v % NS, ra[set], rb[set]);
-        load(vclamp(v + LD), ra[set], rb[set]);
-        __syncthreads();  // B_u
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < LD - 1; ++j) {  // the remaining nst % LD iterations
-      if (u0 + j < nst) {
-        const int v = u0 + j + NS - 1;
-        const int set = (j + NS - 1) % LD;
-        if (v < nst) write(v % NS, ra[set], rb[set]);
-        __syncthreads();
-      }
-    }
-  } else {
-    // ------------------------------------------------------------ compute
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int li = lane & 31, lh = lane >> 5;
-    bf16x8 fa[3][TM], fb[3][TN];
-    int ao[TM], bo[TN];  // fragment offsets inside a plane
-#pragma unroll
-    for (int i = 0; i < TM; ++i) ao[i] = swz16((wr * TM + i) * 32 + li, lh * 8);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bo[j] = swz16((wc * TN + j) * 32 + li, lh * 8);
-    auto rd = [&](int buf, int pa, int pb) {
-      const uint16_t* A16 = smem + buf * STAGE;
-      const uint16_t* B16 = A16 + A_H;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        fa[pa][i] = *reinterpret_cast<const bf16x8*>(&A16[pa * BM * 16 + ao[i]]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        fb[pb][j] = *reinterpret_cast<const bf16x8*>(&B16[pb * BN * 16 + bo[j]]);
-    };
-    auto mm1 = [&](int pa, int pb) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] =
-              __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
-    };
-    const int prio = a.prio;
-    __syncthreads();  // B_init
-    rd(0, 1, 1);
-    rd(0, 2, 0);
-    rd(0, 0, 2);
-    int nb = 1 % NS;  // the stage of step u + 1
-    for (int u = 0; u < nst; ++u) {
-      if (prio & 1) __builtin_amdgcn_s_setprio(1);
-      // products in the split kernel's order {mm, lh, hl, hm, mh, hh}
-      mm1(1, 1);
-      mm1(2, 0);
-      mm1(0, 2);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(nb, 2, 2);  // fa[2] (last read by l*h) and fb[2] (h*l) are free
-      mm1(0, 1);
-      mm1(1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(nb, 1, 1);  // fb[1] (h*m), fa[1] (m*h)
-      mm1(0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(nb, 0, 0);
-      if (prio & 1) __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();  // B_u
-      nb = nb + 1 == NS ? 0 : nb + 1;
-    }
-  }
-  if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
-    if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
-    return;
-  }
-  store_outputs_lds<4, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
-                                         reinterpret_cast<float*>(smem));
 }
 
 // Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
@@ -1842,37 +1680,39 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
 // stagers' register prefetch depth (k-steps).
 static int ws_depth() { return tuning(kTuneConvWS); }
 
-template <bool SPLIT>
+// BP: the weight operand as bf16 planes (ConvArgs::w3; split-product kernels
+// of the shipped configurations only).
+template <bool SPLIT, bool BP = false>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  static_assert(SPLIT || !BP, "weight planes feed the split-product kernels only");
   if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
     if (a.sk)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true>), grid, dim3(1024), 0, st, a);
-    else if (ws_depth() == 4)
-      hipLaunchKernelGGL((conv_ws16_kernel<3, 4>), grid, dim3(1024), 0, st, a);
-    else if (ws_depth() == 5)
-      hipLaunchKernelGGL((conv_ws16_kernel<4, 4>), grid, dim3(1024), 0, st, a);
-    else if (ws_depth() == 6)
-      hipLaunchKernelGGL((conv_ws16_kernel<3, 2>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true, BP>), grid, dim3(1024), 0, st, a);
     else if (ws_depth() == 1)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false, false, BP>), grid, dim3(1024), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, false, BP>), grid, dim3(1024), 0, st, a);
     return;
   }
   if (cfg == 0 && !db && occ3_enabled()) {
-    hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3, false, BP>), grid, dim3(256), 0,
+                       st, a);
     return;
   }
   if (cfg == 0) {
     if (db)
-      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT, 2, false, BP>), grid, dim3(256),
+                         0, st, a);
     else
-      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 2, false, BP>), grid, dim3(256),
+                         0, st, a);
   } else if (cfg == 1) {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT, 2, false, BP>), grid, dim3(256), 0,
+                       st, a);
   } else {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT, 2, false, BP>), grid, dim3(256), 0,
+                       st, a);
   }
 }
 
@@ -1920,6 +1760,19 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
   if (conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH, OW)) return 0;
   const Plan p = make_plan(N * OH * OW, Cout, KH, KW, Cin, Cout % 4 == 0);
   return p.ws_bytes;
+}
+
+// Weight planes (w3) with f32 activations, per kernel configuration (tuning
+// "conv_bp", A/B): bit 1 the warp-specialised kernel (cfg 3), bit 2 the
+// 3-per-CU 128x128 kernel (cfg 0; its B staging ring spills 3 VGPRs with
+// planes), bit 4 the narrow-Cout kernels (cfg 1 / 2).  Without an f32 copy
+// (w_packed null) every configuration takes the planes.
+static bool bp_for(int cfg, bool db, bool have_f32) {
+  if (!have_f32) return true;
+  const int t = tuning(kTuneConvBP);
+  if (cfg == 3) return (t & 1) != 0;
+  if (cfg == 0) return (t & 2) != 0 && !db;
+  return (t & 4) != 0;
 }
 
 // Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
@@ -2020,6 +1873,8 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     const dim3 g(c.sk ? c.sk_P : c.ntiles, c.sk ? 1 : c.splits);
     if (x3)
       launch_x3(p.cfg, db, g, st, c);
+    else if ((flags & kSplit3) && w3 && bp_for(p.cfg, db, w_packed != nullptr))
+      launch_conv<true, true>(p.cfg, db, g, st, c);
     else if (flags & kSplit3)
       launch_conv<true>(p.cfg, db, g, st, c);
     else
@@ -2057,7 +1912,7 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
                     const float* topdown, const float* residual, const float* gate, float* y,
                     int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                     int pad_beg, int pad_end, int flags, void* workspace, size_t workspace_bytes,
-                    void* stream) {
+                    void* stream, const uint16_t* w3 = nullptr) {
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
@@ -2080,14 +1935,30 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
           x + n0 * xs, w_packed, bias, topdown ? topdown + n0 * ts : nullptr,
           residual ? residual + n0 * ys : nullptr, gate ? gate + n0 * ys : nullptr, y + n0 * ys,
           nn, H, W, Cin, Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace,
-          workspace_bytes, stream);
+          workspace_bytes, stream, w3);
       if (rc) return rc;
     }
     return 0;
   }
-  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, gate, y, N, H, W, Cin,
+  return conv_core(x, nullptr, w_packed, w3, bias, topdown, residual, gate, y, N, H, W, Cin,
                    Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
                    stream);
+}
+
+extern "C" int d2mi_conv2d_nhwc_w3(const float* x, const float* w_packed, const uint16_t* w3,
+                                   const float* bias,
+                                   const float* topdown, const float* residual, const float* gate,
+                                   float* y, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                                   int stride, int pad_beg, int pad_end, int flags,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE((flags & ~15) == 0 && (flags & kSplit3),
+               "w3 conv flags: bit0 relu, bit1 relu after the add, bit2 (required) split-bf16 "
+               "MFMA products, bit3 flipped weight taps");
+  D2MI_REQUIRE(w3 != nullptr && ((uintptr_t)w3 & 7) == 0, "w3 planes must be 8-byte aligned");
+  D2MI_REQUIRE(!gate || (!topdown && !(flags & 3)), "the gate excludes relu / top-down");
+  D2MI_REQUIRE((int64_t)KH * KW * Cin * Cout * 6 < (1ll << 31), "w3 planes must be < 2 GiB");
+  return conv_f32(x, w_packed, bias, topdown, residual, gate, y, N, H, W, Cin, Cout, KH, KW, stride,
+                  pad_beg, pad_end, flags, workspace, workspace_bytes, stream, w3);
 }
 
 extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
@@ -2279,6 +2150,71 @@ extern "C" int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void*
                      reinterpret_cast<const float4*>(x), n4, reinterpret_cast<uint2*>(out));
   D2MI_LAUNCH_CHECK();
   return 0;
+}
+
+// Batched split of many f32 tensors (the weight operands of a step's convs,
+// their bf16 planes for the BP kernels): entry e owns workgroups
+// [blk0[e], blk0[e + 1]); out[e] = [3][n[e]] planes.
+constexpr int kMaxSplitMany = 48;
+struct SplitMany {
+  const float4* src[kMaxSplitMany];
+  uint2* dst[kMaxSplitMany];
+  long long n4[kMaxSplitMany];
+  int blk0[kMaxSplitMany + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void split3_many_kernel(SplitMany t) {
+  int lo = 0, hi = t.n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {  // the entry whose block range holds b
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.blk0[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long n4 = t.n4[lo];
+  const float4* src = t.src[lo];
+  uint2* dst = t.dst[lo];
+  const int nb = t.blk0[lo + 1] - t.blk0[lo];
+  for (long long i = (long long)(b - t.blk0[lo]) * 256 + threadIdx.x; i < n4;
+       i += (long long)nb * 256) {
+    uint2 h, m, l;
+    split3(src[i], h, m, l);
+    dst[i] = h;
+    dst[n4 + i] = m;
+    dst[2 * n4 + i] = l;
+  }
+}
+
+extern "C" int d2mi_split_bf16x3_many(int n, const float* const* src, const int64_t* numel,
+                                      uint16_t* const* out, void* stream) {
+  D2MI_REQUIRE(n >= 0 && (n == 0 || (src && numel && out)), "bad split table");
+  SplitMany t = {};
+  auto flush = [&]() -> int {
+    if (t.n == 0) return 0;
+    hipLaunchKernelGGL(split3_many_kernel, dim3(t.blk0[t.n]), dim3(256), 0, as_stream(stream), t);
+    D2MI_LAUNCH_CHECK();
+    t = SplitMany{};
+    return 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    D2MI_REQUIRE(numel[i] >= 0 && numel[i] % 4 == 0, "split: numel must be a multiple of 4");
+    D2MI_REQUIRE(((uintptr_t)src[i] & 15) == 0 && ((uintptr_t)out[i] & 7) == 0,
+                 "split: misaligned buffers (entry %d)", i);
+    if (numel[i] == 0) continue;
+    const long long n4 = numel[i] / 4;
+    const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
+    if (t.n == kMaxSplitMany) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    t.src[t.n] = reinterpret_cast<const float4*>(src[i]);
+    t.dst[t.n] = reinterpret_cast<uint2*>(out[i]);
+    t.n4[t.n] = n4;
+    t.blk0[t.n + 1] = t.blk0[t.n] + blocks;
+    ++t.n;
+  }
+  return flush();
 }
 
 extern "C" int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
