@@ -107,9 +107,6 @@ _SIGS = {
     "d2mi_conv2d_nhwc_levels": (c_int, [P, P, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_split_bf16x3": (c_int, [P, ctypes.c_int64, P, P]),
-    "d2mi_split_bf16x3_many": (c_int, [c_int, P, P, P, P]),
-    "d2mi_conv2d_nhwc_w3": (c_int, [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
-                                    c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_paste_masks": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "d2mi_wgrad_skinny_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "d2mi_wgrad_skinny": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),

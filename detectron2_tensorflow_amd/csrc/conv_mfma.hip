@@ -418,21 +418,6 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& 
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
-// Staging registers of one weight-operand row chunk (4 K-elements): f32 to
-// be split, or (BP) its three bf16 planes as loaded.
-template <bool BP>
-struct BReg {
-  float4 v;
-  __device__ static BReg ones() { return BReg{make_float4(1.f, 2.f, 3.f, 4.f)}; }
-};
-template <>
-struct BReg<true> {
-  uint2 h, m, l;
-  __device__ static BReg ones() {
-    return BReg{make_uint2(0x3f80u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u)};
-  }
-};
-
 // XCD-contiguous remap of a (tiles x splits) grid: hardware dispatch puts
 // linear workgroup L = x + y * gridDim.x on XCD L % 8; logical index l = the
 // (L / 8)-th of XCD L % 8's contiguous block, tile fastest, so consecutive
@@ -450,8 +435,7 @@ __device__ __forceinline__ int xcd_tile(int xcd2, int& split) {
   return xcd2 ? l - split * nx : l;
 }
 
-template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false,
-          bool BP = false>
+template <int WM, int WN, int TM, int TN, bool DB, bool SPLIT, int OCC = 2, bool ML = false>
 __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int RA = BM / 32, RB = BN / 32;  // staged rows per thread (8 threads per row)
@@ -509,10 +493,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // L2-resident): an activation gather has two compute phases to return, one
   // phase (~0.6 us at 2 workgroups/CU) being below its loaded latency.
   // OCC 3 (three workgroups per CU): a 1-deep activation prefetch (fewer VGPRs)
-  float4 ra[OCC >= 3 ? 1 : 2][RA];
-  BReg<BP> rb[RB];  // BP (SPLIT only): the weight tile's bf16 planes as loaded
-  const __amdgpu_buffer_rsrc_t w3rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.w3), 0, BP ? 3 * a.w_plane_bytes : 0, 0x00020000);
+  float4 ra[OCC >= 3 ? 1 : 2][RA], rb[RB];
   // channel-chunk-major, tap-minor K order: consecutive k-steps read the
   // same 32 channels at neighbouring pixels (the 3x3 taps), which are still
   // in L2 (tap-major order re-fetched them Cin/32 steps later)
@@ -543,22 +524,13 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < RB; ++p) {
       const int co = n0 + srow + 32 * p;
-      const bool bok = cok & (co < a.Cout);
-      const uint32_t e = (uint32_t)((tap * a.Cout + co) * a.Cin + cc + schunk);
-      if constexpr (BP) {
-        const uint32_t off = bok ? e * 2u : kOOB;
-        rb[p].h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 0, 0));
-        rb[p].m = __builtin_bit_cast(
-            uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, a.w_plane_bytes, 0));
-        rb[p].l = __builtin_bit_cast(
-            uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 2 * a.w_plane_bytes, 0));
-      } else {
-        const uint32_t off = bok ? e * 4u : kOOB;
-        rb[p].v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
-      }
+      const uint32_t off = (cok & (co < a.Cout))
+                               ? (uint32_t)((tap * a.Cout + co) * a.Cin + cc + schunk) * 4u
+                               : kOOB;
+      rb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
     }
   };
-  auto store_tile = [&](int buf, const float4 (&la)[RA], const BReg<BP> (&lb)[RB]) {
+  auto store_tile = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
     if constexpr (SPLIT) {
       uint16_t* A16 = reinterpret_cast<uint16_t*>(As[buf]);
       uint16_t* B16 = reinterpret_cast<uint16_t*>(Bs[buf]);
@@ -574,13 +546,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        if constexpr (BP) {
-          h = lb[p].h;
-          m = lb[p].m;
-          l = lb[p].l;
-        } else {
-          split3(lb[p].v, h, m, l);
-        }
+        split3(lb[p], h, m, l);
         const int o = swz(srow + 32 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -592,7 +558,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
         *reinterpret_cast<float4*>(&As[buf][(srow + 32 * p) * LDSP + schunk]) = la[p];
 #pragma unroll
       for (int p = 0; p < RB; ++p)
-        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = lb[p].v;
+        *reinterpret_cast<float4*>(&Bs[buf][(srow + 32 * p) * LDSP + schunk]) = lb[p];
     }
   };
 
@@ -773,7 +739,7 @@ __host__ __device__ __forceinline__ int sk_wg_of(long long i, long long P, long 
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <bool ML, int LD, bool BATCH = true, bool SK = false, bool BP = false>
+template <bool ML, int LD, bool BATCH = true, bool SK = false>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -854,13 +820,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // ablation bits (D2MI_CONV_DBG, timing experiments only): 1 = no global
     // loads, 2 = no split / LDS writes (the loaded values kept live)
     const int dbg = a.dbg;
-    // BP: the weight operand arrives as its three exact bf16 planes (a.w3,
-    // [3][taps][Cout][Cin], plane stride a.w_plane_bytes): the stagers copy
-    // them (three 8-B loads per row chunk) instead of loading f32 and
-    // splitting -- a third of their split VALU (tools/ws_ablate3.sh: bit 16)
-    const __amdgpu_buffer_rsrc_t w3rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(a.w3), 0, BP ? 3 * a.w_plane_bytes : 0, 0x00020000);
-    auto load = [&](int kt, float4 (&la)[RA], BReg<BP> (&lb)[RB]) {
+    auto load = [&](int kt, float4 (&la)[RA], float4 (&lb)[RB]) {
       if (dbg & 1) return;
       const int chunk = kt / taps;
       const int tap = kt - chunk * taps;
@@ -872,19 +832,10 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         const int co = n0 + srow + 64 * p;
-        const bool bok = cok & (co < a.Cout);
-        const uint32_t e = (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk);
-        if constexpr (BP) {
-          const uint32_t off = bok ? e * 2u : kOOB;
-          lb[p].h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 0, 0));
-          lb[p].m = __builtin_bit_cast(
-              uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, a.w_plane_bytes, 0));
-          lb[p].l = __builtin_bit_cast(
-              uint2, __builtin_amdgcn_raw_buffer_load_b64(w3rsrc, off, 2 * a.w_plane_bytes, 0));
-        } else {
-          const uint32_t off = bok ? e * 4u : kOOB;
-          lb[p].v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
-        }
+        const uint32_t off = (cok & (co < a.Cout))
+                                 ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
+                                 : kOOB;
+        lb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
       }
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
@@ -894,10 +845,12 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
       }
     };
-    auto write = [&](int buf, const float4 (&la)[RA], const BReg<BP> (&lb)[RB]) {
+    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
       if (dbg & 2) {
 #pragma unroll
         for (int p = 0; p < RA; ++p) asm volatile("" ::"v"(la[p].x));
+#pragma unroll
+        for (int p = 0; p < RB; ++p) asm volatile("" ::"v"(lb[p].x));
         return;
       }
       uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
@@ -922,15 +875,8 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        if constexpr (BP) {
-          h = lb[p].h;
-          m = lb[p].m;
-          l = lb[p].l;
-        } else if (dbg & 16) {
-          hi_only(lb[p].v, h, m, l);
-        } else {
-          split3(lb[p].v, h, m, l);
-        }
+        if (dbg & 16) hi_only(lb[p], h, m, l);
+        else split3(lb[p], h, m, l);
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -941,15 +887,14 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // LD).  Every load is UNCONDITIONAL (k-steps past the end re-load the last
     // one): with a data-dependent load count hipcc cannot count the loads in
     // flight and drains them all (vmcnt(0)) before each write.
-    float4 ra[LD][RA];
-    BReg<BP> rb[LD][RB];
+    float4 ra[LD][RA], rb[LD][RB];
     if (dbg & 1) {
 #pragma unroll
       for (int j = 0; j < LD; ++j) {
 #pragma unroll
         for (int p = 0; p < RA; ++p) ra[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
 #pragma unroll
-        for (int p = 0; p < RB; ++p) rb[j][p] = BReg<BP>::ones();
+        for (int p = 0; p < RB; ++p) rb[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
       }
     }
     const int klast = kt0 + max(nks, 1) - 1;
@@ -1676,43 +1621,37 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
 }
 
 // D2MI_CONV_WS / d2mi_set_tuning("conv_ws", d): the warp-specialised
-// 256x128 split kernel (conv_ws_kernel, plan cfg 3): 0 off, 2 / 3 the
-// stagers' register prefetch depth (k-steps).
+// 256x128 split kernel (conv_ws_kernel, plan cfg 3): 0 off, 2 on (1: the
+// A/B form reading a k-step's 12 fragments up front).  r3: a 16-deep, 3/4-stage
+// read-ahead variant (values 4-6) measured bit-identical but slower (removed;
+// DESIGN section 5).
 static int ws_depth() { return tuning(kTuneConvWS); }
 
-// BP: the weight operand as bf16 planes (ConvArgs::w3; split-product kernels
-// of the shipped configurations only).
-template <bool SPLIT, bool BP = false>
+template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
-  static_assert(SPLIT || !BP, "weight planes feed the split-product kernels only");
   if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
     if (a.sk)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true, BP>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true>), grid, dim3(1024), 0, st, a);
     else if (ws_depth() == 1)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false, false, BP>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, false, BP>), grid, dim3(1024), 0, st, a);
+      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true>), grid, dim3(1024), 0, st, a);
     return;
   }
   if (cfg == 0 && !db && occ3_enabled()) {
-    hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3, false, BP>), grid, dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3>), grid, dim3(256), 0, st, a);
     return;
   }
   if (cfg == 0) {
     if (db)
-      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT, 2, false, BP>), grid, dim3(256),
-                         0, st, a);
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 2, false, BP>), grid, dim3(256),
-                         0, st, a);
+      hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT>), grid, dim3(256), 0, st, a);
   } else if (cfg == 1) {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT, 2, false, BP>), grid, dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 2, true, SPLIT>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT, 2, false, BP>), grid, dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT>), grid, dim3(256), 0, st, a);
   }
 }
 
@@ -1760,19 +1699,6 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
   if (conv_dims(H, W, KH, KW, stride, pad_beg, pad_end, OH, OW)) return 0;
   const Plan p = make_plan(N * OH * OW, Cout, KH, KW, Cin, Cout % 4 == 0);
   return p.ws_bytes;
-}
-
-// Weight planes (w3) with f32 activations, per kernel configuration (tuning
-// "conv_bp", A/B): bit 1 the warp-specialised kernel (cfg 3), bit 2 the
-// 3-per-CU 128x128 kernel (cfg 0; its B staging ring spills 3 VGPRs with
-// planes), bit 4 the narrow-Cout kernels (cfg 1 / 2).  Without an f32 copy
-// (w_packed null) every configuration takes the planes.
-static bool bp_for(int cfg, bool db, bool have_f32) {
-  if (!have_f32) return true;
-  const int t = tuning(kTuneConvBP);
-  if (cfg == 3) return (t & 1) != 0;
-  if (cfg == 0) return (t & 2) != 0 && !db;
-  return (t & 4) != 0;
 }
 
 // Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
@@ -1873,8 +1799,6 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     const dim3 g(c.sk ? c.sk_P : c.ntiles, c.sk ? 1 : c.splits);
     if (x3)
       launch_x3(p.cfg, db, g, st, c);
-    else if ((flags & kSplit3) && w3 && bp_for(p.cfg, db, w_packed != nullptr))
-      launch_conv<true, true>(p.cfg, db, g, st, c);
     else if (flags & kSplit3)
       launch_conv<true>(p.cfg, db, g, st, c);
     else
@@ -1912,7 +1836,7 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
                     const float* topdown, const float* residual, const float* gate, float* y,
                     int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                     int pad_beg, int pad_end, int flags, void* workspace, size_t workspace_bytes,
-                    void* stream, const uint16_t* w3 = nullptr) {
+                    void* stream) {
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
@@ -1935,30 +1859,14 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
           x + n0 * xs, w_packed, bias, topdown ? topdown + n0 * ts : nullptr,
           residual ? residual + n0 * ys : nullptr, gate ? gate + n0 * ys : nullptr, y + n0 * ys,
           nn, H, W, Cin, Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace,
-          workspace_bytes, stream, w3);
+          workspace_bytes, stream);
       if (rc) return rc;
     }
     return 0;
   }
-  return conv_core(x, nullptr, w_packed, w3, bias, topdown, residual, gate, y, N, H, W, Cin,
+  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, gate, y, N, H, W, Cin,
                    Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
                    stream);
-}
-
-extern "C" int d2mi_conv2d_nhwc_w3(const float* x, const float* w_packed, const uint16_t* w3,
-                                   const float* bias,
-                                   const float* topdown, const float* residual, const float* gate,
-                                   float* y, int N, int H, int W, int Cin, int Cout, int KH, int KW,
-                                   int stride, int pad_beg, int pad_end, int flags,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE((flags & ~15) == 0 && (flags & kSplit3),
-               "w3 conv flags: bit0 relu, bit1 relu after the add, bit2 (required) split-bf16 "
-               "MFMA products, bit3 flipped weight taps");
-  D2MI_REQUIRE(w3 != nullptr && ((uintptr_t)w3 & 7) == 0, "w3 planes must be 8-byte aligned");
-  D2MI_REQUIRE(!gate || (!topdown && !(flags & 3)), "the gate excludes relu / top-down");
-  D2MI_REQUIRE((int64_t)KH * KW * Cin * Cout * 6 < (1ll << 31), "w3 planes must be < 2 GiB");
-  return conv_f32(x, w_packed, bias, topdown, residual, gate, y, N, H, W, Cin, Cout, KH, KW, stride,
-                  pad_beg, pad_end, flags, workspace, workspace_bytes, stream, w3);
 }
 
 extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
@@ -2150,71 +2058,6 @@ extern "C" int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void*
                      reinterpret_cast<const float4*>(x), n4, reinterpret_cast<uint2*>(out));
   D2MI_LAUNCH_CHECK();
   return 0;
-}
-
-// Batched split of many f32 tensors (the weight operands of a step's convs,
-// their bf16 planes for the BP kernels): entry e owns workgroups
-// [blk0[e], blk0[e + 1]); out[e] = [3][n[e]] planes.
-constexpr int kMaxSplitMany = 48;
-struct SplitMany {
-  const float4* src[kMaxSplitMany];
-  uint2* dst[kMaxSplitMany];
-  long long n4[kMaxSplitMany];
-  int blk0[kMaxSplitMany + 1];
-  int n;
-};
-
-__global__ __launch_bounds__(256) void split3_many_kernel(SplitMany t) {
-  int lo = 0, hi = t.n - 1;
-  const int b = blockIdx.x;
-  while (lo < hi) {  // the entry whose block range holds b
-    const int mid = (lo + hi + 1) >> 1;
-    if (t.blk0[mid] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  const long long n4 = t.n4[lo];
-  const float4* src = t.src[lo];
-  uint2* dst = t.dst[lo];
-  const int nb = t.blk0[lo + 1] - t.blk0[lo];
-  for (long long i = (long long)(b - t.blk0[lo]) * 256 + threadIdx.x; i < n4;
-       i += (long long)nb * 256) {
-    uint2 h, m, l;
-    split3(src[i], h, m, l);
-    dst[i] = h;
-    dst[n4 + i] = m;
-    dst[2 * n4 + i] = l;
-  }
-}
-
-extern "C" int d2mi_split_bf16x3_many(int n, const float* const* src, const int64_t* numel,
-                                      uint16_t* const* out, void* stream) {
-  D2MI_REQUIRE(n >= 0 && (n == 0 || (src && numel && out)), "bad split table");
-  SplitMany t = {};
-  auto flush = [&]() -> int {
-    if (t.n == 0) return 0;
-    hipLaunchKernelGGL(split3_many_kernel, dim3(t.blk0[t.n]), dim3(256), 0, as_stream(stream), t);
-    D2MI_LAUNCH_CHECK();
-    t = SplitMany{};
-    return 0;
-  };
-  for (int i = 0; i < n; ++i) {
-    D2MI_REQUIRE(numel[i] >= 0 && numel[i] % 4 == 0, "split: numel must be a multiple of 4");
-    D2MI_REQUIRE(((uintptr_t)src[i] & 15) == 0 && ((uintptr_t)out[i] & 7) == 0,
-                 "split: misaligned buffers (entry %d)", i);
-    if (numel[i] == 0) continue;
-    const long long n4 = numel[i] / 4;
-    const int blocks = (int)std::min<long long>((n4 + 255) / 256, 4096);
-    if (t.n == kMaxSplitMany) {
-      const int rc = flush();
-      if (rc) return rc;
-    }
-    t.src[t.n] = reinterpret_cast<const float4*>(src[i]);
-    t.dst[t.n] = reinterpret_cast<uint2*>(out[i]);
-    t.n4[t.n] = n4;
-    t.blk0[t.n + 1] = t.blk0[t.n] + blocks;
-    ++t.n;
-  }
-  return flush();
 }
 
 extern "C" int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,

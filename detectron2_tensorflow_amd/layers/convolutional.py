@@ -45,31 +45,30 @@ def same_pads(kernel_size, rate=1):
     return pb, pad_total - pb
 
 
-def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None, add2=None, w_planes=None):
+def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None, add2=None):
     """Input gradient (+ add, then the relu_gate mask, when given).  Stride 1:
     a forward conv of gy with the spatially flipped kernel — whose HWIO layout IS the packed [KH, KW, out', in'] layout
     of the transposed conv, flipped by the kernel's tap indexing (kFlipTaps) —
     on the MFMA kernel, padded (KH-1-pb, KH-1-pe).
     1x1 stride s: the MFMA GEMM gy . W^T on the strided grid, scattered into
-    zeros.  Anything else: torch.nn.grad (MIOpen).  w_planes: split_bf16x3
-    planes of w (the step's cached weight planes, WeightPlanes)."""
+    zeros.  Anything else: torch.nn.grad (MIOpen)."""
     KH, KW, Cin, Cout = w.shape
     gy = gy.contiguous()
     if add2 is not None:  # (dgrad + add) + add2, gated: the strided 1x1 scatter only
         if not (KH == 1 and KW == 1 and pb == 0 and pe == 0 and stride > 1 and Cin % 4 == 0
                 and Cout % 4 == 0):
-            gx = _dgrad(gy, w, x_shape, stride, pb, pe, add=add, w_planes=w_planes).add_(add2)
+            gx = _dgrad(gy, w, x_shape, stride, pb, pe, add=add).add_(add2)
             return gx if relu_gate is None else torch.ops.aten.threshold_backward(gx, relu_gate, 0.0)
-        g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0), w_planes=w_planes)
+        g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
         return ops.stride_scatter(g, x_shape, stride, add, add2, relu_gate)
     if KH == KW and Cout % 4 == 0:
         if stride == 1 and max(pb, pe) <= KH - 1:
             # the flip is an index flip inside the kernel (no flipped copy)
             return ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1,
                                    (KH - 1 - pb, KH - 1 - pe), flip_taps=KH > 1,
-                                   residual=add, relu_gate=relu_gate, w_planes=w_planes)
+                                   residual=add, relu_gate=relu_gate)
         if KH == 1 and pb == 0 and pe == 0:
-            g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0), w_planes=w_planes)
+            g = ops.conv2d_nhwc(gy, w.detach().contiguous(), None, 1, (0, 0))
             if Cin % 4 == 0:  # zero holes + scatter (+ add) (+ gate) in one pass
                 return ops.stride_scatter(g, x_shape, stride, add, gate=relu_gate)
             gx = torch.zeros(x_shape, dtype=gy.dtype, device=gy.device)
@@ -152,15 +151,13 @@ class _ConvMFMAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
                 relu_after=False, gate_input=False, res_grad_to=None, grad_from=None,
-                pair_grad=None, join=None, planes=None):
+                pair_grad=None, join=None):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
-        pp, wp = planes if planes is not None else (None, None)
         y = ops.conv2d_nhwc(x, w_packed, bias, stride, pads, relu, topdown, residual,
-                            relu_after_add=relu_after, w_planes=pp)
+                            relu_after_add=relu_after)
         ctx.save_for_backward(x, w_hwio, y if relu else None)
-        ctx.w_planes = wp  # planes of w_hwio: the dgrad's weight operand
         ctx.conf = (stride, pads, relu, bias is not None, topdown is not None, residual is not None)
         ctx.in_info = getattr(x, "_d2mi_relu_info", None) if gate_input else None
         ctx.res_grad_to = res_grad_to if residual is not None else None
@@ -210,11 +207,10 @@ class _ConvMFMAFn(torch.autograd.Function):
                     add = add + other
             info = None if deposit else ctx.in_info
             if info is not None and _gate_eligible(w.shape, stride, pb, pe):
-                gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=add,
-                           w_planes=ctx.w_planes)
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=add)
                 info["masked"] = True
             else:
-                gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add, w_planes=ctx.w_planes)
+                gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add)
             if deposit:
                 handoff.deposit(pair, "g", gx, "pair")
                 gx = None
@@ -223,8 +219,7 @@ class _ConvMFMAFn(torch.autograd.Function):
             gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
         if want_b and gb is None:
             gb = ops.column_sum(gy)
-        return (gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None,
-                None)
+        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None
 
 
 def _join_active(ctx):
@@ -253,73 +248,29 @@ def _join_backward(ctx, gy, x, w, stride, pb, pe):
         p = ctx.join
         s = p.pop("sum", None)
         if s is None:
-            handoff.deposit(p, "lat", _dgrad(gy, w, x.shape, stride, pb, pe, w_planes=ctx.w_planes),
-                        "join (lateral)")
+            handoff.deposit(p, "lat", _dgrad(gy, w, x.shape, stride, pb, pe), "join (lateral)")
             return None
         p["last"] = "lateral"  # (tests: which member completed the join)
         if info is not None and _gate_eligible(w.shape, stride, pb, pe):
-            gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=s,
-                        w_planes=ctx.w_planes)
+            gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=x, add=s)
             info["masked"] = True
             return gx
-        return _dgrad(gy, w, x.shape, stride, pb, pe, add=s, w_planes=ctx.w_planes)
+        return _dgrad(gy, w, x.shape, stride, pb, pe, add=s)
     p = ctx.pair_grad
     other = p.pop("g", None)
     if other is None:  # first of the pair
-        handoff.deposit(p, "g", _dgrad(gy, w, x.shape, stride, pb, pe, w_planes=ctx.w_planes),
-                        "join (pair)")
+        handoff.deposit(p, "g", _dgrad(gy, w, x.shape, stride, pb, pe), "join (pair)")
         return None
     lat = p.pop("lat", None)
     if lat is None:
-        handoff.deposit(p, "sum", _dgrad(gy, w, x.shape, stride, pb, pe, add=other,
-                                          w_planes=ctx.w_planes), "join (sum)")
+        handoff.deposit(p, "sum", _dgrad(gy, w, x.shape, stride, pb, pe, add=other), "join (sum)")
         return None
     p["last"] = "pair"
     gate = x if info is not None else None
-    gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=gate, add=other, add2=lat,
-                w_planes=ctx.w_planes)
+    gx = _dgrad(gy, w, x.shape, stride, pb, pe, relu_gate=gate, add=other, add2=lat)
     if info is not None:
         info["masked"] = True
     return gx
-
-
-class WeightPlanes:
-    """The exact bf16 planes (ops.split_bf16x3) of the weight operands of a
-    step's split-product convs -- the packed forward weights and the HWIO
-    weights the input gradient reads -- made in ONE launch wherever a fold /
-    pack group refreshes its members (ops.split_bf16x3_many), so the conv
-    kernels copy planes instead of splitting the same weights in every
-    workgroup (d2mi_conv2d_nhwc_w3).  A layer's planes are valid only for the
-    exact tensors they were made from (identity), i.e. until the next refold /
-    repack.  ENABLED = False: no planes (A/B)."""
-    ENABLED = True
-
-    @classmethod
-    def make(cls, items):
-        """items: (layer, weights HWIO, packed or None)."""
-        if not cls.ENABLED:
-            return
-        srcs, owners = [], []
-        for layer, w, p in items:
-            if p is None or not w.is_cuda or w.numel() % 4 or ops.CONV_MATH != "split":
-                layer._w_planes = None
-                continue
-            srcs += [p.detach(), w.detach()]
-            owners.append((layer, p, w))
-        if not srcs:
-            return
-        with torch.no_grad():
-            planes = ops.split_bf16x3_many(srcs)
-        for i, (layer, p, w) in enumerate(owners):
-            layer._w_planes = (p, w, planes[2 * i], planes[2 * i + 1])
-
-    @staticmethod
-    def get(layer, w, packed):
-        """(packed planes, HWIO planes) made from exactly these tensors, or None."""
-        t = layer.__dict__.get("_w_planes")
-        if t is None or t[0] is not packed or t[1] is not w:
-            return None
-        return t[2], t[3]
 
 
 class FoldGroup:
@@ -364,7 +315,6 @@ class FoldGroup:
                             n.epsilon, m.wants_packed()))
         outs = ops.fold_frozen_bn_many(entries)
         self.slots = {id(m): [w, b, p, False, m._param_key()] for m, (w, b, p) in zip(members, outs)}
-        WeightPlanes.make([(m, w, p) for m, (w, b, p) in zip(members, outs)])
 
 
 class PackGroup:
@@ -405,7 +355,6 @@ class PackGroup:
         outs = ops.pack_conv_weights_many([m.weights.detach() for m in stale])
         for m, k, o in zip(stale, keys, outs):
             m._packed, m._packed_key = o, k
-        WeightPlanes.make([(m, m.weights, o) for m, o in zip(stale, outs)])
         return layer._packed
 
 
@@ -502,7 +451,6 @@ class Conv2D(Layer):
                                           want_packed)
         if cacheable:
             self._fold_w, self._fold_b, self._fold_p, self._fold_key = w, b, packed, key
-            WeightPlanes.make([(self, w, packed)])  # (once per parameter version)
         return w, b, None, packed
 
     def fold_trainable(self):
@@ -528,8 +476,6 @@ class Conv2D(Layer):
         if self._packed is None or self._packed_key != key:
             self._packed = ops.pack_conv_weights(w.detach())
             self._packed_key = key
-            if w is self.weights:  # (a Cin-padded w_eff is a new tensor per call)
-                WeightPlanes.make([(self, w, self._packed)])
         return self._packed
 
     def call_levels(self, inputs):
@@ -614,7 +560,7 @@ class Conv2D(Layer):
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add,
                                     bool(relu_input_sole_consumer), res_grad_to, grad_from,
-                                    pair_grad, join, WeightPlanes.get(self, w, packed))
+                                    pair_grad, join)
             if raw:  # the conv (+ bias) alone: the caller applies the normalizer / activation
                 return ret
             if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \

@@ -538,25 +538,6 @@ def split_bf16x3(x):
     return out
 
 
-def split_bf16x3_many(ts):
-    """split_bf16x3 of every tensor in ``ts`` in one launch
-    (d2mi_split_bf16x3_many); int16 [3, *t.shape] each."""
-    ts = [_f32c(t) for t in ts]
-    if not ts:
-        return []
-    _C.require_device(*ts)
-    for t in ts:
-        if t.numel() % 4:
-            raise ValueError("split_bf16x3_many: numel must be a multiple of 4")
-    outs = [torch.empty((3,) + tuple(t.shape), dtype=torch.int16, device=t.device) for t in ts]
-    rc = _C.lib().d2mi_split_bf16x3_many(
-        len(ts), _C.host_array(_C.c_void_p, [t.data_ptr() for t in ts]),
-        _C.host_array(_C.ctypes.c_int64, [t.numel() for t in ts]),
-        _C.host_array(_C.c_void_p, [o.data_ptr() for o in outs]), _C.stream_of(ts[0].device))
-    _C.check(rc, "d2mi_split_bf16x3_many")
-    return outs
-
-
 # workspace sizes per conv / wgrad shape (pure functions of the shape and the
 # device's CU count: one ctypes query per distinct shape)
 _CONV_WS, _WGRAD_WS = {}, {}
@@ -575,15 +556,12 @@ def _presplit_ok(x, Cin):
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
                 residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None,
-                flip_taps=False, relu_gate=None, out=None, w_planes=None):
+                flip_taps=False, relu_gate=None, out=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
     CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x.
     flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
-    w_planes: split_bf16x3 planes of w_packed (the step's cached weight
-    planes): the split-product kernels copy them instead of splitting the
-    weights per workgroup (d2mi_conv2d_nhwc_w3; bit-identical output).
     relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv
     (+ residual) : 0 (a dgrad with its producer's ReLU backward fused, and the
     gradient of the producer's other consumer added first)."""
@@ -645,11 +623,6 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
         rc = lib.d2mi_conv2d_nhwc_x3(_C.ptr(x3), _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
                                      _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
                                      int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb, st)
-    elif w_planes is not None and math_mode == "split":
-        rc = lib.d2mi_conv2d_nhwc_w3(_C.ptr(x), _C.ptr(w_packed), _C.ptr(w_planes), _C.ptr(bias),
-                                     _C.ptr(topdown), _C.ptr(residual), _C.ptr(relu_gate),
-                                     _C.ptr(y), N, H, W, Cin, Cout, KH, KW, int(stride), int(pb),
-                                     int(pe), flags, _C.ptr(ws), wsb, st)
     elif relu_gate is not None:
         rc = lib.d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,

@@ -449,25 +449,6 @@ int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* dims, int nle
  * above) on operands already split by it: x3 = split of x [N,H,W,Cin],
  * w3 = split of w_packed; Cin % 8 == 0; each operand's 3 planes < 2 GiB. */
 int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream);
-/* d2mi_split_bf16x3_many: the same split of n tensors in one launch
- * (out[i] = [3][numel[i]]); the conv weight operands of a training step, whose
- * planes d2mi_conv2d_nhwc_w3 reads.  numel[i] % 4 == 0. */
-int d2mi_split_bf16x3_many(int n, const float* const* src, const int64_t* numel,
-                           uint16_t* const* out, void* stream);
-/* d2mi_conv2d_nhwc_w3: d2mi_conv2d_nhwc_ex / _gated (gate nullable) whose
- * weight operand also arrives as its three bf16 planes w3 = [3][KH][KW][Cout]
- * [Cin] (d2mi_split_bf16x3 of w_packed): the split-product kernels copy the
- * planes instead of splitting the f32 weights in every workgroup (tuning
- * "conv_bp" picks the kernels that take them; w_packed may be null, then all
- * do).  Same arithmetic, bit-identical output.  The Conv2D forward / input
- * gradient of lib/layers/convolutional.py:225-243 (as d2mi_conv2d_nhwc).
- * flags: bit0 relu, bit1 relu after the add, bit2 (required) split products,
- * bit3 flipped taps. */
-int d2mi_conv2d_nhwc_w3(const float* x, const float* w_packed, const uint16_t* w3,
-                        const float* bias, const float* topdown, const float* residual,
-                        const float* gate, float* y, int N, int H, int W, int Cin, int Cout,
-                        int KH, int KW, int stride, int pad_beg, int pad_end, int flags,
-                        void* workspace, size_t workspace_bytes, void* stream);
 int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
                         const float* topdown, const float* residual, float* y, int N, int H,
                         int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,

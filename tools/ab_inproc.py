@@ -64,12 +64,7 @@ def _conv_epi(on):
     ops.set_tuning("conv_epi", 1 if on else 0)
 
 
-def _weight_planes(on):
-    from detectron2_tensorflow_amd.layers.convolutional import WeightPlanes
-    WeightPlanes.ENABLED = on
-
-
-SWITCHES = {"weight_planes": _weight_planes, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 

@@ -27,8 +27,6 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default=None, help="';'-separated N,H,W,Cin,Cout,k,s,form")
-    ap.add_argument("--planes", action="store_true",
-                    help="pass the weight operand's bf16 planes (w_planes) to the convs")
     a = ap.parse_args()
     arms = [int(v) for v in a.arms.split(",")]
     names = list(SETS) if a.set == "all" else a.set.split(",")
@@ -57,8 +55,6 @@ def main():
             res = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "r" in form else None
             gate = torch.randn(N, OH, OW, Cout, generator=g).to(dev) if "g" in form else None
             kw = dict(residual=res, relu_gate=gate, relu_after_add=(form == "r"), relu=(form == "r"))
-            if a.planes:
-                kw["w_planes"] = ops.split_bf16x3(wp)
             run = lambda: ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode="split", **kw)
         outs, times = {}, {v: [] for v in arms}
         for v in arms:
