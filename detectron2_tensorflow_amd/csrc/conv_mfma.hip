@@ -418,6 +418,43 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& 
 // DB: double-buffered LDS (one barrier per k-step, 2 workgroups/CU for the
 // 128x128 tile) vs single-buffered (two barriers per k-step, 36 KiB LDS, up to
 // 3 workgroups/CU).  Large-M shapes prefer the higher occupancy.
+// Position of a k-step in the channel-chunk-major, tap-minor K order.  The
+// staging loads walk k-steps in order: kseek() advances by one step with a
+// few scalar adds and only re-derives the position by division on a jump.
+struct KCursor {
+  int kt, chunk, tap, kh, kw;
+};
+__device__ __forceinline__ void kseek(KCursor& c, int kt, int taps, int KW) {
+  if (kt == c.kt) return;
+  if (kt == c.kt + 1) {
+    c.kt = kt;
+    ++c.tap;
+    if (++c.kw == KW) {
+      c.kw = 0;
+      ++c.kh;
+    }
+    if (c.tap == taps) {
+      c.tap = c.kh = c.kw = 0;
+      ++c.chunk;
+    }
+    return;
+  }
+  c.kt = kt;
+  c.chunk = kt / taps;
+  c.tap = kt - c.chunk * taps;
+  c.kh = c.tap / KW;
+  c.kw = c.tap - c.kh * KW;
+}
+__device__ __forceinline__ KCursor kcursor(int kt, int taps, int KW) {
+  KCursor c;
+  c.kt = kt;
+  c.chunk = kt / taps;
+  c.tap = kt - c.chunk * taps;
+  c.kh = c.tap / KW;
+  c.kw = c.tap - c.kh * KW;
+  return c;
+}
+
 // XCD-contiguous remap of a (tiles x splits) grid: hardware dispatch puts
 // linear workgroup L = x + y * gridDim.x on XCD L % 8; logical index l = the
 // (L / 8)-th of XCD L % 8's contiguous block, tile fastest, so consecutive
@@ -497,12 +534,12 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // channel-chunk-major, tap-minor K order: consecutive k-steps read the
   // same 32 channels at neighbouring pixels (the 3x3 taps), which are still
   // in L2 (tap-major order re-fetched them Cin/32 steps later)
+  const int taps = a.KH * a.KW;
+  KCursor ca = kcursor(kt0, taps, a.KW), cb = ca;  // (A and B loads run in k-step order)
   auto load_a = [&](int kt, float4 (&la)[RA]) {
-    const int taps = a.KH * a.KW;
-    const int chunk = kt / taps;
-    const int tap = kt - chunk * taps;
-    const int cc = chunk * BK;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    kseek(ca, kt, taps, a.KW);
+    const int cc = ca.chunk * BK;
+    const int kh = ca.kh, kw = ca.kw;
     const bool cok = cc + schunk < a.Cin;
     const int toff = (kh * g.W + kw) * a.Cin + cc;
 #pragma unroll
@@ -515,11 +552,9 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
     }
   };
   auto load_b = [&](int kt) {
-    const int taps = a.KH * a.KW;
-    const int chunk = kt / taps;
-    const int tap0 = kt - chunk * taps;
-    const int tap = (a.flags & kFlipTaps) ? taps - 1 - tap0 : tap0;
-    const int cc = chunk * BK;
+    kseek(cb, kt, taps, a.KW);
+    const int tap = (a.flags & kFlipTaps) ? taps - 1 - cb.tap : cb.tap;
+    const int cc = cb.chunk * BK;
     const bool cok = cc + schunk < a.Cin;
 #pragma unroll
     for (int p = 0; p < RB; ++p) {
@@ -817,32 +852,67 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
     constexpr uint32_t kOOB = 0x80000000u;
     const int taps = a.KH * a.KW;
+    // Per staged row, which taps land inside the image (bit t: tap t; the
+    // plan gives this kernel <= 32 taps), so a k-step's range test is one bit
+    // extract.
+    uint32_t tv[RA];
+#pragma unroll
+    for (int p = 0; p < RA; ++p) {
+      uint32_t b = 0;
+      for (int kh = 0; kh < a.KH; ++kh) {
+        const bool rok = (unsigned)(ih0[p] + kh) < (unsigned)g.H;
+        for (int kw = 0; kw < a.KW; ++kw)
+          b |= (rok & ((unsigned)(iw0[p] + kw) < (unsigned)g.W) ? 1u : 0u) << (kh * a.KW + kw);
+      }
+      tv[p] = b;
+    }
+    // weight rows: element offset of (co, schunk) inside a tap's [Cout][Cin]
+    int boff[RB];
+    bool bco[RB];
+#pragma unroll
+    for (int p = 0; p < RB; ++p) {
+      const int co = n0 + srow + 64 * p;
+      bco[p] = co < a.Cout;
+      boff[p] = co * a.Cin + schunk;
+    }
     // ablation bits (D2MI_CONV_DBG, timing experiments only): 1 = no global
     // loads, 2 = no split / LDS writes (the loaded values kept live)
     const int dbg = a.dbg;
-    auto load = [&](int kt, float4 (&la)[RA], float4 (&lb)[RB]) {
+    // The loads run in k-step order (kt0, kt0 + 1, ..., then the last one
+    // again): a uniform cursor (chunk, tap, kh, kw) advanced by one step
+    // replaces two integer divisions per k-step.
+    const int klast = kt0 + max(nks, 1) - 1;
+    int c_kt = kt0, c_chunk = kt0 / taps, c_tap = kt0 - (kt0 / taps) * taps;
+    int c_kh = c_tap / a.KW, c_kw = c_tap - (c_tap / a.KW) * a.KW;
+    auto load = [&](float4 (&la)[RA], float4 (&lb)[RB]) {
       if (dbg & 1) return;
-      const int chunk = kt / taps;
-      const int tap = kt - chunk * taps;
-      const int cc = chunk * BK;
-      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+      const int cc = c_chunk * BK;
       const bool cok = cc + schunk < a.Cin;
-      const int toff = (kh * g.W + kw) * a.Cin + cc;
-      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
+      const int toff = (c_kh * g.W + c_kw) * a.Cin + cc;
+      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - c_tap : c_tap;
+      const int wsc = wtap * a.Cout * a.Cin + cc;
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
-        const int co = n0 + srow + 64 * p;
-        const uint32_t off = (cok & (co < a.Cout))
-                                 ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + schunk) * 4u
-                                 : kOOB;
+        const uint32_t off = (cok & bco[p]) ? (uint32_t)(boff[p] + wsc) * 4u : kOOB;
         lb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
       }
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
-        const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
-                        ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
-        const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 4u : kOOB;
+        const bool inb = ((tv[p] >> c_tap) & 1u) != 0;
+        const uint32_t off = (cok & inb) ? (uint32_t)(base[p] + toff) * 4u : kOOB;
         la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+      }
+      if (c_kt < klast) {  // advance the cursor (uniform)
+        ++c_kt;
+        ++c_tap;
+        if (++c_kw == a.KW) {
+          c_kw = 0;
+          ++c_kh;
+        }
+        if (c_tap == taps) {
+          c_tap = c_kh = c_kw = 0;
+          ++c_chunk;
+        }
       }
     };
     auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
@@ -855,18 +925,10 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       }
       uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
       uint16_t* B16 = A16 + 3 * BM * LDSB;
-      // ablation bits 32 / 16: no split VALU for A / B (the high halves
-      // packed, m = l = 0: wrong sums, timing only)
-      auto hi_only = [](const float4 v, uint2& h, uint2& m, uint2& l) {
-        h.x = (__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u);
-        h.y = (__float_as_uint(v.z) >> 16) | (__float_as_uint(v.w) & 0xffff0000u);
-        m = l = make_uint2(0u, 0u);
-      };
 #pragma unroll
       for (int p = 0; p < RA; ++p) {
         uint2 h, m, l;
-        if (dbg & 32) hi_only(la[p], h, m, l);
-        else split3(la[p], h, m, l);
+        split3(la[p], h, m, l);
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&A16[o]) = h;
         *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
@@ -875,8 +937,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
       for (int p = 0; p < RB; ++p) {
         uint2 h, m, l;
-        if (dbg & 16) hi_only(lb[p], h, m, l);
-        else split3(lb[p], h, m, l);
+        split3(lb[p], h, m, l);
         const int o = swz(srow + 64 * p, schunk);
         *reinterpret_cast<uint2*>(&B16[o]) = h;
         *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
@@ -897,12 +958,10 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         for (int p = 0; p < RB; ++p) rb[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
       }
     }
-    const int klast = kt0 + max(nks, 1) - 1;
-    auto kclamp = [&](int v) { return min(kt0 + v, klast); };
 #pragma unroll
-    for (int j = 0; j < LD; ++j) load(kclamp(j), ra[j], rb[j]);
+    for (int j = 0; j < LD; ++j) load(ra[j], rb[j]);
     if (nks > 0) write(0, ra[0], rb[0]);  // prologue: k-step 0 into buffer 0
-    load(kclamp(LD), ra[0], rb[0]);
+    load(ra[0], rb[0]);
     __syncthreads();  // B_{-1}
     // iteration u: k-step v = u + 1 -> buffer v % 2 from register set v % LD,
     // that set re-filled with k-step v + LD; then B_u
@@ -913,7 +972,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         const int v = u0 + j + 1;
         const int set = (j + 1) % LD;  // (unrolled: a constant index)
         if (v < nks) write(v & 1, ra[set], rb[set]);
-        load(kclamp(v + LD), ra[set], rb[set]);
+        load(ra[set], rb[set]);  // k-step v + LD (clamped)
         __syncthreads();  // B_u
       }
     }
@@ -1464,7 +1523,8 @@ static int wg_slots(int cfg) {
 Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool split = true) {
   Plan p;
   p.cfg = Cout <= 32 ? 2 : (Cout <= 64 || !wide_ok ? 1 : 0);
-  if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 && KH * KW * ((Cin + BK - 1) / BK) >= 16)
+  if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 && KH * KW * ((Cin + BK - 1) / BK) >= 16 &&
+      KH * KW <= 32)  // (the WS stagers keep a 32-bit tap mask per row)
     p.cfg = 3;
   p.BM = p.cfg == 3 ? 256 : 128;
   p.BN = (p.cfg == 0 || p.cfg == 3) ? 128 : (p.cfg == 1 ? 64 : 32);

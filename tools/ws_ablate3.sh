@@ -1,5 +1,6 @@
 # WS conv ablations (D2MI_CONV_DBG bits: 1 no loads, 2 no LDS staging, 4 no MFMA
-# loop, 8 no epilogue, 16 no B split VALU, 32 no A split VALU)
+# loop, 8 no epilogue; r3 also had 16 / 32 = no B / A split VALU, since removed:
+# profiles/r3b_ws_ablate3.log)
 set -o pipefail
 mkdir -p gpurun_out
 S="2,200,336,256,256,3,1,plain;2,50,84,256,256,3,1,plain;2,50,84,1024,256,1,1,plain;2,100,168,128,128,3,1,plain"
