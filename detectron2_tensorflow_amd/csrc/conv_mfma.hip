@@ -86,12 +86,13 @@ __device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2
     mb[e] = __float_as_uint(r) & 0xffff0000u;
     lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
   }
-  h.x = (hb[0] >> 16) | hb[1];
-  h.y = (hb[2] >> 16) | hb[3];
-  m.x = (mb[0] >> 16) | mb[1];
-  m.y = (mb[2] >> 16) | mb[3];
-  l.x = (lb[0] >> 16) | (lb[1] & 0xffff0000u);
-  l.y = (lb[2] >> 16) | (lb[3] & 0xffff0000u);
+  // each pair packed by one byte permute (the high halves of two words)
+  h.x = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+  h.y = __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u);
+  m.x = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+  m.y = __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u);
+  l.x = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+  l.y = __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u);
 }
 
 struct ConvArgs {
@@ -1523,7 +1524,9 @@ static int wg_slots(int cfg) {
 Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool split = true) {
   Plan p;
   p.cfg = Cout <= 32 ? 2 : (Cout <= 64 || !wide_ok ? 1 : 0);
-  if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 && KH * KW * ((Cin + BK - 1) / BK) >= 16 &&
+  // tuning "conv_ws_mink": the fewest k-steps that go to the WS kernel (A/B)
+  if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 &&
+      KH * KW * ((Cin + BK - 1) / BK) >= tuning(kTuneConvWSMinK) &&
       KH * KW <= 32)  // (the WS stagers keep a 32-bit tap mask per row)
     p.cfg = 3;
   p.BM = p.cfg == 3 ? 256 : 128;

@@ -282,12 +282,13 @@ __device__ __forceinline__ void split3w(const float4 v, uint2& h, uint2& m, uint
     mb[e] = __float_as_uint(r) & 0xffff0000u;
     lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
   }
-  h.x = (hb[0] >> 16) | hb[1];
-  h.y = (hb[2] >> 16) | hb[3];
-  m.x = (mb[0] >> 16) | mb[1];
-  m.y = (mb[2] >> 16) | mb[3];
-  l.x = (lb[0] >> 16) | (lb[1] & 0xffff0000u);
-  l.y = (lb[2] >> 16) | (lb[3] & 0xffff0000u);
+  // each pair packed by one byte permute (the high halves of two words)
+  h.x = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+  h.y = __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u);
+  m.x = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+  m.y = __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u);
+  l.x = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+  l.y = __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u);
 }
 
 // n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery).
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_split_kernel(WgradArgs a,
 // its bias-gradient partial sums, reduced in the fixed order of the 128 x 128
 // kernel).  Same pixel order, product order and accumulation sequence as
 // conv_wgrad_split_kernel: bit-identical for equal pixel splits.
-template <int LD>
+template <int LD, bool INC = false>
 __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, FastDiv fd_hw,
                                                                 FastDiv fd_w) {
   constexpr int TM = 2, TN = 2, BM = 256, BN = 128, S = 2;
@@ -527,22 +528,69 @@ __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, Fas
         const_cast<float*>(a.dy), 0, a.dy_bytes, 0x00020000);
     constexpr uint32_t kOOB = 0x80000000u;
     float4 ra[LD][4], rb[LD][4];
-    auto load = [&](int ch, float4 (&la)[4], float4 (&lb)[4]) {
+    // The loads walk the split's chunks in order (then the last one again).
+    // INC (same-size stride-1 convs: the 3x3 / 1x1 this kernel takes, see
+    // the launch): input pixel = output pixel + a uniform tap shift, so a
+    // per-thread (oy, ox) cursor of its first pixel, advanced by 32 pixels
+    // per chunk, gives the range test, and 24-bit multiplies the offsets --
+    // two fast divisions and four 32-bit multiplies per pixel fewer.  Else
+    // per-pixel division.  dY offsets advance by one uniform stride.  Same
+    // addresses either way.
+    const int clast = c_begin + max(nks, 1) - 1;
+    int c_ch = c_begin;
+    int p0 = c_begin * KP + 4 * pga;   // first of this thread's 4 X pixels
+    int pb0 = c_begin * KP + 4 * pgb;  // (dY)
+    int oy0 = 0, ox0 = 0;
+    if (INC) {
+      const int r2 = p0 - (int)fdiv((uint32_t)p0, fd_hw) * (a.OH * a.OW);
+      oy0 = (int)fdiv((uint32_t)r2, fd_w);
+      ox0 = r2 - oy0 * a.OW;
+    }
+    const int dy32 = KP / a.OW, dx32 = KP - (KP / a.OW) * a.OW;  // (uniform)
+    const int ybase = kh - a.pad, xbase = kw - a.pad;
+    const int tsh = ybase * a.W + xbase;  // INC: input pixel - output pixel
+    const uint32_t bstride = (uint32_t)KP * (uint32_t)a.Cout * 4u;
+    uint32_t boff = (uint32_t)(pb0 * a.Cout + co) * 4u;
+    auto load = [&](float4 (&la)[4], float4 (&lb)[4]) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int p = ch * KP + 4 * pga + q;
-        const uint32_t n = fdiv((uint32_t)p, fd_hw);
-        const int r2 = p - (int)n * (a.OH * a.OW);
-        const int oy = (int)fdiv((uint32_t)r2, fd_w), ox = r2 - oy * a.OW;
-        const int iy = oy * a.stride - a.pad + kh, ix = ox * a.stride - a.pad + kw;
-        const bool ok = ci_ok & (p < a.P) & ((unsigned)iy < (unsigned)a.H) &
-                        ((unsigned)ix < (unsigned)a.W);
-        const uint32_t off =
-            ok ? (uint32_t)(((((int)n * a.H + iy) * a.W + ix) * a.Cin + ci) * 4) : kOOB;
+        const int p = p0 + q;
+        uint32_t off;
+        if (INC) {
+          int ox = ox0 + q, oy = oy0;
+          const bool wrap = ox >= a.OW;
+          ox = wrap ? ox - a.OW : ox;
+          oy = wrap ? oy + 1 : oy;
+          oy = oy >= a.OH ? oy - a.OH : oy;
+          const bool ok = ci_ok & (p < a.P) & ((unsigned)(oy + ybase) < (unsigned)a.H) &
+                          ((unsigned)(ox + xbase) < (unsigned)a.W);
+          off = ok ? (__umul24((uint32_t)(p + tsh), (uint32_t)a.Cin) + (uint32_t)ci) * 4u : kOOB;
+        } else {
+          const int n = (int)fdiv((uint32_t)p, fd_hw);
+          const int r2 = p - n * (a.OH * a.OW);
+          const int oy = (int)fdiv((uint32_t)r2, fd_w), ox = r2 - oy * a.OW;
+          const int iy = oy * a.stride - a.pad + kh, ix = ox * a.stride - a.pad + kw;
+          const bool ok = ci_ok & (p < a.P) & ((unsigned)iy < (unsigned)a.H) &
+                          ((unsigned)ix < (unsigned)a.W);
+          off = ok ? (uint32_t)(((((int)n * a.H + iy) * a.W + ix) * a.Cin + ci) * 4) : kOOB;
+        }
         la[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
-        const int pb = ch * KP + 4 * pgb + q;
-        const uint32_t offb = (co_ok & (pb < a.P)) ? (uint32_t)((pb * a.Cout + co) * 4) : kOOB;
+        const uint32_t offb = (co_ok & (pb0 + q < a.P)) ? boff + (uint32_t)(q * a.Cout * 4) : kOOB;
         lb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, offb, 0, 0));
+      }
+      if (c_ch < clast) {  // advance to the next chunk (uniform condition)
+        ++c_ch;
+        p0 += KP;
+        pb0 += KP;
+        boff += bstride;
+        if (INC) {
+          ox0 += dx32;
+          oy0 += dy32;
+          const bool wrap = ox0 >= a.OW;
+          ox0 = wrap ? ox0 - a.OW : ox0;
+          oy0 = wrap ? oy0 + 1 : oy0;
+          oy0 = oy0 >= a.OH ? oy0 - a.OH : oy0;
+        }
       }
     };
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
@@ -576,12 +624,10 @@ __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, Fas
     };
     // unconditional loads (chunks past the end re-load the last one): hipcc
     // then counts the loads in flight instead of draining them
-    const int clast = c_begin + max(nks, 1) - 1;
-    auto cclamp = [&](int v) { return min(c_begin + v, clast); };
 #pragma unroll
-    for (int j = 0; j < LD; ++j) load(cclamp(j), ra[j], rb[j]);
+    for (int j = 0; j < LD; ++j) load(ra[j], rb[j]);
     if (nks > 0) write(0, ra[0], rb[0]);
-    load(cclamp(LD), ra[0], rb[0]);
+    load(ra[0], rb[0]);
     __syncthreads();  // B_{-1}
     int u0 = 0;
     for (; u0 + LD <= nks; u0 += LD) {
@@ -590,7 +636,7 @@ __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, Fas
         const int v = u0 + j + 1;
         const int set = (j + 1) % LD;
         if (v < nks) write(v & 1, ra[set], rb[set]);
-        load(cclamp(v + LD), ra[set], rb[set]);
+        load(ra[set], rb[set]);  // chunk v + LD (clamped)
         __syncthreads();  // B_u
       }
     }
@@ -849,8 +895,16 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
     const FastDiv fhw = make_fastdiv((uint32_t)(a.OH * a.OW)), fw = make_fastdiv((uint32_t)a.OW);
     // tuning wgrad_ws: 1 = loads one chunk ahead (no spills), 2 = two chunks
     // ahead (10 VGPRs of the stagers' ring spill at the 128-VGPR budget)
+    // the incremental pixel cursor (conv_wgrad_ws_kernel INC): same-size
+    // stride-1 convs whose per-thread runs of 4 pixels and 32-pixel chunk
+    // steps wrap at most one row and one image, pixel indices < 2^24
+    const bool inc = a.stride == 1 && a.OH == H && a.OW == W && a.OW >= 4 &&
+                     KP / a.OW + 1 <= a.OH && (int64_t)a.P + KP < (1 << 24) &&
+                     tuning(kTuneWgradInc) > 0;
     if (p.ws && tuning(kTuneWgradWS) >= 2)
       hipLaunchKernelGGL((conv_wgrad_ws_kernel<2>), grid, dim3(1024), 0, st, a, fhw, fw);
+    else if (p.ws && inc)
+      hipLaunchKernelGGL((conv_wgrad_ws_kernel<1, true>), grid, dim3(1024), 0, st, a, fhw, fw);
     else if (p.ws)
       hipLaunchKernelGGL((conv_wgrad_ws_kernel<1>), grid, dim3(1024), 0, st, a, fhw, fw);
     else if (p.occ3)
