@@ -55,6 +55,10 @@ _SIGS = {
     "d2mi_rpn_proposals_workspace_size": (c_size_t, [c_int, c_int, P, c_int, c_int, c_int]),
     "d2mi_rpn_proposals": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int, c_float,
                                    c_float, P, c_float, P, P, P, P, c_size_t, P]),
+    "d2mi_rpn_proposals_ex": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_int, c_int,
+                                      c_float, c_float, P, c_float, P, P, P, P, c_size_t, P]),
+    "d2mi_rpn_head_gather": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),
+    "d2mi_rpn_head_scatter": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_fast_rcnn_workspace_size": (c_size_t, [c_int, c_int, c_int, c_float, c_int]),
     "d2mi_fast_rcnn_inference": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P,
                                          c_float, c_float, c_float, c_int, P, P, P, P, P, P,

@@ -22,6 +22,10 @@ constexpr int kMaxA = 12;
 struct Levels {
   int64_t off_a[D2MI_MAX_LEVELS];  // element offset of level l's tensor from base_a
   int64_t off_b[D2MI_MAX_LEVELS];  // element offset of level l's tensor from base_b
+  // image strides of level l's tensors (a: elements per K, b: float4s); by
+  // default H * W * A (each level a dense [N, H, W, A(*K)] tensor)
+  int64_t img_a[D2MI_MAX_LEVELS];
+  int64_t img_b[D2MI_MAX_LEVELS];
   int H[D2MI_MAX_LEVELS], W[D2MI_MAX_LEVELS];
   int stride[D2MI_MAX_LEVELS];
   float cell[D2MI_MAX_LEVELS][kMaxA][4];
@@ -73,7 +77,7 @@ __global__ void seg_setup_kernel(Levels lv, int N, int K, int topk, int64_t* seg
   if (s >= N * lv.L) return;
   const int n = s / lv.L, l = s - n * lv.L;
   const int64_t hwa = (int64_t)lv.H[l] * lv.W[l] * lv.A;
-  seg_start[s] = lv.off_a[l] + n * hwa * K;
+  seg_start[s] = lv.off_a[l] + n * lv.img_a[l] * K;
   seg_len[s] = (int32_t)(hwa * K);
   if (seg_k) seg_k[s] = (int32_t)min((int64_t)topk, hwa);
 }
@@ -96,7 +100,7 @@ __global__ void rpn_decode_kernel(const float* __restrict__ base_d, Levels lv, i
     const int id = tidx[o];
     const int hw = id / lv.A, a = id - hw * lv.A;
     const float4 anc = anchor_at(lv, l, hw, a);
-    const float4 d = d4[((size_t)n * HW + hw) * lv.A + a];
+    const float4 d = d4[(size_t)n * lv.img_b[l] + (size_t)hw * lv.A + a];
     float4 b = apply_delta(anc, d, dc.wy, dc.wx, dc.wh, dc.ww, dc.clamp);
     b = clip_box(b, hmax, wmax);
     bool ok = true;
@@ -428,6 +432,7 @@ int make_levels(Levels& lv, const float* const* a_ptrs, const float* const* b_pt
     D2MI_REQUIRE((float)lv.stride[l] == strides[l], "anchor strides must be integers");
     lv.off_a[l] = a_ptrs ? (int64_t)((const float*)a_ptrs[l] - (const float*)a_ptrs[0]) : 0;
     lv.off_b[l] = b_ptrs ? (int64_t)((const float*)b_ptrs[l] - (const float*)b_ptrs[0]) : 0;
+    lv.img_a[l] = lv.img_b[l] = (int64_t)lv.H[l] * lv.W[l] * A;
     if (b_ptrs) D2MI_REQUIRE(((uintptr_t)b_ptrs[l] & 15) == 0, "delta tensors must be 16B aligned");
     for (int a = 0; a < A; ++a)
       for (int c = 0; c < 4; ++c) lv.cell[l][a][c] = cell[(l * A + a) * 4 + c];
@@ -555,6 +560,23 @@ extern "C" int d2mi_rpn_proposals(const float* const* logits, const float* const
                                   const float* weights4_host, float scale_clamp, float* out_boxes,
                                   float* out_scores, uint8_t* out_valid, void* workspace,
                                   size_t workspace_bytes, void* stream) {
+  return d2mi_rpn_proposals_ex(logits, deltas, nullptr, nullptr, level_hw, strides, cell_anchors,
+                               L, A, N, image_hw, pre_nms_topk, post_nms_topk, nms_thresh,
+                               min_box_side_len, weights4_host, scale_clamp, out_boxes, out_scores,
+                               out_valid, workspace, workspace_bytes, stream);
+}
+
+extern "C" int d2mi_rpn_proposals_ex(const float* const* logits, const float* const* deltas,
+                                     const int64_t* logits_image_stride,
+                                     const int64_t* deltas_image_stride,
+                                     const int32_t* level_hw, const float* strides,
+                                     const float* cell_anchors, int L, int A, int N,
+                                     const int32_t* image_hw, int pre_nms_topk,
+                                     int post_nms_topk, float nms_thresh,
+                                     float min_box_side_len, const float* weights4_host,
+                                     float scale_clamp, float* out_boxes, float* out_scores,
+                                     uint8_t* out_valid, void* workspace, size_t workspace_bytes,
+                                     void* stream) {
   hipStream_t st = as_stream(stream);
   D2MI_REQUIRE(N >= 1 && pre_nms_topk >= 1 && post_nms_topk >= 1, "bad RPN sizes");
   D2MI_REQUIRE(L * post_nms_topk <= kLdsSortCap, "L*post_nms_topk=%d exceeds %d", L * post_nms_topk,
@@ -562,6 +584,17 @@ extern "C" int d2mi_rpn_proposals(const float* const* logits, const float* const
   Levels lv = {};
   int rc = make_levels(lv, logits, deltas, level_hw, strides, cell_anchors, L, A);
   if (rc) return rc;
+  for (int l = 0; l < L; ++l) {  // strided levels (views of one concatenated buffer)
+    if (logits_image_stride) {
+      D2MI_REQUIRE(logits_image_stride[l] >= lv.img_a[l], "logits image stride too small");
+      lv.img_a[l] = logits_image_stride[l];
+    }
+    if (deltas_image_stride) {
+      D2MI_REQUIRE(deltas_image_stride[l] % 4 == 0 && deltas_image_stride[l] / 4 >= lv.img_b[l],
+                   "deltas image stride must be a multiple of 4 covering the level");
+      lv.img_b[l] = deltas_image_stride[l] / 4;
+    }
+  }
   int maxlen = 0;
   for (int l = 0; l < L; ++l) maxlen = std::max(maxlen, lv.H[l] * lv.W[l] * A);
   const int k = std::max(1, std::min(pre_nms_topk, maxlen));

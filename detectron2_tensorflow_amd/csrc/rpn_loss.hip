@@ -173,3 +173,102 @@ extern "C" int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const
   D2MI_LAUNCH_CHECK();
   return 0;
 }
+
+// ------------------------------------------------ RPN head output layout
+namespace d2mi {
+namespace {
+constexpr int kMaxHeadLevels = 8;
+struct HeadLevels {
+  const float* y[kMaxHeadLevels];
+  float* gy[kMaxHeadLevels];
+  int t0[kMaxHeadLevels + 1];  // first pixel of level l in the concatenation
+  int L;
+};
+
+__device__ __forceinline__ int head_level(const HeadLevels& h, int t) {
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxHeadLevels; ++i)
+    if (i < h.L && t >= h.t0[i]) l = i;
+  return l;
+}
+
+// One thread per (image, pixel): its A logits and 4A deltas.
+__global__ __launch_bounds__(256) void rpn_head_gather_kernel(HeadLevels h, int N, int A, int C,
+                                                              float* __restrict__ logits,
+                                                              float* __restrict__ deltas) {
+  const int T = h.t0[h.L];
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * T) return;
+  const int n = (int)(i / T), t = (int)(i - (long long)n * T);
+  const int l = head_level(h, t);
+  const int hw = t - h.t0[l], HW = h.t0[l + 1] - h.t0[l];
+  const float* src = h.y[l] + ((size_t)n * HW + hw) * C;
+  float* lo = logits + i * A;
+  float* de = deltas + i * 4 * A;
+  for (int a = 0; a < A; ++a) lo[a] = src[a];
+  for (int j = 0; j < 4 * A; ++j) de[j] = src[A + j];
+}
+
+__global__ __launch_bounds__(256) void rpn_head_scatter_kernel(HeadLevels h, int N, int A, int C,
+                                                               const float* __restrict__ gl,
+                                                               const float* __restrict__ gd) {
+  const int T = h.t0[h.L];
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * T) return;
+  const int n = (int)(i / T), t = (int)(i - (long long)n * T);
+  const int l = head_level(h, t);
+  const int hw = t - h.t0[l], HW = h.t0[l + 1] - h.t0[l];
+  float* dst = h.gy[l] + ((size_t)n * HW + hw) * C;
+  for (int c = 0; c < C; ++c) {
+    float v = 0.f;
+    if (c < A) v = gl ? gl[i * A + c] : 0.f;
+    else if (c < 5 * A) v = gd ? gd[i * 4 * A + (c - A)] : 0.f;
+    dst[c] = v;
+  }
+}
+
+int head_levels(HeadLevels& h, const int32_t* hw, int L) {
+  D2MI_REQUIRE(L >= 1 && L <= kMaxHeadLevels, "RPN head: %d levels (1..%d)", L, kMaxHeadLevels);
+  h.L = L;
+  h.t0[0] = 0;
+  for (int l = 0; l < L; ++l) {
+    D2MI_REQUIRE(hw[l] > 0, "RPN head: empty level %d", l);
+    h.t0[l + 1] = h.t0[l] + hw[l];
+  }
+  return 0;
+}
+}  // namespace
+}  // namespace d2mi
+
+using namespace d2mi;
+
+extern "C" int d2mi_rpn_head_gather(const float* const* ys, const int32_t* level_hw_flat, int L,
+                                    int N, int A, int C, float* logits, float* deltas,
+                                    void* stream) {
+  HeadLevels h = {};
+  const int rc = head_levels(h, level_hw_flat, L);
+  if (rc) return rc;
+  D2MI_REQUIRE(N >= 1 && A >= 1 && C >= 5 * A && ys && logits && deltas, "bad RPN head gather");
+  for (int l = 0; l < L; ++l) h.y[l] = ys[l];
+  const long long n = (long long)N * h.t0[L];
+  hipLaunchKernelGGL(rpn_head_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), h, N, A, C, logits, deltas);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int d2mi_rpn_head_scatter(const float* g_logits, const float* g_deltas,
+                                     const int32_t* level_hw_flat, int L, int N, int A, int C,
+                                     float* const* gys, void* stream) {
+  HeadLevels h = {};
+  const int rc = head_levels(h, level_hw_flat, L);
+  if (rc) return rc;
+  D2MI_REQUIRE(N >= 1 && A >= 1 && C >= 5 * A && gys, "bad RPN head scatter");
+  for (int l = 0; l < L; ++l) h.gy[l] = gys[l];
+  const long long n = (long long)N * h.t0[L];
+  hipLaunchKernelGGL(rpn_head_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), h, N, A, C, g_logits, g_deltas);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}

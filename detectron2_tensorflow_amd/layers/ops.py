@@ -1431,13 +1431,26 @@ def _level_arrays(tensors, hw, strides, cell_anchors):
     return ptrs, lhw, st, cells, n // (4 * L)
 
 
+def _image_strided(t):
+    """t [N, H, W, C] f32 on the device, dense within each image (any image
+    stride, e.g. a level view of a concatenated [N, sum HWC] buffer)."""
+    N, H, W, C = t.shape
+    return (t.dtype == torch.float32 and t.stride(3) == 1 and t.stride(2) == C
+            and t.stride(1) == W * C and t.stride(0) >= H * W * C)
+
+
 def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk, post_nms_topk,
                   nms_thresh, min_box_side_len=0.0, weights=(1.0, 1.0, 1.0, 1.0),
                   scale_clamp=_DEFAULT_SCALE_CLAMP):
     """find_top_rpn_proposals (rpn_outputs.py:29-132) fused with anchor
-    generation and decode.  logits[l] [N,H,W,A], deltas[l] [N,H,W,A*4]."""
-    logits = [_f32c(t) for t in logits]
-    deltas = [_f32c(t) for t in deltas]
+    generation and decode.  logits[l] [N,H,W,A], deltas[l] [N,H,W,A*4]; each
+    dense within an image, any image stride (level views of the training
+    head's concatenated outputs go in without copies: d2mi_rpn_proposals_ex)."""
+    strided = (all(_image_strided(t) for t in list(logits) + list(deltas))
+               and all(t.data_ptr() % 16 == 0 for t in deltas))
+    if not strided:
+        logits = [_f32c(t) for t in logits]
+        deltas = [_f32c(t) for t in deltas]
     image_hw = _i32c(image_hw)
     _C.require_device(image_hw, *logits, *deltas)
     N = logits[0].shape[0]
@@ -1451,7 +1464,9 @@ def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk,
     ov = torch.empty((N, post_nms_topk), dtype=torch.uint8, device=dev)
     wsb = _C.lib().d2mi_rpn_proposals_workspace_size(N, L, lhw, A, pre_nms_topk, post_nms_topk)
     ws = _C.workspace(wsb, dev)
-    rc = _C.lib().d2mi_rpn_proposals(lp, dp, lhw, st, cells, L, A, N, _C.ptr(image_hw),
+    sl = _C.host_array(_C.ctypes.c_int64, [t.stride(0) for t in logits])
+    sd = _C.host_array(_C.ctypes.c_int64, [t.stride(0) for t in deltas])
+    rc = _C.lib().d2mi_rpn_proposals_ex(lp, dp, sl, sd, lhw, st, cells, L, A, N, _C.ptr(image_hw),
                                      int(pre_nms_topk), int(post_nms_topk), float(nms_thresh),
                                      float(min_box_side_len),
                                      _C.host_array(_C.c_float, [float(w) for w in weights]),
@@ -1459,6 +1474,42 @@ def rpn_proposals(logits, deltas, strides, cell_anchors, image_hw, pre_nms_topk,
                                      _C.ptr(ws), wsb, _C.stream_of(dev))
     _C.check(rc, "d2mi_rpn_proposals")
     return ob, os_, ov.bool()
+
+
+def rpn_head_gather(ys, A):
+    """d2mi_rpn_head_gather: the fused head's per-level outputs ys[l] [N, H, W, C]
+    -> (logits [N, T*A], deltas [N, T*A, 4]) in the RPNOutputs layout."""
+    ys = [_f32c(y) for y in ys]
+    _C.require_device(*ys)
+    N, C = ys[0].shape[0], ys[0].shape[-1]
+    hw = [y.shape[1] * y.shape[2] for y in ys]
+    T = sum(hw)
+    dev = ys[0].device
+    pl = torch.empty((N, T * A), dtype=torch.float32, device=dev)
+    pd = torch.empty((N, T * A, 4), dtype=torch.float32, device=dev)
+    rc = _C.lib().d2mi_rpn_head_gather(_C.host_array(_C.c_void_p, [y.data_ptr() for y in ys]),
+                                       _C.host_array(_C.ctypes.c_int32, hw), len(ys), N, A, C,
+                                       _C.ptr(pl), _C.ptr(pd), _C.stream_of(dev))
+    _C.check(rc, "d2mi_rpn_head_gather")
+    return pl, pd
+
+
+def rpn_head_scatter(g_logits, g_deltas, shapes, A):
+    """Adjoint of rpn_head_gather: -> per-level [N, H, W, C] gradients (every
+    element written; either input may be None = zero)."""
+    g_logits = _f32c(g_logits) if g_logits is not None else None
+    g_deltas = _f32c(g_deltas) if g_deltas is not None else None
+    ref = g_logits if g_logits is not None else g_deltas
+    dev = ref.device
+    N, C = shapes[0][0], shapes[0][-1]
+    outs = [torch.empty(tuple(s), dtype=torch.float32, device=dev) for s in shapes]
+    hw = [s[1] * s[2] for s in shapes]
+    rc = _C.lib().d2mi_rpn_head_scatter(_C.ptr(g_logits), _C.ptr(g_deltas),
+                                        _C.host_array(_C.ctypes.c_int32, hw), len(shapes), N, A, C,
+                                        _C.host_array(_C.c_void_p, [o.data_ptr() for o in outs]),
+                                        _C.stream_of(dev))
+    _C.check(rc, "d2mi_rpn_head_scatter")
+    return outs
 
 
 def fast_rcnn_inference(logits, deltas, proposals, roi_img, roi_slot, num_images, P, image_hw,

@@ -29,6 +29,10 @@ def build_rpn_head(cfg, input_shape, **kwargs):
 
 @RPN_HEAD_REGISTRY.register()
 class StandardRPNHead(Layer):
+    # training: the fused head's outputs gathered into the RPNOutputs layout
+    # in one launch (False: per-level slice copies + concatenation, A/B)
+    CONCAT_OUT = True
+
     def __init__(self, cfg, input_shape, **kwargs):
         super().__init__(**kwargs)
         in_channels = {s.channels for s in input_shape}
@@ -80,6 +84,7 @@ class StandardRPNHead(Layer):
         # returns the sum): autograd's per-level adds and slices go away
         wacc = ({"n": len(features), "k": 0}
                 if fuse and torch.is_grad_enabled() and _RPNHead1x1Fn.ACC_LEVELS else None)
+        ys = []
         for x in features:
             # a level the ROI poolers also read hands its input gradient over
             # (GeneralizedRCNN tags them; the pair_grad protocol)
@@ -94,16 +99,59 @@ class StandardRPNHead(Layer):
                 rpn_features.append(share)
             if fuse:
                 w16, wp, b16 = self._fused_1x1()
-                lg, dl = _RPNHead1x1Fn.apply(share, self.objectness_logits.weights,
-                                             self.objectness_logits.bias,
-                                             self.anchor_deltas.weights, self.anchor_deltas.bias,
-                                             w16, wp, b16, wacc)
-                logits.append(lg)
-                deltas.append(dl)
+                ys.append(_RPNHead1x1Fn.apply(share, self.objectness_logits.weights,
+                                              self.objectness_logits.bias,
+                                              self.anchor_deltas.weights, self.anchor_deltas.bias,
+                                              w16, wp, b16, wacc))
             else:
                 logits.append(self.objectness_logits(share))
                 deltas.append(self.anchor_deltas(share))
+        if fuse and not StandardRPNHead.CONCAT_OUT:  # (A/B: per-level slice copies)
+            A = self.objectness_logits.weights.shape[3]
+            logits = [y[..., :A].contiguous() for y in ys]
+            deltas = [y[..., A:5 * A].contiguous() for y in ys]
+        elif fuse:
+            # the RPNOutputs layout (rpn_outputs.py:346-357) straight from the
+            # fused outputs, one launch each way (_RPNGatherFn); the per-level
+            # logits / deltas handed on are views of it
+            A = self.objectness_logits.weights.shape[3]
+            pl, pd = _RPNGatherFn.apply(A, *ys)
+            logits, deltas = _LevelViews(), _LevelViews()
+            off = 0
+            for y in ys:
+                N, H, W, _ = y.shape
+                logits.append(pl[:, off * A:(off + H * W) * A].view(N, H, W, A))
+                deltas.append(pd[:, off * A:(off + H * W) * A].view(N, H, W, 4 * A))
+                off += H * W
+            logits.concat = deltas.concat = (pl, pd)
         return rpn_features, logits, deltas
+
+
+class _LevelViews(list):
+    """Per-level views of one concatenated [N, sum_l H_l W_l A] (x4) tensor;
+    ``concat`` is that (logits, deltas) pair."""
+    concat = None
+
+
+class _RPNGatherFn(torch.autograd.Function):
+    """The fused 1x1's per-level [N, H, W, 16] outputs -> (objectness logits
+    [N, T*A], anchor deltas [N, T*A, 4]) in the level-major per-image layout
+    of RPNOutputs (rpn_outputs.py:346-357), by d2mi_rpn_head_gather; backward
+    = d2mi_rpn_head_scatter straight into the per-level 16-wide gradients
+    (padding channel zero): no slice copies, concatenations or zero-fills."""
+
+    @staticmethod
+    def forward(ctx, A, *ys):
+        ctx.A = A
+        ctx.shapes = [tuple(y.shape) for y in ys]
+        ctx.set_materialize_grads(False)
+        return ops.rpn_head_gather(ys, A)
+
+    @staticmethod
+    def backward(ctx, g_logits, g_deltas):
+        if g_logits is None and g_deltas is None:
+            return (None,) * (1 + len(ctx.shapes))
+        return (None, *ops.rpn_head_scatter(g_logits, g_deltas, ctx.shapes, ctx.A))
 
 
 class _RPNHead1x1Fn(torch.autograd.Function):
@@ -128,21 +176,17 @@ class _RPNHead1x1Fn(torch.autograd.Function):
         A, D = wo.shape[3], wd.shape[3]
         ctx.save_for_backward(share, w16)
         ctx.relu_info = getattr(share, "_d2mi_relu_info", None) if _RPNHead1x1Fn.GATE else None
-        ctx.set_materialize_grads(False)  # a missing head gradient is zero-filled below
+        ctx.set_materialize_grads(False)  # a missing gradient is a zero one below
         ctx.dims = (A, D, y.shape[-1])
         ctx.wacc = wacc
-        return y[..., :A].contiguous(), y[..., A:A + D].contiguous()
+        return y  # [.., 16]: A logits, 4A deltas, zero padding (_RPNGatherFn splits it)
 
     @staticmethod
-    def backward(ctx, g_logits, g_deltas):
+    def backward(ctx, g16):
         share, w16 = ctx.saved_tensors
         A, D, C16 = ctx.dims
-        lead = share.shape[:-1]
-        parts = [g_logits if g_logits is not None else share.new_zeros(*lead, A),
-                 g_deltas if g_deltas is not None else share.new_zeros(*lead, D)]
-        if C16 > A + D:
-            parts.append(share.new_zeros(*lead, C16 - A - D))
-        g16 = torch.cat(parts, dim=-1)
+        if g16 is None:
+            g16 = share.new_zeros(*share.shape[:-1], C16)
         gx = None
         if ctx.needs_input_grad[0]:
             # 1x1 stride-1 dgrad: the forward weights' HWIO [1, 1, C, 16] is
@@ -228,8 +272,12 @@ class RPN(Layer):
             labels = torch.where(inside, labels, torch.full_like(labels, -1))
         pos, neg = subsample_labels(labels, self.batch_size_per_image, self.positive_fraction, 0)
         norm = 1.0 / (self.batch_size_per_image * N)
-        pl = torch.cat([x.reshape(N, -1) for x in logits], dim=1)
-        pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
+        concat = getattr(logits, "concat", None)
+        if concat is not None:  # the fused head's outputs are already in this layout
+            pl, pd = concat
+        else:
+            pl = torch.cat([x.reshape(N, -1) for x in logits], dim=1)
+            pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
         if pl.is_cuda and gt_boxes.shape[1] > 0:
             # one HIP pass each way: targets, sigmoid CE and smooth-L1 fused
             loss_cls, loss_loc = ops.rpn_loss(pl, pd, anchors, gt_boxes, matches, pos, pos | neg,

@@ -226,6 +226,32 @@ int d2mi_rpn_proposals(const float* const* logits, const float* const* deltas,
                        float min_box_side_len, const float* weights4_host, float scale_clamp,
                        float* out_boxes, float* out_scores, uint8_t* out_valid,
                        void* workspace, size_t workspace_bytes, void* stream);
+/* d2mi_rpn_proposals over strided levels: level l of image n starts
+ * logits_image_stride[l] elements (deltas: deltas_image_stride[l], a multiple
+ * of 4) after image n - 1's, i.e. per-level views of ONE concatenated
+ * [N, sum_l H_l W_l A] (x4) buffer -- the training path's RPN head output
+ * (d2mi_rpn_head_gather), with no per-level copies.  Null strides: dense. */
+int d2mi_rpn_proposals_ex(const float* const* logits, const float* const* deltas,
+                          const int64_t* logits_image_stride, const int64_t* deltas_image_stride,
+                          const int32_t* level_hw, const float* strides,
+                          const float* cell_anchors, int L, int A, int N, const int32_t* image_hw,
+                          int pre_nms_topk, int post_nms_topk, float nms_thresh,
+                          float min_box_side_len, const float* weights4_host, float scale_clamp,
+                          float* out_boxes, float* out_scores, uint8_t* out_valid,
+                          void* workspace, size_t workspace_bytes, void* stream);
+/* RPN head outputs of a training step in the RPNOutputs layout
+ * (rpn_outputs.py:346-357: per-image level-major concatenation): ys[l]
+ * device [N, HW_l, C] (the fused objectness / anchor-delta 1x1 output,
+ * C >= 5A channels: A logits then 4A deltas, the rest padding) ->
+ * logits [N, T*A], deltas [N, T*A, 4], T = sum_l HW_l.  One launch instead
+ * of a slice copy per level and head and two concatenations. */
+int d2mi_rpn_head_gather(const float* const* ys, const int32_t* level_hw_flat, int L, int N,
+                         int A, int C, float* logits, float* deltas, void* stream);
+/* Its adjoint: g_logits [N, T*A], g_deltas [N, T*A, 4] (either nullable =
+ * zero) -> gys[l] [N, HW_l, C], every element written (padding channels 0). */
+int d2mi_rpn_head_scatter(const float* g_logits, const float* g_deltas,
+                          const int32_t* level_hw_flat, int L, int N, int A, int C,
+                          float* const* gys, void* stream);
 
 /* --------------------------------------------------- Fast R-CNN inference
  * FastRCNNOutputs.predict_boxes/predict_probs + fast_rcnn_inference

@@ -64,7 +64,12 @@ def _conv_epi(on):
     ops.set_tuning("conv_epi", 1 if on else 0)
 
 
-SWITCHES = {"fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+def _rpn_concat(on):
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
+    StandardRPNHead.CONCAT_OUT = on
+
+
+SWITCHES = {"rpn_concat": _rpn_concat, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
