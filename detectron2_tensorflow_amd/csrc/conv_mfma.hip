@@ -856,15 +856,16 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // Per staged row, which taps land inside the image (bit t: tap t; the
     // plan gives this kernel <= 32 taps), so a k-step's range test is one bit
     // extract.
+    // Closed form: the valid kw form one run of bits, [max(0, -iw0),
+    // min(KW, W - iw0)), replicated at the KW-bit offsets of the valid kh.
     uint32_t tv[RA];
 #pragma unroll
     for (int p = 0; p < RA; ++p) {
+      const int kw0 = max(0, -iw0[p]), kw1 = min(a.KW, g.W - iw0[p]);
+      const uint32_t cols = kw1 > kw0 ? (uint32_t)((1ull << kw1) - (1ull << kw0)) : 0u;
       uint32_t b = 0;
-      for (int kh = 0; kh < a.KH; ++kh) {
-        const bool rok = (unsigned)(ih0[p] + kh) < (unsigned)g.H;
-        for (int kw = 0; kw < a.KW; ++kw)
-          b |= (rok & ((unsigned)(iw0[p] + kw) < (unsigned)g.W) ? 1u : 0u) << (kh * a.KW + kw);
-      }
+      for (int kh = 0; kh < a.KH; ++kh)
+        b |= ((unsigned)(ih0[p] + kh) < (unsigned)g.H ? cols : 0u) << (kh * a.KW);
       tv[p] = b;
     }
     // weight rows: element offset of (co, schunk) inside a tap's [Cout][Cin]

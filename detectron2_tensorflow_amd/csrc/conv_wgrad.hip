@@ -774,8 +774,9 @@ WPlan wplan(int N, int OH, int OW, int Cin, int Cout, int KH, int KW, bool split
   // too few 256x128 tiles x 16-chunk splits to fill the chip (tools/wgrad_ws1_ab.sh:
   // the FPN p2 lateral 165 -> 140 us, the strided shortcuts 8-13 % faster,
   // the 4.4 GFLOP res4 1x1s 7 % slower)
+  // (tuning value = the GFLOP threshold; 0 = off)
   const bool ws1 = KH * KW == 1 && tuning(kTuneWgradWS1) > 0 &&
-                   2.0 * N * OH * OW * (double)Cin * Cout >= 6e9;
+                   2.0 * N * OH * OW * (double)Cin * Cout >= tuning(kTuneWgradWS1) * 1e9;
   p.ws = split3 && tuning(kTuneWgradWS) > 0 && (KH * KW > 1 || ws1) && Cin % 256 == 0 &&
          Cout % 128 == 0;
   p.BM = p.ws ? 256 : 64 * p.TM;

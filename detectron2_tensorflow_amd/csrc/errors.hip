@@ -22,7 +22,7 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS", "D2MI_ROI_FWD", "D2MI_
                                           "D2MI_WGRAD_XCD", "D2MI_CONV_XCD",
                                           "D2MI_WGRAD_INC", "D2MI_CONV_WS_MINK"};
 // defaults: measured per shape and in the training step
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 0, 1, 1, 1, 1, 16};
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 0, 6, 1, 1, 1, 16};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

@@ -1099,11 +1099,13 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   // long runs (degenerate piles of boxes) in slot order, then their segment
   // partials: grid-stride loops over the device-side task / segment counts
   // (zero in an ordinary step: the launches exit at once)
+  // (small grids: the dispatch of a large grid that only reads a zero count
+  // and exits is most of these launches' cost in an ordinary step)
   hipLaunchKernelGGL(roi_bwd_long_sort_kernel,
-                     dim3((unsigned)std::max(1LL, std::min<long long>(p.max_tasks, 512LL))),
+                     dim3((unsigned)std::max(1LL, std::min<long long>(p.max_tasks, 64LL))),
                      dim3(1024), 0, st, arrival, count, run_start, tasks, ctr, sorted_long);
   D2MI_LAUNCH_CHECK();
-  const dim3 sgrid((unsigned)std::max(1LL, std::min<long long>((p.max_segs + 3) / 4, 1024LL)));
+  const dim3 sgrid((unsigned)std::max(1LL, std::min<long long>((p.max_segs + 3) / 4, 128LL)));
   if (vec4)
     hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
                        count, run_start, seg_first, seg_pixel, ctr, partial);

@@ -800,7 +800,7 @@ def test_conv2d_wgrad_ws_1x1_vs_float64(dev, conf):
                                        dy.permute(0, 3, 1, 2).double(), s, p).permute(2, 3, 1, 0)
     run = lambda: ops().conv2d_wgrad(x.to(dev), dy.to(dev), k, s, (p, p), with_bias=True,
                                      math_mode="split")
-    ops().set_tuning("wgrad_ws1", 1)  # (the default)
+    ops().set_tuning("wgrad_ws1", 6)  # (the default: >= 6 GFLOP)
     dw, db = run()
     dw2, db2 = run()
     scale = float(want.abs().max())

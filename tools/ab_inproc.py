@@ -44,7 +44,7 @@ def _conv_sk(on):
 
 def _wgrad_ws1(on):
     from detectron2_tensorflow_amd.layers import ops
-    ops.set_tuning("wgrad_ws1", 1 if on else 0)
+    ops.set_tuning("wgrad_ws1", 6 if on else 0)
 
 
 def _stem_mfma(on):
