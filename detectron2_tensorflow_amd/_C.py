@@ -123,6 +123,8 @@ _SIGS = {
     "d2mi_match_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_match_boxes": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_float,
                                  c_float, P, P, P, c_size_t, P]),
+    "d2mi_match_boxes_ex": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
+                                    c_float, c_float, P, P, P, c_size_t, P]),
     "d2mi_stem_pool": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_stem_conv": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "d2mi_rpn_loss_blocks": (c_int, []),

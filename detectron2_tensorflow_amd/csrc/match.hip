@@ -47,9 +47,25 @@ struct MatchConf {
   float crowd_thr, diff_thr;
 };
 
-// flags: bit0 valid (matchable), bit1 crowd, bit2 difficult
+// flags: bit0 valid (matchable), bit1 crowd, bit2 difficult -- packed int32
+// per GT, or (packed null) three byte masks (crowd / difficult nullable):
+// d2mi_match_boxes_ex takes the bool tensors as they are, no packing passes.
+struct FlagSrc {
+  const int* packed;
+  const uint8_t* m;
+  const uint8_t* c;
+  const uint8_t* d;
+};
+__device__ __forceinline__ int flag_at(const FlagSrc& f, size_t i) {
+  if (f.packed) return f.packed[i];
+  int v = f.m[i] ? 1 : 0;
+  if (f.c && f.c[i]) v |= 2;
+  if (f.d && f.d[i]) v |= 4;
+  return v;
+}
+
 __global__ __launch_bounds__(256) void best_gt_kernel(const float4* __restrict__ gt,
-                                                      const int* __restrict__ flags,
+                                                      const FlagSrc flags,
                                                       const float4* __restrict__ boxes,
                                                       long long box_stride, int G, int P,
                                                       unsigned* __restrict__ best) {
@@ -59,7 +75,7 @@ __global__ __launch_bounds__(256) void best_gt_kernel(const float4* __restrict__
   const int n = blockIdx.y;
   for (int g = threadIdx.x; g < G; g += 256) {
     g_s[g] = gt[(size_t)n * G + g];
-    f_s[g] = flags[(size_t)n * G + g];
+    f_s[g] = flag_at(flags, (size_t)n * G + g);
   }
   __syncthreads();
   constexpr int kPer = 4;
@@ -91,7 +107,7 @@ __global__ __launch_bounds__(256) void best_gt_kernel(const float4* __restrict__
 }
 
 __global__ __launch_bounds__(256) void match_kernel(const float4* __restrict__ gt,
-                                                    const int* __restrict__ flags,
+                                                    const FlagSrc flags,
                                                     const float4* __restrict__ boxes,
                                                     long long box_stride, int G, int P,
                                                     MatchConf c, const unsigned* __restrict__ best,
@@ -103,7 +119,7 @@ __global__ __launch_bounds__(256) void match_kernel(const float4* __restrict__ g
   const int n = blockIdx.y;
   for (int g = threadIdx.x; g < G; g += 256) {
     g_s[g] = gt[(size_t)n * G + g];
-    f_s[g] = flags[(size_t)n * G + g];
+    f_s[g] = flag_at(flags, (size_t)n * G + g);
     b_s[g] = (c.allow_low && (f_s[g] & 1)) ? unord(best[(size_t)n * G + g]) : 0.f;
   }
   __syncthreads();
@@ -151,12 +167,44 @@ extern "C" size_t d2mi_match_workspace_size(int N, int G) {
   return (size_t)(N > 0 ? N : 0) * (size_t)(G > 0 ? G : 0) * sizeof(unsigned);
 }
 
+static int match_core(const float* gt_boxes, FlagSrc gt_flags, const float* boxes,
+                      int boxes_per_image, int N, int G, int P, const float* thresholds,
+                      const int* labels_of, int n_intervals, int allow_low_quality,
+                      float crowd_thr, float difficult_thr, long long* matches, long long* labels,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
 extern "C" int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, const float* boxes,
                                 int boxes_per_image, int N, int G, int P,
                                 const float* thresholds, const int* labels_of, int n_intervals,
                                 int allow_low_quality, float crowd_thr, float difficult_thr,
                                 long long* matches, long long* labels, void* workspace,
                                 size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(gt_flags != nullptr || G == 0, "match: null flags");
+  return match_core(gt_boxes, FlagSrc{gt_flags, nullptr, nullptr, nullptr}, boxes,
+                    boxes_per_image, N, G, P, thresholds, labels_of, n_intervals,
+                    allow_low_quality, crowd_thr, difficult_thr, matches, labels, workspace,
+                    workspace_bytes, stream);
+}
+
+extern "C" int d2mi_match_boxes_ex(const float* gt_boxes, const uint8_t* matchable,
+                                   const uint8_t* crowd, const uint8_t* difficult,
+                                   const float* boxes, int boxes_per_image, int N, int G, int P,
+                                   const float* thresholds, const int* labels_of, int n_intervals,
+                                   int allow_low_quality, float crowd_thr, float difficult_thr,
+                                   long long* matches, long long* labels, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  D2MI_REQUIRE(matchable != nullptr || G == 0, "match: null matchable mask");
+  return match_core(gt_boxes, FlagSrc{nullptr, matchable, crowd, difficult}, boxes,
+                    boxes_per_image, N, G, P, thresholds, labels_of, n_intervals,
+                    allow_low_quality, crowd_thr, difficult_thr, matches, labels, workspace,
+                    workspace_bytes, stream);
+}
+
+static int match_core(const float* gt_boxes, FlagSrc gt_flags, const float* boxes,
+                      int boxes_per_image, int N, int G, int P, const float* thresholds,
+                      const int* labels_of, int n_intervals, int allow_low_quality,
+                      float crowd_thr, float difficult_thr, long long* matches, long long* labels,
+                      void* workspace, size_t workspace_bytes, void* stream) {
   D2MI_REQUIRE(N > 0 && G >= 0 && P >= 0, "bad match shape");
   D2MI_REQUIRE(G <= kMaxGt, "match: at most %d ground-truth boxes per image (got %d)", kMaxGt, G);
   D2MI_REQUIRE(n_intervals >= 1 && n_intervals <= 4, "match: 1..4 threshold intervals");

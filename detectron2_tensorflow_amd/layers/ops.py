@@ -809,6 +809,47 @@ def match_boxes(gt_boxes, gt_flags, boxes, thresholds, labels_of, allow_low_qual
     return matches, labels
 
 
+def _mask_u8(m):
+    """A [N, G] bool / integer mask as contiguous bytes (bool: a free view)."""
+    if m is None:
+        return None
+    m = m.contiguous()
+    return m.view(torch.uint8) if m.dtype == torch.bool else (m != 0).view(torch.uint8)
+
+
+def match_boxes_masks(gt_boxes, matchable, boxes, thresholds, labels_of, allow_low_quality,
+                      crowd=None, difficult=None, crowd_thr=1e-3, difficult_thr=float("inf")):
+    """match_boxes with the GT flags as [N, G] masks (d2mi_match_boxes_ex):
+    matchable required, crowd / difficult optional -- the bool tensors are
+    passed as they are, no int32 packing launches."""
+    gt_boxes = _f32c(gt_boxes)
+    boxes = _f32c(boxes)
+    m, c, d = _mask_u8(matchable), _mask_u8(crowd), _mask_u8(difficult)
+    _C.require_device(gt_boxes, m, boxes, *[t for t in (c, d) if t is not None])
+    N, G = m.shape
+    for t in (c, d):
+        if t is not None and tuple(t.shape) != (N, G):
+            raise ValueError("match_boxes_masks: crowd / difficult must be [N, G] like matchable")
+    per_image = boxes.dim() == 3
+    P = boxes.shape[-2]
+    matches = torch.empty((N, P), dtype=torch.int64, device=boxes.device)
+    labels = torch.empty((N, P), dtype=torch.int64, device=boxes.device)
+    thr = _C.host_array(_C.c_float, [float(t) for t in thresholds])
+    lab = _C.host_array(_C.ctypes.c_int32, [int(v) for v in labels_of])
+    wsb = _C.lib().d2mi_match_workspace_size(N, G)
+    ws = _C.workspace(wsb, boxes.device)
+    nul = _C.c_void_p(None)
+    rc = _C.lib().d2mi_match_boxes_ex(_C.ptr(gt_boxes), _C.ptr(m),
+                                      _C.ptr(c) if c is not None else nul,
+                                      _C.ptr(d) if d is not None else nul, _C.ptr(boxes),
+                                      int(per_image), N, G, P, thr, lab, len(labels_of),
+                                      int(bool(allow_low_quality)), float(crowd_thr),
+                                      float(difficult_thr), _C.ptr(matches), _C.ptr(labels),
+                                      _C.ptr(ws), wsb, _C.stream_of(boxes.device))
+    _C.check(rc, "d2mi_match_boxes_ex")
+    return matches, labels
+
+
 class _RPNLossFn(torch.autograd.Function):
     """(loss_cls_sum, loss_loc_sum) of the RPN (d2mi_rpn_loss_fwd / _bwd);
     differentiable w.r.t. logits and deltas."""

@@ -73,14 +73,10 @@ def match_boxes(matcher, gt_boxes, matchable, boxes, crowd=None, difficult=None)
     the tensor formulation.  boxes [P, 4] shared or [N, P, 4]."""
     N = gt_boxes.shape[0]
     if boxes.is_cuda:
-        flags = matchable.to(torch.int32)
-        if crowd is not None:
-            flags = flags | (crowd.to(torch.int32) << 1)
-        if difficult is not None:
-            flags = flags | (difficult.to(torch.int32) << 2)
-        return ops.match_boxes(gt_boxes, flags, boxes, matcher.thresholds, matcher.labels,
-                               matcher.allow_low_quality_matches, crowd_thr=1e-3,
-                               difficult_thr=matcher.thresholds[1])
+        return ops.match_boxes_masks(gt_boxes, matchable, boxes, matcher.thresholds,
+                                     matcher.labels, matcher.allow_low_quality_matches,
+                                     crowd=crowd, difficult=difficult, crowd_thr=1e-3,
+                                     difficult_thr=matcher.thresholds[1])
     b = boxes if boxes.dim() == 3 else boxes[None].expand(N, -1, -1)
     iou = pairwise_iou(gt_boxes, b)
     zq = torch.zeros_like(iou)

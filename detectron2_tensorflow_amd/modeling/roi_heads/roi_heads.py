@@ -22,6 +22,28 @@ from .mask_head import build_mask_head, mask_rcnn_inference, mask_rcnn_loss
 
 from ...layers import Layer
 
+
+# Per-step constant index tensors (image id of each row, per-image bases),
+# cached per shape and device: read-only, so one tensor serves every step
+# (two launches each fewer per use).
+_INDEX_CACHE = {}
+
+
+def _cached_index(kind, n, m, device):
+    key = (kind, int(n), int(m), str(device))
+    t = _INDEX_CACHE.get(key)
+    if t is None:
+        if len(_INDEX_CACHE) > 256:
+            _INDEX_CACHE.clear()
+        if kind == "img":  # arange(n).repeat_interleave(m), int32
+            t = torch.arange(n, dtype=torch.int32, device=device).repeat_interleave(m)
+        elif kind == "slot":  # arange(m).repeat(n), int32
+            t = torch.arange(m, dtype=torch.int32, device=device).repeat(n)
+        else:  # "base": arange(n)[:, None] * m, int64
+            t = torch.arange(n, device=device)[:, None] * m
+        _INDEX_CACHE[key] = t
+    return t
+
 ROI_HEADS_REGISTRY = Registry("ROI_HEADS")
 
 # GPU: the sampled ROI batch in fg-first order straight from the fused
@@ -170,8 +192,8 @@ class StandardROIHeads(ROIHeads):
         valid = proposals.get_field("is_valid")
         N, P = valid.shape
         dev = boxes.device
-        img = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(P)
-        slot = torch.arange(P, dtype=torch.int32, device=dev).repeat(N)
+        img = _cached_index("img", N, P, dev)
+        slot = _cached_index("slot", N, P, dev)
         slot = torch.where(valid.reshape(-1), slot, torch.full_like(slot, -1))
         x = self.box_pooler.pool(feats, boxes.reshape(-1, 4), img)
         x = self.box_head(x)
@@ -190,7 +212,7 @@ class StandardROIHeads(ROIHeads):
     def _box_losses(self, feats, sampled, grad_share=None):
         boxes = sampled["boxes"]
         N, S = boxes.shape[:2]
-        img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(S)
+        img = _cached_index("img", N, S, boxes.device)
         x = self.box_pooler.pool(feats, boxes.reshape(-1, 4).contiguous(), img,
                                  grad_share=grad_share)
         logits, deltas = self.box_predictor(self.box_head(x))
@@ -214,10 +236,10 @@ class StandardROIHeads(ROIHeads):
         dev = boxes.device
         cls = sampled["gt_classes"][:, :F_].reshape(-1)
         fg = self._mask_fg(sampled)
-        img = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(F_)
+        img = _cached_index("img", N, F_, dev)
         gm = targets["gt_masks"]
         G = gm.shape[1]
-        mind = (sampled["gt_index"][:, :F_] + torch.arange(N, device=dev)[:, None] * G).reshape(-1)
+        mind = (sampled["gt_index"][:, :F_] + _cached_index("base", N, G, dev)).reshape(-1)
         gt_boxes = sampled["gt_boxes"][:, :F_].reshape(-1, 4)
         if self.mask_compact_rows:
             # The reference runs the mask head on the foreground proposals only
@@ -229,8 +251,8 @@ class StandardROIHeads(ROIHeads):
                    else host_sync.read_ints(fg.sum()))[0]
             B = fg.numel()
             R = min(B, max(self.MASK_ROW_BUCKET, -(-nfg // self.MASK_ROW_BUCKET) * self.MASK_ROW_BUCKET))
-            key = (~fg).to(torch.int64) * B + torch.arange(B, device=dev)
-            rows = key.sort().values[:R] % B
+            # fg rows first, each group in index order (a stable sort of ~fg)
+            rows = torch.argsort((~fg).to(torch.uint8), stable=True)[:R]
             boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))
             self.last_mask_rows = R
         else:
@@ -248,7 +270,7 @@ class StandardROIHeads(ROIHeads):
         feats = [features[f] for f in self.in_features]
         boxes = instances.boxes
         N, D = boxes.shape[:2]
-        img = torch.arange(N, dtype=torch.int32, device=boxes.device).repeat_interleave(D)
+        img = _cached_index("img", N, D, boxes.device)
         x = self.mask_pooler.pool(feats, boxes.reshape(-1, 4), img)
         deconv, logits = self.mask_head(x)
         masks = mask_rcnn_inference(logits, instances.get_field("pred_classes").reshape(-1))

@@ -1200,6 +1200,35 @@ def test_fused_match_equals_tensor_matcher(dev, allow_low, per_image):
     assert (want[1] == 1).any() and (want[1] == -1).any() and (want[1] == 0).any()
 
 
+def test_match_masks_abi_equals_packed_flags(dev):
+    """d2mi_match_boxes_ex (byte masks, crowd / difficult optional) == the
+    packed-int32 d2mi_match_boxes on the same GT, with and without the
+    optional masks."""
+    from detectron2_tensorflow_amd.layers import ops
+    g = torch.Generator().manual_seed(9)
+    N, G, P = 2, 12, 3000
+    def boxes(k):
+        c = torch.rand(k, 2, generator=g) * 400
+        hw = torch.rand(k, 2, generator=g) * 150 + 4
+        return torch.cat([c - hw / 2, c + hw / 2], 1)
+    gt = boxes(N * G).reshape(N, G, 4).to(dev)
+    bx = boxes(P).to(dev)
+    valid = (torch.rand(N, G, generator=g) < 0.8).to(dev)
+    crowd = (torch.rand(N, G, generator=g) < 0.3).to(dev)
+    diff = (torch.rand(N, G, generator=g) < 0.3).to(dev)
+    thr, lab = [-math.inf, 0.3, 0.7, math.inf], [0, -1, 1]
+    for c, d in ((crowd, diff), (None, diff), (crowd, None), (None, None)):
+        flags = valid.to(torch.int32)
+        if c is not None:
+            flags = flags | (c.to(torch.int32) << 1)
+        if d is not None:
+            flags = flags | (d.to(torch.int32) << 2)
+        kw = dict(crowd_thr=1e-3, difficult_thr=0.3)
+        want = ops.match_boxes(gt, flags, bx, thr, lab, True, **kw)
+        got = ops.match_boxes_masks(gt, valid, bx, thr, lab, True, crowd=c, difficult=d, **kw)
+        assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+
+
 def test_sampling_smallest_keys_on_hip_topk(dev):
     """subsample_labels' k-smallest selection on the HIP segmented radix select
     equals torch.topk's on the CPU (distinct keys): per-row limits, rows with
