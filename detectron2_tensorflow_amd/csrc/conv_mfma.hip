@@ -44,6 +44,9 @@
 #include "common.h"
 #include "internal.h"
 
+#include <mutex>
+#include <vector>
+
 namespace d2mi {
 namespace {
 
@@ -123,6 +126,10 @@ struct ConvArgs {
   // over gridDim.x workgroups; partial slabs [piece][M][Cout]
   int sk, sk_T, sk_P;
   int xcd2;  // xcd_tile(): the 2-D XCD-contiguous remap (tuning conv_xcd, default 1)
+  // split-K fix-up inside the launch (splitk_fixup, tuning conv_fix): one
+  // arrival counter per tile (the stream's zeroed pool); null: the separate
+  // splitk_reduce4_kernel launch
+  unsigned* tile_cnt;
   // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
   // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
   // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
@@ -330,6 +337,87 @@ __device__ __forceinline__ void store_partial(const ConvArgs& a, const Geo& g,
       for (int r = 0; r < 16; ++r) {
         const int dm = (r & 3) + 8 * (r >> 2);
         if (mb + dm < g.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// Split-K fix-up inside the conv launch (ConvArgs::tile_cnt): every
+// workgroup of a split tile stores its raw partial slab, drains its stores and
+// draws an arrival ticket on the tile's counter behind one agent-scope release
+// (the XCD L2s are not coherent with each other); the workgroup that draws the
+// last ticket takes one agent-scope acquire, sums the tile's slabs in split
+// order 0..S-1 -- splitk_reduce4_kernel's order, so the outputs are
+// bit-identical to the two-launch form -- applies the epilogue and resets the
+// counter.  Nobody waits on anybody (no residency assumption); the counters
+// start zeroed (fix_counters) and every launch leaves them zero.  All NT
+// threads call it; `lds` is the kernel's own LDS array (free after the main
+// loop: one __shared__ object, so the k-loop's waits are unaffected).
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void splitk_fixup(const ConvArgs& a, const Geo& g, int tile, int m0,
+                                             int n0, float* lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(a.tile_cnt + tile, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(a.splits - 1);
+    if (last) {
+      __hip_atomic_exchange(a.tile_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    reinterpret_cast<int*>(lds)[0] = last;
+  }
+  __syncthreads();
+  if (!reinterpret_cast<volatile int*>(lds)[0]) return;
+  constexpr int F4 = BN / 4;
+  constexpr int Q = BM * F4 / NT;  // float4 per thread
+  constexpr int QB = Q < 8 ? Q : 8;
+  static_assert(Q % QB == 0, "fix-up batch");
+  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
+  const size_t slab4 = (size_t)g.pstride * a.Cout / 4;
+#pragma unroll
+  for (int q0 = 0; q0 < Q; q0 += QB) {
+    size_t off[QB];
+    int mm[QB], cc[QB];
+    float4 acc[QB];
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int idx = threadIdx.x + NT * (q0 + q);
+      const int r = idx / F4, c4 = idx - r * F4;
+      mm[q] = m0 + r;
+      cc[q] = n0 + 4 * c4;
+      // clamped addresses: every load is issued (no per-element branches
+      // around loads), only the stores are masked
+      const int ml = min(mm[q], g.M - 1) - g.prow0, cl = min(cc[q], a.Cout - 4);
+      off[q] = ((size_t)ml * a.Cout + cl) / 4;
+      acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int s = 0; s < a.splits; ++s) {
+      float4 v[QB];
+#pragma unroll
+      for (int q = 0; q < QB; ++q) v[q] = p4[(size_t)s * slab4 + off[q]];
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        acc[q].x += v[q].x;
+        acc[q].y += v[q].y;
+        acc[q].z += v[q].z;
+        acc[q].w += v[q].w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int m = mm[q], co = cc[q];
+      if (m < g.M && co < a.Cout) {
+        float4 o;
+        o.x = epilogue(a, g, acc[q].x, m, co);
+        o.y = epilogue(a, g, acc[q].y, m, co + 1);
+        o.z = epilogue(a, g, acc[q].z, m, co + 2);
+        o.w = epilogue(a, g, acc[q].w, m, co + 3);
+        *reinterpret_cast<float4*>(g.y + (size_t)m * a.Cout + co) = o;
       }
     }
   }
@@ -743,9 +831,12 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // split-K partial slabs leave straight from the accumulators (each store
   // instruction writes two whole 128-B row segments; no LDS round trip and
   // none of its barriers) unless tuning conv_epi = 0
-  if (a.splits > 1 && a.reg_partials)
+  if (a.splits > 1 && a.reg_partials) {
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, true);
-  else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
+    if constexpr (!ML) {
+      if (a.tile_cnt) splitk_fixup<BM, BN, 256>(a, g, tile, m0, n0, &As[0][0]);
+    }
+  } else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
     store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                       &As[0][0]);
   else
@@ -1118,6 +1209,9 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   const int m0 = mt * BM, n0 = nt * BN;
   if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
     if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
+    if constexpr (!ML) {
+      if (a.tile_cnt) splitk_fixup<BM, BN, 1024>(a, g, tile, m0, n0, smem);
+    }
     return;
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
@@ -1487,6 +1581,35 @@ struct Plan {
   int sk, sk_T, sk_P, sk_slabs;
   size_t ws_bytes;
 };
+
+// Tile counters of the in-launch split-K fix-up (splitk_fixup): one pool
+// per (device, stream), zeroed by a stream-ordered memset when it is made.
+// Launches on one stream never overlap and each leaves its counters zero
+// again, so one pool serves every launch on its stream.  Null (allocation
+// failed): the caller keeps the separate reduce launch.
+constexpr int kFixCounters = 1 << 16;
+static unsigned* fix_counters(hipStream_t st) {
+  struct Pool {
+    int dev;
+    hipStream_t st;
+    unsigned* p;
+  };
+  static std::mutex mu;
+  static std::vector<Pool> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Pool& e : pools)
+    if (e.dev == dev && e.st == st) return e.p;
+  unsigned* p = nullptr;
+  if (hipMalloc(&p, kFixCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kFixCounters * sizeof(unsigned), st) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  pools.push_back(Pool{dev, st, p});
+  return p;
+}
 
 // Resident workgroups of the 128-wide conv tiles: 2 per CU.
 // Resident workgroups per CU of a plan's kernel: the 128x128 split kernel
@@ -1859,8 +1982,21 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   static const char* force = getenv("D2MI_CONV_DB");
   bool db = false;
   if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
-  auto launch = [&](const ConvArgs& c) {
+  // tuning conv_fix (default 0): the split-K sum and epilogue in the conv
+  // launch itself (the last-arriving workgroup of each tile), not a second
+  // launch.  Bit-identical, but SLOWER (tools/fix_check.sh): the last
+  // arriver reads its tile's S slabs of 64-128 KiB alone (~100 GB/s per
+  // workgroup), where the reduce launch spreads the same bytes over the chip
+  // -- the 16 forward shapes 1634 -> 1721 us (res5 3x3 67 -> 85, mask-head
+  // 3x3 54 -> 68), the training step +6.2 % in-process.  Kept as the A/B knob.
+  const bool fix = tuning(kTuneConvFix) > 0 && !x3 && a.reg_partials && Cout % 4 == 0 &&
+                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)workspace & 15) == 0 &&
+                   a.nM * a.nN <= kFixCounters;
+  unsigned* const cnt = fix ? fix_counters(st) : nullptr;
+  auto launch = [&](ConvArgs c) {
     const dim3 g(c.sk ? c.sk_P : c.ntiles, c.sk ? 1 : c.splits);
+    const bool fused = cnt && !c.sk && c.splits > 1;
+    c.tile_cnt = fused ? cnt : nullptr;
     if (x3)
       launch_x3(p.cfg, db, g, st, c);
     else if (flags & kSplit3)
@@ -1872,7 +2008,7 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
       const int gr = (int)std::min<int64_t>(((int64_t)c.M * Cout / 4 + 255) / 256, 8192);
       hipLaunchKernelGGL(sk_reduce4_kernel, dim3(gr), dim3(256), 0, st, c);
       D2MI_LAUNCH_CHECK();
-    } else if (c.splits > 1) {
+    } else if (c.splits > 1 && !fused) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
       if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
         const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);

@@ -575,6 +575,36 @@ def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
 
 
 @pytest.mark.parametrize("shape", [
+    (2, 25, 42, 512, 512, 3),    # res5 3x3 on the WS kernel: 36 tiles x 7 splits
+    (2, 50, 84, 1024, 256, 1),   # res4 1x1 reduce: WS, 3 splits
+    (1, 20, 30, 64, 64, 3),      # Cout 64: the 128x64 kernel's split-K (5 tiles x 2)
+])
+def test_conv2d_in_launch_fixup_bit_identical(dev, shape):
+    """Tuning conv_fix (the split-K slabs summed by each tile's last-arriving
+    workgroup inside the conv launch, agent-scope release / acquire across
+    XCDs) gives the separate reduce launch's outputs bit for bit -- with a
+    residual + ReLU epilogue, and twice in a row (the counters are left zero)."""
+    N, H, W, Cin, Cout, k = shape
+    pad = (k - 1) // 2
+    g = torch.Generator().manual_seed(7 + sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    w = (torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    res = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    wp = ops().pack_conv_weights(w)
+    run = lambda: ops().conv2d_nhwc(x, wp, b, 1, (pad, pad), math_mode="split", relu=True,
+                                    residual=res, relu_after_add=True)
+    try:
+        ops().set_tuning("conv_fix", 0)
+        y0 = run()
+        ops().set_tuning("conv_fix", 1)
+        y1, y2 = run(), run()
+    finally:
+        ops().set_tuning("conv_fix", 0)  # the default
+    assert torch.equal(y1, y0) and torch.equal(y2, y0)
+
+
+@pytest.mark.parametrize("shape", [
     (2, 100, 168, 128, 128, 3),  # res3 3x3: 132 tiles of a 256-CU chip
     (2, 50, 84, 1024, 512, 1),   # res4 -> res5 1x1: 132 tiles
 ])

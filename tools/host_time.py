@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="train")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cprofile", type=int, default=0,
+                    help="also cProfile this many steps and print the top host functions")
     a = ap.parse_args()
     import bench
     sys.argv = [sys.argv[0], "--mode", a.mode]
@@ -61,6 +63,18 @@ def main():
             hs.append((t1 - t0) * 1e3)
             ws.append((t2 - t0) * 1e3)
             bs.append(host_sync.blocked_s * 1e3)
+        if a.cprofile:
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(a.cprofile):
+                step()
+            pr.disable()
+            torch.cuda.synchronize()
+            st = pstats.Stats(pr)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumulative").print_stats(60)
     med = lambda v: sorted(v)[len(v) // 2]
     busy = [h - b for h, b in zip(hs, bs)]
     print(f"host_ms median {med(hs):.2f}  blocked_in_syncs_ms {med(bs):.2f}  "
