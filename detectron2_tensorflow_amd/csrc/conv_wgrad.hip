@@ -38,6 +38,9 @@ struct WgradArgs {
   int P;                      // N*OH*OW
   int nCi, nCo, ntiles;       // channel tiles per tap, co tiles, total tiles
   int splits, chunks_per_split, nchunks;
+  // the partial slabs are written (splits > 1, or an accumulating call:
+  // the reduce then adds the sum into dw / dbias)
+  int part;
   int x_bytes, dy_bytes;  // buffer ranges (split kernel; < 2 GiB)
   // D2MI_WGRAD_PRIO (default 1, 0 off): wave priority 1 while issuing the
   // chunk's MFMAs, as conv_mfma.hip.  Measured (tools/ab_prio.sh): the wgrad
@@ -183,13 +186,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   }
 
   if (do_bias && tid < BN && co0 + tid < a.Cout) {
-    if (a.splits > 1) a.pbias[(size_t)split * a.Cout + co0 + tid] = bsum;
+    if (a.part) a.pbias[(size_t)split * a.Cout + co0 + tid] = bsum;
     else a.dbias[co0 + tid] = bsum;
   }
 
   // C/D map for 32x32: col (co) = lane & 31, row (ci) = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const size_t wsz = (size_t)a.KH * a.KW * a.Cin * a.Cout;
-  float* out = a.splits > 1 ? a.partial + (size_t)split * wsz : a.dw;
+  float* out = a.part ? a.partial + (size_t)split * wsz : a.dw;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int co = co0 + (wc * TN + j) * 32 + li;
@@ -210,9 +213,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
 // gradient when pbias follows the weight partials.
 // float4 form (total % 4 == 0, 16-B aligned): the same per-element split
 // order, four elements and their split loads in flight per thread.
+// accum: dw / dbias += the sum (a level accumulator: the old value plus this
+// call's gradient, autograd's order for a weight shared by several calls).
 __global__ void wgrad_reduce4_kernel(const float4* __restrict__ partial, int splits, size_t total4,
                                      float4* __restrict__ dw, const float* __restrict__ pbias,
-                                     int Cout, float* __restrict__ dbias) {
+                                     int Cout, float* __restrict__ dbias, int accum) {
   const size_t n = total4 + (dbias ? (size_t)Cout : 0);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -226,30 +231,37 @@ __global__ void wgrad_reduce4_kernel(const float4* __restrict__ partial, int spl
         s.z += v.z;
         s.w += v.w;
       }
+      if (accum) {
+        const float4 o = dw[i];
+        s.x = o.x + s.x;
+        s.y = o.y + s.y;
+        s.z = o.z + s.z;
+        s.w = o.w + s.w;
+      }
       dw[i] = s;
     } else {
       const size_t c = i - total4;
       float s = 0.f;
       for (int k = 0; k < splits; ++k) s += pbias[(size_t)k * Cout + c];
-      dbias[c] = s;
+      dbias[c] = accum ? dbias[c] + s : s;
     }
   }
 }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int splits, size_t total,
                                     float* __restrict__ dw, const float* __restrict__ pbias,
-                                    int Cout, float* __restrict__ dbias) {
+                                    int Cout, float* __restrict__ dbias, int accum) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total + Cout;
        i += (size_t)gridDim.x * blockDim.x) {
     if (i < total) {
       float s = 0.f;
       for (int k = 0; k < splits; ++k) s += partial[(size_t)k * total + i];
-      dw[i] = s;
+      dw[i] = accum ? dw[i] + s : s;
     } else if (dbias) {
       const size_t c = i - total;
       float s = 0.f;
       for (int k = 0; k < splits; ++k) s += pbias[(size_t)k * Cout + c];
-      dbias[c] = s;
+      dbias[c] = accum ? dbias[c] + s : s;
     }
   }
 }
@@ -441,13 +453,13 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_split_kernel(WgradArgs a,
       float s = 0.f;
 #pragma unroll
       for (int g = 0; g < 8; ++g) s += bred[g][tid];
-      if (a.splits > 1) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
+      if (a.part) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
       else a.dbias[co0 + tid] = s;
     }
   }
 
   const size_t wsz = (size_t)a.KH * a.KW * a.Cin * a.Cout;
-  float* out = a.splits > 1 ? a.partial + (size_t)split * wsz : a.dw;
+  float* out = a.part ? a.partial + (size_t)split * wsz : a.dw;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int oc = co0 + (wc * TN + j) * 32 + li;
@@ -708,13 +720,13 @@ __global__ __launch_bounds__(1024, 1) void conv_wgrad_ws_kernel(WgradArgs a, Fas
       float s = 0.f;
 #pragma unroll
       for (int g = 0; g < 8; ++g) s += bred[g][tid];
-      if (a.splits > 1) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
+      if (a.part) a.pbias[(size_t)split * a.Cout + co0 + tid] = s;
       else a.dbias[co0 + tid] = s;
     }
   }
   if (wave >= 8) return;
   const size_t wsz = (size_t)a.KH * a.KW * a.Cin * a.Cout;
-  float* out = a.splits > 1 ? a.partial + (size_t)split * wsz : a.dw;
+  float* out = a.part ? a.partial + (size_t)split * wsz : a.dw;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int oc = co0 + (wc * TN + j) * 32 + li;
@@ -838,7 +850,9 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
                                     float* dbias, int N, int H, int W, int Cin, int Cout, int KH,
                                     int KW, int stride, int pad_beg, int pad_end, int flags,
                                     void* workspace, size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE((flags & ~4) == 0, "wgrad flags: bit2 = split-bf16 products");
+  D2MI_REQUIRE((flags & ~12) == 0,
+               "wgrad flags: bit2 = split-bf16 products, bit3 = accumulate into dw / dbias");
+  const bool accum = (flags & 8) != 0;
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0 && Cout % 4 == 0, "Cin and Cout must be multiples of 4 (%d, %d)",
@@ -877,14 +891,20 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
     p.splits = 1;
     p.chunks_per_split = p.nchunks;
   }
+  if (accum)  // the sum goes through the reduce, which adds it: one slab at least
+    D2MI_REQUIRE(workspace != nullptr &&
+                     workspace_bytes >= (size_t)p.splits *
+                                            ((size_t)KH * KW * Cin * Cout + Cout) * sizeof(float),
+                 "accumulating wgrad: workspace must hold %d slab(s)", p.splits);
   a.nCi = (Cin + p.BM - 1) / p.BM;
   a.nCo = (Cout + p.BN - 1) / p.BN;
   a.ntiles = p.ntiles;
   a.splits = p.splits;
   a.chunks_per_split = p.chunks_per_split;
   a.nchunks = p.nchunks;
-  a.partial = p.splits > 1 ? (float*)workspace : nullptr;
-  a.pbias = p.splits > 1 ? (float*)workspace + (size_t)p.splits * KH * KW * Cin * Cout : nullptr;
+  a.part = p.splits > 1 || accum;
+  a.partial = a.part ? (float*)workspace : nullptr;
+  a.pbias = a.part ? (float*)workspace + (size_t)p.splits * KH * KW * Cin * Cout : nullptr;
   hipStream_t st = as_stream(stream);
   dim3 grid(a.ntiles, a.splits);
   if (split3) {
@@ -927,18 +947,18 @@ extern "C" int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_h
   else
     hipLaunchKernelGGL((conv_wgrad_kernel<1, 1>), grid, dim3(256), 0, st, a);
   D2MI_LAUNCH_CHECK();
-  if (a.splits > 1) {
+  if (a.part) {
     const size_t total = (size_t)KH * KW * Cin * Cout;
     if (total % 4 == 0 && ((uintptr_t)a.partial & 15) == 0 && ((uintptr_t)dw_hwio & 15) == 0) {
       const size_t total4 = total / 4;
       const int g4 = (int)std::min<size_t>((total4 + Cout + 255) / 256, 8192);
       hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3(g4), dim3(256), 0, st,
                          reinterpret_cast<const float4*>(a.partial), a.splits, total4,
-                         reinterpret_cast<float4*>(dw_hwio), a.pbias, Cout, dbias);
+                         reinterpret_cast<float4*>(dw_hwio), a.pbias, Cout, dbias, (int)accum);
     } else {
       const int g = (int)std::min<size_t>((total + Cout + 255) / 256, 4096);
       hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g), dim3(256), 0, st, a.partial, a.splits,
-                         total, dw_hwio, a.pbias, Cout, dbias);
+                         total, dw_hwio, a.pbias, Cout, dbias, (int)accum);
     }
     D2MI_LAUNCH_CHECK();
   }

@@ -87,8 +87,14 @@ def _dgrad(gy, w, x_shape, stride, pb, pe, relu_gate=None, add=None, add2=None):
 _WGRAD_1X1_MIN_P = int(os.environ.get("D2MI_WGRAD_1X1_MIN_P", "8192"))
 
 
-def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
+def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False, accumulate_into=None):
     """(weight gradient HWIO, bias gradient or None).
+
+    accumulate_into: (gw, gb) of earlier calls of the same shared weight
+    (gb None without a bias): this call's gradient is added into them --
+    inside the MFMA wgrad's reduce pass where it runs, else by an in-place
+    add -- and the accumulators are returned (gb None when this path made
+    no bias gradient: the caller adds its column sum).
 
     Routed by measurement (tools/bench_kernels.py --only wgrad, MI355X):
     with split products (the default, ops.CONV_MATH) every KxK and every 1x1
@@ -99,25 +105,58 @@ def _wgrad(x, gy, w_shape, stride, pb, pe, want_bias=False):
     KH, KW, Cin, Cout = w_shape
     split = ops.CONV_MATH == "split"
     eligible = Cin % 4 == 0 and Cout % 4 == 0
+    acc_w, acc_b = accumulate_into if accumulate_into is not None else (None, None)
+
+    def mfma(k, pads):
+        if want_bias and (acc_w is None or acc_b is not None):
+            acc = (acc_w, acc_b) if acc_w is not None else None
+            return ops.conv2d_wgrad(x, gy, k, stride, pads, with_bias=True, accumulate_into=acc)
+        return ops.conv2d_wgrad(x, gy, k, stride, pads, accumulate_into=acc_w), None
+
+    def added(gw):  # a path without the fused accumulate
+        return (gw if acc_w is None else acc_w.add_(gw)), None
+
     if KH == 1 and KW == 1 and pb == 0 and pe == 0:
         P = gy.numel() // Cout
         # tools/exp_wgrad_1x1.py: MFMA from 8400 pixels (res4: 54 vs 64-79 us
         # on hipBLASLt), and the strided 1024->2048 at 2100; hipBLASLt below
         if eligible and (P >= _WGRAD_1X1_MIN_P or (stride > 1 and Cin * Cout >= 2 ** 21)):
-            if want_bias:
-                return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0), with_bias=True)
-            return ops.conv2d_wgrad(x, gy, 1, stride, (0, 0)), None
+            return mfma(1, (0, 0))
         xs = x if stride == 1 else x[:, ::stride, ::stride]
         xs = xs.reshape(-1, Cin)
-        return torch.mm(xs.t(), gy.reshape(-1, Cout)).reshape(1, 1, Cin, Cout), None
+        return added(torch.mm(xs.t(), gy.reshape(-1, Cout)).reshape(1, 1, Cin, Cout))
     if split and eligible and KH == KW and 6 * max(x.numel(), gy.numel()) < 2 ** 31:
-        if want_bias:
-            return ops.conv2d_wgrad(x, gy, KH, stride, (pb, pe), with_bias=True)
-        return ops.conv2d_wgrad(x, gy, KH, stride, (pb, pe)), None
+        return mfma(KH, (pb, pe))
     xin = F.pad(x, (0, 0, pb, pe, pb, pe)) if (pb or pe) else x
     gw = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (Cout, Cin, KH, KW),
                                      gy.permute(0, 3, 1, 2), stride, 0)
-    return gw.permute(2, 3, 1, 0), None
+    return added(gw.permute(2, 3, 1, 0))
+
+
+def _wgrad_shared(acc, x, gy, w_shape, stride, pb, pe, want_bias):
+    """One call's share of a weight used by several calls of one forward
+    (``wacc`` = {"n": calls, "k": done}: the RPN head's 3x3 over the FPN
+    levels): its (gw, gb) go into the accumulator (the reduce pass adds them:
+    old + new, autograd's order for the summed gradients); every call but the
+    last returns (None, None), the last the sums."""
+    acc["k"] += 1
+    if acc["k"] == 1:
+        # every call's backward must run in this pass, else the gradient
+        # never leaves and a stale buffer would poison a later backward
+        handoff.expect_complete(acc, lambda a: a["k"] == 0,
+                                lambda a: (a.pop("buf", None), a.__setitem__("k", 0)),
+                                "shared conv weight-gradient calls")
+    buf = acc.get("buf")
+    gw, gb = _wgrad(x, gy, w_shape, stride, pb, pe, want_bias, accumulate_into=buf)
+    if want_bias and gb is None:
+        cs = ops.column_sum(gy)
+        gb = cs if buf is None or buf[1] is None else buf[1].add_(cs)
+    acc["buf"] = (gw, gb)
+    if acc["k"] < acc["n"]:
+        return None, None
+    acc.pop("buf")
+    acc["k"] = 0  # (a second backward of the same graph starts over)
+    return gw, gb
 
 
 def _gate_eligible(w_shape, stride, pb, pe):
@@ -151,7 +190,7 @@ class _ConvMFMAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_hwio, bias, w_packed, stride, pads, relu, topdown, residual=None,
                 relu_after=False, gate_input=False, res_grad_to=None, grad_from=None,
-                pair_grad=None, join=None):
+                pair_grad=None, join=None, wacc=None):
         has_add = topdown is not None or residual is not None
         if relu and has_add and not relu_after:
             raise ValueError("relu(conv) + add is not differentiable here; use relu_after_add")
@@ -164,6 +203,7 @@ class _ConvMFMAFn(torch.autograd.Function):
         ctx.grad_from = grad_from
         ctx.pair_grad = pair_grad
         ctx.join = join
+        ctx.wacc = wacc  # a weight shared by several calls: _wgrad_shared
         # the producer's ReLU tag, used if a join is registered by backward time
         ctx.relu_cand = getattr(x, "_d2mi_relu_info", None)
         ctx.out_info = None
@@ -215,11 +255,15 @@ class _ConvMFMAFn(torch.autograd.Function):
                 handoff.deposit(pair, "g", gx, "pair")
                 gx = None
         want_b = has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1]:
-            gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
-        if want_b and gb is None:
-            gb = ops.column_sum(gy)
-        return gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None
+        if ctx.needs_input_grad[1] and ctx.wacc is not None:
+            gw, gb = _wgrad_shared(ctx.wacc, x, gy, w.shape, stride, pb, pe, want_b)
+        else:
+            if ctx.needs_input_grad[1]:
+                gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
+            if want_b and gb is None:
+                gb = ops.column_sum(gy)
+        return (gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None,
+                None)
 
 
 def _join_active(ctx):
@@ -521,7 +565,7 @@ class Conv2D(Layer):
 
     def call(self, inputs, topdown=None, residual=None, relu_after_add=False, final_relu=False,
              relu_input_sole_consumer=False, res_grad_to=None, grad_from=None, pair_grad=None,
-             raw=False, join=None):
+             raw=False, join=None, wacc=None):
         """topdown: fused + up2(topdown) (FPN merge); residual: fused + residual;
         relu_after_add: the layer's ReLU runs after those adds; final_relu: an
         extra ReLU after the adds for a layer without activation (the
@@ -560,7 +604,7 @@ class Conv2D(Layer):
             ret = _ConvMFMAFn.apply(inputs, w, b, packed, self.stride, pads,
                                     fuse_relu, topdown, residual, relu_after_add,
                                     bool(relu_input_sole_consumer), res_grad_to, grad_from,
-                                    pair_grad, join)
+                                    pair_grad, join, wacc)
             if raw:  # the conv (+ bias) alone: the caller applies the normalizer / activation
                 return ret
             if norm is not None and is_relu(self.act_fn) and hasattr(norm, "fused_ok") \

@@ -687,10 +687,14 @@ def conv2d_nhwc_levels(xs, w_packed, bias=None, stride=1, pad=(0, 0), relu=False
     return ys
 
 
-def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math_mode=None):
+def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math_mode=None,
+                 accumulate_into=None):
     """HWIO weight gradient of conv2d_nhwc on the MFMA wgrad kernel; with_bias
     also returns the bias gradient (dy summed over pixels) from the same pass.
-    math_mode: "f32" | "split" (None: CONV_MATH), as conv2d_nhwc."""
+    math_mode: "f32" | "split" (None: CONV_MATH), as conv2d_nhwc.
+    accumulate_into: the (dw, db) -- or dw -- of an earlier call to add this
+    one's gradient into (d2mi_conv2d_wgrad_ex bit 3: old + new in the reduce
+    pass, autograd's order for a weight shared by several calls)."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -700,15 +704,23 @@ def conv2d_wgrad(x, dy, kernel_size, stride=1, pad=(0, 0), with_bias=False, math
     Cout = dy.shape[-1]
     KH = KW = int(kernel_size)
     pb, pe = pad
-    dw = torch.empty((KH, KW, Cin, Cout), dtype=torch.float32, device=x.device)
-    db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
+    if accumulate_into is not None:
+        dw, db = accumulate_into if with_bias else (accumulate_into, None)
+        if (dw.shape != (KH, KW, Cin, Cout) or dw.dtype != torch.float32
+                or not dw.is_contiguous() or (with_bias and (db is None or db.shape != (Cout,)))):
+            raise ValueError("accumulate_into must be the (dw, db) of a wgrad of this shape")
+    else:
+        dw = torch.empty((KH, KW, Cin, Cout), dtype=torch.float32, device=x.device)
+        db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if with_bias else None
     args = (N, H, W, Cin, Cout, KH, KW, int(stride), int(pb), int(pe))
     wsb = _WGRAD_WS.get(args)
     if wsb is None:
         wsb = _WGRAD_WS[args] = _C.lib().d2mi_conv2d_wgrad_workspace_size(*args)
+    if accumulate_into is not None:  # (the reduce pass adds: one slab at least)
+        wsb = max(wsb, (KH * KW * Cin * Cout + Cout) * 4)
     ws = _C.scratch(wsb, x.device) if wsb else None
     ev = KernelTimer.start()
-    flags = 4 if math_mode == "split" else 0
+    flags = (4 if math_mode == "split" else 0) | (8 if accumulate_into is not None else 0)
     rc = _C.lib().d2mi_conv2d_wgrad_ex(_C.ptr(x), _C.ptr(dy), _C.ptr(dw), _C.ptr(db), *args,
                                        flags, _C.ptr(ws), wsb, _C.stream_of(x.device))
     KernelTimer.stop(ev, "conv2d_wgrad_split" if flags else "conv2d_wgrad_mfma",

@@ -32,6 +32,10 @@ class StandardRPNHead(Layer):
     # training: the fused head's outputs gathered into the RPNOutputs layout
     # in one launch (False: per-level slice copies + concatenation, A/B)
     CONCAT_OUT = True
+    # True: the shared 3x3's weight / bias gradient accumulates over the FPN
+    # levels in one buffer (the MFMA wgrad's reduce adds each level into it;
+    # layers/convolutional.py:_wgrad_shared) -- autograd's per-level adds go
+    ACC_CONV_LEVELS = True
 
     def __init__(self, cfg, input_shape, **kwargs):
         super().__init__(**kwargs)
@@ -84,11 +88,13 @@ class StandardRPNHead(Layer):
         # returns the sum): autograd's per-level adds and slices go away
         wacc = ({"n": len(features), "k": 0}
                 if fuse and torch.is_grad_enabled() and _RPNHead1x1Fn.ACC_LEVELS else None)
+        cacc = ({"n": len(features), "k": 0}
+                if fuse and torch.is_grad_enabled() and StandardRPNHead.ACC_CONV_LEVELS else None)
         ys = []
         for x in features:
             # a level the ROI poolers also read hands its input gradient over
             # (GeneralizedRCNN tags them; the pair_grad protocol)
-            share = self.conv(x, pair_grad=getattr(x, "_d2mi_grad_pair", None))
+            share = self.conv(x, pair_grad=getattr(x, "_d2mi_grad_pair", None), wacc=cacc)
             if fuse:
                 # the fused 1x1 is the declared SOLE consumer of the 3x3's ReLU
                 # output (its dgrad applies the ReLU mask, _RPNHead1x1Fn): the

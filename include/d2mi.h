@@ -494,7 +494,11 @@ int d2mi_conv2d_wgrad(const float* x, const float* dy, float* dw_hwio, float* db
                       int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
                       int pad_end, void* workspace, size_t workspace_bytes, void* stream);
 /* flags bit2: the split-bf16 products of d2mi_conv2d_nhwc_ex (exact 3-term
- * split of x and dy, six bf16 MFMA products, f32 accumulation). */
+ * split of x and dy, six bf16 MFMA products, f32 accumulation).  bit3:
+ * accumulate -- dw_hwio (and dbias) += this call's gradient, in the reduce
+ * pass (a weight shared by several calls, e.g. one head over the FPN levels);
+ * the workspace must then hold the plan's slabs even for one split
+ * (d2mi_conv2d_wgrad_workspace_size, or one slab when that returns 0). */
 int d2mi_conv2d_wgrad_ex(const float* x, const float* dy, float* dw_hwio, float* dbias, int N,
                          int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad_beg, int pad_end, int flags, void* workspace,

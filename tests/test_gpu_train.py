@@ -535,12 +535,14 @@ def test_fpn_join_engages_and_matches_plain_step(dev, monkeypatch):
 
 
 def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch):
-    """The RPN head's fused 1x1 accumulates its weight / bias gradient over the
-    FPN levels in one buffer (d2mi_wgrad_skinny_ex accumulate): the model's
-    gradients equal those of per-level gradients summed by autograd, bit for
-    bit."""
+    """The RPN head's fused 1x1 and its shared 3x3 accumulate their weight /
+    bias gradients over the FPN levels in one buffer each
+    (d2mi_wgrad_skinny_ex accumulate; d2mi_conv2d_wgrad_ex bit 3, levels with
+    one split included): the model's gradients equal those of per-level
+    gradients summed by autograd, bit for bit."""
     from detectron2_tensorflow_amd.modeling import build_model
-    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import _RPNHead1x1Fn
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import (StandardRPNHead,
+                                                                           _RPNHead1x1Fn)
     from detectron2_tensorflow_amd.utils.synthetic import (calibrate_rcnn_scores,
                                                            synthetic_train_batch)
     cfg = _cfg(True)
@@ -552,6 +554,7 @@ def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch):
     grads = {}
     for acc in (True, False):
         monkeypatch.setattr(_RPNHead1x1Fn, "ACC_LEVELS", acc)
+        monkeypatch.setattr(StandardRPNHead, "ACC_CONV_LEVELS", acc)
         model.zero_grad(set_to_none=True)
         torch.manual_seed(1)
         losses = model(batch)

@@ -64,12 +64,17 @@ def _conv_epi(on):
     ops.set_tuning("conv_epi", 1 if on else 0)
 
 
+def _rpn_conv_acc(on):
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
+    StandardRPNHead.ACC_CONV_LEVELS = on
+
+
 def _rpn_concat(on):
     from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
     StandardRPNHead.CONCAT_OUT = on
 
 
-SWITCHES = {"rpn_concat": _rpn_concat, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+SWITCHES = {"rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
