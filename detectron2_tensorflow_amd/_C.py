@@ -131,6 +131,8 @@ _SIGS = {
     "d2mi_rpn_loss_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P]),
     "d2mi_rpn_loss_bwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P, P,
                                   P]),
+    "d2mi_rpn_loss_bwd_ex": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P,
+                                     c_float, P, P, P]),
     "d2mi_fast_rcnn_loss_workspace_size": (c_size_t, [c_int]),
     "d2mi_fast_rcnn_loss_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P,
                                         c_size_t, P]),

@@ -84,12 +84,18 @@ __global__ __launch_bounds__(256) void rpn_loss_fwd_kernel(RpnLossArgs a, float2
   }
 }
 
+// g_cls / g_loc: device scalars (null: a zero gradient), times `scale`
+// (the loss normaliser folded in: g * f32(scale), the value autograd's
+// multiply by that scale would give)
 __global__ __launch_bounds__(256) void rpn_loss_bwd_kernel(RpnLossArgs a,
-                                                           const float* __restrict__ grads,
+                                                           const float* __restrict__ g_cls_p,
+                                                           const float* __restrict__ g_loc_p,
+                                                           float scale,
                                                            float* __restrict__ d_logits,
                                                            float4* __restrict__ d_deltas) {
   const int n = blockIdx.y;
-  const float g_cls = grads[0], g_loc = grads[1];
+  const float g_cls = g_cls_p ? g_cls_p[0] * scale : 0.f;
+  const float g_loc = g_loc_p ? g_loc_p[0] * scale : 0.f;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < a.P; p += gridDim.x * 256) {
     const size_t i = (size_t)n * a.P + p;
     float dl = 0.f;
@@ -157,21 +163,33 @@ extern "C" int d2mi_rpn_loss_fwd(const float* logits, const float* deltas, const
   return 0;
 }
 
+extern "C" int d2mi_rpn_loss_bwd_ex(const float* logits, const float* deltas,
+                                    const float* anchors, const float* gt_boxes,
+                                    const long long* matches, const unsigned char* pos,
+                                    const unsigned char* sampled, int N, int P, int G,
+                                    const float* weights, float beta, const float* g_cls,
+                                    const float* g_loc, float scale, float* d_logits,
+                                    float* d_deltas, void* stream) {
+  D2MI_REQUIRE(N > 0 && P > 0 && G > 0, "bad rpn-loss shape");
+  D2MI_REQUIRE(((uintptr_t)d_deltas & 15) == 0, "rpn loss: 16-byte aligned d_deltas");
+  const RpnLossArgs a = make_args(logits, deltas, anchors, gt_boxes, matches, pos, sampled, N, P,
+                                  G, weights, beta);
+  hipLaunchKernelGGL(rpn_loss_bwd_kernel, dim3((P + 255) / 256 < 2048 ? (P + 255) / 256 : 2048, N),
+                     dim3(256), 0, as_stream(stream), a, g_cls, g_loc, scale, d_logits,
+                     reinterpret_cast<float4*>(d_deltas));
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const float* anchors,
                                  const float* gt_boxes, const long long* matches,
                                  const unsigned char* pos, const unsigned char* sampled, int N,
                                  int P, int G, const float* weights, float beta,
                                  const float* grads, float* d_logits, float* d_deltas,
                                  void* stream) {
-  D2MI_REQUIRE(N > 0 && P > 0 && G > 0, "bad rpn-loss shape");
-  D2MI_REQUIRE(((uintptr_t)d_deltas & 15) == 0, "rpn loss: 16-byte aligned d_deltas");
-  const RpnLossArgs a = make_args(logits, deltas, anchors, gt_boxes, matches, pos, sampled, N, P,
-                                  G, weights, beta);
-  hipLaunchKernelGGL(rpn_loss_bwd_kernel, dim3((P + 255) / 256 < 2048 ? (P + 255) / 256 : 2048, N),
-                     dim3(256), 0, as_stream(stream), a, grads, d_logits,
-                     reinterpret_cast<float4*>(d_deltas));
-  D2MI_LAUNCH_CHECK();
-  return 0;
+  D2MI_REQUIRE(grads != nullptr, "rpn loss: null grads");
+  return d2mi_rpn_loss_bwd_ex(logits, deltas, anchors, gt_boxes, matches, pos, sampled, N, P, G,
+                              weights, beta, grads, grads + 1, 1.0f, d_logits, d_deltas, stream);
 }
 
 // ------------------------------------------------ RPN head output layout

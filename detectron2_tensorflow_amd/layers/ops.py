@@ -863,11 +863,14 @@ def match_boxes_masks(gt_boxes, matchable, boxes, thresholds, labels_of, allow_l
 
 
 class _RPNLossFn(torch.autograd.Function):
-    """(loss_cls_sum, loss_loc_sum) of the RPN (d2mi_rpn_loss_fwd / _bwd);
-    differentiable w.r.t. logits and deltas."""
+    """(loss_cls_sum, loss_loc_sum) * scale of the RPN (d2mi_rpn_loss_fwd /
+    d2mi_rpn_loss_bwd_ex); differentiable w.r.t. logits and deltas.  The scale
+    (the normaliser x loss weight) is applied to the two sums here and to the
+    upstream gradients inside the backward kernel: no multiply launches."""
 
     @staticmethod
-    def forward(ctx, logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta):
+    def forward(ctx, logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta,
+                scale=1.0):
         N, P = logits.shape
         G = gt_boxes.shape[1]
         nb = _C.lib().d2mi_rpn_loss_blocks()
@@ -879,29 +882,35 @@ class _RPNLossFn(torch.autograd.Function):
                                         _C.stream_of(logits.device))
         _C.check(rc, "d2mi_rpn_loss_fwd")
         ctx.save_for_backward(logits, deltas, anchors, gt_boxes, matches, pos, sampled)
-        ctx.conf = (tuple(float(v) for v in weights), float(beta))
-        # fixed-size reductions of the partials (deterministic order)
-        return part[:, 0].sum(), part[:, 1].sum()
+        ctx.conf = (tuple(float(v) for v in weights), float(beta), float(scale))
+        ctx.set_materialize_grads(False)  # a missing gradient is a zero one (null pointer)
+        # fixed-size reduction of the partials (deterministic order), scaled
+        out = part.sum(0)
+        if scale != 1.0:
+            out.mul_(scale)
+        return out[0], out[1]
 
     @staticmethod
     def backward(ctx, g_cls, g_loc):
         logits, deltas, anchors, gt_boxes, matches, pos, sampled = ctx.saved_tensors
-        weights, beta = ctx.conf
+        weights, beta, scale = ctx.conf
         N, P = logits.shape
         dev = logits.device
-        z = torch.zeros((), dtype=torch.float32, device=dev)
-        grads = torch.stack([g_cls if g_cls is not None else z,
-                             g_loc if g_loc is not None else z]).float().contiguous()
+        g_cls = _f32c(g_cls) if g_cls is not None else None
+        g_loc = _f32c(g_loc) if g_loc is not None else None
         d_logits = torch.empty_like(logits)
         d_deltas = torch.empty_like(deltas)
         w = _C.host_array(_C.c_float, list(weights))
-        rc = _C.lib().d2mi_rpn_loss_bwd(_C.ptr(logits), _C.ptr(deltas), _C.ptr(anchors),
-                                        _C.ptr(gt_boxes), _C.ptr(matches), _C.ptr(pos),
-                                        _C.ptr(sampled), N, P, gt_boxes.shape[1], w, beta,
-                                        _C.ptr(grads), _C.ptr(d_logits), _C.ptr(d_deltas),
-                                        _C.stream_of(dev))
-        _C.check(rc, "d2mi_rpn_loss_bwd")
-        return d_logits, d_deltas, None, None, None, None, None, None, None
+        nul = _C.c_void_p(None)
+        rc = _C.lib().d2mi_rpn_loss_bwd_ex(_C.ptr(logits), _C.ptr(deltas), _C.ptr(anchors),
+                                           _C.ptr(gt_boxes), _C.ptr(matches), _C.ptr(pos),
+                                           _C.ptr(sampled), N, P, gt_boxes.shape[1], w, beta,
+                                           _C.ptr(g_cls) if g_cls is not None else nul,
+                                           _C.ptr(g_loc) if g_loc is not None else nul,
+                                           float(scale), _C.ptr(d_logits), _C.ptr(d_deltas),
+                                           _C.stream_of(dev))
+        _C.check(rc, "d2mi_rpn_loss_bwd_ex")
+        return d_logits, d_deltas, None, None, None, None, None, None, None, None
 
 
 class _FastRCNNLossFn(torch.autograd.Function):
@@ -1004,18 +1013,19 @@ def mask_loss(logits, target, classes, fg):
     return _MaskLossFn.apply(logits, target, classes, fg)
 
 
-def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta):
-    """Fused RPN losses (sums; the caller normalises): logits [N, P], deltas
-    [N, P, 4], anchors [P, 4], gt_boxes [N, G, 4], matches [N, P], pos /
-    sampled [N, P] bool -> (loss_cls_sum, loss_loc_sum)."""
+def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, beta,
+             scale=1.0):
+    """Fused RPN losses: logits [N, P], deltas [N, P, 4], anchors [P, 4],
+    gt_boxes [N, G, 4], matches [N, P], pos / sampled [N, P] bool ->
+    (loss_cls_sum * scale, loss_loc_sum * scale); scale = the caller's
+    normaliser (1.0: the plain sums)."""
     logits, deltas = _f32c(logits), _f32c(deltas)
     anchors, gt_boxes = _f32c(anchors), _f32c(gt_boxes)
     matches = matches.to(torch.int64).contiguous()
-    pos = pos.to(torch.uint8).contiguous()
-    sampled = sampled.to(torch.uint8).contiguous()
+    pos, sampled = _mask_u8(pos), _mask_u8(sampled)
     _C.require_device(logits, deltas, anchors, gt_boxes, matches, pos, sampled)
     return _RPNLossFn.apply(logits, deltas, anchors, gt_boxes, matches, pos, sampled,
-                            tuple(weights), float(beta))
+                            tuple(weights), float(beta), float(scale))
 
 
 def stem_conv_weights(w):

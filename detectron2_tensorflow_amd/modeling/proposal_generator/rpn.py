@@ -286,11 +286,13 @@ class RPN(Layer):
             pd = torch.cat([x.reshape(N, -1, 4) for x in deltas], dim=1)
         if pl.is_cuda and gt_boxes.shape[1] > 0:
             # one HIP pass each way: targets, sigmoid CE and smooth-L1 fused
+            # the normaliser x loss weight folded into the op (no multiply
+            # launches either way)
             loss_cls, loss_loc = ops.rpn_loss(pl, pd, anchors, gt_boxes, matches, pos, pos | neg,
                                               self.box2box_transform.weights,
-                                              self.smooth_l1_beta)
-            return {"loss_rpn_cls": loss_cls * norm * self.loss_weight,
-                    "loss_rpn_loc": loss_loc * norm * self.loss_weight}
+                                              self.smooth_l1_beta,
+                                              scale=norm * self.loss_weight)
+            return {"loss_rpn_cls": loss_cls, "loss_rpn_loc": loss_loc}
         matched = torch.gather(gt_boxes, 1, matches[..., None].expand(-1, -1, 4))
         gt_deltas = self.box2box_transform.get_deltas(
             anchors[None].expand(N, -1, -1).reshape(-1, 4), matched.reshape(-1, 4)).reshape(N, -1, 4)

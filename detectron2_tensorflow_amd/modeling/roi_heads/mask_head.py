@@ -43,12 +43,13 @@ def mask_rcnn_loss(pred_mask_logits, boxes, gt_boxes, gt_classes, gt_masks, mask
     from ...layers.functional import tf_crop_and_resize
     B, Hm, Wm, C = pred_mask_logits.shape
     if use_mini_masks:
-        gy1, gx1, gy2, gx2 = gt_boxes.unbind(-1)
-        gh, gw = gy2 - gy1, gx2 - gx1
-        y1, x1, y2, x2 = boxes.unbind(-1)
-        boxes = torch.stack([(y1 - gy1) / gh, (x1 - gx1) / gw, (y2 - gy1) / gh, (x2 - gx1) / gw], 1)
+        # ((y1 - gy1) / gh, (x1 - gx1) / gw, (y2 - gy1) / gh, (x2 - gx1) / gw)
+        # with gh = gy2 - gy1, gw = gx2 - gx1: the same f32 operations,
+        # broadcast over the two corners (3 launches instead of 11)
+        g0 = gt_boxes[:, None, :2]
+        boxes = ((boxes.reshape(B, 2, 2) - g0) / (gt_boxes[:, None, 2:] - g0)).reshape(B, 4)
     masks = gt_masks.to(torch.float32)[..., None].contiguous()
-    ind = torch.where(fg, mask_ind, torch.zeros_like(mask_ind)).to(torch.int32)
+    ind = torch.where(fg, mask_ind.to(torch.int32), 0)
     with torch.no_grad():
         target = tf_crop_and_resize(masks, boxes.detach().contiguous(), ind, (Hm, Wm))
         target = torch.round(target[..., 0])

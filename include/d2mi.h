@@ -654,6 +654,16 @@ int d2mi_rpn_loss_bwd(const float* logits, const float* deltas, const float* anc
                       const unsigned char* sampled, int N, int P, int G, const float* weights,
                       float beta, const float* grads, float* d_logits, float* d_deltas,
                       void* stream);
+/* d2mi_rpn_loss_bwd with the two upstream gradients as separate device
+ * scalars (null: zero) and the loss normaliser folded in: the gradients used
+ * are g * scale (the losses' `* normalizer * loss_weight`, rpn_outputs.py:
+ * 331-342, without its multiply launches or a gradient pack). */
+int d2mi_rpn_loss_bwd_ex(const float* logits, const float* deltas, const float* anchors,
+                         const float* gt_boxes, const long long* matches,
+                         const unsigned char* pos, const unsigned char* sampled, int N, int P,
+                         int G, const float* weights, float beta, const float* g_cls,
+                         const float* g_loc, float scale, float* d_logits, float* d_deltas,
+                         void* stream);
 
 /* ----------------------------------------------------- ROI-head losses
  * FastRCNNOutputs.losses (lib/modeling/roi_heads/fast_rcnn.py:269-357) on

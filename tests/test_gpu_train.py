@@ -349,6 +349,22 @@ def test_fused_rpn_loss_matches_tensor_formulation(dev):
     assert loc.item() == pytest.approx(loc_r.item(), rel=1e-5)
     torch.testing.assert_close(lf.grad, lr.grad, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(df.grad, dr.grad, rtol=1e-5, atol=1e-6)
+    # the normaliser folded into the op (d2mi_rpn_loss_bwd_ex): the sums times
+    # scale, and the gradients of the scaled losses; only one loss used (the
+    # other's gradient is a null pointer = zero)
+    s = 1.0 / 512
+    ls, ds = t(logits).requires_grad_(True), t(deltas).requires_grad_(True)
+    cls_s, loc_s = ops.rpn_loss(ls, ds, t(anchors), t(gt), t(matches), t(pos), t(sampled),
+                                weights, beta, scale=s)
+    assert cls_s.item() == pytest.approx(cls.item() * s, rel=1e-6)
+    assert loc_s.item() == pytest.approx(loc.item() * s, rel=1e-6)
+    cls_s.backward()
+    lr2 = t(logits).requires_grad_(True)
+    obj2 = torch.nn.functional.binary_cross_entropy_with_logits(lr2, t(pos).float(),
+                                                                reduction="none")
+    (torch.where(t(sampled), obj2, torch.zeros_like(obj2)).sum() * s).backward()
+    torch.testing.assert_close(ls.grad, lr2.grad, rtol=1e-5, atol=1e-9)
+    assert ds.grad is not None and not ds.grad.any()
 
 
 def test_whole_training_step_matches_cpu_restatement(dev):
