@@ -49,7 +49,9 @@ struct MatchConf {
 
 // flags: bit0 valid (matchable), bit1 crowd, bit2 difficult -- packed int32
 // per GT, or (packed null) three byte masks (crowd / difficult nullable):
-// d2mi_match_boxes_ex takes the bool tensors as they are, no packing passes.
+// d2mi_match_boxes_ex takes the bool tensors as they are, no packing passes,
+// and matches against the valid GT that are neither crowd nor difficult (the
+// reference's valid_gt_boxlist, rpn_outputs.py:255-264, roi_heads.py:160-180).
 struct FlagSrc {
   const int* packed;
   const uint8_t* m;
@@ -58,10 +60,8 @@ struct FlagSrc {
 };
 __device__ __forceinline__ int flag_at(const FlagSrc& f, size_t i) {
   if (f.packed) return f.packed[i];
-  int v = f.m[i] ? 1 : 0;
-  if (f.c && f.c[i]) v |= 2;
-  if (f.d && f.d[i]) v |= 4;
-  return v;
+  const bool c = f.c && f.c[i], d = f.d && f.d[i];
+  return (f.m[i] && !c && !d ? 1 : 0) | (c ? 2 : 0) | (d ? 4 : 0);
 }
 
 __global__ __launch_bounds__(256) void best_gt_kernel(const float4* __restrict__ gt,
@@ -186,15 +186,15 @@ extern "C" int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, cons
                     workspace_bytes, stream);
 }
 
-extern "C" int d2mi_match_boxes_ex(const float* gt_boxes, const uint8_t* matchable,
+extern "C" int d2mi_match_boxes_ex(const float* gt_boxes, const uint8_t* valid,
                                    const uint8_t* crowd, const uint8_t* difficult,
                                    const float* boxes, int boxes_per_image, int N, int G, int P,
                                    const float* thresholds, const int* labels_of, int n_intervals,
                                    int allow_low_quality, float crowd_thr, float difficult_thr,
                                    long long* matches, long long* labels, void* workspace,
                                    size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE(matchable != nullptr || G == 0, "match: null matchable mask");
-  return match_core(gt_boxes, FlagSrc{nullptr, matchable, crowd, difficult}, boxes,
+  D2MI_REQUIRE(valid != nullptr || G == 0, "match: null valid mask");
+  return match_core(gt_boxes, FlagSrc{nullptr, valid, crowd, difficult}, boxes,
                     boxes_per_image, N, G, P, thresholds, labels_of, n_intervals,
                     allow_low_quality, crowd_thr, difficult_thr, matches, labels, workspace,
                     workspace_bytes, stream);

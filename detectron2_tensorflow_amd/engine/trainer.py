@@ -52,7 +52,9 @@ class Trainer:
         self.optimizer.zero_grad()
         self.reducer.reset()
         losses = self.model(batched_inputs)
-        total = sum(losses.values())
+        # one stack + one sum (not a chain of adds: 2 launches, and the
+        # backward hands every loss the same seed without a kernel)
+        total = torch.stack(list(losses.values())).sum()
         total.backward()
         self.reducer.finish()
         self.optimizer.step(self.lr(self.iter))

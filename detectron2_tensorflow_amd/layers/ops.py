@@ -829,14 +829,15 @@ def _mask_u8(m):
     return m.view(torch.uint8) if m.dtype == torch.bool else (m != 0).view(torch.uint8)
 
 
-def match_boxes_masks(gt_boxes, matchable, boxes, thresholds, labels_of, allow_low_quality,
+def match_boxes_masks(gt_boxes, valid, boxes, thresholds, labels_of, allow_low_quality,
                       crowd=None, difficult=None, crowd_thr=1e-3, difficult_thr=float("inf")):
     """match_boxes with the GT flags as [N, G] masks (d2mi_match_boxes_ex):
-    matchable required, crowd / difficult optional -- the bool tensors are
-    passed as they are, no int32 packing launches."""
+    valid required, crowd / difficult optional -- the bool tensors are passed
+    as they are, no int32 packing launches; the matchable GT are valid and
+    neither crowd nor difficult."""
     gt_boxes = _f32c(gt_boxes)
     boxes = _f32c(boxes)
-    m, c, d = _mask_u8(matchable), _mask_u8(crowd), _mask_u8(difficult)
+    m, c, d = _mask_u8(valid), _mask_u8(crowd), _mask_u8(difficult)
     _C.require_device(gt_boxes, m, boxes, *[t for t in (c, d) if t is not None])
     N, G = m.shape
     for t in (c, d):

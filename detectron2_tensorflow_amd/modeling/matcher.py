@@ -66,17 +66,24 @@ class Matcher:
         return matches, labels
 
 
-def match_boxes(matcher, gt_boxes, matchable, boxes, crowd=None, difficult=None):
+def match_boxes(matcher, gt_boxes, valid, boxes, crowd=None, difficult=None):
     """pairwise_iou(gt_boxes, boxes) + matcher(...) with crowd / difficult
-    quality rows (rpn_outputs.py:306-330, roi_heads.py:160-216).  On the GPU
-    one fused HIP pass (ops.match_boxes: no [N, G, P] IoU matrix); elsewhere
-    the tensor formulation.  boxes [P, 4] shared or [N, P, 4]."""
+    quality rows (rpn_outputs.py:306-330, roi_heads.py:160-216): the GT
+    matched against are the valid ones that are neither crowd nor difficult
+    (valid_gt_boxlist).  On the GPU one fused HIP pass
+    (ops.match_boxes_masks: no [N, G, P] IoU matrix, no mask arithmetic);
+    elsewhere the tensor formulation.  boxes [P, 4] shared or [N, P, 4]."""
     N = gt_boxes.shape[0]
     if boxes.is_cuda:
-        return ops.match_boxes_masks(gt_boxes, matchable, boxes, matcher.thresholds,
+        return ops.match_boxes_masks(gt_boxes, valid, boxes, matcher.thresholds,
                                      matcher.labels, matcher.allow_low_quality_matches,
                                      crowd=crowd, difficult=difficult, crowd_thr=1e-3,
                                      difficult_thr=matcher.thresholds[1])
+    matchable = valid
+    if crowd is not None:
+        matchable = matchable & ~crowd
+    if difficult is not None:
+        matchable = matchable & ~difficult
     b = boxes if boxes.dim() == 3 else boxes[None].expand(N, -1, -1)
     iou = pairwise_iou(gt_boxes, b)
     zq = torch.zeros_like(iou)

@@ -53,6 +53,7 @@ class StandardRPNHead(Layer):
                                     scope="anchor_deltas")
         self._fused = None
         self._fused_key = None
+        self._fused_pad = None
 
     def _fused_1x1(self):
         """The objectness (A) and anchor-delta (4A) 1x1 convs as ONE conv of
@@ -64,8 +65,13 @@ class StandardRPNHead(Layer):
         if self._fused is None or self._fused_key != key:
             n = wo.shape[3] + wd.shape[3]
             pad = (-n) % 4
-            w = torch.cat([wo.detach(), wd.detach(), wo.new_zeros(*wo.shape[:3], pad)], dim=3)
-            b = torch.cat([bo.detach(), bd.detach(), bo.new_zeros(pad)])
+            zp = self._fused_pad
+            if zp is None or zp[0].shape[:3] != wo.shape[:3] or zp[0].shape[3] != pad \
+                    or zp[0].device != wo.device:
+                # the zero pad columns, made once (not two fills per step)
+                zp = self._fused_pad = (wo.new_zeros(*wo.shape[:3], pad), bo.new_zeros(pad))
+            w = torch.cat([wo.detach(), wd.detach(), zp[0]], dim=3)
+            b = torch.cat([bo.detach(), bd.detach(), zp[1]])
             self._fused = (w.contiguous(), ops.pack_conv_weights(w), b.contiguous())
             self._fused_key = key
         return self._fused
@@ -267,7 +273,7 @@ class RPN(Layer):
         valid = gt["is_valid"]
         crowd = gt.get("gt_is_crowd")
         crowd = crowd.bool() if crowd is not None else torch.zeros_like(valid)
-        matches, labels = match_boxes(self.anchor_matcher, gt_boxes, valid & ~crowd, anchors,
+        matches, labels = match_boxes(self.anchor_matcher, gt_boxes, valid, anchors,
                                       crowd=crowd)
         if self.boundary_threshold >= 0:
             # legacy inside_window filter (rpn_outputs.py:268-277, box_list_ops.py:150)

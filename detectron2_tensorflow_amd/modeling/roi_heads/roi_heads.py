@@ -94,14 +94,15 @@ class ROIHeads(Layer):
             boxes = torch.cat([boxes, gt_boxes.to(boxes.dtype)], dim=1)
             pvalid = torch.cat([pvalid, gvalid], dim=1)
         M = boxes.shape[1]
-        matches, labels = match_boxes(self.proposal_matcher, gt_boxes, gvalid & ~crowd & ~difficult,
-                                      boxes, crowd=crowd, difficult=difficult)
+        # (matched against the valid GT that are neither crowd nor difficult)
+        matches, labels = match_boxes(self.proposal_matcher, gt_boxes, gvalid, boxes,
+                                      crowd=crowd, difficult=difficult)
         K = self.num_classes
         gcls = torch.gather(targets["gt_classes"].long(), 1, matches)
-        gt_classes = torch.where(labels == 1, gcls,
-                                 torch.where(labels == 0, torch.full_like(gcls, K),
-                                             torch.full_like(gcls, -1)))
-        gt_classes = torch.where(pvalid, gt_classes, torch.full_like(gt_classes, -1))
+        # label 1 -> the matched GT class, 0 -> background K, -1 -> ignored;
+        # invalid proposal slots -> -1
+        gt_classes = torch.where(labels == 1, gcls, torch.where(labels == 0, K, labels))
+        gt_classes = torch.where(pvalid, gt_classes, -1)
         S = self.batch_size_per_image
         if boxes.is_cuda and FUSED_ORDER:
             # fused: the sampled rows come back in fg-first, index order
@@ -177,11 +178,12 @@ class StandardROIHeads(ROIHeads):
             # the mask branch's foreground count is read while the box branch
             # is enqueued (the device never idles at the read)
             pending = None
+            fg = self._mask_fg(sampled) if self.mask_on else None  # (once per step)
             if self.mask_on and self.mask_compact_rows:
-                pending = host_sync.start_read(self._mask_fg(sampled).sum())
+                pending = host_sync.start_read(fg.sum())
             losses = self._box_losses(feats, sampled, share)
             if self.mask_on:
-                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending)
+                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg)
             return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
         pred = self.forward_with_given_boxes(features, pred)
@@ -226,7 +228,7 @@ class StandardROIHeads(ROIHeads):
         return (sampled["is_valid"][:, :F_] & (sampled["gt_classes"][:, :F_] >= 0)
                 & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
 
-    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None):
+    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None):
         """_forward_mask training branch (roi_heads.py:594-600) over the first
         int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
         foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
@@ -235,7 +237,7 @@ class StandardROIHeads(ROIHeads):
         N = sampled["boxes"].shape[0]
         dev = boxes.device
         cls = sampled["gt_classes"][:, :F_].reshape(-1)
-        fg = self._mask_fg(sampled)
+        fg = self._mask_fg(sampled) if fg is None else fg
         img = _cached_index("img", N, F_, dev)
         gm = targets["gt_masks"]
         G = gm.shape[1]

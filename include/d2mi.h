@@ -627,9 +627,10 @@ int d2mi_match_boxes(const float* gt_boxes, const int* gt_flags, const float* bo
                      float crowd_thr, float difficult_thr, long long* matches, long long* labels,
                      void* workspace, size_t workspace_bytes, void* stream);
 /* d2mi_match_boxes with the GT flags as byte masks [N, G] (bool tensors as
- * they are: matchable required, crowd / difficult nullable) instead of the
- * packed int32 word -- no packing passes on the host side. */
-int d2mi_match_boxes_ex(const float* gt_boxes, const uint8_t* matchable, const uint8_t* crowd,
+ * they are: valid required, crowd / difficult nullable) instead of the
+ * packed int32 word -- no packing passes on the host side.  The matchable GT
+ * are valid && !crowd && !difficult (the reference's valid_gt_boxlist). */
+int d2mi_match_boxes_ex(const float* gt_boxes, const uint8_t* valid, const uint8_t* crowd,
                         const uint8_t* difficult, const float* boxes, int boxes_per_image, int N,
                         int G, int P, const float* thresholds, const int* labels_of,
                         int n_intervals, int allow_low_quality, float crowd_thr,

@@ -1231,9 +1231,9 @@ def test_fused_match_equals_tensor_matcher(dev, allow_low, per_image):
 
 
 def test_match_masks_abi_equals_packed_flags(dev):
-    """d2mi_match_boxes_ex (byte masks, crowd / difficult optional) == the
-    packed-int32 d2mi_match_boxes on the same GT, with and without the
-    optional masks."""
+    """d2mi_match_boxes_ex (byte masks, crowd / difficult optional; matchable
+    = valid and neither crowd nor difficult) == the packed-int32
+    d2mi_match_boxes on the same GT, with and without the optional masks."""
     from detectron2_tensorflow_amd.layers import ops
     g = torch.Generator().manual_seed(9)
     N, G, P = 2, 12, 3000
@@ -1248,7 +1248,12 @@ def test_match_masks_abi_equals_packed_flags(dev):
     diff = (torch.rand(N, G, generator=g) < 0.3).to(dev)
     thr, lab = [-math.inf, 0.3, 0.7, math.inf], [0, -1, 1]
     for c, d in ((crowd, diff), (None, diff), (crowd, None), (None, None)):
-        flags = valid.to(torch.int32)
+        m = valid
+        if c is not None:
+            m = m & ~c
+        if d is not None:
+            m = m & ~d
+        flags = m.to(torch.int32)
         if c is not None:
             flags = flags | (c.to(torch.int32) << 1)
         if d is not None:

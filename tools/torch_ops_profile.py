@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--by-count", action="store_true", help="order call sites by launches")
     ap.add_argument("--ops", default="aten::add,aten::add_,aten::copy_,aten::threshold_backward,"
                                       "aten::fill_,aten::zero_,aten::mul,aten::where,aten::cat")
     a = ap.parse_args()
@@ -54,7 +55,8 @@ def main():
         key = (ev.name, tuple(frames[:3]), str(ev.input_shapes)[:100])
         n, t = sites.get(key, (0, 0.0))
         sites[key] = (n + 1, t + ev.device_time_total)
-    for (name, fr, shp), (n, t) in sorted(sites.items(), key=lambda kv: -kv[1][1])[:40]:
+    order = (lambda kv: -kv[1][0]) if a.by_count else (lambda kv: -kv[1][1])
+    for (name, fr, shp), (n, t) in sorted(sites.items(), key=order)[:60]:
         print(f"{t / a.steps:9.1f}us {n // a.steps:4d} {name} {shp}")
         for f in fr:
             print("            ", f)
