@@ -43,6 +43,7 @@ class Trainer:
         self.reducer = BucketedAllReduce(self.optimizer.params, bucket_bytes, group)
         self.lr = build_learning_rate(cfg)
         self.iter = start_step
+        self._seed = None
 
     def step(self, batched_inputs):
         """One iteration: forward + losses, backward with the overlapped
@@ -55,7 +56,11 @@ class Trainer:
         # one stack + one sum (not a chain of adds: 2 launches, and the
         # backward hands every loss the same seed without a kernel)
         total = torch.stack(list(losses.values())).sum()
-        total.backward()
+        # the backward seed: one cached 1.0 per device (not a fill per step)
+        seed = self._seed
+        if seed is None or seed.device != total.device or seed.dtype != total.dtype:
+            seed = self._seed = torch.ones_like(total)
+        total.backward(seed)
         self.reducer.finish()
         self.optimizer.step(self.lr(self.iter))
         self.iter += 1

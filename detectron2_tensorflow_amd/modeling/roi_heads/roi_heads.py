@@ -223,9 +223,12 @@ class StandardROIHeads(ROIHeads):
                                 self.box2box_transform, self.smooth_l1_beta)
 
     def _mask_fg(self, sampled):
-        """Foreground flags of the first int(S * POSITIVE_FRACTION) slots per image."""
+        """Foreground flags of the first int(S * POSITIVE_FRACTION) slots per image:
+        valid and not background.  (A sampled slot is a positive, class in
+        [0, K), or a negative, class K -- the ignored -1 rows are never
+        sampled -- so `class < K` is the reference's `!= -1 and != bg` there.)"""
         F_ = int(self.batch_size_per_image * self.positive_sample_fraction)
-        return (sampled["is_valid"][:, :F_] & (sampled["gt_classes"][:, :F_] >= 0)
+        return (sampled["is_valid"][:, :F_]
                 & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
 
     def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None):
