@@ -69,12 +69,17 @@ def _rpn_conv_acc(on):
     StandardRPNHead.ACC_CONV_LEVELS = on
 
 
+def _rpn_levels(on):
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
+    StandardRPNHead.LEVELS_TRAIN = on
+
+
 def _rpn_concat(on):
     from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
     StandardRPNHead.CONCAT_OUT = on
 
 
-SWITCHES = {"rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+SWITCHES = {"rpn_concat": _rpn_concat, "rpn_levels": _rpn_levels, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
