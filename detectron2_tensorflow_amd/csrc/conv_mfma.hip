@@ -1845,7 +1845,10 @@ static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvA
 // Multi-level launches (ConvArgs::nlev > 0): no split-K, single-buffered.
 template <bool SPLIT>
 static void launch_conv_levels(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
-  if (cfg == 0) {
+  if (cfg == 3) {  // (tuning conv_ws_levels: the warp-specialised kernel, split products only)
+    if constexpr (SPLIT)
+      hipLaunchKernelGGL((conv_ws_kernel<true, 2, true>), grid, dim3(1024), 0, st, a);
+  } else if (cfg == 0) {
     if (occ3_enabled())
       hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3, true>), grid, dim3(256), 0,
                          st, a);
@@ -2191,8 +2194,16 @@ extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* di
     Mtot += (int64_t)N * OH * OW;
   }
   a.lds_epi = al;
-  // multi-level launches keep the 128-row kernels (no cfg 3)
-  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al, false);
+  // multi-level launches keep the 128-row kernels (no cfg 3) unless tuning
+  // conv_ws_levels: then the split-product long-K convs take the
+  // warp-specialised 256x128 kernel (level tables at its BM, no split-K)
+  const bool ws_lv = tuning(kTuneConvWSLevels) > 0 && (flags & kSplit3) != 0 && al;
+  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al, ws_lv);
+  if (p.cfg == 3) {  // the single-level WS launch's scheduling knobs (results unchanged)
+    static const char* prio = getenv("D2MI_CONV_PRIO");
+    a.prio = prio ? atoi(prio) : 5;
+    a.xcd2 = tuning(kTuneConvXCD) != 0;
+  }
   a.nN = (Cout + p.BN - 1) / p.BN;
   int t = 0;
   for (int l = 0; l < nlev; ++l) {
@@ -2208,8 +2219,8 @@ extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* di
     int tt;
     int S = levels_splits(dims, nlev, Cin, Cout, KH, KW, stride, pad_beg, pad_end, &rows, &tt);
     if (S > 1 && (workspace == nullptr || workspace_bytes < (size_t)S * rows * Cout * 4 ||
-                  ((uintptr_t)workspace & 15) != 0 || !al))
-      S = 1;  // no (usable) workspace: one pass per tile
+                  ((uintptr_t)workspace & 15) != 0 || !al || p.cfg == 3))
+      S = 1;  // no (usable) workspace, or the WS kernel: one pass per tile
     a.splits = S;
     a.kt_per_split = (a.nk + S - 1) / S;
     a.partial = S > 1 ? (float*)workspace : nullptr;

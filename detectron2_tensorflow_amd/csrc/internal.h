@@ -49,7 +49,7 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
 // the environment): in-process A/B timing of kernel variants (tools/).
 enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi = 3, kTuneConvSK = 4,
                kTuneWgradWS1 = 5, kTuneWgradXCD = 6, kTuneConvXCD = 7, kTuneWgradInc = 8, kTuneConvWSMinK = 9,
-               kTuneConvFix = 10,
+               kTuneConvFix = 10, kTuneConvWSLevels = 11,
                kTuneCount };
 int tuning(TuneKey k);
 

@@ -1354,13 +1354,16 @@ def _grad_share_case(dev):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("cout,relu", [(256, True), (720, False), (36, False)])
-def test_conv_levels_matches_per_level_convs(dev, cout, relu):
+@pytest.mark.parametrize("cout,relu,ws", [(256, True, False), (720, False, False),
+                                          (36, False, False), (256, True, True),
+                                          (720, False, True)])
+def test_conv_levels_matches_per_level_convs(dev, cout, relu, ws):
     """d2mi_conv2d_nhwc_levels (one launch over RetinaNet's P3..P7 at 640x640,
     shared weights) == conv2d_nhwc per level: the same per-tile arithmetic,
     summation order differing only where a small level alone would split K;
     and level 0 vs float64.  Cout 720 = the cls_score head (a partial N tile),
-    36 = bbox_pred (narrow: f32 MFMA)."""
+    36 = bbox_pred (narrow: f32 MFMA).  ws: tuning conv_ws_levels, the
+    warp-specialised 256x128 kernel over the levels (conv_ws_kernel<ML>)."""
     from detectron2_tensorflow_amd.layers import ops
     g = torch.Generator(device="cpu").manual_seed(11)
     shapes = [(2, 80, 80), (2, 40, 40), (2, 20, 20), (2, 10, 10), (2, 5, 5)]
@@ -1368,7 +1371,14 @@ def test_conv_levels_matches_per_level_convs(dev, cout, relu):
     w = (torch.randn(3, 3, 256, cout, generator=g) * 0.02).to(dev)
     b = (torch.randn(cout, generator=g) * 0.1).to(dev)
     wp = ops.pack_conv_weights(w)
-    ys = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
+    try:
+        ops.set_tuning("conv_ws_levels", 1 if ws else 0)
+        ys = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
+        ys2 = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
+    finally:
+        ops.set_tuning("conv_ws_levels", 0)  # the default
+    for y, y2 in zip(ys, ys2):
+        assert torch.equal(y, y2)
     for x, y in zip(xs, ys):
         ref = ops.conv2d_nhwc(x, wp, b, 1, (1, 1), relu=relu)
         assert y.shape == ref.shape

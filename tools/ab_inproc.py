@@ -74,12 +74,19 @@ def _rpn_levels(on):
     StandardRPNHead.LEVELS_TRAIN = on
 
 
+def _rpn_levels_ws(on):  # the levels form on the warp-specialised kernel vs per level
+    from detectron2_tensorflow_amd.layers import ops
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
+    StandardRPNHead.LEVELS_TRAIN = on
+    ops.set_tuning("conv_ws_levels", 1 if on else 0)
+
+
 def _rpn_concat(on):
     from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
     StandardRPNHead.CONCAT_OUT = on
 
 
-SWITCHES = {"rpn_concat": _rpn_concat, "rpn_levels": _rpn_levels, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+SWITCHES = {"rpn_concat": _rpn_concat, "rpn_levels": _rpn_levels, "rpn_levels_ws": _rpn_levels_ws, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
@@ -91,9 +98,11 @@ def main():
                     % ", ".join(sorted(SWITCHES)))
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--mode", default="train", help="train | infer (bench.py's modes)")
+    ap.add_argument("--model", default=None, help="bench.py --model (default: its own)")
     a = ap.parse_args()
     import bench
-    sys.argv = [sys.argv[0]]
+    sys.argv = [sys.argv[0], "--mode", a.mode] + (["--model", a.model] if a.model else [])
     args = bench.parse()
     dev = torch.device("cuda", 0)
     from detectron2_tensorflow_amd import _C
@@ -102,7 +111,13 @@ def main():
     cfg, model = bench.build(args, dev)
     batch = bench.synthetic_batch(args, dev, 0)
     bench.calibrate_scores(model, batch)
-    tr = Trainer(cfg, model)
+    if a.mode == "train":
+        tr = Trainer(cfg, model)
+        run = lambda: tr.step(batch)  # noqa: E731
+    else:
+        torch.set_grad_enabled(False)
+        fwd = model if bench.is_single_stage(model) else model.inference
+        run = lambda: fwd(batch)  # noqa: E731
     if a.switch.startswith("tune:"):
         from detectron2_tensorflow_amd.layers import ops
         key, _, vals = a.switch[5:].partition("=")
@@ -113,17 +128,17 @@ def main():
     for on in (True, False, True):
         sw(on)
         for _ in range(2):
-            tr.step(batch)
+            run()
     torch.cuda.synchronize()
     times = {True: [], False: []}
     for b in range(a.blocks):
         for on in ((True, False) if b % 2 == 0 else (False, True)):
             sw(on)
-            tr.step(batch)  # one untimed step after the switch
+            run()  # one untimed step after the switch
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.steps):
-                tr.step(batch)
+                run()
             torch.cuda.synchronize()
             times[on].append((time.perf_counter() - t0) * 1e3 / a.steps)
         print(f"block {b}: on {times[True][-1]:.3f} ms  off {times[False][-1]:.3f} ms", flush=True)
