@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations (median)")
     p.add_argument("--cpu-one-core", type=int, default=1, help="also time 1 image on 1 core")
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--no-calibration", action="store_true",
+                   help="skip the box calibration GEMM / conv before the timed region")
     p.add_argument("--timed-step-sample", type=int, default=-1,
                    help="timed step whose kernel launches carry HIP events (-1: the last)")
     p.add_argument("--mode", default="train", choices=["train", "infer"])
@@ -169,6 +171,12 @@ def _latest_pmc():
 
 
 PMC_FILE = _latest_pmc()
+# ``traffic`` is NOT measured by this run: it is the builder's committed
+# rocprofv3 PMC bytes per launch (same bench command, builder's box); the
+# ``achieved_counter`` / ``frac_counter`` figures divide those bytes by THIS
+# run's kernel times
+TRAFFIC_SOURCE = ("builder-committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE per launch), "
+                  + os.path.relpath(PMC_FILE, ROOT))
 
 
 # kernels whose PMC-counted bytes belong to the default (foreground-row)
@@ -217,7 +225,8 @@ def kernel_report(summary, mode="infer", extras=None):
         ach = flops / (ms * 1e-3) / 1e12
         rep[name] = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                     "traffic": pmc_traffic(pmc_group, mode), "launches": n,
+                     "traffic": pmc_traffic(pmc_group, mode), "traffic_source": TRAFFIC_SOURCE,
+                     "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
     for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_postprocess",
                  "solo_mask_stats",
@@ -233,7 +242,8 @@ def kernel_report(summary, mode="infer", extras=None):
         r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
              "bytes_model": "unique" if uniq is not None else "algorithmic",
-             "traffic": traffic, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+             "traffic": traffic, "traffic_source": TRAFFIC_SOURCE if traffic else None,
+             "launches": n, "avg_us": round(ms * 1e3 / n, 2),
              "algorithmic_per_launch": model / n}
         if uniq is not None:
             r["achieved_d4"] = round(byts / sec / 1e9, 1)
@@ -244,6 +254,131 @@ def kernel_report(summary, mode="infer", extras=None):
             r["frac_counter"] = round(ac / HBM_PEAK_GBPS, 4)
         rep[name] = r
     return rep
+
+
+def box_calibration(device, iters=20):
+    """Same-process calibration of THIS box, timed before the timed region so
+    that a slow box can be told apart from a code regression:
+    ``box_mfma_tflops`` = a fixed vendor bf16 GEMM (torch.matmul ->
+    hipBLASLt, 8192^3, dense TF/s; the library is fixed by the image, so it
+    moves only with the box's clocks / power), ``box_conv_p2_us`` = this
+    repo's split-product conv on the FPN p2 3x3 shape (2x200x336x256 -> 256,
+    the step's largest conv) in us per launch, with its f32-equivalent TF/s."""
+    out = {}
+    try:
+        n = 8192
+        a = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+        b = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+        for _ in range(3):
+            torch.matmul(a, b)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            torch.matmul(a, b)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        out["box_mfma_tflops"] = round(2.0 * n ** 3 / (ms * 1e-3) / 1e12, 1)
+        out["box_mfma_gemm"] = f"bf16 torch.matmul {n}^3 (hipBLASLt), mean of {iters} launches"
+        del a, b
+        from detectron2_tensorflow_amd.layers import ops
+        g = torch.Generator(device=device).manual_seed(0)
+        x = torch.randn(2, 200, 336, 256, device=device, generator=g)
+        w = torch.randn(3, 3, 256, 256, device=device, generator=g) * 0.02
+        for _ in range(3):
+            ops.conv2d_nhwc(x, w, None, 1, (1, 1))
+        e0.record()
+        for _ in range(iters):
+            ops.conv2d_nhwc(x, w, None, 1, (1, 1))
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / iters
+        out["box_conv_p2_us"] = round(us, 1)
+        out["box_conv_p2_tflops"] = round(2.0 * 2 * 200 * 336 * 256 * 9 * 256 / (us * 1e-6) / 1e12, 1)
+    except Exception as e:  # calibration is informative only
+        out["box_calibration_error"] = f"{type(e).__name__}: {e}"
+    return out
+
+
+class GpuSampler:
+    """Samples the GPU's gfx clock, memory clock, socket power and hotspot
+    temperature (amdsmi gpu_metrics) every ``period`` s on a host thread while
+    the timed region runs; summary() gives min / median / max of each.  If
+    amdsmi is absent or refuses (a non-root user may not read every sensor)
+    the line says so instead."""
+
+    def __init__(self, device, period=0.05):
+        import threading
+        self.period = period
+        self.samples = []
+        self.error = None
+        self._stop = threading.Event()
+        self._thread = None
+        self._h = None
+        try:
+            import amdsmi
+            self._smi = amdsmi
+            amdsmi.amdsmi_init()
+            hs = amdsmi.amdsmi_get_processor_handles()
+            props = torch.cuda.get_device_properties(device)
+            want = (props.pci_domain_id, props.pci_bus_id, props.pci_device_id)
+            for h in hs:
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)  # "dddd:bb:dd.f"
+                dom, bus, rest = bdf.split(":")
+                if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                    self._h = h
+                    break
+            if self._h is None:
+                self.error = f"no amdsmi handle matches the device's PCI address {want}"
+        except Exception as e:
+            self.error = f"amdsmi unavailable: {type(e).__name__}: {e}"
+
+    def _read(self):
+        m = self._smi.amdsmi_get_gpu_metrics_info(self._h)
+
+        def num(v):
+            if isinstance(v, (list, tuple)):
+                v = [x for x in v if isinstance(x, (int, float)) and x < 0xFFFF]
+                return sum(v) / len(v) if v else None
+            return v if isinstance(v, (int, float)) and v < 0xFFFF else None
+        return {"gfxclk_mhz": num(m.get("current_gfxclks")) or num(m.get("current_gfxclk")),
+                "uclk_mhz": num(m.get("current_uclk")),
+                "power_w": num(m.get("current_socket_power")) or num(m.get("average_socket_power")),
+                "hotspot_c": num(m.get("temperature_hotspot"))}
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self.samples.append(self._read())
+            except Exception as e:
+                self.error = f"amdsmi read failed: {type(e).__name__}: {e}"
+                return
+            self._stop.wait(self.period)
+
+    def start(self):
+        if self._h is None:
+            return
+        import threading
+        self._thread = threading.Thread(target=self._run, daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join()
+
+    def summary(self):
+        if not self.samples:
+            return {"error": self.error or "no samples"}
+        out = {"samples": len(self.samples), "period_s": self.period}
+        for k in self.samples[0]:
+            v = sorted(s[k] for s in self.samples if s.get(k) is not None)
+            if v:
+                out[k] = {"min": round(v[0], 1), "median": round(v[len(v) // 2], 1),
+                          "max": round(v[-1], 1)}
+        if self.error:
+            out["error"] = self.error
+        return out
 
 
 def cpu_model_name():
@@ -445,6 +580,11 @@ def main():
         for _ in range(args.warmup):
             out = step()
         torch.cuda.synchronize()
+        # box calibration (fixed vendor GEMM + this repo's p2 conv) and the
+        # clock / power sampler: outside the timed region
+        calib = box_calibration(device) if not args.no_calibration else {}
+        sampler = GpuSampler(device)
+        torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         # Per-launch HIP events (the live roofline) are recorded during ONE of
@@ -455,6 +595,7 @@ def main():
         sample = args.steps - 1 if args.timed_step_sample < 0 else min(args.timed_step_sample,
                                                                         args.steps - 1)
         torch.cuda.nvtx.range_push("timed_region")  # roctx: tools/prof_window.py
+        sampler.start()
         t0 = time.perf_counter()
         for i in range(args.steps):
             KernelTimer.enabled = (i == sample) and not args.no_kernel_timing
@@ -463,6 +604,7 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
+        sampler.stop()
         torch.cuda.nvtx.range_pop()
         KernelTimer.enabled = False
     summary = KernelTimer.summary()
@@ -522,6 +664,10 @@ def main():
             "roofline": kernels.get("conv2d_split", kernels.get("conv2d_mfma")),
             **({"replicas_in_sync": in_sync} if in_sync is not None else {}),
             "kernels": kernels,
+            # this box: a fixed vendor GEMM + this repo's p2 conv timed in the
+            # same process before the timed region, and the clocks / power
+            # sampled during it (a slow box vs a code regression)
+            "box": dict(calib, gpu_during_timed_region=sampler.summary()),
         }
         if args.cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(args, model, batch, cfg)

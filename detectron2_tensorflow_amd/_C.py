@@ -104,8 +104,6 @@ _SIGS = {
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_nhwc_gated": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                        c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
-    "d2mi_conv2d_nhwc_x3": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
-                                    c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_levels_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int,
                                                   c_int, c_int]),
     "d2mi_conv2d_nhwc_levels": (c_int, [P, P, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,

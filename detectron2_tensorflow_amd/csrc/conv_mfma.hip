@@ -77,6 +77,26 @@ enum EpiFlags {
   kRelu = 1, kReluAfterResidual = 2, kSplit3 = 4, kFlipTaps = 8, kMaskByResidual = 16
 };
 
+// Compile-time ablation bits of the split conv kernels, for timing
+// experiments only: an ablation build of the library (tools/, D2MI_LIB)
+// passes -DD2MI_CONV_ABLATE=<bits>; the production build has 0 and every
+// ablation branch is compiled out.  1 = no global loads, 2 = no split / LDS
+// writes (loaded values kept live), 4 = no MFMAs (fragments kept live),
+// 8 = no epilogue.
+#ifndef D2MI_CONV_ABLATE
+#define D2MI_CONV_ABLATE 0
+#endif
+constexpr int kAblate = D2MI_CONV_ABLATE;
+
+// Wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
+// SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
+// writes of the other resident workgroups (or the stager waves).  Measured
+// (r2, tools/ab_prio.sh, 16 Mask R-CNN shapes): 1.3 % faster in total, 2-5 %
+// on the res3-res5 3x3s and 1x1s; on the double-buffered narrow-Cout kernels
+// 2-4 %; priority during the load-issue phase instead gained 0.2 %.  Fixed
+// since r4 (was the runtime D2MI_CONV_PRIO).
+constexpr bool kPrioMfma = true;
+
 // Exact 3-term bf16 split of four floats (truncation; see the header).
 // Each output packs 4 bf16 (element order = float4 order).
 __device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2& l) {
@@ -115,34 +135,9 @@ struct ConvArgs {
   int tile_base, m_base, m_end;
   int lds_epi;  // store_outputs_lds usable (Cout % 4 == 0, 16-B aligned operands)
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
-  // pre-split operands (conv_x3_kernel): 3 bf16 planes each, plane strides in bytes
-  const uint16_t* x3;
-  const uint16_t* w3;
-  int x_plane_bytes, w_plane_bytes;
   int tdH, tdW;
-  int dbg;  // ablation bits (D2MI_CONV_DBG, timing experiments only; 0 in production)
   int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
-  // stream-K launch of conv_ws_kernel (plan sk): sk_T = ntiles * nk k-steps
-  // over gridDim.x workgroups; partial slabs [piece][M][Cout]
-  int sk, sk_T, sk_P;
   int xcd2;  // xcd_tile(): the 2-D XCD-contiguous remap (tuning conv_xcd, default 1)
-  // split-K fix-up inside the launch (splitk_fixup, tuning conv_fix): one
-  // arrival counter per tile (the stream's zeroed pool); null: the separate
-  // splitk_reduce4_kernel launch
-  unsigned* tile_cnt;
-  // wave priority 1 while a wave issues its k-step's MFMAs (s_setprio): the
-  // SIMD's arbiter then prefers the MFMA stream over the staging VALU / LDS
-  // writes of the other resident workgroups.  D2MI_CONV_PRIO (A/B): 1 (the
-  // default, with bit 4) MFMA phase, 2 the load-issue phase instead, 0 off;
-  // bit 4: the MFMA phase of the double-buffered narrow-Cout kernels too
-  // (default 5 = 1 | 4).  Measured (tools/ab_prio.sh, 16 Mask R-CNN shapes):
-  // 1 is 1.3 % faster in total, 2-5 % on the res3-res5 3x3s and 1x1s; 2 is
-  // 0.2 %; bit 4 (tools/ab_prio_narrow.sh) 2-4 % on the Cout <= 64 shapes,
-  // training bench +1 % in alternating pairs.  A/B-only bits: 8 = loads
-  // issued at priority 1 and the MFMA phase at 2; 16 = the activation loads
-  // issued before the weight loads (tools/ab_prio2.sh: 13 / 21 / 29 within
-  // 0.45 % of 5 on the 16 shapes, below the run-to-run spread; 5 kept).
-  int prio;
   // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
   // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
   // input / output / gate maps.  The kernel swaps them into the fields above
@@ -337,87 +332,6 @@ __device__ __forceinline__ void store_partial(const ConvArgs& a, const Geo& g,
       for (int r = 0; r < 16; ++r) {
         const int dm = (r & 3) + 8 * (r >> 2);
         if (mb + dm < g.M) pp[(size_t)dm * a.Cout] = acc[i][j][r];
-      }
-    }
-  }
-}
-
-// Split-K fix-up inside the conv launch (ConvArgs::tile_cnt): every
-// workgroup of a split tile stores its raw partial slab, drains its stores and
-// draws an arrival ticket on the tile's counter behind one agent-scope release
-// (the XCD L2s are not coherent with each other); the workgroup that draws the
-// last ticket takes one agent-scope acquire, sums the tile's slabs in split
-// order 0..S-1 -- splitk_reduce4_kernel's order, so the outputs are
-// bit-identical to the two-launch form -- applies the epilogue and resets the
-// counter.  Nobody waits on anybody (no residency assumption); the counters
-// start zeroed (fix_counters) and every launch leaves them zero.  All NT
-// threads call it; `lds` is the kernel's own LDS array (free after the main
-// loop: one __shared__ object, so the k-loop's waits are unaffected).
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void splitk_fixup(const ConvArgs& a, const Geo& g, int tile, int m0,
-                                             int n0, float* lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(a.tile_cnt + tile, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (unsigned)(a.splits - 1);
-    if (last) {
-      __hip_atomic_exchange(a.tile_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    reinterpret_cast<int*>(lds)[0] = last;
-  }
-  __syncthreads();
-  if (!reinterpret_cast<volatile int*>(lds)[0]) return;
-  constexpr int F4 = BN / 4;
-  constexpr int Q = BM * F4 / NT;  // float4 per thread
-  constexpr int QB = Q < 8 ? Q : 8;
-  static_assert(Q % QB == 0, "fix-up batch");
-  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
-  const size_t slab4 = (size_t)g.pstride * a.Cout / 4;
-#pragma unroll
-  for (int q0 = 0; q0 < Q; q0 += QB) {
-    size_t off[QB];
-    int mm[QB], cc[QB];
-    float4 acc[QB];
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int idx = threadIdx.x + NT * (q0 + q);
-      const int r = idx / F4, c4 = idx - r * F4;
-      mm[q] = m0 + r;
-      cc[q] = n0 + 4 * c4;
-      // clamped addresses: every load is issued (no per-element branches
-      // around loads), only the stores are masked
-      const int ml = min(mm[q], g.M - 1) - g.prow0, cl = min(cc[q], a.Cout - 4);
-      off[q] = ((size_t)ml * a.Cout + cl) / 4;
-      acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    for (int s = 0; s < a.splits; ++s) {
-      float4 v[QB];
-#pragma unroll
-      for (int q = 0; q < QB; ++q) v[q] = p4[(size_t)s * slab4 + off[q]];
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        acc[q].x += v[q].x;
-        acc[q].y += v[q].y;
-        acc[q].z += v[q].z;
-        acc[q].w += v[q].w;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int m = mm[q], co = cc[q];
-      if (m < g.M && co < a.Cout) {
-        float4 o;
-        o.x = epilogue(a, g, acc[q].x, m, co);
-        o.y = epilogue(a, g, acc[q].y, m, co + 1);
-        o.z = epilogue(a, g, acc[q].z, m, co + 2);
-        o.w = epilogue(a, g, acc[q].w, m, co + 3);
-        *reinterpret_cast<float4*>(g.y + (size_t)m * a.Cout + co) = o;
       }
     }
   }
@@ -764,9 +678,9 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
           load_a(kt + 1, ra[0]);
           load_b(kt + 1);
         }
-        if (a.prio & 4) __builtin_amdgcn_s_setprio(1);
+        if (kPrioMfma) __builtin_amdgcn_s_setprio(1);
         compute(buf);
-        if (a.prio & 4) __builtin_amdgcn_s_setprio(0);
+        if (kPrioMfma) __builtin_amdgcn_s_setprio(0);
         if (more) store_tile(buf ^ 1, ra[0], rb);
         __syncthreads();
         buf ^= 1;
@@ -776,28 +690,18 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
       load_b(kt0);
       store_tile(0, ra[0], rb);
       __syncthreads();
-      const int dbg = a.dbg;
-      const int prio = a.prio;
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (prio & (2 | 8)) __builtin_amdgcn_s_setprio(1);
-        if (more && !(dbg & 1)) {
-          if (prio & 16) {
-            load_a(kt + 1, ra[0]);
-            load_b(kt + 1);
-          } else {
-            load_b(kt + 1);
-            load_a(kt + 1, ra[0]);
-          }
+        if (more && !(kAblate & 1)) {
+          load_b(kt + 1);
+          load_a(kt + 1, ra[0]);
         }
-        if (prio & 2) __builtin_amdgcn_s_setprio(0);
-        if (prio & 8) __builtin_amdgcn_s_setprio(2);
-        else if (prio & 1) __builtin_amdgcn_s_setprio(1);
-        if (!(dbg & 4)) compute(0);
-        if (prio & (1 | 8)) __builtin_amdgcn_s_setprio(0);
+        if (kPrioMfma) __builtin_amdgcn_s_setprio(1);
+        if (!(kAblate & 4)) compute(0);
+        if (kPrioMfma) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         if (more) {
-          if (!(dbg & 2)) store_tile(0, ra[0], rb);
+          if (!(kAblate & 2)) store_tile(0, ra[0], rb);
           __syncthreads();
         }
       }
@@ -827,30 +731,17 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
     }
   }
 
-  if (a.dbg & 8) return;
+  if constexpr ((kAblate & 8) != 0) return;
   // split-K partial slabs leave straight from the accumulators (each store
   // instruction writes two whole 128-B row segments; no LDS round trip and
   // none of its barriers) unless tuning conv_epi = 0
   if (a.splits > 1 && a.reg_partials) {
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, true);
-    if constexpr (!ML) {
-      if (a.tile_cnt) splitk_fixup<BM, BN, 256>(a, g, tile, m0, n0, &As[0][0]);
-    }
   } else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
     store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                       &As[0][0]);
   else
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1);
-}
-
-// Stream-K partition of T = ntiles * nk k-steps over P workgroups:
-// workgroup b owns [sk_lo(b), sk_lo(b + 1)); sk_wg_of(i) is the workgroup
-// owning iteration i.
-__host__ __device__ __forceinline__ long long sk_lo(long long b, long long P, long long T) {
-  return b * T / P;
-}
-__host__ __device__ __forceinline__ int sk_wg_of(long long i, long long P, long long T) {
-  return (int)(((i + 1) * P - 1) / T);
 }
 
 // Warp-specialised split-product conv: a 256x128 tile, 16 waves (1024
@@ -866,7 +757,7 @@ __host__ __device__ __forceinline__ int sk_wg_of(long long i, long long P, long 
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <bool ML, int LD, bool BATCH = true, bool SK = false>
+template <int LD>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -880,49 +771,20 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;  // (stagers: wr >= 4, never an acc slab)
 
-  // XCD-contiguous order of the workgroup index: consecutive tiles (or
-  // stream-K ranges), which share input halo rows and weight tiles, land on
-  // one XCD's L2.
-  const int nwg = gridDim.x;
-  int split_xy;
-  const int lw = xcd_tile(SK ? 0 : a.xcd2, split_xy);
-  // Stream-K (SK, ConvArgs::sk): the workgroup runs iterations [it, it_end)
-  // of the tile-major, k-minor sequence of all ntiles * nk k-steps -- one
-  // piece per tile it touches, each stored raw from the accumulators to
-  // partial slab (its index among the tile's pieces); sk_reduce4_kernel sums
-  // every tile's pieces in k order and applies the epilogue.  Otherwise one
-  // piece: tile lw, split blockIdx.y.  The stagers and the compute waves walk
-  // the same pieces, so their barriers pair up.
-  int it = 0, it_end = 1;
-  if constexpr (SK) {
-    it = (int)sk_lo(lw, nwg, a.sk_T);
-    it_end = (int)sk_lo(lw + 1, nwg, a.sk_T);
-    if (it >= it_end) return;
-  }
-  auto piece = [&](int i, int& tile, int& kt0, int& kt1, int& split) {
-    if constexpr (SK) {
-      tile = i / a.nk;
-      kt0 = i - tile * a.nk;
-      kt1 = min(a.nk, kt0 + (it_end - i));
-      split = lw - sk_wg_of((long long)tile * a.nk, nwg, a.sk_T);
-    } else {
-      tile = a.tile_base + lw;
-      split = split_xy;
-      kt0 = split * a.kt_per_split;
-      kt1 = min(a.nk, kt0 + a.kt_per_split);
-    }
-  };
+  // XCD-contiguous order of the workgroup index: consecutive tiles, which
+  // share input halo rows and weight tiles, land on one XCD's L2.
+  int split;
+  const int tile = a.tile_base + xcd_tile(a.xcd2, split);
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
+  const int nks = max(kt1 - kt0, 0);
+  const Geo g = geo_of(a);
+  const int mt = tile / a.nN, nt = tile - mt * a.nN;
+  const int m0 = mt * BM, n0 = nt * BN;
 
   floatx16 acc[TM][TN];
   if (wave >= 8) {
     // ------------------------------------------------------------ stagers
-    for (int pit = it;;) {
-    int tile, kt0, kt1, split;
-    piece(pit, tile, kt0, kt1, split);
-    const Geo g = ML ? select_level(a, tile) : geo_of(a);
-    const int mt = tile / a.nN, nt = tile - mt * a.nN;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int nks = max(kt1 - kt0, 0);
     const int st = tid - 512;
     const int srow = st >> 3, schunk = (st & 7) * 4;  // rows srow + 64 p
     int ih0[RA], iw0[RA], base[RA];
@@ -968,9 +830,6 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       bco[p] = co < a.Cout;
       boff[p] = co * a.Cin + schunk;
     }
-    // ablation bits (D2MI_CONV_DBG, timing experiments only): 1 = no global
-    // loads, 2 = no split / LDS writes (the loaded values kept live)
-    const int dbg = a.dbg;
     // The loads run in k-step order (kt0, kt0 + 1, ..., then the last one
     // again): a uniform cursor (chunk, tap, kh, kw) advanced by one step
     // replaces two integer divisions per k-step.
@@ -978,7 +837,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     int c_kt = kt0, c_chunk = kt0 / taps, c_tap = kt0 - (kt0 / taps) * taps;
     int c_kh = c_tap / a.KW, c_kw = c_tap - (c_tap / a.KW) * a.KW;
     auto load = [&](float4 (&la)[RA], float4 (&lb)[RB]) {
-      if (dbg & 1) return;
+      if constexpr ((kAblate & 1) != 0) return;
       const int cc = c_chunk * BK;
       const bool cok = cc + schunk < a.Cin;
       const int toff = (c_kh * g.W + c_kw) * a.Cin + cc;
@@ -1009,7 +868,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       }
     };
     auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
-      if (dbg & 2) {
+      if constexpr ((kAblate & 2) != 0) {
 #pragma unroll
         for (int p = 0; p < RA; ++p) asm volatile("" ::"v"(la[p].x));
 #pragma unroll
@@ -1042,7 +901,7 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // one): with a data-dependent load count hipcc cannot count the loads in
     // flight and drains them all (vmcnt(0)) before each write.
     float4 ra[LD][RA], rb[LD][RB];
-    if (dbg & 1) {
+    if constexpr ((kAblate & 1) != 0) {
 #pragma unroll
       for (int j = 0; j < LD; ++j) {
 #pragma unroll
@@ -1078,15 +937,8 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         __syncthreads();
       }
     }
-    pit += kt1 - kt0;
-    if (!SK || pit >= it_end) break;
-    }  // pieces
   } else {
     // ------------------------------------------------------------ compute
-    for (int pit = it;;) {
-    int tile, kt0, kt1, split;
-    piece(pit, tile, kt0, kt1, split);
-    const int nks = max(kt1 - kt0, 0);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1094,45 +946,12 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int li = lane & 31, lh = lane >> 5;
-    const int cdbg = a.dbg;
     bf16x8 fa[3][TM], fb[3][TN];
-    auto ldf = [&](int buf, int ks) {
-      const uint16_t* A16 = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
-      const uint16_t* B16 = A16 + 3 * BM * LDSB;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[pl][i] = *reinterpret_cast<const bf16x8*>(
-              &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[pl][j] = *reinterpret_cast<const bf16x8*>(
-              &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
-      }
-    };
-    auto mma = [&]() {
-      if (cdbg & 4) {  // ablation: no MFMAs (the fragments kept live)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          asm volatile("" ::"v"(fa[pl][0]), "v"(fa[pl][1]), "v"(fb[pl][0]), "v"(fb[pl][1]));
-        return;
-      }
-      constexpr int PA[6] = {1, 2, 0, 0, 1, 0};
-      constexpr int PB[6] = {1, 0, 2, 1, 0, 0};
-#pragma unroll
-      for (int t = 0; t < 6; ++t)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[t]][i], fb[PB[t]][j],
-                                                                 acc[i][j], 0, 0, 0);
-    };
     // One 16-deep step with its LDS reads in three plane batches, each
     // issued one MFMA group ahead of its first use (products in the PA / PB
-    // order): after a barrier all eight compute waves read at once, and 4
-    // reads per wave before the first MFMA (not 12) shorten that burst.
+    // order of conv_mfma_kernel: small terms first, h*h last): after a
+    // barrier all eight compute waves read at once, and 4 reads per wave
+    // before the first MFMA (not 12) shorten that burst.
     auto ld1 = [&](const uint16_t* A16, const uint16_t* B16, int pa, int pb, int ks) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -1144,6 +963,10 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
             &B16[pb * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
     };
     auto mm1 = [&](int pa, int pb) {
+      if constexpr ((kAblate & 4) != 0) {  // ablation: no MFMAs (the fragments kept live)
+        asm volatile("" ::"v"(fa[pa][0]), "v"(fa[pa][1]), "v"(fb[pb][0]), "v"(fb[pb][1]));
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1152,11 +975,6 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
               __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
     };
     auto step16 = [&](int buf, int ks) {
-      if (cdbg & 4) {
-        ldf(buf, ks);
-        mma();
-        return;
-      }
       const uint16_t* A16 = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
       const uint16_t* B16 = A16 + 3 * BM * LDSB;
       ld1(A16, B16, 1, 1, ks);
@@ -1172,217 +990,26 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       mm1(1, 0);  // m*h
       mm1(0, 0);  // h*h
     };
-    const int prio = a.prio;
     __syncthreads();  // B_{-1}
     for (int u = 0; u < nks; ++u) {
       const int buf = u & 1;
-      if (prio & 1) __builtin_amdgcn_s_setprio(1);
-      if constexpr (BATCH) {
-        step16(buf, 0);
-        step16(buf, 1);
-      } else {  // (A/B, tuning conv_ws = 1: all 12 reads of a step up front)
-        ldf(buf, 0);
-        mma();
-        ldf(buf, 1);
-        mma();
-      }
-      if (prio & 1) __builtin_amdgcn_s_setprio(0);
+      if (kPrioMfma) __builtin_amdgcn_s_setprio(1);
+      step16(buf, 0);
+      step16(buf, 1);
+      if (kPrioMfma) __builtin_amdgcn_s_setprio(0);
       // keep the MFMAs ahead of the barrier: moved past it, they would wait
       // for the stagers instead of overlapping them
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();  // B_u
     }
-    if (SK && !(a.dbg & 8)) {
-      const Geo g = ML ? select_level(a, tile) : geo_of(a);
-      const int mt = tile / a.nN, nt = tile - mt * a.nN;
-      store_partial<WN, TM, TN>(a, g, acc, mt * BM, nt * BN, wr, wc, lane, split);
-    }
-    pit += kt1 - kt0;
-    if (!SK || pit >= it_end) break;
-    }  // pieces
   }
-  if (SK || (a.dbg & 8)) return;  // (dbg 8: ablation, no epilogue)
-  int tile, kt0, kt1, split;
-  piece(it, tile, kt0, kt1, split);
-  const Geo g = ML ? select_level(a, tile) : geo_of(a);
-  const int mt = tile / a.nN, nt = tile - mt * a.nN;
-  const int m0 = mt * BM, n0 = nt * BN;
+  if constexpr ((kAblate & 8) != 0) return;  // (ablation: no epilogue)
   if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
     if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
-    if constexpr (!ML) {
-      if (a.tile_cnt) splitk_fixup<BM, BN, 1024>(a, g, tile, m0, n0, smem);
-    }
     return;
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                           smem);
-}
-
-// Pre-split variant: x and w arrive as three bf16 planes each (h, m, l of the
-// exact split, d2mi_split_bf16x3 / a producer that wrote them), so staging is
-// a plain copy global -> LDS (no VALU split per tap and per Cout tile) and the
-// MFMA loop is the SPLIT one.  4 threads per staged row, 8 channels each:
-// one 16-B buffer load per (row, plane).  Requires Cin % 8 == 0.
-template <int WM, int WN, int TM, int TN, bool DB>
-__global__ __launch_bounds__(256, 2) void conv_x3_kernel(ConvArgs a) {
-  const Geo g = geo_of(a);
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int PA = (BM * 4 + 255) / 256, PB = (BN * 4 + 255) / 256;
-  constexpr int NB = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t As[NB][3 * BM * LDSB];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[NB][3 * BN * LDSB];
-  static_assert(NB * 3 * BM * LDSB / 2 >= 32 * (BN + 4), "LDS epilogue slab does not fit in As");
-
-  const int orig = blockIdx.x;
-  const int q = a.ntiles / 8, r8 = a.ntiles % 8, xcd = orig % 8;
-  const int tile =
-      a.tile_base + (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-  const int mt = tile / a.nN, nt = tile - mt * a.nN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int split = blockIdx.y;
-  const int kt0 = split * a.kt_per_split;
-  const int kt1 = min(a.nk, kt0 + a.kt_per_split);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
-  const int r4 = tid >> 2, c8 = (tid & 3) * 8;
-
-  int ih0[PA], iw0[PA], base[PA];
-#pragma unroll
-  for (int p = 0; p < PA; ++p) {
-    const int m = m0 + r4 + 64 * p;
-    const int mm = m < g.M ? m : 0;
-    const int n = mm / (g.OH * g.OW);
-    const int rem = mm - n * g.OH * g.OW;
-    const int oh = rem / g.OW, ow = rem - oh * g.OW;
-    const int ihv = oh * a.stride - a.pad;
-    ih0[p] = m < g.M ? ihv : -(1 << 29);
-    iw0[p] = ow * a.stride - a.pad;
-    base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + c8;
-  }
-  __amdgpu_buffer_rsrc_t xr[3], wr3[3];
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-    xr[pl] = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(a.x3) + (size_t)pl * (a.x_plane_bytes / 2), 0, a.x_plane_bytes,
-        0x00020000);
-    wr3[pl] = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(a.w3) + (size_t)pl * (a.w_plane_bytes / 2), 0, a.w_plane_bytes,
-        0x00020000);
-  }
-  constexpr uint32_t kOOB = 0x80000000u;
-
-  uint4 ra[PA][3], rb[PB][3];
-  auto load_tile = [&](int kt) {
-    // channel-chunk-major, tap-minor K order: consecutive k-steps read the
-    // same 32 channels at neighbouring pixels (the 3x3 taps), which are
-    // still in L2 (tap-major order re-fetched them Cin/32 steps later)
-    const int taps = a.KH * a.KW;
-    const int chunk = kt / taps;
-    const int tap = kt - chunk * taps;
-    const int cc = chunk * BK;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const bool cok = cc + c8 < a.Cin;
-    const int toff = (kh * g.W + kw) * a.Cin + cc;
-#pragma unroll
-    for (int p = 0; p < PA; ++p) {
-      const bool ok = cok & ((unsigned)(ih0[p] + kh) < (unsigned)g.H) &
-                      ((unsigned)(iw0[p] + kw) < (unsigned)g.W);
-      const uint32_t off = ok ? (uint32_t)(base[p] + toff) * 2u : kOOB;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        ra[p][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr[pl], off, 0, 0));
-    }
-#pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const int co = n0 + r4 + 64 * p;
-      const int wtap = (a.flags & kFlipTaps) ? taps - 1 - tap : tap;
-      const uint32_t off = (cok & (co < a.Cout) & (r4 + 64 * p < BN))
-                               ? (uint32_t)((wtap * a.Cout + co) * a.Cin + cc + c8) * 2u
-                               : kOOB;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        rb[p][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr3[pl], off, 0, 0));
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < PA; ++p)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        *reinterpret_cast<uint4*>(&As[buf][pl * BM * LDSB + swz(r4 + 64 * p, c8)]) = ra[p][pl];
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-      if (BN % 64 == 0 || r4 + 64 * p < BN)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          *reinterpret_cast<uint4*>(&Bs[buf][pl * BN * LDSB + swz(r4 + 64 * p, c8)]) =
-              rb[p][pl];
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int li = lane & 31, lh = lane >> 5;
-  if (kt0 < kt1) {
-    load_tile(kt0);
-    store_tile(0);
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
-      const uint16_t* A16 = As[buf];
-      const uint16_t* B16 = Bs[buf];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[3][TM], fb[3][TN];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            fa[pl][i] = *reinterpret_cast<const bf16x8*>(
-                &A16[pl * BM * LDSB + swz((wr * TM + i) * 32 + li, ks * 16 + lh * 8)]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            fb[pl][j] = *reinterpret_cast<const bf16x8*>(
-                &B16[pl * BN * LDSB + swz((wc * TN + j) * 32 + li, ks * 16 + lh * 8)]);
-        }
-        constexpr int PAi[6] = {1, 2, 0, 0, 1, 0};
-        constexpr int PBi[6] = {1, 0, 2, 1, 0, 0};
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PAi[t]][i], fb[PBi[t]][j],
-                                                                   acc[i][j], 0, 0, 0);
-      }
-      if (DB) {
-        if (more) store_tile(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-      } else {
-        __syncthreads();
-        if (more) {
-          store_tile(0);
-          __syncthreads();
-        }
-      }
-    }
-  }
-  if (WN * TN * 32 == 128 || a.lds_epi)
-    store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
-                                      reinterpret_cast<float*>(&As[0][0]));
-  else
-    store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1);
 }
 
 // x [n] f32 -> [3][n] bf16 planes (h, m, l of the exact truncation split).
@@ -1431,39 +1058,6 @@ __global__ void splitk_reduce4_kernel(ConvArgs a) {
     const int64_t e = 4 * i;
     const int ml = (int)(e / a.Cout), co = (int)(e - (int64_t)ml * a.Cout);
     const int m = a.m_base + ml;
-    float4 o;
-    o.x = epilogue(a, g, acc.x, m, co);
-    o.y = epilogue(a, g, acc.y, m, co + 1);
-    o.z = epilogue(a, g, acc.z, m, co + 2);
-    o.w = epilogue(a, g, acc.w, m, co + 3);
-    *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
-  }
-}
-
-// Stream-K fix-up (ConvArgs::sk): every output element of a tile that is
-// split over workgroups gets its pieces summed in k order (slab s = the
-// tile's s-th piece; a tile inside one workgroup's range has one), then the
-// epilogue.  float4 over channels (the WS kernel's plans have Cout % 4 == 0).
-__global__ void sk_reduce4_kernel(ConvArgs a) {
-  constexpr int BM = 256, BN = 128;  // conv_ws_kernel's tile
-  const Geo g = geo_of(a);
-  const int C4 = a.Cout / 4;
-  const int64_t total4 = (int64_t)a.M * C4;
-  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int m = (int)(i / C4), co = (int)(i - (int64_t)m * C4) * 4;
-    const long long t0 = (long long)((m / BM) * a.nN + co / BN) * a.nk;
-    const int b0 = sk_wg_of(t0, a.sk_P, a.sk_T);
-    const int np = sk_wg_of(t0 + a.nk - 1, a.sk_P, a.sk_T) - b0 + 1;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < np; ++s) {
-      const float4 v = p4[(size_t)s * total4 + i];
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
-    }
     float4 o;
     o.x = epilogue(a, g, acc.x, m, co);
     o.y = epilogue(a, g, acc.y, m, co + 1);
@@ -1576,40 +1170,8 @@ struct Plan {
   // tail_tiles (whole pixel-row blocks) split K tail_splits ways
   int full_tiles, tail_tiles, tail_splits, tail_kt_per_split;
   int main_m_end;  // output rows of the main launch (its split-K partial rows)
-  // stream-K (cfg 3 only): sk_T = ntiles * nk k-steps over sk_P workgroups,
-  // at most sk_slabs pieces per tile
-  int sk, sk_T, sk_P, sk_slabs;
   size_t ws_bytes;
 };
-
-// Tile counters of the in-launch split-K fix-up (splitk_fixup): one pool
-// per (device, stream), zeroed by a stream-ordered memset when it is made.
-// Launches on one stream never overlap and each leaves its counters zero
-// again, so one pool serves every launch on its stream.  Null (allocation
-// failed): the caller keeps the separate reduce launch.
-constexpr int kFixCounters = 1 << 16;
-static unsigned* fix_counters(hipStream_t st) {
-  struct Pool {
-    int dev;
-    hipStream_t st;
-    unsigned* p;
-  };
-  static std::mutex mu;
-  static std::vector<Pool> pools;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const Pool& e : pools)
-    if (e.dev == dev && e.st == st) return e.p;
-  unsigned* p = nullptr;
-  if (hipMalloc(&p, kFixCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(p, 0, kFixCounters * sizeof(unsigned), st) != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
-  }
-  pools.push_back(Pool{dev, st, p});
-  return p;
-}
 
 // Resident workgroups of the 128-wide conv tiles: 2 per CU.
 // Resident workgroups per CU of a plan's kernel: the 128x128 split kernel
@@ -1705,48 +1267,6 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool spli
       }
     }
   }
-  // Stream-K for the WS kernel (tuning "conv_sk"): when the tile grid leaves
-  // CUs idle -- 132 tiles of a 256-CU chip (res3 3x3, 33,600 pixels x 128) --
-  // every CU takes an equal contiguous range of the ntiles * nk k-steps; the
-  // pieces of every tile are summed in a fixed-order fix-up pass.  Cost model
-  // in microseconds, fitted to tools/ws_ab.py on MI355X: a WS k-step 2.4, the
-  // second piece's pipeline fill 2 k-steps, a reduce launch 3, and each M x
-  // Cout f32 slab written or read at 4 TB/s.  Stream-K only where it wins by
-  // 10 %: the partial traffic of the fix-up (every tile, 3-5 slabs) eats the
-  // balance gain on the short-K 1x1s (tools/sk_ab.sh).  Off by default: the
-  // three shapes it takes run 6-17 % faster alone (res3 3x3 84 -> 70 us), but
-  // the training step ran 0.9 % SLOWER with it (in-process A/B, 8 blocks; the
-  // fix-up's slab traffic displaces neighbouring layers' data from the MALL).
-  p.sk = 0;
-  p.sk_T = p.sk_P = p.sk_slabs = 0;
-  if (p.cfg == 3 && tuning(kTuneConvSK) > 0) {
-    const int P = wg_slots(3);
-    const long long T = (long long)p.ntiles * p.nk;
-    const long long per = T / P;
-    const double kstep = 2.4, slab = (double)M * Cout * 4.0 / 4.0e6;
-    double std_us;
-    if (p.tail_tiles > 0)
-      std_us = ((p.full_tiles / G) * p.nk + p.tail_kt_per_split) * kstep;
-    else
-      std_us = ((p.ntiles * p.splits + G - 1) / G) * p.kt_per_split * kstep;
-    if (p.splits > 1) std_us += 3.0 + (p.splits + 1) * slab;
-    if (per >= 6 && T < (1LL << 31)) {
-      const double pieces = (double)p.nk / (double)per + 1.0;  // per tile, about
-      const double sk_us = ((T + P - 1) / P + 2) * kstep + 3.0 + (pieces + 1.0) * slab;
-      if (sk_us < 0.9 * std_us) {
-        p.sk = 1;
-        p.sk_T = (int)T;
-        p.sk_P = P;
-        p.sk_slabs = (int)std::min<long long>(p.nk, (p.nk + per - 1) / per + 1);
-        p.splits = 1;
-        p.kt_per_split = p.nk;
-        p.full_tiles = p.ntiles;
-        p.tail_tiles = 0;
-        p.main_m_end = M;
-        p.ws_bytes = (size_t)p.sk_slabs * M * Cout * sizeof(float);
-      }
-    }
-  }
   return p;
 }
 
@@ -1808,22 +1328,17 @@ extern "C" int d2mi_conv_pack_weights(const float* w_hwio, int KH, int KW, int C
 }
 
 // D2MI_CONV_WS / d2mi_set_tuning("conv_ws", d): the warp-specialised
-// 256x128 split kernel (conv_ws_kernel, plan cfg 3): 0 off, 2 on (1: the
-// A/B form reading a k-step's 12 fragments up front).  r3: a 16-deep, 3/4-stage
-// read-ahead variant (values 4-6) measured bit-identical but slower (removed;
-// DESIGN section 5).
-static int ws_depth() { return tuning(kTuneConvWS); }
+// 256x128 split kernel (conv_ws_kernel, plan cfg 3): 0 off, > 0 on.  r3: a
+// 16-deep, 3/4-stage read-ahead variant measured bit-identical but slower;
+// r4 removed the other measured-slower A/B forms (stream-K, the in-launch
+// split-K fix-up, the multi-level WS launch, the pre-split-plane kernel) --
+// DESIGN section 5 keeps their numbers.
 
 template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
-  if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan_ws)
+  if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan cfg 3)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
-    if (a.sk)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true, true>), grid, dim3(1024), 0, st, a);
-    else if (ws_depth() == 1)
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, false>), grid, dim3(1024), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_ws_kernel<false, 2, true>), grid, dim3(1024), 0, st, a);
+    if constexpr (SPLIT) hipLaunchKernelGGL((conv_ws_kernel<2>), grid, dim3(1024), 0, st, a);
     return;
   }
   if (cfg == 0 && !db && occ3_enabled()) {
@@ -1845,10 +1360,7 @@ static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvA
 // Multi-level launches (ConvArgs::nlev > 0): no split-K, single-buffered.
 template <bool SPLIT>
 static void launch_conv_levels(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
-  if (cfg == 3) {  // (tuning conv_ws_levels: the warp-specialised kernel, split products only)
-    if constexpr (SPLIT)
-      hipLaunchKernelGGL((conv_ws_kernel<true, 2, true>), grid, dim3(1024), 0, st, a);
-  } else if (cfg == 0) {
+  if (cfg == 0) {
     if (occ3_enabled())
       hipLaunchKernelGGL((conv_mfma_kernel<2, 2, 2, 2, false, SPLIT, 3, true>), grid, dim3(256), 0,
                          st, a);
@@ -1861,19 +1373,6 @@ static void launch_conv_levels(int cfg, dim3 grid, hipStream_t st, const ConvArg
   } else {
     hipLaunchKernelGGL((conv_mfma_kernel<4, 1, 1, 1, true, SPLIT, 2, true>), grid, dim3(256), 0, st,
                        a);
-  }
-}
-
-static void launch_x3(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
-  if (cfg == 0) {
-    if (db)
-      hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, true>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_x3_kernel<2, 2, 2, 2, false>), grid, dim3(256), 0, st, a);
-  } else if (cfg == 1) {
-    hipLaunchKernelGGL((conv_x3_kernel<4, 1, 1, 2, true>), grid, dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((conv_x3_kernel<4, 1, 1, 1, true>), grid, dim3(256), 0, st, a);
   }
 }
 
@@ -1891,21 +1390,18 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
   return p.ws_bytes;
 }
 
-// Shared launcher: f32 operands (x, w_packed) or pre-split planes (x3, w3).
-static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
-                     const uint16_t* w3, const float* bias, const float* topdown,
-                     const float* residual, const float* gate, float* y, int N, int H, int W,
-                     int Cin, int Cout, int KH, int KW, int stride, int pad_beg, int pad_end,
-                     int flags, void* workspace, size_t workspace_bytes, void* stream) {
+// Shared launcher of the f32-operand convs (the split or native-f32 MFMA
+// products, flags bit 2).
+static int conv_core(const float* x, const float* w_packed, const float* bias,
+                     const float* topdown, const float* residual, const float* gate, float* y,
+                     int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                     int pad_beg, int pad_end, int flags, void* workspace,
+                     size_t workspace_bytes, void* stream) {
   ConvArgs a = {};
   a.x = x;
-  a.x3 = x3;
-  a.w3 = w3;
   const int64_t xe = (int64_t)N * H * W * Cin, we = (int64_t)KH * KW * Cin * Cout;
-  a.x_bytes = x ? (int)(xe * 4) : 0;
-  a.w_bytes = w_packed ? (int)(we * 4) : 0;
-  a.x_plane_bytes = x3 ? (int)(xe * 2) : 0;
-  a.w_plane_bytes = w3 ? (int)(we * 2) : 0;
+  a.x_bytes = (int)(xe * 4);
+  a.w_bytes = (int)(we * 4);
   a.w = w_packed;
   a.bias = bias;
   a.topdown = topdown;
@@ -1927,21 +1423,13 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.M = N * a.OH * a.OW;
   {
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    static const char* off = getenv("D2MI_CONV_LDS_EPI");  // "0": register epilogue (A/B)
     a.lds_epi = Cout % 4 == 0 && al16(y) && al16(residual) && al16(gate) && al16(topdown) &&
-                al16(workspace) && !(off && off[0] == '0');
+                al16(workspace);
   }
-  {
-    static const char* dbg = getenv("D2MI_CONV_DBG");
-    a.dbg = dbg ? atoi(dbg) : 0;
-    static const char* prio = getenv("D2MI_CONV_PRIO");
-    a.prio = prio ? atoi(prio) : 5;
-    a.reg_partials = tuning(kTuneConvEpi) != 0;
-    a.xcd2 = tuning(kTuneConvXCD) != 0;
-  }
-  Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0 && !x3);
+  a.reg_partials = tuning(kTuneConvEpi) != 0;
+  a.xcd2 = tuning(kTuneConvXCD) != 0;
+  Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
-    p.sk = 0;
     p.splits = 1;
     p.kt_per_split = p.nk;
     p.full_tiles = p.ntiles;
@@ -1962,11 +1450,6 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
   a.tdH = (a.OH + 1) / 2;
   a.tdW = (a.OW + 1) / 2;
   hipStream_t st = as_stream(stream);
-  dim3 grid(a.ntiles, a.splits);
-  a.sk = p.sk;
-  a.sk_T = p.sk_T;
-  a.sk_P = p.sk_P;
-  if (p.sk) a.partial = (float*)workspace;
   ConvArgs t = a;  // the tail launch (when planned)
   if (p.tail_tiles > 0) {
     t.tile_base = p.full_tiles;
@@ -1978,40 +1461,24 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     t.partial = (float*)workspace +
                 (p.splits > 1 ? (size_t)p.splits * p.main_m_end * Cout : (size_t)0);
   }
-  // 128x128 tiles: single-buffered LDS (two barriers per k-step, 2 workgroups
-  // per CU) measured faster than double-buffered (1 workgroup per CU) on every
-  // Mask R-CNN shape, f32 and split, large grids and small
-  // (tools/exp_conv_db.sh).  D2MI_CONV_DB=1 forces double buffering (tuning).
-  static const char* force = getenv("D2MI_CONV_DB");
-  bool db = false;
-  if (force && (force[0] == '0' || force[0] == '1')) db = force[0] == '1';
-  // tuning conv_fix (default 0): the split-K sum and epilogue in the conv
-  // launch itself (the last-arriving workgroup of each tile), not a second
-  // launch.  Bit-identical, but SLOWER (tools/fix_check.sh): the last
-  // arriver reads its tile's S slabs of 64-128 KiB alone (~100 GB/s per
-  // workgroup), where the reduce launch spreads the same bytes over the chip
-  // -- the 16 forward shapes 1634 -> 1721 us (res5 3x3 67 -> 85, mask-head
-  // 3x3 54 -> 68), the training step +6.2 % in-process.  Kept as the A/B knob.
-  const bool fix = tuning(kTuneConvFix) > 0 && !x3 && a.reg_partials && Cout % 4 == 0 &&
-                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)workspace & 15) == 0 &&
-                   a.nM * a.nN <= kFixCounters;
-  unsigned* const cnt = fix ? fix_counters(st) : nullptr;
-  auto launch = [&](ConvArgs c) {
-    const dim3 g(c.sk ? c.sk_P : c.ntiles, c.sk ? 1 : c.splits);
-    const bool fused = cnt && !c.sk && c.splits > 1;
-    c.tile_cnt = fused ? cnt : nullptr;
-    if (x3)
-      launch_x3(p.cfg, db, g, st, c);
-    else if (flags & kSplit3)
+  // 128x128 tiles: single-buffered LDS (two barriers per k-step, 3 workgroups
+  // per CU) measured faster than double-buffered on every Mask R-CNN shape,
+  // f32 and split, large grids and small.
+  const bool db = false;
+  // Split-K partials go to the workspace and a second launch sums them in a
+  // fixed order + applies the epilogue (deterministic).  r3 measured the
+  // in-launch alternative (the last-arriving workgroup of each tile sums its
+  // tile, agent-scope release / acquire): bit-identical but 6 % slower in the
+  // step -- one workgroup reads its tile's 64-128 KiB slabs at ~100 GB/s --
+  // and r4 removed it.
+  auto launch = [&](const ConvArgs& c) {
+    const dim3 g(c.ntiles, c.splits);
+    if (flags & kSplit3)
       launch_conv<true>(p.cfg, db, g, st, c);
     else
       launch_conv<false>(p.cfg, db, g, st, c);
     D2MI_LAUNCH_CHECK();
-    if (c.sk) {
-      const int gr = (int)std::min<int64_t>(((int64_t)c.M * Cout / 4 + 255) / 256, 8192);
-      hipLaunchKernelGGL(sk_reduce4_kernel, dim3(gr), dim3(256), 0, st, c);
-      D2MI_LAUNCH_CHECK();
-    } else if (c.splits > 1 && !fused) {
+    if (c.splits > 1) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
       if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
         const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);
@@ -2024,7 +1491,6 @@ static int conv_core(const float* x, const uint16_t* x3, const float* w_packed,
     }
     return 0;
   };
-  (void)grid;
   if (a.ntiles > 0) {
     const int rc = launch(a);
     if (rc) return rc;
@@ -2067,9 +1533,8 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
     }
     return 0;
   }
-  return conv_core(x, nullptr, w_packed, nullptr, bias, topdown, residual, gate, y, N, H, W, Cin,
-                   Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
-                   stream);
+  return conv_core(x, w_packed, bias, topdown, residual, gate, y, N, H, W, Cin, Cout, KH, KW,
+                   stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
 }
 
 extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,
@@ -2194,16 +1659,11 @@ extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* di
     Mtot += (int64_t)N * OH * OW;
   }
   a.lds_epi = al;
-  // multi-level launches keep the 128-row kernels (no cfg 3) unless tuning
-  // conv_ws_levels: then the split-product long-K convs take the
-  // warp-specialised 256x128 kernel (level tables at its BM, no split-K)
-  const bool ws_lv = tuning(kTuneConvWSLevels) > 0 && (flags & kSplit3) != 0 && al;
-  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al, ws_lv);
-  if (p.cfg == 3) {  // the single-level WS launch's scheduling knobs (results unchanged)
-    static const char* prio = getenv("D2MI_CONV_PRIO");
-    a.prio = prio ? atoi(prio) : 5;
-    a.xcd2 = tuning(kTuneConvXCD) != 0;
-  }
+  // multi-level launches keep the 128-row kernels (no cfg 3: r3 measured the
+  // multi-level warp-specialised form neutral for Mask R-CNN and 2-8 %
+  // slower for the RetinaNet / SOLOv2 towers; removed in r4)
+  a.reg_partials = 0;
+  const Plan p = make_plan((int)std::min<int64_t>(Mtot, 1 << 30), Cout, KH, KW, Cin, al, false);
   a.nN = (Cout + p.BN - 1) / p.BN;
   int t = 0;
   for (int l = 0; l < nlev; ++l) {
@@ -2219,8 +1679,8 @@ extern "C" int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* di
     int tt;
     int S = levels_splits(dims, nlev, Cin, Cout, KH, KW, stride, pad_beg, pad_end, &rows, &tt);
     if (S > 1 && (workspace == nullptr || workspace_bytes < (size_t)S * rows * Cout * 4 ||
-                  ((uintptr_t)workspace & 15) != 0 || !al || p.cfg == 3))
-      S = 1;  // no (usable) workspace, or the WS kernel: one pass per tile
+                  ((uintptr_t)workspace & 15) != 0 || !al))
+      S = 1;  // no (usable) workspace: one pass per tile
     a.splits = S;
     a.kt_per_split = (a.nk + S - 1) / S;
     a.partial = S > 1 ? (float*)workspace : nullptr;
@@ -2269,23 +1729,4 @@ extern "C" int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void*
                      reinterpret_cast<const float4*>(x), n4, reinterpret_cast<uint2*>(out));
   D2MI_LAUNCH_CHECK();
   return 0;
-}
-
-extern "C" int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
-                                   const float* topdown, const float* residual, float* y, int N,
-                                   int H, int W, int Cin, int Cout, int KH, int KW, int stride,
-                                   int pad_beg, int pad_end, int flags, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
-               "bad conv shape");
-  D2MI_REQUIRE(Cin % 8 == 0, "pre-split conv: Cin must be a multiple of 8 (got %d)", Cin);
-  D2MI_REQUIRE(((uintptr_t)x3 & 15) == 0 && ((uintptr_t)w3 & 15) == 0,
-               "x3 and w3 must be 16-byte aligned");
-  D2MI_REQUIRE((flags & ~3) == 0, "flags: bit0 relu, bit1 relu after the residual/top-down add");
-  D2MI_REQUIRE(3 * 2 * (int64_t)N * H * W * Cin < (1ll << 31),
-               "pre-split conv input (3 bf16 planes) must be < 2 GiB; use d2mi_conv2d_nhwc_ex");
-  D2MI_REQUIRE(3 * 2 * (int64_t)KH * KW * Cin * Cout < (1ll << 31), "conv weights too large");
-  return conv_core(nullptr, x3, nullptr, w3, bias, topdown, residual, nullptr, y, N, H, W, Cin,
-                   Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace, workspace_bytes,
-                   stream);
 }

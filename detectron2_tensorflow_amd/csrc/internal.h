@@ -47,10 +47,9 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
 
 // Process-wide kernel-selection knobs (d2mi_set_tuning; initial values from
 // the environment): in-process A/B timing of kernel variants (tools/).
-enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi = 3, kTuneConvSK = 4,
-               kTuneWgradWS1 = 5, kTuneWgradXCD = 6, kTuneConvXCD = 7, kTuneWgradInc = 8, kTuneConvWSMinK = 9,
-               kTuneConvFix = 10, kTuneConvWSLevels = 11,
-               kTuneCount };
+enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi = 3,
+               kTuneWgradWS1 = 4, kTuneWgradXCD = 5, kTuneConvXCD = 6, kTuneWgradInc = 7,
+               kTuneConvWSMinK = 8, kTuneCount };
 int tuning(TuneKey k);
 
 }  // namespace d2mi

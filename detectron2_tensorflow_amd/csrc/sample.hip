@@ -6,7 +6,7 @@
 // fg-first, index order.  The reference shuffles (tf.random_shuffle) and
 // takes the first k; here each masked element's rank r among its kind (a
 // scan) is mapped through a keyed pseudo-random bijection of [0, n) (a
-// 4-round Feistel network on the next power of 4, cycle-walked into range)
+// 6-round Feistel network on the next power of 4, cycle-walked into range)
 // and kept iff perm(r) < k: exactly k of the n, a different uniform draw.
 // Three launches per call (block counts, selection + selected counts, order)
 // replace ~50 small torch / top-k launches per training step.
@@ -26,17 +26,33 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {  // lowbias32 finaliser
   return x;
 }
 
-// Keyed bijection of [0, n) (n >= 1): Feistel on 2 * hb bits (2^(2 hb) >= n),
-// cycle walking (expected < 4 steps: the domain is < 4n).
-__device__ __forceinline__ uint32_t perm(uint32_t x, uint32_t n, uint32_t key) {
+// Keyed bijection of [0, n) (n >= 1): a 6-round Feistel network on 2 * hb
+// bits (2^(2 hb) >= n) whose round keys come from the whole 64-bit seed and
+// the row (round_keys), cycle-walked into range (expected < 4 steps: the
+// domain is < 4n).  Six rounds (Luby-Rackoff needs 4 for a pseudo-random
+// permutation; the extra two cost a few VALU per element) with independent
+// round keys, not one 32-bit key replayed per round.
+constexpr int kFeistelRounds = 6;
+struct RoundKeys {
+  uint32_t k[kFeistelRounds];
+};
+__device__ __forceinline__ RoundKeys round_keys(uint64_t seed, uint32_t stream) {
+  RoundKeys rk;
+  const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < kFeistelRounds; ++i)
+    rk.k[i] = mix32(lo ^ mix32(hi + 0x9e3779b9u * (uint32_t)(i + 1) + mix32(stream)));
+  return rk;
+}
+__device__ __forceinline__ uint32_t perm(uint32_t x, uint32_t n, const RoundKeys& rk) {
   int hb = 1;
   while ((1u << (2 * hb)) < n) ++hb;
   const uint32_t mask = (1u << hb) - 1u;
   do {
     uint32_t l = x >> hb, r = x & mask;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t t = l ^ (mix32(r ^ key ^ (0x9e3779b9u * (uint32_t)(k + 1))) & mask);
+    for (int k = 0; k < kFeistelRounds; ++k) {
+      const uint32_t t = l ^ (mix32(r ^ rk.k[k]) & mask);
       l = r;
       r = t;
     }
@@ -139,8 +155,7 @@ __global__ __launch_bounds__(256) void sample_select_kernel(
   const int kp = min(num_pos, na);
   const int kn = min(num_samples - kp, nb);
   const uint64_t sd = (uint64_t)seed[0];
-  const uint32_t key_p = mix32((uint32_t)sd ^ mix32((uint32_t)(sd >> 32) + 2u * row));
-  const uint32_t key_n = mix32(key_p ^ 0x85ebca6bu);
+  const RoundKeys key_p = round_keys(sd, 2u * row), key_n = round_keys(sd, 2u * row + 1u);
   int kind[4];
   int a = 0, b = 0;
 #pragma unroll

@@ -45,6 +45,32 @@ class Trainer:
         self.iter = start_step
         self._seed = None
 
+    @staticmethod
+    def _loss_terms(losses):
+        """Every loss as a 0-d float32 tensor on one device (what the stack
+        needs).  A Python number becomes a constant tensor; a tensor of
+        another float dtype is cast (no launch when it already is f32); a
+        non-scalar or integer loss raises, naming its key."""
+        terms, dev = [], None
+        for k, v in losses.items():
+            if torch.is_tensor(v):
+                if v.numel() != 1 or not (v.is_floating_point()):
+                    raise TypeError(f"loss {k!r} must be a scalar float tensor, got "
+                                    f"{v.dtype} of shape {tuple(v.shape)}")
+                dev = dev or v.device
+                if v.device != dev:
+                    raise ValueError(f"loss {k!r} is on {v.device}, the others on {dev}")
+                terms.append(v.reshape(()) if v.dtype == torch.float32
+                             else v.reshape(()).to(torch.float32))
+            elif isinstance(v, (int, float)):
+                terms.append(float(v))
+            else:
+                raise TypeError(f"loss {k!r} has unsupported type {type(v).__name__}")
+        if dev is None:
+            raise ValueError("no tensor loss to differentiate")
+        return [t if torch.is_tensor(t) else torch.tensor(t, dtype=torch.float32, device=dev)
+                for t in terms]
+
     def step(self, batched_inputs):
         """One iteration: forward + losses, backward with the overlapped
         all-reduce, clip + momentum update.  Returns the loss dict (device)."""
@@ -55,7 +81,7 @@ class Trainer:
         losses = self.model(batched_inputs)
         # one stack + one sum (not a chain of adds: 2 launches, and the
         # backward hands every loss the same seed without a kernel)
-        total = torch.stack(list(losses.values())).sum()
+        total = torch.stack(self._loss_terms(losses)).sum()
         # the backward seed: one cached 1.0 per device (not a fill per step)
         seed = self._seed
         if seed is None or seed.device != total.device or seed.dtype != total.dtype:

@@ -266,71 +266,6 @@ class _ConvMFMAFn(torch.autograd.Function):
                 None)
 
 
-class _LevelCtx:
-    """The per-level view of a _ConvLevelsFn context, with the attributes
-    _ConvMFMAFn.backward reads (one level of a plain conv + bias + ReLU)."""
-
-    def __init__(self, x, w, y, pads, has_bias, needs, pair, out_info, wacc):
-        self.saved_tensors = (x, w, y)
-        self.conf = (1, pads, True, has_bias, False, False)
-        self.needs_input_grad = needs
-        self.in_info = None
-        self.res_grad_to = None
-        self.grad_from = None
-        self.pair_grad = pair
-        self.join = None
-        self.relu_cand = None
-        self.out_info = out_info
-        self.wacc = wacc
-
-
-class _ConvLevelsFn(torch.autograd.Function):
-    """A conv + bias + ReLU shared by the FPN levels (the RPN head's 3x3,
-    rpn.py:83-96) in training: ONE multi-level forward launch
-    (ops.conv2d_nhwc_levels, the small levels' tiles in the big level's grid)
-    and, per level, _ConvMFMAFn's own backward -- the dgrad with the ROI
-    poolers' pair hand-off and the consumer's ReLU gate, the weight gradient
-    through the level accumulator.  inputs: (w, b, packed, pads, pairs, wacc,
-    *xs); outputs: the levels' ys, each tagged as a fused-ReLU output."""
-
-    @staticmethod
-    def forward(ctx, w, b, packed, pads, pairs, wacc, *xs):
-        ys = ops.conv2d_nhwc_levels(list(xs), packed, b, 1, pads, relu=True)
-        ctx.save_for_backward(w, *xs, *ys)
-        ctx.n, ctx.pads, ctx.pairs, ctx.wacc = len(xs), pads, pairs, wacc
-        ctx.has_bias = b is not None
-        ctx.out_infos = []
-        for y in ys:
-            info = {"masked": False}
-            y._d2mi_relu_info = info
-            ctx.out_infos.append(info)
-        return tuple(ys)
-
-    @staticmethod
-    def backward(ctx, *gys):
-        n = ctx.n
-        saved = ctx.saved_tensors
-        w, xs, ys = saved[0], saved[1:1 + n], saved[1 + n:]
-        nw, nb = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        gxs, gw, gb = [], None, None
-        for l in range(n):
-            needs = (ctx.needs_input_grad[6 + l], nw, nb) + (False,) * 12
-            sub = _LevelCtx(xs[l], w, ys[l], ctx.pads, ctx.has_bias, needs, ctx.pairs[l],
-                            ctx.out_infos[l], ctx.wacc if nw else None)
-            g = gys[l] if gys[l] is not None else torch.zeros_like(ys[l])
-            r = _ConvMFMAFn.backward(sub, g)
-            gxs.append(r[0])
-            if ctx.wacc is None or not nw:
-                # no shared accumulator: autograd's order, the level sum here
-                if r[1] is not None:
-                    gw = r[1] if gw is None else gw + r[1]
-                if r[2] is not None:
-                    gb = r[2] if gb is None else gb + r[2]
-            elif r[1] is not None:  # (the accumulator's last level returns the sums)
-                gw, gb = r[1], r[2]
-        return (gw, gb, None, None, None, None, *gxs)
-
-
 def _join_active(ctx):
     p = ctx.join if ctx.join is not None else ctx.pair_grad
     return p is not None and p.get("join", False) and ctx.grad_from is None
@@ -586,25 +521,6 @@ class Conv2D(Layer):
             self._packed = ops.pack_conv_weights(w.detach())
             self._packed_key = key
         return self._packed
-
-    def levels_train_ok(self, inputs):
-        """call_levels_train applies: an MFMA conv + bias + ReLU (no
-        normaliser, stride 1, SAME) over <= 6 CUDA levels."""
-        return (torch.is_grad_enabled() and self.impl in ("mfma", "auto") and 1 <= len(inputs) <= 6
-                and self.normalizer_fn is None and is_relu(self.act_fn) and self.stride == 1
-                and self.rate == 1 and self.num_groups == 1 and self.in_channels % 4 == 0
-                and self.padding == "SAME" and all(self._mfma_eligible(x) for x in inputs))
-
-    def call_levels_train(self, inputs, pairs=None, wacc=None):
-        """This layer over the FPN levels in training as one multi-level
-        forward launch (_ConvLevelsFn); pairs: each level's pair_grad dict (or
-        None), wacc: the weight-gradient level accumulator."""
-        w, b, _, packed = self.effective_params(want_packed=True)
-        if packed is None:
-            packed = self.packed_weights(w)
-        pads = same_pads(self.kernel_size, self.rate)
-        pairs = list(pairs) if pairs is not None else [None] * len(inputs)
-        return list(_ConvLevelsFn.apply(w, b, packed, pads, pairs, wacc, *inputs))
 
     def call_levels(self, inputs):
         """This layer applied to each of ``inputs`` (feature levels sharing the

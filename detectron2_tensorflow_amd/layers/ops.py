@@ -513,16 +513,9 @@ def pack_conv_weights_many(ws):
 # Conv MFMA product form: "f32" = v_mfma_f32_32x32x2_f32 (exact f32 products);
 # "split" = the same f32 operands split exactly into three bf16 terms
 # (h + m + l == x) and multiplied with six v_mfma_f32_32x32x16_bf16 products
-# (f32-class error, see csrc/conv_mfma.hip).  With Cin % 8 == 0 the split is
-# done once per operand (d2mi_split_bf16x3) and the conv reads the planes
-# (d2mi_conv2d_nhwc_x3); otherwise the conv splits while staging.
-# Process-wide default from D2MI_CONV_MATH.
+# (f32-class error, see csrc/conv_mfma.hip), split while the kernel stages
+# its tiles.  Process-wide default from D2MI_CONV_MATH.
 CONV_MATH = os.environ.get("D2MI_CONV_MATH", "split")
-# Pre-splitting a KxK conv's input (one extra pass) measured slower than
-# splitting while staging once the conv runs 2 workgroups per CU
-# (tools/exp_conv_presplit.sh); kept as a knob and for callers that already
-# hold the planes (x_split).
-PRESPLIT_KXK = os.environ.get("D2MI_CONV_PRESPLIT", "0") == "1"
 
 
 def split_bf16x3(x):
@@ -550,18 +543,13 @@ _CONV_WS, _WGRAD_WS = {}, {}
 _NARROW_SPLIT = os.environ.get("D2MI_NARROW_SPLIT", "1") != "0"
 
 
-def _presplit_ok(x, Cin):
-    return Cin % 8 == 0 and 6 * x.numel() < 2 ** 31
-
-
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
-                residual=None, relu_after_add=False, math_mode=None, w_split=None, x_split=None,
-                flip_taps=False, relu_gate=None, out=None):
+                residual=None, relu_after_add=False, math_mode=None, flip_taps=False,
+                relu_gate=None, out=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
-    CONV_MATH).  w_split / x_split: cached split_bf16x3 planes of w_packed / x.
-    flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
+    CONV_MATH).  flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
     relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv
     (+ residual) : 0 (a dgrad with its producer's ReLU backward fused, and the
     gradient of the producer's other consumer added first)."""
@@ -601,11 +589,8 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
         raise ValueError(f"residual {tuple(residual.shape)} != output {tuple(y.shape)}")
     if math_mode == "split" and Cout <= 64 and not _NARROW_SPLIT:
         math_mode = "f32"
-    presplit = (math_mode == "split" and _presplit_ok(x, Cin) and not flip_taps
-                and relu_gate is None) and (
-        x_split is not None or (KH * KW > 1 and PRESPLIT_KXK))
     flags = (1 if relu else 0) | (2 if relu_after_add else 0) | (8 if flip_taps else 0)
-    if math_mode == "split" and not presplit:
+    if math_mode == "split":
         flags |= 4
     lib = _C.lib()
     wkey = (N, H, W, Cin, Cout, KH, KW, stride, pb, pe)
@@ -615,15 +600,8 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                                               int(stride), int(pb), int(pe))
     ws = _C.scratch(wsb, x.device) if wsb else None
     st = _C.stream_of(x.device)
-    if presplit:
-        x3 = x_split if x_split is not None else split_bf16x3(x)
-        w3 = w_split if w_split is not None else split_bf16x3(w_packed)
     ev = KernelTimer.start()
-    if presplit:
-        rc = lib.d2mi_conv2d_nhwc_x3(_C.ptr(x3), _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
-                                     _C.ptr(residual), _C.ptr(y), N, H, W, Cin, Cout, KH, KW,
-                                     int(stride), int(pb), int(pe), flags, _C.ptr(ws), wsb, st)
-    elif relu_gate is not None:
+    if relu_gate is not None:
         rc = lib.d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,
                                         H, W, Cin, Cout, KH, KW, int(stride), int(pb),
@@ -1472,13 +1450,28 @@ def solo_inference(cate_logits, kernels, mask_features, strides, out_hw, score_t
 _CELLS = {}
 
 
+def _cell_values(c):
+    """The float32 values of one level's cell anchors as a tuple.  A tensor
+    keeps its host copy as an attribute of the tensor object itself (checked
+    against its in-place version counter), so the copy lives and dies with
+    that tensor: no cache key that another tensor at a reused address could
+    match."""
+    if not torch.is_tensor(c):
+        return tuple(np.asarray(c, np.float32).reshape(-1).tolist())
+    got = getattr(c, "_d2mi_host_cells", None)
+    if got is None or got[0] != c._version:
+        got = (c._version, tuple(c.detach().to(torch.float32).reshape(-1).cpu().tolist()))
+        c._d2mi_host_cells = got
+    return got[1]
+
+
 def _cell_host_array(cell_anchors):
-    key = tuple((c.data_ptr(), c._version, tuple(c.shape), str(c.device)) if torch.is_tensor(c)
-                else tuple(np.asarray(c, np.float32).reshape(-1).tolist()) for c in cell_anchors)
+    """ctypes array of every level's cell anchors, cached by VALUE (tens of
+    floats per level)."""
+    key = tuple(_cell_values(c) for c in cell_anchors)
     got = _CELLS.get(key)
     if got is None:
-        cells = torch.cat([torch.as_tensor(c, dtype=torch.float32).reshape(-1).cpu()
-                           for c in cell_anchors]).tolist()
+        cells = [v for lv in key for v in lv]
         got = (_C.host_array(_C.c_float, cells), len(cells))
         if len(_CELLS) > 64:
             _CELLS.clear()

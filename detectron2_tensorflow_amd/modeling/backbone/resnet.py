@@ -2,7 +2,8 @@
 
 A caller of the hot path: the bottleneck 1x1
 and 3x3 convs run on the MFMA conv kernel with FrozenBN folded into the
-weights at run time; the stem's 7x7 (Cin = 3) stays on MIOpen.
+weights at run time; the frozen stem's 7x7 (Cin = 3) runs on its own
+split-bf16 MFMA kernel (d2mi_stem_conv, since r3).
 Structure, strides (STRIDE_IN_1X1), the stem's zero pad + 3x3/2 VALID max
 pool and FREEZE_AT follow the reference.
 """

@@ -36,13 +36,6 @@ class StandardRPNHead(Layer):
     # levels in one buffer (the MFMA wgrad's reduce adds each level into it;
     # layers/convolutional.py:_wgrad_shared) -- autograd's per-level adds go
     ACC_CONV_LEVELS = True
-    # True: in training the shared 3x3 runs as ONE multi-level forward launch
-    # over the FPN levels (layers/convolutional.py:_ConvLevelsFn), backward per
-    # level as before.  Off: correct (tests) and 10 launches fewer per step,
-    # but the training step ran 2.9 % SLOWER in the in-process A/B
-    # (profiles/r3b_rpn_levels_inproc.log) -- the multi-level launch takes the
-    # 128x128 kernel where the p2 level alone runs on the warp-specialised one
-    LEVELS_TRAIN = False
 
     def __init__(self, cfg, input_shape, **kwargs):
         super().__init__(**kwargs)
@@ -105,14 +98,10 @@ class StandardRPNHead(Layer):
                 if fuse and torch.is_grad_enabled() and StandardRPNHead.ACC_CONV_LEVELS else None)
         ys = []
         pairs = [getattr(x, "_d2mi_grad_pair", None) for x in features]
-        shares = None
-        if fuse and StandardRPNHead.LEVELS_TRAIN and self.conv.levels_train_ok(features):
-            shares = self.conv.call_levels_train(list(features), pairs, cacc)
         for li, x in enumerate(features):
             # a level the ROI poolers also read hands its input gradient over
             # (GeneralizedRCNN tags them; the pair_grad protocol)
-            share = (shares[li] if shares is not None
-                     else self.conv(x, pair_grad=pairs[li], wacc=cacc))
+            share = self.conv(x, pair_grad=pairs[li], wacc=cacc)
             if fuse:
                 # the fused 1x1 is the declared SOLE consumer of the 3x3's ReLU
                 # output (its dgrad applies the ReLU mask, _RPNHead1x1Fn): the

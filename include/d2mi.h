@@ -471,15 +471,8 @@ int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* dims, int nle
  * terms are below f32's own rounding of the product) and accumulated in f32.
  *
  * d2mi_split_bf16x3: x [n] f32 -> out [3][n] (bf16 bit patterns of h, m, l);
- * n % 4 == 0.  d2mi_conv2d_nhwc_x3: the same convolution (flags bits 0-1 as
- * above) on operands already split by it: x3 = split of x [N,H,W,Cin],
- * w3 = split of w_packed; Cin % 8 == 0; each operand's 3 planes < 2 GiB. */
+ * n % 4 == 0 (the stem conv's weight planes, d2mi_stem_conv). */
 int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream);
-int d2mi_conv2d_nhwc_x3(const uint16_t* x3, const uint16_t* w3, const float* bias,
-                        const float* topdown, const float* residual, float* y, int N, int H,
-                        int W, int Cin, int Cout, int KH, int KW, int stride, int pad_beg,
-                        int pad_end, int flags, void* workspace, size_t workspace_bytes,
-                        void* stream);
 
 /* Weight gradient of the same convolution (the tf.gradients of Conv2D.call,
  * lib/layers/convolutional.py:198-263, w.r.t. its HWIO kernel):

@@ -45,8 +45,21 @@ seeded detections: tie-free scores, bool and weighted-float labels, a class
 with no detections; the file uses np.float / np.bool / np.NAN, which numpy 2
 removed, so those aliases (float, bool, nan) are restored before it loads.
 
-    python tests/golden/make_golden.py [/root/reference]
+convert_d2_golden.npz: the reference's lib/convert_models/convert_d2.py
+(convert_weights, convert_d2.py:4-187; it imports only numpy) applied to
+seeded detectron2-named state dicts of five model layouts -- Mask R-CNN
+R50-FPN (FrozenBN statistics, num_batches_tracked), RetinaNet R50 (P6P7,
+4-conv towers, per-anchor box order), a Res5ROIHeads (C4) Mask R-CNN with
+class-agnostic box regression, a Cascade R-CNN with a conv box head and GN
+norms plus a deformable-conv offset, and a PanopticFPN semantic head.
+Channel counts are shrunk (the conversion only transposes, renames and
+permutes; the shapes that matter -- box-delta groups of 4, fc1's (C, h, w)
+rows -- keep their structure).  Stored per case: the cfg fields the
+conversion reads (JSON), every input array and every output array.
+
+    python tests/golden/make_golden.py [/root/reference] [--only convert_d2]
 """
+import json
 import importlib.util
 import os
 import sys
@@ -58,6 +71,7 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "nms_golden.npz")
 OUT_MC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "multiclass_nms_golden.npz")
 OUT_BOX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "box_ops_golden.npz")
 OUT_VOC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "voc_metrics_golden.npz")
+OUT_D2 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "convert_d2_golden.npz")
 
 
 def load_reference_metrics(ref_root):
@@ -224,7 +238,186 @@ def multiclass_case(mods, rng, R=120, K=6, thr=0.5, score_thresh=0.3):
     raise RuntimeError("could not draw a threshold-safe multi-class case")
 
 
-def main(ref_root="/root/reference"):
+class _NS:
+    """A cfg-like attribute tree (the fields convert_weights reads)."""
+
+    def __init__(self, d):
+        for k, v in d.items():
+            setattr(self, k, _NS(v) if isinstance(v, dict) else v)
+
+
+def d2_state_dict(cfgd, rng):
+    """A detectron2-named state dict for the layout cfgd describes (small,
+    seeded values; the keys follow detectron2's module names)."""
+    M = cfgd["MODEL"]
+    d = {}
+    C = 3  # shrunk channel count of every plain conv
+
+    def arr(*shape):
+        return rng.standard_normal(shape).astype(np.float32)
+
+    def conv(name, o=C, i=C, k=1, norm="bn", bias=False, offset=False):
+        d[name + ".weight"] = arr(o, i, k, k)
+        if norm in ("bn", "bn_nbt"):
+            d[name + ".norm.weight"] = arr(o)
+            d[name + ".norm.bias"] = arr(o)
+            d[name + ".norm.running_mean"] = arr(o)
+            d[name + ".norm.running_var"] = np.abs(arr(o)) + 0.5
+            if norm == "bn_nbt":
+                d[name + ".norm.num_batches_tracked"] = np.array(7, np.int64)
+        elif norm == "gn":
+            d[name + ".norm.weight"] = arr(o)
+            d[name + ".norm.bias"] = arr(o)
+        if offset:
+            d[name + "_offset.weight"] = arr(18, i, k, k)
+            d[name + "_offset.bias"] = arr(18)
+        if bias:
+            d[name + ".bias"] = arr(o)
+
+    def fc(name, o, i):
+        d[name + ".weight"] = arr(o, i)
+        d[name + ".bias"] = arr(o)
+
+    fpn = M["NECK"]["NAME"] == "FPN"
+    retina = M["NECK"]["TOP_BLOCK_TYPE"] == "P6P7"
+    res5_head = M["ROI_HEADS"]["NAME"] == "Res5ROIHeads"
+    bb = "backbone.bottom_up." if fpn else "backbone."
+    conv(bb + "stem.conv1", k=7, norm="bn_nbt")
+    blocks = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3]}[M["RESNETS"]["DEPTH"]]
+    for g in range(4):
+        pre = "roi_heads." if (res5_head and g == 3 and not retina) else bb
+        for b in range(blocks[g]):
+            conv(f"{pre}res{g + 2}.{b}.conv1", norm="bn_nbt" if b % 2 else "bn")
+            conv(f"{pre}res{g + 2}.{b}.conv2", k=3, norm="bn", offset=(g == 2 and b == 1 and
+                                                                        M.get("_DEFORM", False)))
+            conv(f"{pre}res{g + 2}.{b}.conv3")
+            if b == 0:
+                conv(f"{pre}res{g + 2}.{b}.shortcut")
+    if retina:
+        for lvl in (6, 7):
+            conv(f"backbone.top_block.p{lvl}", k=3, norm=None, bias=True)
+        lvls = (3, 4, 5)
+    else:
+        lvls = (2, 3, 4, 5) if fpn else ()
+    for lvl in lvls:
+        conv(f"backbone.fpn_lateral{lvl}", norm=None, bias=True)
+        conv(f"backbone.fpn_output{lvl}", k=3, norm=None, bias=True)
+    if retina:
+        A = 9
+        for i in range(M["RETINANET"]["NUM_CONVS"]):
+            conv(f"head.cls_subnet.{2 * i}", k=3, norm=None, bias=True)
+            conv(f"head.bbox_subnet.{2 * i}", k=3, norm=None, bias=True)
+        conv("head.cls_score", o=A * 2, k=3, norm=None, bias=True)
+        conv("head.bbox_pred", o=A * 4, k=3, norm=None, bias=True)
+    elif M["META_ARCHITECTURE"] != "SemanticSegmentor":
+        A = 3
+        conv("proposal_generator.rpn_head.conv", k=3, norm=None, bias=True)
+        conv("proposal_generator.rpn_head.objectness_logits", o=A, norm=None, bias=True)
+        conv("proposal_generator.rpn_head.anchor_deltas", o=4 * A, norm=None, bias=True)
+        h = M["ROI_BOX_HEAD"]
+        K = 1 if h["CLS_AGNOSTIC_BBOX_REG"] else M["ROI_HEADS"]["NUM_CLASSES"]
+        res = h["POOLER_RESOLUTION"]
+        fc_in = M["NECK"]["OUT_CHANNELS"] if fpn else M["RESNETS"]["RES2_OUT_CHANNELS"] * 8
+        if h["NUM_CONV"] > 0:
+            fc_in = h["CONV_DIM"]
+        fcd = h["FC_DIM"]
+        stages = [f".{k}" for k in range(3)] if M["ROI_HEADS"]["NAME"] in (
+            "CascadeROIHeads", "CascadeLCCHeads") else [""]
+        for st in stages:
+            for i in range(h["NUM_CONV"]):
+                conv(f"roi_heads.box_head{st}.conv{i + 1}", o=h["CONV_DIM"], i=h["CONV_DIM"], k=3,
+                     norm="gn")
+            for i in range(h["NUM_FC"]):
+                fc(f"roi_heads.box_head{st}.fc{i + 1}", fcd, fc_in * res * res if i == 0 else fcd)
+            fc(f"roi_heads.box_predictor{st}.cls_score", M["ROI_HEADS"]["NUM_CLASSES"] + 1,
+               fcd if h["NUM_FC"] else fc_in)
+            fc(f"roi_heads.box_predictor{st}.bbox_pred", 4 * K, fcd if h["NUM_FC"] else fc_in)
+        if M["MASK_ON"]:
+            for i in range(M["ROI_MASK_HEAD"]["NUM_CONV"]):
+                conv(f"roi_heads.mask_head.mask_fcn{i + 1}", k=3, norm=None, bias=True)
+            conv("roi_heads.mask_head.deconv", k=2, norm=None, bias=True)
+            conv("roi_heads.mask_head.predictor", o=M["ROI_HEADS"]["NUM_CLASSES"], norm=None,
+                 bias=True)
+    if M["META_ARCHITECTURE"] in ("PanopticFPN", "SemanticSegmentor"):
+        ss = M["SEM_SEG_HEAD"]
+        for i, feat in enumerate(ss["IN_FEATURES"]):
+            for k in range(max(1, int(i + 2 - np.log2(ss["COMMON_STRIDE"])))):
+                conv(f"sem_seg_head.{feat}.{2 * k}", k=3, norm="gn")
+        conv("sem_seg_head.predictor", o=ss["NUM_CLASSES"], norm=None, bias=True)
+    # detectron2 checkpoints carry the anchor generator's buffers too
+    d["proposal_generator.anchor_generator.cell_anchors.0" if not retina
+      else "anchor_generator.cell_anchors.0"] = arr(3, 4)
+    return d
+
+
+def d2_layouts():
+    base = {"META_ARCHITECTURE": "GeneralizedRCNN", "MASK_ON": True,
+            "NECK": {"NAME": "FPN", "TOP_BLOCK_TYPE": "LastLevelMaxPool", "OUT_CHANNELS": 3},
+            "RESNETS": {"DEPTH": 50, "RES2_OUT_CHANNELS": 3},
+            "ROI_HEADS": {"NAME": "StandardROIHeads", "NUM_CLASSES": 5},
+            "ROI_BOX_HEAD": {"POOLER_RESOLUTION": 3, "NUM_CONV": 0, "CONV_DIM": 4, "NUM_FC": 2,
+                             "FC_DIM": 6, "CLS_AGNOSTIC_BBOX_REG": False},
+            "ROI_MASK_HEAD": {"NUM_CONV": 4},
+            "RETINANET": {"NUM_CONVS": 4},
+            "SEM_SEG_HEAD": {"IN_FEATURES": ["p2", "p3", "p4", "p5"], "COMMON_STRIDE": 4,
+                             "NUM_CLASSES": 4}}
+
+    def v(**over):
+        m = json.loads(json.dumps(base))
+        for path, val in over.items():
+            node = m
+            keys = path.split("__")
+            for k in keys[:-1]:
+                node = node[k]
+            node[keys[-1]] = val
+        return {"MODEL": m}
+
+    return [
+        ("mask_rcnn_R_50_FPN", v()),
+        ("retinanet_R_50_FPN", v(META_ARCHITECTURE="RetinaNet", MASK_ON=False,
+                                 NECK__TOP_BLOCK_TYPE="P6P7")),
+        ("mask_rcnn_R_50_C4_agnostic", v(NECK__NAME="None", ROI_HEADS__NAME="Res5ROIHeads",
+                                         ROI_BOX_HEAD__NUM_FC=0,
+                                         ROI_BOX_HEAD__CLS_AGNOSTIC_BBOX_REG=True)),
+        ("cascade_conv_head_gn_deform", v(MASK_ON=False, ROI_HEADS__NAME="CascadeROIHeads",
+                                          ROI_BOX_HEAD__NUM_CONV=2,
+                                          ROI_BOX_HEAD__CLS_AGNOSTIC_BBOX_REG=True, _DEFORM=True)),
+        ("panoptic_fpn", v(META_ARCHITECTURE="PanopticFPN")),
+    ]
+
+
+def load_reference_convert_d2(ref_root):
+    spec = importlib.util.spec_from_file_location(
+        "_refconvert", os.path.join(ref_root, "lib", "convert_models", "convert_d2.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def convert_d2_cases(ref, rng):
+    """{case}|cfg (JSON), {case}|in|<d2 name>, {case}|out|<reference name>."""
+    data, names = {}, []
+    for name, cfgd in d2_layouts():
+        d = d2_state_dict(cfgd, rng)
+        src = {k: v.copy() for k, v in d.items()}
+        out = ref.convert_weights(d, _NS(cfgd))  # consumes d
+        assert not d
+        data[f"{name}|cfg"] = np.array(json.dumps(cfgd))
+        for k, v in src.items():
+            data[f"{name}|in|{k}"] = v
+        for k, v in out.items():
+            data[f"{name}|out|{k}"] = np.ascontiguousarray(v)
+        names.append(name)
+    data["cases"] = np.array(names)
+    return data
+
+
+def main(ref_root="/root/reference", *flags):
+    if "--only" in flags and "convert_d2" in flags:
+        d2 = convert_d2_cases(load_reference_convert_d2(ref_root), np.random.default_rng(20261019))
+        np.savez_compressed(OUT_D2, **d2)
+        print("wrote", OUT_D2, len(d2), "arrays")
+        return
     mods = load_reference_np_ops(ref_root)
     rng = np.random.default_rng(20261015)
     cases = [
@@ -250,6 +443,9 @@ def main(ref_root="/root/reference"):
     voc = voc_metrics_cases(load_reference_metrics(ref_root), np.random.default_rng(20261018))
     np.savez_compressed(OUT_VOC, **voc)
     print("wrote", OUT_VOC, {k: v.shape for k, v in voc.items()})
+    d2 = convert_d2_cases(load_reference_convert_d2(ref_root), np.random.default_rng(20261019))
+    np.savez_compressed(OUT_D2, **d2)
+    print("wrote", OUT_D2, len(d2), "arrays")
 
 
 if __name__ == "__main__":

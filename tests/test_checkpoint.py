@@ -5,8 +5,11 @@ No detectron2 checkpoint is in the container: the mapping is checked by a
 round trip (a model exported to detectron2 names and layouts with the
 inverse transforms, converted and loaded into a second model) and by
 known answers for the two non-trivial layout rules (box-delta order, fc1 row
-order).  Against a real detectron2 checkpoint the conversion is parity
-unpinned."""
+order), and since r4 pinned against the reference's own converter
+(lib/convert_models/convert_d2.py, pure numpy) by the committed
+tests/golden/convert_d2_golden.npz (five layouts, bit-equal arrays).  No
+real detectron2 checkpoint is here, so the AP of converted weights is
+unmeasured."""
 import os
 
 import numpy as np
@@ -136,3 +139,33 @@ def test_conversion_kats(tmp_path):
     p = str(tmp_path / "w.npz")
     np.savez(p, **{"a.b": np.arange(3.0)})
     assert list(read_tensor_file(p)) == ["a.b"]
+
+
+class _NS:
+    def __init__(self, d):
+        for k, v in d.items():
+            setattr(self, k, _NS(v) if isinstance(v, dict) else v)
+
+
+def test_convert_weights_matches_reference_fixture():
+    """checkpoint.convert_weights against the REFERENCE's own pure-numpy
+    convert_d2.convert_weights (lib/convert_models/convert_d2.py:4-187), run
+    by tests/golden/make_golden.py on seeded detectron2-named state dicts of
+    five layouts (Mask R-CNN R50-FPN, RetinaNet R50 P6P7, C4 Res5ROIHeads with
+    class-agnostic boxes, Cascade with a GN conv box head + a deformable
+    offset, PanopticFPN): the same reference names, every array equal bit
+    for bit (transposes, box-order permutations, fc1 row order)."""
+    import json
+    from detectron2_tensorflow_amd.checkpoint.convert_d2 import convert_weights
+    z = np.load(os.path.join(ROOT, "tests", "golden", "convert_d2_golden.npz"))
+    cases = [str(c) for c in z["cases"]]
+    assert len(cases) == 5
+    for case in cases:
+        cfg = _NS(json.loads(str(z[f"{case}|cfg"])))
+        pin, pout = f"{case}|in|", f"{case}|out|"
+        src = {k[len(pin):]: z[k] for k in z.files if k.startswith(pin)}
+        want = {k[len(pout):]: z[k] for k in z.files if k.startswith(pout)}
+        got = convert_weights(src, cfg)
+        assert sorted(got) == sorted(want), (case, set(got) ^ set(want))
+        for k, v in want.items():
+            assert got[k].shape == v.shape and np.array_equal(got[k], v), (case, k)

@@ -126,9 +126,9 @@ def test_faster_rcnn_batch_shapes_and_determinism(dev):
     model = _model(dev, mask=False)
     img = torch.rand(2, 320, 480, 3, device=dev) * 255
     inp = {"image": img, "image_shape": torch.tensor([[320, 480], [300, 470]], device=dev)}
-    # the backbone's 3x3 convs / stem run on MIOpen, whose default solutions
-    # include atomic split-K kernels: ask for deterministic ones (the HIP hot
-    # path itself is deterministic: fixed-order split-K, sorted NMS / top-k)
+    # every conv of this model runs on the HIP kernels (deterministic:
+    # fixed-order split-K, sorted NMS / top-k); the flag only guards a torch
+    # fallback conv (MIOpen, whose default solutions include atomic split-K)
     old = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:

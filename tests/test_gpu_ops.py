@@ -574,75 +574,6 @@ def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
         assert es <= 4 * ef + 1e-6, (es, ef)
 
 
-@pytest.mark.parametrize("shape", [
-    (2, 25, 42, 512, 512, 3),    # res5 3x3 on the WS kernel: 36 tiles x 7 splits
-    (2, 50, 84, 1024, 256, 1),   # res4 1x1 reduce: WS, 3 splits
-    (1, 20, 30, 64, 64, 3),      # Cout 64: the 128x64 kernel's split-K (5 tiles x 2)
-])
-def test_conv2d_in_launch_fixup_bit_identical(dev, shape):
-    """Tuning conv_fix (the split-K slabs summed by each tile's last-arriving
-    workgroup inside the conv launch, agent-scope release / acquire across
-    XCDs) gives the separate reduce launch's outputs bit for bit -- with a
-    residual + ReLU epilogue, and twice in a row (the counters are left zero)."""
-    N, H, W, Cin, Cout, k = shape
-    pad = (k - 1) // 2
-    g = torch.Generator().manual_seed(7 + sum(shape))
-    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
-    w = (torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)).to(dev)
-    b = torch.randn(Cout, generator=g).to(dev)
-    res = torch.randn(N, H, W, Cout, generator=g).to(dev)
-    wp = ops().pack_conv_weights(w)
-    run = lambda: ops().conv2d_nhwc(x, wp, b, 1, (pad, pad), math_mode="split", relu=True,
-                                    residual=res, relu_after_add=True)
-    try:
-        ops().set_tuning("conv_fix", 0)
-        y0 = run()
-        ops().set_tuning("conv_fix", 1)
-        y1, y2 = run(), run()
-    finally:
-        ops().set_tuning("conv_fix", 0)  # the default
-    assert torch.equal(y1, y0) and torch.equal(y2, y0)
-
-
-@pytest.mark.parametrize("shape", [
-    (2, 100, 168, 128, 128, 3),  # res3 3x3: 132 tiles of a 256-CU chip
-    (2, 50, 84, 1024, 512, 1),   # res4 -> res5 1x1: 132 tiles
-])
-def test_conv2d_stream_k_matches_split_k(dev, shape):
-    """The WS kernel's stream-K plan (tuning "conv_sk", chosen where the tile
-    grid would leave CUs idle) forms the same products in other K groups:
-    within f32 rounding of the tile-per-workgroup plan, within 1e-4 of float64
-    on a crop, deterministic, and through the fix-up's epilogue (bias,
-    residual, ReLU after the add)."""
-    N, H, W, Cin, Cout, k = shape
-    pad = (k - 1) // 2
-    g = torch.Generator().manual_seed(sum(shape))
-    x = torch.randn(N, H, W, Cin, generator=g)
-    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
-    b = torch.randn(Cout, generator=g)
-    res = torch.randn(N, H, W, Cout, generator=g)
-    wp = ops().pack_conv_weights(w.to(dev))
-    kw = dict(relu=True, residual=res.to(dev), relu_after_add=True)
-    run = lambda: ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), 1, (pad, pad), math_mode="split", **kw)
-    try:
-        ops().set_tuning("conv_sk", 0)
-        y0 = run()
-        ops().set_tuning("conv_sk", 1)
-        y1, y2 = run(), run()
-    finally:
-        ops().set_tuning("conv_sk", 0)  # the default
-    assert torch.equal(y1, y2)
-    np.testing.assert_allclose(y1.cpu().numpy(), y0.cpu().numpy(), rtol=2e-5, atol=2e-5)
-    # float64 on the first image's first 8 output rows (input rows 0..8 + pad)
-    rows = 8
-    xc = x[:1, :rows + k - 1 - pad].permute(0, 3, 1, 2).double()
-    ref = torch.nn.functional.conv2d(xc, w.permute(3, 2, 0, 1).double(), b.double(),
-                                     padding=pad).permute(0, 2, 3, 1)[:, :rows]
-    want = torch.relu(ref + res[:1, :rows].double())
-    np.testing.assert_allclose(y1[:1, :rows].cpu().double().numpy(), want.numpy(), rtol=1e-4,
-                               atol=1e-4)
-
-
 def test_split_bf16x3_is_exact(dev):
     """h + m + l == x bit for bit (evaluated in float64), each term a bf16.
     Exact wherever the residuals stay normal f32 (|x| >= 2^-110 or so); below
@@ -653,28 +584,6 @@ def test_split_bf16x3_is_exact(dev):
     x3 = ops().split_bf16x3(x.to(dev)).cpu()
     parts = [(x3[i].to(torch.int32) << 16).view(torch.float32).double() for i in range(3)]
     assert torch.equal(parts[0] + parts[1] + parts[2], x.double())
-
-
-def test_conv2d_presplit_matches_split_at_load(dev):
-    """d2mi_conv2d_nhwc_x3 (operands split once) computes exactly what the
-    split-while-staging kernel computes (same products, same order)."""
-    g = torch.Generator().manual_seed(21)
-    x = torch.randn(2, 21, 30, 64, generator=g).to(dev)
-    w = (torch.randn(3, 3, 64, 96, generator=g) / 24).to(dev)
-    b = torch.randn(96, generator=g).to(dev)
-    wp = ops().pack_conv_weights(w)
-    y_pre = ops().conv2d_nhwc(x, wp, b, 1, (1, 1), True, math_mode="split")
-    ops_mod = ops()
-    flags_ref = ops_mod.conv2d_nhwc(x[..., :60].contiguous(),
-                                    ops_mod.pack_conv_weights(w[:, :, :60].contiguous()), b, 1, (1, 1),
-                                    True, math_mode="split")  # Cin 60: split while staging
-    y_ref60 = ops_mod.conv2d_nhwc(x[..., :60].contiguous(),
-                                  ops_mod.pack_conv_weights(w[:, :, :60].contiguous()), b, 1, (1, 1),
-                                  True, math_mode="f32")
-    assert float((flags_ref - y_ref60).abs().max()) < 1e-4
-    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(3, 2, 0, 1).double(),
-                                     b.double(), padding=1).relu().permute(0, 2, 3, 1)
-    np.testing.assert_allclose(y_pre.cpu().double().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=1e-4)
 
 
 def test_conv2d_split_bf16_exact_on_bf16_representable_integers(dev):
@@ -1354,16 +1263,13 @@ def _grad_share_case(dev):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("cout,relu,ws", [(256, True, False), (720, False, False),
-                                          (36, False, False), (256, True, True),
-                                          (720, False, True)])
-def test_conv_levels_matches_per_level_convs(dev, cout, relu, ws):
+@pytest.mark.parametrize("cout,relu", [(256, True), (720, False), (36, False)])
+def test_conv_levels_matches_per_level_convs(dev, cout, relu):
     """d2mi_conv2d_nhwc_levels (one launch over RetinaNet's P3..P7 at 640x640,
     shared weights) == conv2d_nhwc per level: the same per-tile arithmetic,
     summation order differing only where a small level alone would split K;
     and level 0 vs float64.  Cout 720 = the cls_score head (a partial N tile),
-    36 = bbox_pred (narrow: f32 MFMA).  ws: tuning conv_ws_levels, the
-    warp-specialised 256x128 kernel over the levels (conv_ws_kernel<ML>)."""
+    36 = bbox_pred (narrow: f32 MFMA)."""
     from detectron2_tensorflow_amd.layers import ops
     g = torch.Generator(device="cpu").manual_seed(11)
     shapes = [(2, 80, 80), (2, 40, 40), (2, 20, 20), (2, 10, 10), (2, 5, 5)]
@@ -1371,12 +1277,8 @@ def test_conv_levels_matches_per_level_convs(dev, cout, relu, ws):
     w = (torch.randn(3, 3, 256, cout, generator=g) * 0.02).to(dev)
     b = (torch.randn(cout, generator=g) * 0.1).to(dev)
     wp = ops.pack_conv_weights(w)
-    try:
-        ops.set_tuning("conv_ws_levels", 1 if ws else 0)
-        ys = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
-        ys2 = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
-    finally:
-        ops.set_tuning("conv_ws_levels", 0)  # the default
+    ys = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
+    ys2 = ops.conv2d_nhwc_levels(xs, wp, b, 1, (1, 1), relu=relu)
     for y, y2 in zip(ys, ys2):
         assert torch.equal(y, y2)
     for x, y in zip(xs, ys):
@@ -1523,3 +1425,30 @@ def test_fused_subsample_counts_order_and_uniformity(dev):
     sd = math.sqrt(pk * (1 - pk) / T)
     assert abs(f.mean() - pk) < 1e-6 + 1e-3  # exact k per draw
     assert (np.abs(f - pk) < 6 * sd).mean() > 0.999, (pk, f.min(), f.max())
+
+
+@pytest.mark.gpu
+def test_fused_subsample_pairwise_co_inclusion(dev):
+    """Second-order uniformity of d2mi_subsample: with k of n kept, every pair
+    of candidates must be kept together with probability k(k-1) / (n(n-1)),
+    as for a uniform shuffle (tf.random_shuffle(...)[:k]).  4,000 independent
+    draws (rows: each row's Feistel round keys differ), n = 40, k = 10: all
+    780 pair frequencies within 5 sd, and neighbouring ranks (where a weak
+    permutation would correlate) no further off on average than the rest."""
+    T, n, k, bg = 4000, 40, 10, 80
+    lab = torch.full((T, n), 3, dtype=torch.int64, device=dev)
+    seed = torch.tensor([987654321987], dtype=torch.int64, device=dev)
+    pos, neg = ops().subsample(lab, k, k, bg, seed)
+    assert not neg.any()
+    p = pos.double()
+    assert bool((p.sum(1) == k).all())
+    first = (p.sum(0) / T).cpu().numpy()
+    pk = k / n
+    assert np.all(np.abs(first - pk) < 5 * math.sqrt(pk * (1 - pk) / T)), first
+    co = ((p.t() @ p) / T).cpu().numpy()
+    p2 = k * (k - 1) / (n * (n - 1))
+    sd = math.sqrt(p2 * (1 - p2) / T)
+    off = co[~np.eye(n, dtype=bool)]
+    assert np.all(np.abs(off - p2) < 5 * sd), (off.min(), off.max(), p2)
+    near = np.array([co[i, i + 1] for i in range(n - 1)])
+    assert abs(near.mean() - p2) < 5 * sd / math.sqrt(n - 1) + 1e-3, (near.mean(), p2)

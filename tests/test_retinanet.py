@@ -178,7 +178,7 @@ def test_c4_retinanet_r101_1333x800_dense_anchors(dev):
     batch = {"image": img.to(dev), "image_shape": torch.tensor([[800, 1333], [800, 1333]], device=dev)}
     model = _calibrated_gpu_model(dev, 101, batch)
     old = torch.backends.cudnn.deterministic
-    torch.backends.cudnn.deterministic = True  # the MIOpen stem: no atomic split-K
+    torch.backends.cudnn.deterministic = True  # any torch fallback conv (MIOpen): no atomic split-K
     try:
         with torch.no_grad():
             cls, box = _gpu_head(model, batch)

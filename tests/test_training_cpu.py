@@ -396,3 +396,38 @@ def test_cpu_training_step_restatement_runs_and_updates():
     assert all(np.isfinite(v) for v in losses.values()), losses
     assert not torch.equal(w_tr, step.m.roi_heads.box_head.fcs[0].weights.detach())
     assert torch.equal(w_fz, step.m.backbone.stem.conv1.weights.detach())
+
+
+def test_cell_anchor_host_cache_follows_values():
+    """ops._cell_host_array (the host copy of the cell anchors handed to the
+    fused proposal / RetinaNet decoders) must follow the anchors' VALUES:
+    models with different anchor sizes built and freed in one process (tensors
+    at reused addresses), and in-place edits, never see a stale copy."""
+    from detectron2_tensorflow_amd.layers import ops
+    from detectron2_tensorflow_amd.modeling.anchor_generator import generate_cell_anchors
+    for i in range(40):
+        sizes = (32 * (1 + i % 3),)
+        cells = [generate_cell_anchors(sizes, (0.5, 1, 2))]
+        arr, n = ops._cell_host_array(cells)
+        want = torch.as_tensor(cells[0], dtype=torch.float32).reshape(-1).tolist()
+        assert n == len(want) and list(arr)[:n] == want
+        del cells, arr
+    c = generate_cell_anchors((64,), (1,))
+    ops._cell_host_array([c])
+    c.mul_(2)  # in place: the version counter moves, the copy is refreshed
+    arr, n = ops._cell_host_array([c])
+    assert list(arr)[:n] == c.reshape(-1).tolist()
+
+
+def test_trainer_loss_terms_cast_and_reject():
+    """Trainer._loss_terms: mixed float dtypes and Python numbers are summed as
+    f32 scalars; a non-scalar or integer loss raises naming its key."""
+    from detectron2_tensorflow_amd.engine.trainer import Trainer
+    t = Trainer._loss_terms({"a": torch.tensor(1.5), "b": torch.tensor(2.0, dtype=torch.float64),
+                             "c": 0.25, "d": torch.tensor([3.0])})
+    assert all(x.dtype == torch.float32 and x.dim() == 0 for x in t)
+    assert float(torch.stack(t).sum()) == 6.75
+    with pytest.raises(TypeError, match="'bad'"):
+        Trainer._loss_terms({"a": torch.tensor(1.0), "bad": torch.ones(2)})
+    with pytest.raises(TypeError, match="'n'"):
+        Trainer._loss_terms({"n": torch.tensor(3)})

@@ -37,11 +37,6 @@ def _conv_ws(on):
     ops.set_tuning("conv_ws", 2 if on else 0)
 
 
-def _conv_sk(on):
-    from detectron2_tensorflow_amd.layers import ops
-    ops.set_tuning("conv_sk", 1 if on else 0)
-
-
 def _wgrad_ws1(on):
     from detectron2_tensorflow_amd.layers import ops
     ops.set_tuning("wgrad_ws1", 6 if on else 0)
@@ -69,25 +64,13 @@ def _rpn_conv_acc(on):
     StandardRPNHead.ACC_CONV_LEVELS = on
 
 
-def _rpn_levels(on):
-    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
-    StandardRPNHead.LEVELS_TRAIN = on
-
-
-def _rpn_levels_ws(on):  # the levels form on the warp-specialised kernel vs per level
-    from detectron2_tensorflow_amd.layers import ops
-    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
-    StandardRPNHead.LEVELS_TRAIN = on
-    ops.set_tuning("conv_ws_levels", 1 if on else 0)
-
-
 def _rpn_concat(on):
     from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import StandardRPNHead
     StandardRPNHead.CONCAT_OUT = on
 
 
-SWITCHES = {"rpn_concat": _rpn_concat, "rpn_levels": _rpn_levels, "rpn_levels_ws": _rpn_levels_ws, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
-            "conv_ws": _conv_ws, "conv_epi": _conv_epi, "conv_sk": _conv_sk,
+SWITCHES = {"rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+            "conv_ws": _conv_ws, "conv_epi": _conv_epi,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
 

@@ -71,15 +71,11 @@ def bench_conv(dev, iters):
             res = torch.randn(N, OH, OW, Cout, device=dev)
         if name.endswith("+td"):
             td = torch.randn(N, (OH + 1) // 2, (OW + 1) // 2, Cout, device=dev)
-        w3 = ops.split_bf16x3(wp)
-        x3 = ops.split_bf16x3(x)
-        run = lambda mm, xs=None: ops.conv2d_nhwc(x, wp, b, s, (p, p), relu=res is not None,  # noqa: E731
-                                                  residual=res, topdown=td,
-                                                  relu_after_add=res is not None, math_mode=mm,
-                                                  w_split=w3, x_split=xs)
+        run = lambda mm: ops.conv2d_nhwc(x, wp, b, s, (p, p), relu=res is not None,  # noqa: E731
+                                         residual=res, topdown=td,
+                                         relu_after_add=res is not None, math_mode=mm)
         ms = timeit(lambda: run("f32"), iters)
         ms_s = timeit(lambda: run("split"), iters)
-        ms_k = timeit(lambda: run("split", x3), iters)
         err = {}
         if N * H * W <= 140000:  # float64 reference on a slice of the batch
             n1 = 1 if N <= 2 else 8
@@ -100,7 +96,6 @@ def bench_conv(dev, iters):
         out.append({"kernel": "conv", "shape": name, "mfma_us": round(ms * 1e3, 1),
                     "mfma_tflops": round(flops / ms / 1e9, 1),
                     "split_us": round(ms_s * 1e3, 1), "split_tflops": round(flops / ms_s / 1e9, 1),
-                    "x3conv_us": round(ms_k * 1e3, 1), "x3conv_tflops": round(flops / ms_k / 1e9, 1),
                     "max_rel_err_f32": err.get("f32"), "max_rel_err_split": err.get("split"),
                     "miopen_us": round(ms_t * 1e3, 1),
                     "miopen_tflops": round(flops / ms_t / 1e9, 1)})

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Run one conv shape repeatedly (for rocprofv3 PMC passes on the conv kernel).
 
-    python tools/conv_one.py --shape 2,200,336,256,256,3,1 --mode x3|split|f32 --iters 20
+    python tools/conv_one.py --shape 2,200,336,256,256,3,1 --mode split|f32 --iters 20
 """
 import argparse
 import os
@@ -17,7 +17,7 @@ from detectron2_tensorflow_amd.layers import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="2,200,336,256,256,3,1")
-    ap.add_argument("--mode", default="x3")
+    ap.add_argument("--mode", default="split")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     N, H, W, Cin, Cout, k, s = map(int, a.shape.split(","))
@@ -27,15 +27,13 @@ def main():
     w = torch.randn(k, k, Cin, Cout, device=dev) / (k * k * Cin) ** 0.5
     wp = ops.pack_conv_weights(w)
     p = (k - 1) // 2
-    x3 = ops.split_bf16x3(x) if a.mode == "x3" else None
-    w3 = ops.split_bf16x3(wp) if a.mode == "x3" else None
     mm = "f32" if a.mode == "f32" else "split"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode=mm, x_split=x3, w_split=w3)
+    ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode=mm)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(a.iters):
-        ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode=mm, x_split=x3, w_split=w3)
+        ops.conv2d_nhwc(x, wp, None, s, (p, p), math_mode=mm)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters

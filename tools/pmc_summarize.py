@@ -30,8 +30,8 @@ import sys
 SPLIT_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), true"
 F32_CONV = r"conv_mfma_kernel<\d+, \d+, \d+, \d+, (?:true|false), false"
 GROUPS = {
-    "conv2d_split": (re.compile(SPLIT_CONV + r"|conv_x3_kernel|conv_ws_kernel|splitk_reduce\w*_kernel"),
-                     re.compile(SPLIT_CONV + r"|conv_x3_kernel|conv_ws_kernel")),
+    "conv2d_split": (re.compile(SPLIT_CONV + r"|conv_ws_kernel|splitk_reduce\w*_kernel"),
+                     re.compile(SPLIT_CONV + r"|conv_ws_kernel")),
     "conv2d_mfma": (re.compile(F32_CONV), None),
     "roi_align_fwd": (re.compile(r"roi_align_fwd_kernel<true"), None),  # split below
     "roi_align_bwd": (re.compile(r"roi_bwd_"), re.compile(r"roi_bwd_clear_kernel")),
