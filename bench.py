@@ -597,8 +597,11 @@ def main():
         torch.cuda.nvtx.range_push("timed_region")  # roctx: tools/prof_window.py
         sampler.start()
         t0 = time.perf_counter()
+        reducer = trainer.reducer if args.mode == "train" else None
         for i in range(args.steps):
             KernelTimer.enabled = (i == sample) and not args.no_kernel_timing
+            if reducer is not None:  # per-bucket all-reduce events (world > 1)
+                reducer.timing = i == sample and not args.no_kernel_timing
             out = step()
         torch.cuda.synchronize()
         if world > 1:
@@ -625,6 +628,12 @@ def main():
         in_sync = all(bool(torch.equal(allck[0], c)) for c in allck)
     if args.mode == "train":
         extra = {"losses_last_step_rank0": {k: round(float(v.detach()), 4) for k, v in out.items()}}
+        tl = trainer.reducer.timeline() if world > 1 else None
+        if tl is not None:
+            # rank 0's buckets on the sampled step: when each became ready and
+            # when its all-reduce completed, relative to the end of backward;
+            # exposed_ms = the all-reduce time the backward did not hide
+            extra["allreduce_rank0"] = tl
         rh = getattr(model, "roi_heads", None)
         if getattr(rh, "last_mask_rows", None) is not None:
             # mask head rows of the last step: the foreground ROIs (as the

@@ -102,6 +102,9 @@ _SIGS = {
     "d2mi_conv2d_wgrad_ex": (c_int, [P, P, P, P] + [c_int] * 11 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "d2mi_conv2d_nhwc_planes": (c_int, [P, P, ctypes.c_int64, P, P, P, P, P, P, P, c_int, c_int,
+                                        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        c_int, P, c_size_t, P]),
     "d2mi_conv2d_nhwc_gated": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                        c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_levels_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int,

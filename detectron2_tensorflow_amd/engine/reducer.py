@@ -26,6 +26,15 @@ launches early in backward.  The LAST bucket (the earliest-registered
 parameters, whose gradients backward produces last) is capped at
 ``tail_bytes`` (4 MB, or bucket_bytes if smaller): its all-reduce is the one that cannot overlap the
 backward, so it is kept short.
+
+Timing (``timing = True``, bench.py's sampled step at world > 1): HIP events
+record when each bucket became ready (on the compute stream, at its launch),
+when its all-reduce completed (a side stream that waits only on that
+collective), and the end of backward (the compute stream at ``finish()``);
+``timeline()`` turns them into per-bucket ready / done times relative to the
+end of backward, the all-reduce time the backward did NOT hide
+(``exposed_ms``) and the collectives' busy time (reference semantics: the
+clones' gradient sum of model_deploy.py:408-438 happens after the backward).
 """
 import torch
 import torch.distributed as dist
@@ -40,9 +49,14 @@ class _Bucket:
 
 
 class BucketedAllReduce:
-    def __init__(self, params, bucket_bytes=32 << 20, group=None, tail_bytes=None):
+    def __init__(self, params, bucket_bytes=32 << 20, group=None, tail_bytes=None, always=False):
+        """always: arm the hooks and collectives at world size 1 too (the
+        RCCL path exercised on one GPU: an all-reduce of one rank is exact)."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = self.world > 1 or (always and dist.is_initialized())
+        self.timing = False
+        self._tl = None
         self.params = [p for p in params if p.requires_grad]
         # partition in registration order starting from the tail bucket (at
         # most tail_bytes), then launch order = reverse registration order
@@ -69,7 +83,7 @@ class BucketedAllReduce:
             self.buckets.append(b)
         self._next = 0
         self._hooks = []
-        if self.world > 1:
+        if self.active:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self.reset()
@@ -80,6 +94,11 @@ class BucketedAllReduce:
             b.pending = len(b.params)
             b.work = None
         self._next = 0
+        self._tl = None
+        if self.timing:  # t0: the step's start (every time below is after it)
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record()
+            self._tl = {"t0": t0, "ready": [], "done": [], "end": None}
 
     def _flat(self, b, like):
         if b.flat is None:
@@ -98,13 +117,37 @@ class BucketedAllReduce:
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
             b = self.buckets[self._next]
+            tl = self._tl
+            if tl is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                tl["ready"].append(ev)
             b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+            if tl is not None:
+                # a side stream that waits on this collective alone: its event
+                # marks the all-reduce's completion, not the compute stream's
+                side = self._side_stream(b.flat.device)
+                with torch.cuda.stream(side):
+                    b.work.wait()
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record(side)
+                tl["done"].append(ev)
             self._next += 1
+
+    def _side_stream(self, device):
+        st = getattr(self, "_side", None)
+        if st is None:
+            st = self._side = torch.cuda.Stream(device=device)
+        return st
 
     def finish(self):
         """Wait for every bucket and expose the averaged gradients as .grad."""
-        if self.world == 1:
+        if not self.active:
             return
+        if self._tl is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._tl["end"] = ev
         for b in self.buckets:
             if b.pending:
                 # a parameter got no gradient this step: contribute zeros (all ranks
@@ -119,7 +162,36 @@ class BucketedAllReduce:
             b.work.wait()
             for p, off in zip(b.params, b.offsets):
                 p.grad = b.flat[off: off + p.numel()].view_as(p)
+        self.last_timeline = self._tl
         self.reset()
+
+    def timeline(self):
+        """Per-bucket ready / done times (ms, relative to the end of backward;
+        negative = before it) of the last timed step, the all-reduce time left
+        exposed after backward (``exposed_ms`` = last completion - end of
+        backward, >= 0) and the collectives' busy time (each bucket from
+        max(its ready time, the previous completion) to its completion).
+        Synchronises; None if no step was timed."""
+        tl = getattr(self, "last_timeline", None)
+        if not tl or tl["end"] is None or not tl["done"]:
+            return None
+        torch.cuda.synchronize()
+        t0 = tl["t0"]
+        end = t0.elapsed_time(tl["end"])
+        ready = [t0.elapsed_time(e) - end for e in tl["ready"]]
+        done = [t0.elapsed_time(e) - end for e in tl["done"]]
+        busy, prev = 0.0, float("-inf")
+        for r, d in zip(ready, done):
+            busy += max(0.0, d - max(r, prev))
+            prev = d
+        exposed = max(0.0, done[-1])
+        return {"buckets": len(done),
+                "bucket_mb": [round(b.numel * 4 / 2 ** 20, 2) for b in self.buckets],
+                "ready_ms_vs_backward_end": [round(v, 3) for v in ready],
+                "done_ms_vs_backward_end": [round(v, 3) for v in done],
+                "step_start_to_backward_end_ms": round(end, 3),
+                "exposed_ms": round(exposed, 3), "busy_ms": round(busy, 3),
+                "hidden_frac": round(1.0 - exposed / busy, 4) if busy > 0 else None}
 
     def remove(self):
         for h in self._hooks:

@@ -33,14 +33,18 @@ def broadcast_parameters(model, src=0, group=None):
 
 
 class Trainer:
-    def __init__(self, cfg, model, bucket_bytes=32 << 20, group=None, start_step=0):
+    def __init__(self, cfg, model, bucket_bytes=32 << 20, group=None, start_step=0,
+                 reducer_always=False):
+        """reducer_always: run the bucketed all-reduce (hooks + collectives)
+        at world size 1 too -- the RCCL code path on one GPU (tests)."""
         self.cfg = cfg
         self.model = model
         self.world, self.rank = get_world()
         broadcast_parameters(model, group=group)
         self.optimizer = MomentumSGD(param_groups(model, cfg), momentum=cfg.SOLVER.MOMENTUM,
                                      clip_norm=cfg.SOLVER.CLIP_GRADIENTS_BY_NORM)
-        self.reducer = BucketedAllReduce(self.optimizer.params, bucket_bytes, group)
+        self.reducer = BucketedAllReduce(self.optimizer.params, bucket_bytes, group,
+                                         always=reducer_always)
         self.lr = build_learning_rate(cfg)
         self.iter = start_step
         self._seed = None

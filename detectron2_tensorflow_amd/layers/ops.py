@@ -545,14 +545,17 @@ _NARROW_SPLIT = os.environ.get("D2MI_NARROW_SPLIT", "1") != "0"
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
                 residual=None, relu_after_add=False, math_mode=None, flip_taps=False,
-                relu_gate=None, out=None):
+                relu_gate=None, out=None, x3=None, w3=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
     CONV_MATH).  flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
     relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv
     (+ residual) : 0 (a dgrad with its producer's ReLU backward fused, and the
-    gradient of the producer's other consumer added first)."""
+    gradient of the producer's other consumer added first).
+    x3 / w3: the exact bf16 planes (split_bf16x3) of x / w_packed, read by the
+    warp-specialised kernel instead of splitting f32 rows while staging
+    (d2mi_conv2d_nhwc_planes; bit-identical outputs)."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -600,13 +603,25 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                                               int(stride), int(pb), int(pe))
     ws = _C.scratch(wsb, x.device) if wsb else None
     st = _C.stream_of(x.device)
-    ev = KernelTimer.start()
-    if relu_gate is not None:
+    if (x3 is not None or w3 is not None) and math_mode == "split":
+        for t, ref, nm in ((x3, x, "x3"), (w3, w_packed, "w3")):
+            if t is not None and (t.dtype != torch.int16 or tuple(t.shape) != (3,) + tuple(ref.shape)
+                                  or not t.is_contiguous()):
+                raise ValueError(f"{nm} must be the contiguous int16 [3, *shape] planes of its operand")
+        ev = KernelTimer.start()
+        rc = lib.d2mi_conv2d_nhwc_planes(_C.ptr(x), _C.ptr(x3), x.numel(), _C.ptr(w_packed),
+                                         _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
+                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N, H, W,
+                                         Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
+                                         _C.ptr(ws), wsb, st)
+    elif relu_gate is not None:
+        ev = KernelTimer.start()
         rc = lib.d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,
                                         H, W, Cin, Cout, KH, KW, int(stride), int(pb),
                                         int(pe), flags, _C.ptr(ws), wsb, st)
     else:
+        ev = KernelTimer.start()
         rc = lib.d2mi_conv2d_nhwc_ex(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                      _C.ptr(topdown), _C.ptr(residual), _C.ptr(y), N, H, W,
                                      Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,

@@ -62,3 +62,33 @@ def test_dp_two_ranks_real_model(dev, tmp_path):
         assert d.max().item() <= 1e-5 * scale, d.max().item()
     # the mask branches ran on different (padded) foreground row counts
     assert any(a != b for a, b in rows), rows
+
+
+def test_rccl_backend_one_rank_runs_the_reducer(dev, tmp_path):
+    """The "nccl" (RCCL) backend initialised in a fresh child process at
+    world size 1 (tests/rccl_worker.py): two Trainer.steps of the real model
+    with the bucketed all-reduce forced on give parameters bit-identical to
+    the same steps without the reducer, and the timed step's per-bucket
+    events form a consistent timeline (every bucket ready before it
+    completes, the last completion no earlier than the end of backward
+    minus nothing: exposed_ms >= 0)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0", OMP_NUM_THREADS="4")
+    p = subprocess.Popen([sys.executable, os.path.join(HERE, "rccl_worker.py"), str(tmp_path)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        out = p.communicate(timeout=240)[0]
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 0, f"rccl worker exit {p.returncode}:\n{out[-4000:]}"
+    res = torch.load(os.path.join(tmp_path, "rccl.pt"), weights_only=True)
+    assert res["backend"] == "nccl"
+    assert torch.equal(res["rccl"], res["plain"]), float((res["rccl"] - res["plain"]).abs().max())
+    assert res["rccl_losses"] == res["plain_losses"]
+    tl = res["timeline"]
+    print("rccl timeline:", tl)
+    assert tl is not None and tl["buckets"] == res["buckets"] >= 5
+    assert all(r <= d + 1e-3 for r, d in zip(tl["ready_ms_vs_backward_end"],
+                                              tl["done_ms_vs_backward_end"]))
+    assert tl["exposed_ms"] >= 0.0 and tl["busy_ms"] > 0.0

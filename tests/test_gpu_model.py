@@ -191,3 +191,87 @@ def test_mask_rcnn_pasted_masks_match_oracle_paste(dev, fmt):
                                   (H, W), valid=raw["is_valid"][n].cpu().numpy(), yx_scale=yx)
         np.testing.assert_array_equal(masks[n], want)
     assert masks.sum() > 0
+
+
+def test_faster_rcnn_c2_1333x800_vs_oracle_on_its_own_heads(dev):
+    """Config C2 assembled at its own geometry: Faster R-CNN R50-FPN inference
+    (rcnn.py:92-144) on 2 synthetic 1333x800 images (padded to 1344x800),
+    BASELINE.md score injection.  (1) two forwards are identical and the
+    output has the reference layout (100 slots per image, valid-first,
+    scores descending); (2) the RPN proposals equal the oracle's
+    find_top_rpn_proposals (rpn_outputs.py:29-132) run on the model's OWN
+    RPN-head outputs over all 268,569 anchors per image: scores and valid
+    flags bit-exact, boxes within max(1e-4, 2 ulp); (3) the detections equal
+    the oracle's fast_rcnn_inference (fast_rcnn.py:28-187) on the model's
+    OWN box-head outputs and proposals: classes, kept ROI rows and valid
+    flags bit-exact, scores within 2e-6 relative, boxes within max(1e-4, 2 ulp)."""
+    import oracle
+    from test_gpu_ops import assert_boxes_close
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_rcnn_scores, synthetic_images
+    model = _model(dev, mask=False)
+    batch = synthetic_images(2, 800, 1333, 1000, dev)
+    calibrate_rcnn_scores(model, batch)
+    model.eval()
+    cap = {}
+    pg, rh = model.proposal_generator, model.roi_heads
+    hooks = [pg.rpn_head.register_forward_hook(lambda m, i, o: cap.__setitem__("rpn", o)),
+             pg.register_forward_hook(lambda m, i, o: cap.__setitem__("props", o[0])),
+             rh.box_predictor.register_forward_hook(lambda m, i, o: cap.__setitem__("box", o))]
+    try:
+        with torch.no_grad():
+            a = model.inference(batch)["instances"]
+            rpn_out = [[t.detach().contiguous().cpu().numpy() for t in lst] for lst in cap["rpn"][1:]]
+            props = cap["props"]
+            pboxes = props.boxes.cpu().numpy()
+            pscores = props.get_field("objectness_logits").cpu().numpy()
+            pvalid = props.get_field("is_valid").cpu().numpy()
+            logits, deltas = (t.detach().cpu().numpy() for t in cap["box"])
+            b = model.inference(batch)["instances"]
+    finally:
+        for h in hooks:
+            h.remove()
+    # (1) determinism and layout
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    h = {k: v.cpu().numpy() for k, v in a.items()}
+    N, D = h["is_valid"].shape
+    assert (N, D) == (2, 100) and h["boxes"].shape == (2, 100, 4)
+    for n in range(N):
+        v = h["is_valid"][n]
+        k = int(v.sum())
+        assert k > 0 and v[:k].all() and not v[k:].any()
+        assert np.all(np.diff(h["scores"][n][:k]) <= 0)
+    # (2) proposals vs the oracle on the model's own RPN-head outputs
+    image_hw = batch["image_shape"].cpu().numpy()
+    ag = pg.anchor_generator
+    lg, dl = rpn_out
+    A = lg[0].shape[-1]
+    assert sum(x.shape[1] * x.shape[2] * A for x in lg) == 268569
+    cells = [np.asarray(c.cpu() if torch.is_tensor(c) else c, np.float32) for c in ag.cell_anchors]
+    wprops = []
+    for x, d, s, c in zip(lg, dl, ag.strides, cells):
+        anc = oracle.grid_anchors(x.shape[1], x.shape[2], s, c)
+        wprops.append(oracle.apply_deltas(d.reshape(-1, 4), np.tile(anc, (N, 1)), (1, 1, 1, 1))
+                      .reshape(N, -1, 4))
+    wb, ws, wv = oracle.find_top_rpn_proposals(
+        wprops, [x.reshape(N, -1) for x in lg], image_hw, pg.nms_thresh,
+        pg.pre_nms_topk[False], pg.post_nms_topk[False], float(pg.min_box_side_len))
+    np.testing.assert_array_equal(pvalid, wv)
+    np.testing.assert_array_equal(pscores, ws)
+    assert_boxes_close(pboxes, wb)
+    # (3) detections vs the oracle's fast_rcnn_inference on the model's own box head
+    P = pboxes.shape[1]
+    rows = np.nonzero(pvalid.reshape(-1))[0]
+    roi_img, roi_slot = rows // P, rows % P
+    bw = rh.box2box_transform.weights
+    dec = oracle.apply_deltas(deltas[rows], pboxes.reshape(-1, 4)[rows], bw)
+    want = oracle.fast_rcnn_inference(dec, oracle.softmax(logits[rows]), roi_img, roi_slot, P,
+                                      image_hw, rh.test_score_thresh, rh.test_nms_thresh, D,
+                                      rh.test_nms_cls_agnostic)
+    for n in range(N):
+        wbx, wsc, wc, wvd, wroi = want[n]
+        np.testing.assert_array_equal(h["is_valid"][n], wvd)
+        np.testing.assert_array_equal(h["classes"][n], wc)
+        np.testing.assert_allclose(h["scores"][n], wsc, rtol=2e-6, atol=1e-7)
+        assert_boxes_close(h["boxes"][n], wbx)
+        assert int(wvd.sum()) >= 20  # a realistic survivor count (score injection)

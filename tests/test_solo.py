@@ -154,42 +154,92 @@ def _oracle_tail(probs, dbg, strides, grids, Hm, Wm, OH, OW, kernel="gaussian", 
     return res
 
 
-def _assert_tail_equal(got, want, dbg, score_rtol=1e-5, exact_masks=True):
+# A mask pixel's fate is sigmoid(logit) > 0.5.  Within 4 ulp(1.0) = 2^-21 of
+# logit 0 the float sigmoid is 0.5 +- 1 ulp, so an expf one ulp apart (ocml on
+# the device, libm / numpy in the oracle) can flip the test; anywhere else the
+# two sides must agree.
+THRESH_AMBIGUOUS = 4 * 2.0 ** -23
+
+
+def _unpack_bits(words, P):
+    """[k, W64] int64 (bit p % 64 of word p // 64 = pixel p) -> [k, P] bool."""
+    b = np.unpackbits(np.ascontiguousarray(words).view(np.uint8), axis=1, bitorder="little")
+    return b[:, :P].astype(bool)
+
+
+def _assert_tail_equal(got, want, dbg, score_rtol=1e-5, exact_masks=True, proof=None):
     """score_rtol: the mask-score sums run over Hm x Wm pixels in another
     order than the oracle's (1e-5 at 64x80; 200x336 = 67,200-term sums need 5e-5).
-    exact_masks=False (the C5 geometry, 500 masks x 67,200 pixels): the
-    oracle's numpy exp and the device expf round differently for logits
-    within ~1e-7 of 0, where sigmoid meets the 0.5 mask threshold -- a pixel
-    or two of the 33.6 M may flip: mask sums within 2 on at most 1 % of the
-    rows, pasted masks equal on all but 1e-5 of their pixels, boxes (read off
-    the pasted masks) within 4 px; classes and valid flags stay exact."""
+    exact_masks=False (the C5 geometry, 500 masks x 67,200 pixels): instead of
+    bounds, a per-mismatch proof (``proof`` = (probs, row logits, Hm, Wm, OH,
+    OW, kernel)):
+      1. every top-k mask pixel whose GPU bit differs from the oracle's
+         sigmoid(logit) > 0.5 has |logit| <= THRESH_AMBIGUOUS (the only
+         place two correctly-rounded-to-1-ulp expf can disagree);
+      2. the GPU mask sums are its bit counts, and the oracle's differ from
+         them by exactly the flipped pixels of the row;
+      3. given the GPU's masks, the rest of the tail IS the oracle's: the
+         mask scores within the sum-order bar, Matrix NMS decays within
+         2 * score_rtol, and the pasted masks bit-exact with boxes within
+         max(1e-4, 2 ulp);
+      4. rows with no flipped pixel match the oracle's own run exactly as in
+         the exact case; classes and valid flags are exact throughout."""
+    import oracle
+    import solo
     from test_gpu_ops import assert_boxes_close
     masks, boxes, scores, classes, valid = [t.cpu().numpy() for t in got]
+    nflip = 0
     for n, (im, bx, c, s, v, info) in enumerate(want):
         k = int(dbg["top_count"][n])
         assert k == len(info["top_scores"])
         np.testing.assert_array_equal(dbg["top_classes"][n, :k].cpu().numpy(), info["top_classes"])
-        np.testing.assert_allclose(dbg["top_scores"][n, :k].cpu().numpy(), info["top_scores"],
-                                   rtol=score_rtol, atol=0)
-        gsum = dbg["top_sum"][n, :k].cpu().numpy()
-        if exact_masks:
-            np.testing.assert_array_equal(gsum, info["top_sum_masks"])
-        else:
-            d = np.abs(gsum.astype(np.float64) - info["top_sum_masks"])
-            assert d.max() <= 2 and (d > 0).sum() <= max(1, k // 100), (d.max(), (d > 0).sum())
-        drt = 2 * score_rtol if exact_masks else 1e-3
-        np.testing.assert_allclose(dbg["decayed"][n, :k].cpu().numpy(), info["decayed"],
-                                   rtol=drt, atol=1e-7)
         np.testing.assert_array_equal(valid[n], v)
         np.testing.assert_array_equal(classes[n], c)
-        np.testing.assert_allclose(scores[n], s, rtol=2 * score_rtol if exact_masks else 1e-3,
-                                   atol=0)
+        gts = dbg["top_scores"][n, :k].cpu().numpy()
+        gsum = dbg["top_sum"][n, :k].cpu().numpy()
+        gdec = dbg["decayed"][n, :k].cpu().numpy()
         if exact_masks:
+            np.testing.assert_allclose(gts, info["top_scores"], rtol=score_rtol, atol=0)
+            np.testing.assert_array_equal(gsum, info["top_sum_masks"])
+            np.testing.assert_allclose(gdec, info["decayed"], rtol=2 * score_rtol, atol=1e-7)
+            np.testing.assert_allclose(scores[n], s, rtol=2 * score_rtol, atol=0)
             np.testing.assert_array_equal(masks[n], im)
             assert_boxes_close(boxes[n], bx)
-        else:
-            assert (masks[n] != im).mean() <= 1e-5, (masks[n] != im).mean()
-            np.testing.assert_allclose(boxes[n], bx, rtol=0, atol=4.0)
+            continue
+        probs, row_logits, Hm, Wm, OH, OW, kernel = proof
+        cells = info["top_cells"]
+        L = row_logits(n, cells)                                  # [k, P] GPU logits
+        sig = oracle.sigmoid(L)
+        obits = sig > np.float32(0.5)
+        gbits = _unpack_bits(dbg["mask_bits"][n, :k].cpu().numpy(), Hm * Wm)
+        flip = gbits != obits
+        # 1. flips only at threshold-ambiguous logits
+        assert np.all(np.abs(L[flip]) <= THRESH_AMBIGUOUS), np.abs(L[flip]).max()
+        nflip += int(flip.sum())
+        # 2. the sums are the bit counts; the oracle's differ by the flips
+        np.testing.assert_array_equal(gsum, gbits.sum(1).astype(np.float32))
+        np.testing.assert_array_equal(
+            info["top_sum_masks"].astype(np.int64) - gsum.astype(np.int64),
+            (obits & ~gbits).sum(1) - (gbits & ~obits).sum(1))
+        # 3. the tail on the GPU's masks is the oracle's
+        gm = gbits.astype(np.float32)
+        mscore = ((sig * gm).sum(axis=1, dtype=np.float32) / gsum).astype(np.float32)
+        cate = probs[n][cells, info["top_classes"]]
+        np.testing.assert_allclose(gts, (cate * mscore).astype(np.float32), rtol=score_rtol, atol=0)
+        dec = oracle.matrix_nms(gm, info["top_classes"], gts, gsum, kernel, 2.0)
+        np.testing.assert_allclose(gdec, dec, rtol=2 * score_rtol, atol=1e-7)
+        keep = np.nonzero(gdec > np.float32(0.05))[0][:valid.shape[1]]
+        np.testing.assert_array_equal(keep.size, int(valid[n].sum()))
+        pim, pbx = solo.masks_to_image(gm[keep], Hm, Wm, OH, OW)
+        m = keep.size
+        np.testing.assert_array_equal(masks[n][:m], pim)
+        assert not masks[n][m:].any()
+        assert_boxes_close(boxes[n][:m], pbx)
+        # 4. unflipped rows: the oracle's own run, exactly as the exact case
+        clean = ~flip.any(axis=1)
+        np.testing.assert_allclose(gts[clean], info["top_scores"][clean], rtol=score_rtol, atol=0)
+        np.testing.assert_array_equal(gsum[clean], info["top_sum_masks"][clean])
+    return nflip
 
 
 @pytest.mark.gpu
@@ -250,12 +300,19 @@ def test_solo_tail_vs_oracle_c5_geometry(dev, kernel):
                              [torch.from_numpy(k).to(dev) for k in kern],
                              torch.from_numpy(feats).to(dev), strides, (800, 1344),
                              nms_kernel=kernel, debug=dbg)
-    want = _oracle_tail(dbg["probs"].cpu().numpy(), dbg, strides, grids, Hm, Wm, 800, 1344,
-                        kernel=kernel)
+    probs = dbg["probs"].cpu().numpy()
+    want = _oracle_tail(probs, dbg, strides, grids, Hm, Wm, 800, 1344, kernel=kernel)
     assert all(w[5]["num_candidates"] > 500 for w in want)
     assert all(len(w[5]["top_scores"]) == 500 for w in want)
     assert got[0].shape == (2, 100, 800, 1344)
-    _assert_tail_equal(got, want, dbg, score_rtol=5e-5, exact_masks=False)
+    logits = dbg["logits"].cpu().numpy()
+    live_row = dbg["live_row"].cpu().numpy()
+    offs = dbg["row_off"]
+    row_logits = lambda n, cells: logits[offs[n] + live_row[n][cells]]  # noqa: E731
+    nflip = _assert_tail_equal(got, want, dbg, score_rtol=5e-5, exact_masks=False,
+                               proof=(probs.reshape(2, -1, K), row_logits, Hm, Wm, 800, 1344,
+                                      kernel))
+    print(f"{kernel}: {nflip} threshold-ambiguous mask pixels flipped of {2 * 500 * Hm * Wm}")
     for n in range(2):
         d = dbg["decayed"][n, :500].cpu().numpy()
         fin = np.isfinite(d)
