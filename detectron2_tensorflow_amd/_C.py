@@ -43,6 +43,10 @@ _SIGS = {
     "d2mi_roi_align_bwd2": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int,
                                     c_int, c_int, c_int, P, c_int, P, c_size_t, P]),
+    "d2mi_roi_align_bwd2_ex": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P,
+                                       c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int,
+                                       P, c_size_t, P]),
     "d2mi_nms_workspace_size": (c_size_t, [c_int, c_int]),
     "d2mi_nms": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, c_size_t, P]),
     "d2mi_topk_workspace_size": (c_size_t, [c_int, c_int]),
@@ -102,9 +106,6 @@ _SIGS = {
     "d2mi_conv2d_wgrad_ex": (c_int, [P, P, P, P] + [c_int] * 11 + [P, c_size_t, P]),
     "d2mi_conv2d_nhwc_ex": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
-    "d2mi_conv2d_nhwc_planes": (c_int, [P, P, ctypes.c_int64, P, P, P, P, P, P, P, c_int, c_int,
-                                        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                        c_int, P, c_size_t, P]),
     "d2mi_conv2d_nhwc_gated": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                        c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "d2mi_conv2d_levels_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -138,15 +138,6 @@ struct ConvArgs {
   int tdH, tdW;
   int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
   int xcd2;  // xcd_tile(): the 2-D XCD-contiguous remap (tuning conv_xcd, default 1)
-  // Pre-split operands of the warp-specialised kernel (conv_ws_kernel<LD,
-  // PA, PB>): the exact bf16 planes h, m, l of x (x3) and / or of the packed
-  // weights (w3), plane-major [3][elements] with plane stride x3_plane /
-  // w3_plane elements.  The stagers then copy 16-B chunks (8 channels of one
-  // plane) into the LDS planes instead of loading f32 rows and splitting
-  // them -- the same bf16 terms, so the same products and outputs.
-  const uint16_t* x3;
-  const uint16_t* w3;
-  int x3_plane, w3_plane;
   // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
   // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
   // input / output / gate maps.  The kernel swaps them into the fields above
@@ -766,7 +757,7 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 // 48 KiB from L2 per k-step for twice the 128x128 tile's products (32 KiB).
 // Same K order, product order and accumulation sequence as
 // conv_mfma_kernel<..., SPLIT = true>: bit-identical outputs for equal splits.
-template <int LD, bool PA = false, bool PB = false>
+template <int LD>
 __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 2, TM = 2, TN = 2;
   constexpr int BM = 256, BN = 128, RA = 4, RB = 2, S = 2;
@@ -795,21 +786,11 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   if (wave >= 8) {
     // ------------------------------------------------------------ stagers
     const int st = tid - 512;
-    // f32 operands: a thread stages rows srow + 64 p of A (p < 4) and B
-    // (p < 2), 4 channels each (one float4), split into the three planes.
-    // Plane operands (PA / PB): a thread copies 16-B chunks, 8 channels of one
-    // plane -- chunk pc of rows prow and prow + 128 of A in all three planes
-    // (6 chunks), chunk pc of row prow of B in all three planes (3 chunks).
-    const int srow = st >> 3, schunk = (st & 7) * 4;  // f32 rows srow + 64 p
-    const int prow = st >> 2, pc = (st & 3) * 8;      // plane rows prow (+ 128)
-    constexpr int NRA = PA ? 2 : RA;  // distinct A rows per thread
-    constexpr int NLA = PA ? 6 : RA;  // A loads per k-step
-    constexpr int NLB = PB ? 3 : RB;  // B loads per k-step
-    const int ach = PA ? pc : schunk;
-    int ih0[NRA], iw0[NRA], base[NRA];
+    const int srow = st >> 3, schunk = (st & 7) * 4;  // rows srow + 64 p
+    int ih0[RA], iw0[RA], base[RA];
 #pragma unroll
-    for (int p = 0; p < NRA; ++p) {
-      const int m = m0 + (PA ? prow + 128 * p : srow + 64 * p);
+    for (int p = 0; p < RA; ++p) {
+      const int m = m0 + srow + 64 * p;
       const int mm = m < g.M ? m : 0;
       const int n = mm / (g.OH * g.OW);
       const int rem = mm - n * g.OH * g.OW;
@@ -817,16 +798,12 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
       const int ihv = oh * a.stride - a.pad;
       ih0[p] = m < g.M ? ihv : -(1 << 29);
       iw0[p] = ow * a.stride - a.pad;
-      base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + ach;
+      base[p] = ((n * g.H + ihv) * g.W + iw0[p]) * a.Cin + schunk;
     }
-    const __amdgpu_buffer_rsrc_t xrsrc =
-        PA ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.x3), 0, 6 * a.x3_plane,
-                                               0x00020000)
-           : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrsrc =
-        PB ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.w3), 0, 6 * a.w3_plane,
-                                               0x00020000)
-           : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g.x), 0, g.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w), 0, a.w_bytes, 0x00020000);
     constexpr uint32_t kOOB = 0x80000000u;
     const int taps = a.KH * a.KW;
     // Per staged row, which taps land inside the image (bit t: tap t; the
@@ -834,9 +811,9 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     // extract.
     // Closed form: the valid kw form one run of bits, [max(0, -iw0),
     // min(KW, W - iw0)), replicated at the KW-bit offsets of the valid kh.
-    uint32_t tv[NRA];
+    uint32_t tv[RA];
 #pragma unroll
-    for (int p = 0; p < NRA; ++p) {
+    for (int p = 0; p < RA; ++p) {
       const int kw0 = max(0, -iw0[p]), kw1 = min(a.KW, g.W - iw0[p]);
       const uint32_t cols = kw1 > kw0 ? (uint32_t)((1ull << kw1) - (1ull << kw0)) : 0u;
       uint32_t b = 0;
@@ -844,15 +821,14 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         b |= ((unsigned)(ih0[p] + kh) < (unsigned)g.H ? cols : 0u) << (kh * a.KW);
       tv[p] = b;
     }
-    // weight rows: element offset of (co, chunk) inside a tap's [Cout][Cin]
-    constexpr int NRB = PB ? 1 : RB;
-    int boff[NRB];
-    bool bco[NRB];
+    // weight rows: element offset of (co, schunk) inside a tap's [Cout][Cin]
+    int boff[RB];
+    bool bco[RB];
 #pragma unroll
-    for (int p = 0; p < NRB; ++p) {
-      const int co = n0 + (PB ? prow : srow + 64 * p);
+    for (int p = 0; p < RB; ++p) {
+      const int co = n0 + srow + 64 * p;
       bco[p] = co < a.Cout;
-      boff[p] = co * a.Cin + (PB ? pc : schunk);
+      boff[p] = co * a.Cin + schunk;
     }
     // The loads run in k-step order (kt0, kt0 + 1, ..., then the last one
     // again): a uniform cursor (chunk, tap, kh, kw) advanced by one step
@@ -860,28 +836,23 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
     const int klast = kt0 + max(nks, 1) - 1;
     int c_kt = kt0, c_chunk = kt0 / taps, c_tap = kt0 - (kt0 / taps) * taps;
     int c_kh = c_tap / a.KW, c_kw = c_tap - (c_tap / a.KW) * a.KW;
-    auto load = [&](uint4 (&la)[NLA], uint4 (&lb)[NLB]) {
+    auto load = [&](float4 (&la)[RA], float4 (&lb)[RB]) {
       if constexpr ((kAblate & 1) != 0) return;
       const int cc = c_chunk * BK;
-      const bool acok = cc + ach < a.Cin;
-      const bool bcok = cc + (PB ? pc : schunk) < a.Cin;
+      const bool cok = cc + schunk < a.Cin;
       const int toff = (c_kh * g.W + c_kw) * a.Cin + cc;
       const int wtap = (a.flags & kFlipTaps) ? taps - 1 - c_tap : c_tap;
       const int wsc = wtap * a.Cout * a.Cin + cc;
 #pragma unroll
-      for (int q = 0; q < NLB; ++q) {
-        const int p = PB ? 0 : q;
-        const uint32_t e = (uint32_t)(boff[p] + wsc) + (PB ? (uint32_t)(q * a.w3_plane) : 0u);
-        const uint32_t off = (bcok & bco[p]) ? e * (PB ? 2u : 4u) : kOOB;
-        lb[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
+      for (int p = 0; p < RB; ++p) {
+        const uint32_t off = (cok & bco[p]) ? (uint32_t)(boff[p] + wsc) * 4u : kOOB;
+        lb[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, off, 0, 0));
       }
 #pragma unroll
-      for (int q = 0; q < NLA; ++q) {
-        const int p = PA ? (q & 1) : q;  // PA: item q = (plane q >> 1, row q & 1)
+      for (int p = 0; p < RA; ++p) {
         const bool inb = ((tv[p] >> c_tap) & 1u) != 0;
-        const uint32_t e = (uint32_t)(base[p] + toff) + (PA ? (uint32_t)((q >> 1) * a.x3_plane) : 0u);
-        const uint32_t off = (acok & inb) ? e * (PA ? 2u : 4u) : kOOB;
-        la[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
+        const uint32_t off = (cok & inb) ? (uint32_t)(base[p] + toff) * 4u : kOOB;
+        la[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, off, 0, 0));
       }
       if (c_kt < klast) {  // advance the cursor (uniform)
         ++c_kt;
@@ -896,60 +867,47 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
         }
       }
     };
-    auto write = [&](int buf, const uint4 (&la)[NLA], const uint4 (&lb)[NLB]) {
+    auto write = [&](int buf, const float4 (&la)[RA], const float4 (&lb)[RB]) {
       if constexpr ((kAblate & 2) != 0) {
 #pragma unroll
-        for (int p = 0; p < NLA; ++p) asm volatile("" ::"v"(la[p].x));
+        for (int p = 0; p < RA; ++p) asm volatile("" ::"v"(la[p].x));
 #pragma unroll
-        for (int p = 0; p < NLB; ++p) asm volatile("" ::"v"(lb[p].x));
+        for (int p = 0; p < RB; ++p) asm volatile("" ::"v"(lb[p].x));
         return;
       }
       uint16_t* A16 = reinterpret_cast<uint16_t*>(smem + buf * STAGE);
       uint16_t* B16 = A16 + 3 * BM * LDSB;
-      if constexpr (PA) {
 #pragma unroll
-        for (int q = 0; q < NLA; ++q)
-          *reinterpret_cast<uint4*>(&A16[(q >> 1) * BM * LDSB + swz(prow + 128 * (q & 1), pc)]) =
-              la[q];
-      } else {
-#pragma unroll
-        for (int p = 0; p < RA; ++p) {
-          uint2 h, m, l;
-          split3(__builtin_bit_cast(float4, la[p]), h, m, l);
-          const int o = swz(srow + 64 * p, schunk);
-          *reinterpret_cast<uint2*>(&A16[o]) = h;
-          *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
-          *reinterpret_cast<uint2*>(&A16[2 * BM * LDSB + o]) = l;
-        }
+      for (int p = 0; p < RA; ++p) {
+        uint2 h, m, l;
+        split3(la[p], h, m, l);
+        const int o = swz(srow + 64 * p, schunk);
+        *reinterpret_cast<uint2*>(&A16[o]) = h;
+        *reinterpret_cast<uint2*>(&A16[BM * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&A16[2 * BM * LDSB + o]) = l;
       }
-      if constexpr (PB) {
 #pragma unroll
-        for (int q = 0; q < NLB; ++q)
-          *reinterpret_cast<uint4*>(&B16[q * BN * LDSB + swz(prow, pc)]) = lb[q];
-      } else {
-#pragma unroll
-        for (int p = 0; p < RB; ++p) {
-          uint2 h, m, l;
-          split3(__builtin_bit_cast(float4, lb[p]), h, m, l);
-          const int o = swz(srow + 64 * p, schunk);
-          *reinterpret_cast<uint2*>(&B16[o]) = h;
-          *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
-          *reinterpret_cast<uint2*>(&B16[2 * BN * LDSB + o]) = l;
-        }
+      for (int p = 0; p < RB; ++p) {
+        uint2 h, m, l;
+        split3(lb[p], h, m, l);
+        const int o = swz(srow + 64 * p, schunk);
+        *reinterpret_cast<uint2*>(&B16[o]) = h;
+        *reinterpret_cast<uint2*>(&B16[BN * LDSB + o]) = m;
+        *reinterpret_cast<uint2*>(&B16[2 * BN * LDSB + o]) = l;
       }
     };
     // Register ring of LD k-steps (static indices: the loops are unrolled by
     // LD).  Every load is UNCONDITIONAL (k-steps past the end re-load the last
     // one): with a data-dependent load count hipcc cannot count the loads in
     // flight and drains them all (vmcnt(0)) before each write.
-    uint4 ra[LD][NLA], rb[LD][NLB];
+    float4 ra[LD][RA], rb[LD][RB];
     if constexpr ((kAblate & 1) != 0) {
 #pragma unroll
       for (int j = 0; j < LD; ++j) {
 #pragma unroll
-        for (int p = 0; p < NLA; ++p) ra[j][p] = make_uint4(1u, 2u, 3u, 4u);
+        for (int p = 0; p < RA; ++p) ra[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
 #pragma unroll
-        for (int p = 0; p < NLB; ++p) rb[j][p] = make_uint4(1u, 2u, 3u, 4u);
+        for (int p = 0; p < RB; ++p) rb[j][p] = make_float4(1.f, 2.f, 3.f, 4.f);
       }
     }
 #pragma unroll
@@ -1380,16 +1338,7 @@ template <bool SPLIT>
 static void launch_conv(int cfg, bool db, dim3 grid, hipStream_t st, const ConvArgs& a) {
   if (cfg == 3) {  // the warp-specialised 256x128 split kernel (plan cfg 3)
     // (LD = 3 does not fit the 128-VGPR budget of 4 waves per SIMD: it spills)
-    if constexpr (SPLIT) {
-      if (a.x3 && a.w3)
-        hipLaunchKernelGGL((conv_ws_kernel<2, true, true>), grid, dim3(1024), 0, st, a);
-      else if (a.x3)
-        hipLaunchKernelGGL((conv_ws_kernel<2, true, false>), grid, dim3(1024), 0, st, a);
-      else if (a.w3)
-        hipLaunchKernelGGL((conv_ws_kernel<2, false, true>), grid, dim3(1024), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_ws_kernel<2>), grid, dim3(1024), 0, st, a);
-    }
+    if constexpr (SPLIT) hipLaunchKernelGGL((conv_ws_kernel<2>), grid, dim3(1024), 0, st, a);
     return;
   }
   if (cfg == 0 && !db && occ3_enabled()) {
@@ -1447,8 +1396,7 @@ static int conv_core(const float* x, const float* w_packed, const float* bias,
                      const float* topdown, const float* residual, const float* gate, float* y,
                      int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                      int pad_beg, int pad_end, int flags, void* workspace,
-                     size_t workspace_bytes, void* stream, const uint16_t* x3 = nullptr,
-                     int64_t x3_plane = 0, const uint16_t* w3 = nullptr) {
+                     size_t workspace_bytes, void* stream) {
   ConvArgs a = {};
   a.x = x;
   const int64_t xe = (int64_t)N * H * W * Cin, we = (int64_t)KH * KW * Cin * Cout;
@@ -1481,12 +1429,6 @@ static int conv_core(const float* x, const float* w_packed, const float* bias,
   a.reg_partials = tuning(kTuneConvEpi) != 0;
   a.xcd2 = tuning(kTuneConvXCD) != 0;
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0);
-  if (p.cfg == 3) {  // the plane operands serve the warp-specialised kernel only
-    a.x3 = x3;
-    a.x3_plane = (int)x3_plane;
-    a.w3 = w3;
-    a.w3_plane = (int)((int64_t)KH * KW * Cin * Cout);
-  }
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
     p.splits = 1;
     p.kt_per_split = p.nk;
@@ -1563,8 +1505,7 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
                     const float* topdown, const float* residual, const float* gate, float* y,
                     int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                     int pad_beg, int pad_end, int flags, void* workspace, size_t workspace_bytes,
-                    void* stream, const uint16_t* x3 = nullptr, int64_t x3_plane = 0,
-                    const uint16_t* w3 = nullptr) {
+                    void* stream) {
   D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0,
                "bad conv shape");
   D2MI_REQUIRE(Cin % 4 == 0, "Cin must be a multiple of 4 (got %d)", Cin);
@@ -1587,36 +1528,13 @@ static int conv_f32(const float* x, const float* w_packed, const float* bias,
           x + n0 * xs, w_packed, bias, topdown ? topdown + n0 * ts : nullptr,
           residual ? residual + n0 * ys : nullptr, gate ? gate + n0 * ys : nullptr, y + n0 * ys,
           nn, H, W, Cin, Cout, KH, KW, stride, pad_beg, pad_end, flags, workspace,
-          workspace_bytes, stream, x3 ? x3 + n0 * xs : nullptr, x3_plane, w3);
+          workspace_bytes, stream);
       if (rc) return rc;
     }
     return 0;
   }
   return conv_core(x, w_packed, bias, topdown, residual, gate, y, N, H, W, Cin, Cout, KH, KW,
-                   stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream, x3,
-                   x3_plane, w3);
-}
-
-extern "C" int d2mi_conv2d_nhwc_planes(const float* x, const uint16_t* x3, int64_t x3_plane,
-                                       const float* w_packed, const uint16_t* w3,
-                                       const float* bias, const float* topdown,
-                                       const float* residual, const float* gate, float* y, int N,
-                                       int H, int W, int Cin, int Cout, int KH, int KW, int stride,
-                                       int pad_beg, int pad_end, int flags, void* workspace,
-                                       size_t workspace_bytes, void* stream) {
-  D2MI_REQUIRE((flags & ~15) == 0,
-               "flags: bit0 relu, bit1 relu after the residual/top-down add, bit2 split-bf16 "
-               "MFMA products, bit3 flipped weight taps");
-  D2MI_REQUIRE(!gate || (!topdown && !(flags & 3)), "a gated conv takes no relu / top-down");
-  D2MI_REQUIRE(!x3 || (Cin % 8 == 0 && ((uintptr_t)x3 & 15) == 0 &&
-                       x3_plane >= (int64_t)N * H * W * Cin && 6 * x3_plane < (1ll << 31)),
-               "x3: 16-byte aligned [3][plane] bf16 planes of x, Cin %% 8 == 0, < 2 GiB");
-  D2MI_REQUIRE(!w3 || (Cin % 8 == 0 && ((uintptr_t)w3 & 15) == 0 &&
-                       6 * (int64_t)KH * KW * Cin * Cout < (1ll << 31)),
-               "w3: 16-byte aligned [3][KH*KW*Cout*Cin] bf16 planes of w_packed, Cin %% 8 == 0");
-  return conv_f32(x, w_packed, bias, topdown, residual, gate, y, N, H, W, Cin, Cout, KH, KW,
-                  stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream, x3,
-                  x3_plane, w3);
+                   stride, pad_beg, pad_end, flags, workspace, workspace_bytes, stream);
 }
 
 extern "C" int d2mi_conv2d_nhwc_ex(const float* x, const float* w_packed, const float* bias,

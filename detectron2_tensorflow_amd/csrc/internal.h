@@ -6,8 +6,8 @@ namespace d2mi {
 
 // Segmented ascending sort of 64-bit keys stored in "capacity layout":
 // segment s owns keys[s*cap, s*cap + lens[s]).  Keys beyond lens[s] are
-// ignored.  cap <= kLdsSortCap uses the in-LDS bitonic kernel, larger
-// capacities go through rocPRIM's segmented radix sort.
+// ignored.  cap <= kLdsSortCap: the in-LDS counting-rank kernel; larger
+// capacities: that kernel on kLdsSortCap-key tiles, then merge passes.
 constexpr int kLdsSortCap = 8192;
 size_t sort_workspace_size(int S, int cap);
 int sort_keys_segmented(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* lens, int S,

@@ -9,7 +9,7 @@
 // matrix, which is what runs here:
 //
 //   1. keys   desc_key(score, local index) per candidate (NaN / -inf never selected)
-//   2. sort   segmented bitonic in LDS (<= 8192) or rocPRIM radix sort
+//   2. sort   segmented counting-rank sort in LDS (<= 8192), else 8192-key tiles + merge passes (sort.hip)
 //   3. gather boxes into sorted order, count selectable candidates
 //   4. mask   one wave per (segment, 64-row tile, 64-col tile): every lane holds one
 //             column box, the 64 row boxes are broadcast from LDS and

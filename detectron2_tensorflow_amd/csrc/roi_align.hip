@@ -699,7 +699,8 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
     RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
     int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr) {
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, long long pix_lo,
+    long long pix_hi) {
   __shared__ int32_t lds[4][2][kSeg];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int C = a.C;
@@ -708,6 +709,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
   const int nsets = 1 << set_bits;
   for (int t = blockIdx.x * 4 + w; t < nt; t += gridDim.x * 4) {
     const long long pix = touched[t];
+    if (pix < pix_lo || pix >= pix_hi) continue;  // a level-range pass (bwd2 phase 2)
     int l = 0;
     while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
@@ -779,7 +781,8 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
     int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr) {
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, long long pix_lo,
+    long long pix_hi) {
   constexpr int C = 256;
   constexpr int LPP = 64 / PPW;     // lanes per pixel
   constexpr int F = C / LPP / 4;    // float4 per lane
@@ -796,6 +799,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     const int t = tb + grp;
     if (t >= nt) continue;
     const long long pix = touched[t];
+    if (pix < pix_lo || pix >= pix_hi) continue;  // a level-range pass (bwd2 phase 2)
     int l = 0;
     while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
@@ -1027,9 +1031,20 @@ void bwd_layout(WS& w, int C, const BwdPlan& p) {
 
 // The backward over nsets (1 or 2) ROI sets of the same maps; sets[k] holds
 // each set's ROIs / crop / grad_out (everything else equal).
+// phase bit 1 (prepare): the clear launch (pair counters, bookkeeping, and the
+// maps of levels [lv_lo, lv_hi] not in acc_mask), emits, runs, place, long
+// sort, segment partials -- everything but the pixel pass, its results left in
+// the workspace; bit 2 (pixels): the pixel pass over the touched pixels of
+// levels [lv_lo, lv_hi] only.  Phase 3 is the whole backward.  Split phases
+// let the pixel pass of a level run later, into a map another backward has
+// written in full (the RPN head conv's dgrad: no clear of that map, no second
+// read of it): the workspace must then stay untouched in between.
 int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_levels, int C,
                  int acc_mask, bool vec4, void* workspace, size_t workspace_bytes,
-                 hipStream_t st) {
+                 hipStream_t st, int phase = 3, int lv_lo = 0, int lv_hi = -1) {
+  if (lv_hi < 0) lv_hi = num_levels - 1;
+  D2MI_REQUIRE(phase >= 1 && phase <= 3 && 0 <= lv_lo && lv_lo <= lv_hi && lv_hi < num_levels,
+               "ROIAlign backward: bad phase %d / level range [%d, %d]", phase, lv_lo, lv_hi);
   RoiArgs a = sets[0];
   a.acc_mask = acc_mask;
   long long ns[2] = {0, 0};
@@ -1061,6 +1076,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
   int2* tasks = w.take<int2>((size_t)p.max_tasks);
   BwdCounters* ctr = w.take<BwdCounters>(1);
+  if (phase & 1) {
   ClearList cl = {};
   long long clear_words = 0;
   auto clear = [&](void* ptr, long long words, uint32_t value) {
@@ -1070,7 +1086,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     ++cl.n;
     clear_words += words;
   };
-  for (int l = 0; l < num_levels; ++l)  // untouched pixels: zero (accumulated levels: kept)
+  for (int l = lv_lo; l <= lv_hi; ++l)  // untouched pixels: zero (accumulated levels: kept)
     if (!((acc_mask >> l) & 1))
       clear(a.gfeat[l], (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C, 0u);
   clear(count, p.pairs, 0u);
@@ -1113,6 +1129,25 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
                        count, run_start, seg_first, seg_pixel, ctr, partial);
   D2MI_LAUNCH_CHECK();
+  }  // phase 1
+  if (phase == 2) {  // a pixel pass alone: its non-accumulated maps start from zero
+    ClearList cl = {};
+    long long words = 0;
+    for (int l = lv_lo; l <= lv_hi; ++l)
+      if (!((acc_mask >> l) & 1)) {
+        cl.ptr[cl.n] = reinterpret_cast<uint32_t*>(a.gfeat[l]);
+        cl.words[cl.n] = (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2] * C;
+        words += cl.words[cl.n++];
+      }
+    if (cl.n) {
+      hipLaunchKernelGGL(roi_bwd_clear_kernel,
+                         dim3((unsigned)std::max(1LL, std::min((words / 4 + 255) / 256, 8192LL))),
+                         dim3(256), 0, st, cl);
+      D2MI_LAUNCH_CHECK();
+    }
+  }
+  if (!(phase & 2) || p.n_keys == 0) return 0;
+  const long long pix_lo = p.pm.base[lv_lo], pix_hi = p.pm.base[lv_hi + 1];
   // fixed grid (the touched count stays on the device): at most 8192
   // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
   // beyond residency start as earlier ones retire (the kBatch sweep above)
@@ -1125,16 +1160,16 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     const dim3 g4((unsigned)std::max(1LL, std::min((p.max_touched + 4 * ppw - 1) / (4 * ppw), 8192LL)));
     if (ppw == 8)
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr);
+                         sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
     else
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr);
+                         sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
   } else if (vec4) {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
-                       sb, count, run_start, seg_first, partial, touched, ctr);
+                       sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
   } else {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
-                       sb, count, run_start, seg_first, partial, touched, ctr);
+                       sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
   }
   D2MI_LAUNCH_CHECK();
   return 0;
@@ -1193,16 +1228,16 @@ extern "C" size_t d2mi_roi_align_bwd2_workspace_size(const int32_t* dims, int nu
   return w.off;
 }
 
-extern "C" int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims,
-                                   const float* scales, int num_levels, int C, int box_mode,
-                                   int pad_border, int assign, int min_level, int max_level,
-                                   int canonical_box_size, int canonical_level,
-                                   const float* boxes0, const int32_t* box_ind0, int R0,
-                                   int out_h0, int out_w0, int sr0, const float* grad_out0,
-                                   const float* boxes1, const int32_t* box_ind1, int R1,
-                                   int out_h1, int out_w1, int sr1, const float* grad_out1,
-                                   int accumulate_mask, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
+extern "C" int d2mi_roi_align_bwd2_ex(float* const* grad_feats, const int32_t* dims,
+                                      const float* scales, int num_levels, int C, int box_mode,
+                                      int pad_border, int assign, int min_level, int max_level,
+                                      int canonical_box_size, int canonical_level,
+                                      const float* boxes0, const int32_t* box_ind0, int R0,
+                                      int out_h0, int out_w0, int sr0, const float* grad_out0,
+                                      const float* boxes1, const int32_t* box_ind1, int R1,
+                                      int out_h1, int out_w1, int sr1, const float* grad_out1,
+                                      int accumulate_mask, int phase, int level_lo, int level_hi,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
   RoiArgs sets[2] = {};
   int rc = fill_args(sets[0], dims, scales, num_levels, C, boxes0, box_ind0, R0, out_h0, out_w0,
                      sr0, box_mode, pad_border, assign, min_level, max_level, canonical_box_size,
@@ -1214,14 +1249,36 @@ extern "C" int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims
   if (rc) return rc;
   bool vec4 = (C % 4) == 0 && ((uintptr_t)grad_out0 & 15) == 0 && ((uintptr_t)grad_out1 & 15) == 0;
   for (int l = 0; l < num_levels; ++l) {
-    sets[0].gfeat[l] = sets[1].gfeat[l] = grad_feats[l];
-    vec4 = vec4 && (((uintptr_t)grad_feats[l] & 15) == 0);
+    // (a map outside a phase's level range may be null)
+    sets[0].gfeat[l] = sets[1].gfeat[l] = grad_feats ? grad_feats[l] : nullptr;
+    vec4 = vec4 && (((uintptr_t)sets[0].gfeat[l] & 15) == 0);
   }
   sets[0].gout = grad_out0;
   sets[1].gout = grad_out1;
   D2MI_REQUIRE((accumulate_mask >> num_levels) == 0, "accumulate_mask has bits past the levels");
+  for (int l = level_lo; l <= level_hi && l < num_levels; ++l)
+    D2MI_REQUIRE(l < 0 || sets[0].gfeat[l] != nullptr ||
+                     (phase == 1 && ((accumulate_mask >> l) & 1)),
+                 "level %d's gradient map is needed by this phase", l);
   return roi_bwd_core(sets, 2, dims, num_levels, C, accumulate_mask, vec4, workspace,
-                      workspace_bytes, as_stream(stream));
+                      workspace_bytes, as_stream(stream), phase, level_lo, level_hi);
+}
+
+extern "C" int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims,
+                                   const float* scales, int num_levels, int C, int box_mode,
+                                   int pad_border, int assign, int min_level, int max_level,
+                                   int canonical_box_size, int canonical_level,
+                                   const float* boxes0, const int32_t* box_ind0, int R0,
+                                   int out_h0, int out_w0, int sr0, const float* grad_out0,
+                                   const float* boxes1, const int32_t* box_ind1, int R1,
+                                   int out_h1, int out_w1, int sr1, const float* grad_out1,
+                                   int accumulate_mask, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+  return d2mi_roi_align_bwd2_ex(grad_feats, dims, scales, num_levels, C, box_mode, pad_border,
+                                assign, min_level, max_level, canonical_box_size, canonical_level,
+                                boxes0, box_ind0, R0, out_h0, out_w0, sr0, grad_out0, boxes1,
+                                box_ind1, R1, out_h1, out_w1, sr1, grad_out1, accumulate_mask, 3, 0,
+                                num_levels - 1, workspace, workspace_bytes, stream);
 }
 
 extern "C" int d2mi_roi_align_bwd(float* const* grad_feats, const int32_t* dims,

@@ -237,10 +237,22 @@ class _ConvMFMAFn(torch.autograd.Function):
             add = ctx.grad_from.pop("g", None) if ctx.grad_from is not None else None
             pair = ctx.pair_grad
             deposit = False
+            deferred = None
+            gated = ctx.in_info is not None and _gate_eligible(w.shape, stride, pb, pe)
             if pair is not None:
                 other = pair.pop("g", None)
-                if other is None:
+                if isinstance(other, ops.DeferredPixels):
+                    # the ROI poolers' pixel pass of this level, run into this
+                    # dgrad's full map afterwards (no add here); a gated or
+                    # already-adding dgrad takes the pooled map instead
+                    if add is None and not gated:
+                        deferred, other = other, None
+                    else:
+                        other = other.materialize()
+                if other is None and deferred is None:
                     deposit = True  # first of the pair: no gate, no add
+                elif other is None:
+                    pass
                 elif add is None:
                     add = other
                 else:
@@ -251,6 +263,8 @@ class _ConvMFMAFn(torch.autograd.Function):
                 info["masked"] = True
             else:
                 gx = _dgrad(gy, w, x.shape, stride, pb, pe, add=add)
+            if deferred is not None:
+                gx = deferred.add_into(gx.contiguous())
             if deposit:
                 handoff.deposit(pair, "g", gx, "pair")
                 gx = None
@@ -302,6 +316,8 @@ def _join_backward(ctx, gy, x, w, stride, pb, pe):
         return _dgrad(gy, w, x.shape, stride, pb, pe, add=s)
     p = ctx.pair_grad
     other = p.pop("g", None)
+    if isinstance(other, ops.DeferredPixels):
+        other = other.materialize()
     if other is None:  # first of the pair
         handoff.deposit(p, "g", _dgrad(gy, w, x.shape, stride, pb, pe), "join (pair)")
         return None

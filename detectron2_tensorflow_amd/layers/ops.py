@@ -77,7 +77,7 @@ class KernelTimer:
         return out
 
 
-def roi_touched_rows(boxes, box_ind, params, shapes):
+def roi_touched_rows(boxes, box_ind, params, shapes, return_ids=False):
     """Distinct feature rows (level, image, y, x) that one ROIAlign forward
     reads (the 4 bilinear corners of every in-range sample): the unique-bytes
     model of bench.py's roofline (rows x C x 4 bytes is the least HBM
@@ -90,7 +90,7 @@ def roi_touched_rows(boxes, box_ind, params, shapes):
     b = boxes.detach().float().reshape(-1, 4)
     R = b.shape[0]
     if R == 0:
-        return 0
+        return torch.zeros(0, dtype=torch.long, device=dev) if return_ids else 0
     if assign and len(shapes) > 1:
         area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
         v = canon_l + torch.log(torch.sqrt(area) / canon_s + 2.220446049250313e-16) / math.log(2)
@@ -139,7 +139,8 @@ def roi_touched_rows(boxes, box_ind, params, shapes):
     for yy in (ylo, yhi):
         for xx in (xlo, xhi):
             ids.append((img0 + yy[:, :, None] * Ws[:, None, None] + xx[:, None, :]).reshape(-1)[ok])
-    return int(torch.unique(torch.cat(ids)).numel())
+    u = torch.unique(torch.cat(ids))
+    return u if return_ids else int(u.numel())
 
 
 def set_tuning(key, value):
@@ -241,13 +242,19 @@ class _RoIAlignFn(torch.autograd.Function):
                 handoff.deposit(share, "set0", (boxes, box_ind, g, ctx.params), "box/mask poolers")
                 return (None,) * (4 + len(ctx.shapes))
             # levels whose other consumer already left its input gradient:
-            # accumulate into it; the others: written here and left for it
+            # accumulate into it; the others: their pixel pass is deferred
+            # into that consumer's backward, which writes the level's full
+            # map (DEFER_PIXELS), or the map is written here and left for it
             given = [pr.pop("g", None) if pr is not None else None for pr in ctx.pairs]
-            grads = _roi_align_bwd2(first, (boxes, box_ind, g, ctx.params), ctx.shapes, given)
+            defer = [DEFER_PIXELS and pr is not None and gv is None
+                     for pr, gv in zip(ctx.pairs, given)]
+            grads = _roi_align_bwd2(first, (boxes, box_ind, g, ctx.params), ctx.shapes, given,
+                                    defer)
             out = []
             for pr, gv, gr in zip(ctx.pairs, given, grads):
                 if pr is not None and gv is None:
-                    # the other consumer adds it in its dgrad epilogue
+                    # the other consumer adds it: a deferred pixel pass into its
+                    # dgrad, or the map in its dgrad epilogue
                     handoff.deposit(pr, "g", gr, "RPN head / ROI pooler level")
                     out.append(None)
                 else:
@@ -289,12 +296,47 @@ class _RoIAlignFn(torch.autograd.Function):
 # The box and mask poolers' backwards as one merged backward (False: two
 # backwards, the second accumulating into the first's maps; tests compare).
 MERGED_BWD = True
+# r4: a merged backward whose level is also read by another consumer that has
+# not run its backward yet (the RPN head conv) prepares the contributions
+# once (d2mi_roi_align_bwd2_ex phase 1) and leaves each such level's pixel
+# pass (phase 2) to that consumer, which runs it into its own full dgrad map
+# (DeferredPixels.add_into): the level's map is neither cleared here nor
+# written twice nor read again by the consumer's epilogue.  False: the full
+# maps are written here and added in the consumer's dgrad epilogue (A/B).
+DEFER_PIXELS = True
 
 
-def _roi_align_bwd2(set0, set1, shapes, given=None):
+class DeferredPixels:
+    """The pixel pass of ONE level of a merged ROIAlign backward
+    (d2mi_roi_align_bwd2_ex phase 2), deposited for the backward that writes
+    that level's full gradient map.  add_into(gx) adds the pooled
+    contributions into gx in place (old + new at each touched pixel: the
+    rounding of autograd's sum of the two maps); materialize() returns the
+    pooled map alone (a fresh zeroed map + the pass), for a consumer that
+    cannot take it afterwards."""
+
+    def __init__(self, run, level, shape, device):
+        self._run, self.level, self.shape, self.device = run, level, tuple(shape), device
+
+    def add_into(self, gx):
+        if (tuple(gx.shape) != self.shape or gx.dtype != torch.float32 or not gx.is_contiguous()
+                or gx.device != self.device):
+            raise ValueError(f"deferred ROIAlign pixels: need a contiguous f32 {self.shape} map")
+        self._run(self.level, gx, True)
+        return gx
+
+    def materialize(self):
+        m = torch.empty(self.shape, dtype=torch.float32, device=self.device)
+        self._run(self.level, m, False)
+        return m
+
+
+def _roi_align_bwd2(set0, set1, shapes, given=None, defer=None):
     """d2mi_roi_align_bwd2 over two (boxes, box_ind, grad_out, params) sets
     of the same feature maps (equal level / box-mode parameters).  given[l]:
-    a gradient map of level l to accumulate into (returned), or None."""
+    a gradient map of level l to accumulate into (returned), or None.
+    defer[l]: level l's pixel pass is left to a DeferredPixels (returned in
+    its place; d2mi_roi_align_bwd2_ex phase 1 now, phase 2 later)."""
     b0, i0, g0, p0 = set0
     b1, i1, g1, p1 = set1
     if p0[2] != p1[2] or p0[4:11] != p1[4:11]:  # scales, box mode .. canonical level
@@ -302,10 +344,15 @@ def _roi_align_bwd2(set0, set1, shapes, given=None):
     (oh0, ow0, scales, sr0, mode, pad, assign, min_l, max_l, canon_s, canon_l, _) = p0
     oh1, ow1, sr1 = p1[0], p1[1], p1[3]
     dev = b0.device
-    given = given or [None] * len(shapes)
+    L = len(shapes)
+    given = given or [None] * L
+    defer = defer or [False] * L
     grads, acc_mask = [], 0
     for l, (s, gv) in enumerate(zip(shapes, given)):
-        if gv is not None and tuple(gv.shape) == tuple(s) and gv.dtype == torch.float32 \
+        if defer[l]:
+            grads.append(None)
+            acc_mask |= 1 << l  # (phase 1 leaves the deferred maps alone)
+        elif gv is not None and tuple(gv.shape) == tuple(s) and gv.dtype == torch.float32 \
                 and gv.is_contiguous():
             grads.append(gv)
             acc_mask |= 1 << l
@@ -314,28 +361,65 @@ def _roi_align_bwd2(set0, set1, shapes, given=None):
             acc_mask |= 1 << l
         else:
             grads.append(torch.empty(s, dtype=torch.float32, device=dev))
-    gp = _C.host_array(_C.c_void_p, [x.data_ptr() for x in grads])
     dims = _C.host_array(_C.ctypes.c_int32, [v for s in shapes for v in (s[0], s[1], s[2])])
     sc = _C.host_array(_C.c_float, list(scales))
     C = shapes[0][-1]
     R0, R1 = b0.shape[0], b1.shape[0]
     lib = _C.lib()
-    wsb = lib.d2mi_roi_align_bwd2_workspace_size(dims, len(grads), C, R0, oh0, ow0, sr0, R1, oh1,
-                                                 ow1, sr1)
+    wsb = lib.d2mi_roi_align_bwd2_workspace_size(dims, L, C, R0, oh0, ow0, sr0, R1, oh1, ow1, sr1)
     ws = _C.workspace(wsb, dev)
-    ev = KernelTimer.start()
-    rc = lib.d2mi_roi_align_bwd2(gp, dims, sc, len(grads), C, mode, pad, assign, min_l, max_l,
-                                 canon_s, canon_l, _C.ptr(b0), _C.ptr(i0), R0, oh0, ow0, sr0,
-                                 _C.ptr(g0), _C.ptr(b1), _C.ptr(i1), R1, oh1, ow1, sr1, _C.ptr(g1),
-                                 acc_mask, _C.ptr(ws), wsb, _C.stream_of(dev))
+    st = _C.stream_of(dev)
     S0, S1 = max(sr0, 1) ** 2, max(sr1, 1) ** 2
-    # unique-bytes model: both grad_out sets read once + every element of the
-    # dense gradient maps written once
-    maps = sum(int(np.prod(s)) for s in shapes) * 4
-    KernelTimer.stop(ev, "roi_align_bwd", R0 * oh0 * ow0 * C * (4 + 32 * S0) +
-                     R1 * oh1 * ow1 * C * (4 + 32 * S1),
-                     extra=lambda: {"unique_bytes": (R0 * oh0 * ow0 + R1 * oh1 * ow1) * C * 4 + maps})
-    _C.check(rc, "d2mi_roi_align_bwd2")
+    d4 = R0 * oh0 * ow0 * C * (4 + 32 * S0) + R1 * oh1 * ow1 * C * (4 + 32 * S1)
+    gout_bytes = (R0 * oh0 * ow0 + R1 * oh1 * ow1) * C * 4
+
+    def touched_bytes(levels):
+        """unique bytes of a pixel pass: 2 x C x 4 per touched pixel of these
+        levels (read + write of an accumulated map) -- the union of the pixels
+        the two sets' sample corners touch (roi_touched_rows)."""
+        base = np.cumsum([0] + [int(s[0] * s[1] * s[2]) for s in shapes])
+        ids = torch.cat([roi_touched_rows(b, i, p, shapes, return_ids=True)
+                         for b, i, _, p in (set0, set1)]).unique()
+        lo, hi = int(base[min(levels)]), int(base[max(levels) + 1])
+        return 2 * C * 4 * int(((ids >= lo) & (ids < hi)).sum())
+
+    def call(maps, acc, phase, lo, hi):
+        gp = _C.host_array(_C.c_void_p, [m.data_ptr() if m is not None else None for m in maps])
+        return lib.d2mi_roi_align_bwd2_ex(gp, dims, sc, L, C, mode, pad, assign, min_l, max_l,
+                                          canon_s, canon_l, _C.ptr(b0), _C.ptr(i0), R0, oh0, ow0,
+                                          sr0, _C.ptr(g0), _C.ptr(b1), _C.ptr(i1), R1, oh1, ow1,
+                                          sr1, _C.ptr(g1), acc, phase, lo, hi, _C.ptr(ws), wsb, st)
+
+    ev = KernelTimer.start()
+    if not any(defer):
+        rc = call(grads, acc_mask, 3, 0, L - 1)
+        maps = sum(int(np.prod(s)) for s in shapes) * 4
+        # unique-bytes model: both grad_out sets read once + every element of
+        # the dense gradient maps written once
+        KernelTimer.stop(ev, "roi_align_bwd", d4,
+                         extra=lambda: {"unique_bytes": gout_bytes + maps})
+        _C.check(rc, "d2mi_roi_align_bwd2")
+        return grads
+    rc = call(grads, acc_mask, 1, 0, L - 1)
+    fresh = [l for l in range(L) if not defer[l]]
+    # the prepare launches: the grad_out reads (the contributions' records)
+    KernelTimer.stop(ev, "roi_align_bwd", d4, extra=lambda: {"unique_bytes": gout_bytes})
+    _C.check(rc, "d2mi_roi_align_bwd2_ex (prepare)")
+
+    def run(level, m, accumulate):
+        maps = [None] * L
+        maps[level] = m
+        ev = KernelTimer.start()
+        rc = call(maps, (1 << level) if accumulate else 0, 2, level, level)
+        KernelTimer.stop(ev, "roi_align_bwd", 0.0,
+                         extra=lambda: {"unique_bytes": touched_bytes([level])})
+        _C.check(rc, "d2mi_roi_align_bwd2_ex (pixels)")
+
+    for l in fresh:  # levels without a deferral: their passes now (maps zeroed or given)
+        run(l, grads[l], True)
+    for l in range(L):
+        if defer[l]:
+            grads[l] = DeferredPixels(run, l, shapes[l], dev)
     return grads
 
 
@@ -545,17 +629,14 @@ _NARROW_SPLIT = os.environ.get("D2MI_NARROW_SPLIT", "1") != "0"
 
 def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdown=None,
                 residual=None, relu_after_add=False, math_mode=None, flip_taps=False,
-                relu_gate=None, out=None, x3=None, w3=None):
+                relu_gate=None, out=None):
     """MFMA implicit-GEMM conv: x [N,H,W,Cin], w_packed [KH,KW,Cout,Cin].
     relu_after_add: relu(conv + bias + residual/topdown) instead of
     relu(conv + bias) + residual/topdown.  math_mode: "f32" | "split" (None:
     CONV_MATH).  flip_taps: use the spatially flipped kernel (w_packed[KH-1-i, KW-1-j]).
     relu_gate: a ReLU output of the result's shape: out = gate > 0 ? conv
     (+ residual) : 0 (a dgrad with its producer's ReLU backward fused, and the
-    gradient of the producer's other consumer added first).
-    x3 / w3: the exact bf16 planes (split_bf16x3) of x / w_packed, read by the
-    warp-specialised kernel instead of splitting f32 rows while staging
-    (d2mi_conv2d_nhwc_planes; bit-identical outputs)."""
+    gradient of the producer's other consumer added first)."""
     math_mode = math_mode or CONV_MATH
     if math_mode not in ("f32", "split"):
         raise ValueError(f"conv math must be 'f32' or 'split', got {math_mode!r}")
@@ -603,18 +684,7 @@ def conv2d_nhwc(x, w_packed, bias=None, stride=1, pad=(0, 0), relu=False, topdow
                                                               int(stride), int(pb), int(pe))
     ws = _C.scratch(wsb, x.device) if wsb else None
     st = _C.stream_of(x.device)
-    if (x3 is not None or w3 is not None) and math_mode == "split":
-        for t, ref, nm in ((x3, x, "x3"), (w3, w_packed, "w3")):
-            if t is not None and (t.dtype != torch.int16 or tuple(t.shape) != (3,) + tuple(ref.shape)
-                                  or not t.is_contiguous()):
-                raise ValueError(f"{nm} must be the contiguous int16 [3, *shape] planes of its operand")
-        ev = KernelTimer.start()
-        rc = lib.d2mi_conv2d_nhwc_planes(_C.ptr(x), _C.ptr(x3), x.numel(), _C.ptr(w_packed),
-                                         _C.ptr(w3), _C.ptr(bias), _C.ptr(topdown),
-                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N, H, W,
-                                         Cin, Cout, KH, KW, int(stride), int(pb), int(pe), flags,
-                                         _C.ptr(ws), wsb, st)
-    elif relu_gate is not None:
+    if relu_gate is not None:
         ev = KernelTimer.start()
         rc = lib.d2mi_conv2d_nhwc_gated(_C.ptr(x), _C.ptr(w_packed), _C.ptr(bias),
                                         _C.ptr(residual), _C.ptr(relu_gate), _C.ptr(y), N,

@@ -146,6 +146,26 @@ int d2mi_roi_align_bwd2(float* const* grad_feats, const int32_t* dims, const flo
                         const int32_t* box_ind1, int R1, int out_h1, int out_w1, int sr1,
                         const float* grad_out1, int accumulate_mask, void* workspace,
                         size_t workspace_bytes, void* stream);
+/* The same backward in phases (r4).  phase 1 (prepare): every step but the
+ * pixel pass -- the counting sort of the contributions by (pixel, set) and
+ * the long-run partials -- with the maps of levels [level_lo, level_hi] not
+ * in accumulate_mask zeroed; its results stay in the workspace.  phase 2
+ * (pixels): the pixel pass over the touched pixels of levels [level_lo,
+ * level_hi] only, adding into the maps whose accumulate_mask bit is set
+ * (others zeroed first).  phase 3 = d2mi_roi_align_bwd2.  Between a phase 1
+ * and its phase-2 calls the workspace must not be reused; a level's map may
+ * be null in a phase that does not touch it.  Lets a level's pixel pass run
+ * after another backward wrote that map in full (the RPN head conv's dgrad
+ * of the same FPN level): no clear of the map, no second pass over it. */
+int d2mi_roi_align_bwd2_ex(float* const* grad_feats, const int32_t* dims, const float* scales,
+                           int num_levels, int C, int box_mode, int pad_border, int assign,
+                           int min_level, int max_level, int canonical_box_size,
+                           int canonical_level, const float* boxes0, const int32_t* box_ind0,
+                           int R0, int out_h0, int out_w0, int sr0, const float* grad_out0,
+                           const float* boxes1, const int32_t* box_ind1, int R1, int out_h1,
+                           int out_w1, int sr1, const float* grad_out1, int accumulate_mask,
+                           int phase, int level_lo, int level_hi, void* workspace,
+                           size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------- NMS
  * Segmented greedy NMS with TF NonMaxSuppressionV3 semantics
@@ -470,24 +490,9 @@ int d2mi_conv2d_nhwc_levels(const float* const* xs, const int32_t* dims, int nle
  * bf16 MFMA products (v_mfma_f32_32x32x16_bf16; the dropped m*l, l*m, l*l
  * terms are below f32's own rounding of the product) and accumulated in f32.
  *
- * d2mi_conv2d_nhwc_planes: the same convolution (flags bits 0-3; gate as
- * d2mi_conv2d_nhwc_gated, nullable) with optional PRE-SPLIT operands for the
- * warp-specialised kernel: x3 = the exact planes [3][x3_plane] of x (plane p
- * of element e at x3[p * x3_plane + e]), w3 = the planes [3][KH*KW*Cout*Cin]
- * of w_packed (both nullable, Cin % 8 == 0).  The planes hold the very bf16
- * terms the kernel would split (d2mi_split_bf16x3), so the outputs are
- * bit-identical to d2mi_conv2d_nhwc_ex / _gated; x and w_packed are still
- * required (the other kernels of the plan read f32).
- *
  * d2mi_split_bf16x3: x [n] f32 -> out [3][n] (bf16 bit patterns of h, m, l);
  * n % 4 == 0 (the stem conv's weight planes, d2mi_stem_conv). */
 int d2mi_split_bf16x3(const float* x, int64_t n, uint16_t* out, void* stream);
-int d2mi_conv2d_nhwc_planes(const float* x, const uint16_t* x3, int64_t x3_plane,
-                            const float* w_packed, const uint16_t* w3, const float* bias,
-                            const float* topdown, const float* residual, const float* gate,
-                            float* y, int N, int H, int W, int Cin, int Cout, int KH, int KW,
-                            int stride, int pad_beg, int pad_end, int flags, void* workspace,
-                            size_t workspace_bytes, void* stream);
 
 /* Weight gradient of the same convolution (the tf.gradients of Conv2D.call,
  * lib/layers/convolutional.py:198-263, w.r.t. its HWIO kernel):

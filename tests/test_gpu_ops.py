@@ -282,11 +282,19 @@ def test_nms_segmented_vs_oracle_with_ties(dev, thr):
         np.testing.assert_array_equal(k.cpu().numpy(), want_k)
 
 
-def test_nms_large_segment_uses_radix_sort_path(dev):
-    rng = np.random.default_rng(11)
-    n = 12000
+@pytest.mark.parametrize("n,tied", [(12000, False), (40000, True), (70001, False)])
+def test_nms_large_segment_uses_radix_sort_path(dev, n, tied):
+    """Segments over 8,192 candidates: the hand-written tile rank sort + merge
+    passes (csrc/sort.hip; r1-r3 ran rocPRIM's radix sort here) -- 2, 5 and 9
+    tiles (an odd run count, up to 4 merge passes), heavy score ties (order
+    by index) and NaN / -inf scores (never selected)."""
+    rng = np.random.default_rng(11 + n)
     b = rand_boxes(rng, n, 1000, 1300, 8, 300)
     s = rng.uniform(size=n).astype(F32)
+    if tied:
+        s = np.round(s * 50) / 50
+        s[::97] = np.nan
+        s[5::89] = -np.inf
     want = oracle.nms(b, s, 300, 0.5)
     got = ops().non_max_suppression(torch.from_numpy(b).to(dev), torch.from_numpy(s).to(dev), 300, 0.5)
     np.testing.assert_array_equal(got.cpu().numpy(), want)
@@ -1452,43 +1460,3 @@ def test_fused_subsample_pairwise_co_inclusion(dev):
     assert np.all(np.abs(off - p2) < 5 * sd), (off.min(), off.max(), p2)
     near = np.array([co[i, i + 1] for i in range(n - 1)])
     assert abs(near.mean() - p2) < 5 * sd / math.sqrt(n - 1) + 1e-3, (near.mean(), p2)
-
-
-@pytest.mark.parametrize("shape,form", [
-    ((2, 25, 42, 512, 512, 3), ""),      # res5 3x3: WS with split-K partials
-    ((2, 50, 84, 256, 256, 3), "gf"),    # res4 3x3 dgrad: flipped taps + ReLU gate
-    ((2, 50, 84, 1024, 256, 1), "r"),    # 1x1 1024 -> 256 + residual + ReLU
-    ((1, 37, 61, 64, 200, 3), ""),       # Cin 64 (18 k-steps), Cout 200: partial N tile
-    ((3, 23, 29, 96, 128, 3), "t"),      # ragged M, top-down add epilogue
-])
-def test_conv2d_plane_operands_bit_identical(dev, shape, form):
-    """d2mi_conv2d_nhwc_planes: the warp-specialised kernel staging pre-split
-    bf16 planes of x (x3) and / or of the packed weights (w3) -- 16-B chunk
-    copies instead of f32 rows split while staging -- forms the same bf16
-    terms, so its outputs equal the f32-operand path bit for bit, with every
-    epilogue form; and within 1e-4 of float64."""
-    N, H, W, Cin, Cout, k = shape
-    p = (k - 1) // 2
-    g = torch.Generator().manual_seed(sum(shape) + len(form))
-    x = torch.randn(N, H, W, Cin, generator=g)
-    w = torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)
-    b = torch.randn(Cout, generator=g)
-    xd, wp = x.to(dev), ops().pack_conv_weights(w.to(dev))
-    kw = dict(math_mode="split", flip_taps="f" in form)
-    if "r" in form:
-        kw.update(residual=torch.randn(N, H, W, Cout, generator=g).to(dev), relu=True,
-                  relu_after_add=True)
-    if "g" in form:
-        kw.update(relu_gate=torch.randn(N, H, W, Cout, generator=g).to(dev))
-    if "t" in form:
-        kw.update(topdown=torch.randn(N, (H + 1) // 2, (W + 1) // 2, Cout, generator=g).to(dev))
-    x3, w3 = ops().split_bf16x3(xd), ops().split_bf16x3(wp)
-    y0 = ops().conv2d_nhwc(xd, wp, b.to(dev), 1, (p, p), **kw)
-    for extra in ({"x3": x3}, {"w3": w3}, {"x3": x3, "w3": w3}):
-        y = ops().conv2d_nhwc(xd, wp, b.to(dev), 1, (p, p), **kw, **extra)
-        assert torch.equal(y, y0), (sorted(extra), float((y - y0).abs().max()))
-    if not form:
-        ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double(),
-                                         w.permute(3, 2, 0, 1).double(), b.double(),
-                                         padding=p).permute(0, 2, 3, 1)
-        np.testing.assert_allclose(y0.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)

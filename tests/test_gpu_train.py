@@ -584,6 +584,47 @@ def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch):
         assert torch.equal(grads[True][n], grads[False][n]), n
 
 
+def test_deferred_roi_pixel_passes_are_exact(dev, monkeypatch):
+    """ops.DEFER_PIXELS: the merged box / mask pooler backward prepares its
+    contributions once (d2mi_roi_align_bwd2_ex phase 1) and each FPN level's
+    pixel pass runs inside the RPN head conv's backward, into that conv's
+    full dgrad map (phase 2, accumulate) -- no map clear, no epilogue add of
+    a second full map.  Every level is deferred in a training step, and the
+    model's gradients equal the full-map hand-off's bit for bit (old + new at
+    each touched pixel is the same rounding as dgrad + pooled map)."""
+    from detectron2_tensorflow_amd.layers import ops
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.utils.synthetic import (calibrate_rcnn_scores,
+                                                           synthetic_train_batch)
+    cfg = _cfg(True)
+    torch.manual_seed(0)
+    model = build_model(cfg).to(dev).train()
+    batch = synthetic_train_batch(2, 256, 320, 8, dev)
+    calibrate_rcnn_scores(model, batch)
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    applied = []
+    real = ops.DeferredPixels.add_into
+
+    def counted(self, gx):
+        applied.append(self.level)
+        return real(self, gx)
+
+    monkeypatch.setattr(ops.DeferredPixels, "add_into", counted)
+    grads = {}
+    for defer in (True, False):
+        monkeypatch.setattr(ops, "DEFER_PIXELS", defer)
+        model.zero_grad(set_to_none=True)
+        applied.clear()
+        torch.manual_seed(1)
+        losses = model(batch)
+        sum(losses.values()).backward()
+        assert sorted(applied) == ([0, 1, 2, 3] if defer else []), applied
+        grads[defer] = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    assert grads[True].keys() == grads[False].keys() and grads[True]
+    for n in grads[True]:
+        assert torch.equal(grads[True][n], grads[False][n]), n
+
+
 def test_training_step_1333x800_grads_finite_and_deterministic(dev):
     """The bench workload itself (Mask R-CNN R50-FPN, 2 images at 1333x800
     padded to 1344x800, BASELINE config C3 on one GPU): after one Trainer.step

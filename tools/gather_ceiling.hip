@@ -1,0 +1,79 @@
+// Gather ceiling of the ROIAlign forward's access pattern (tools/gather_ceiling.py).
+// gather4: one wave per output row, lanes over C = 256 channels (one float4
+// each): the four source rows idx[4 * b .. 4 * b + 3] (1 KiB each) read, summed
+// and the sum stored -- the ROIAlign forward's memory traffic (4 corner rows
+// per bin, one output row) with its arithmetic reduced to adds, U bins in
+// flight per wave like the kernel.  gather1: one 1 KiB row per output row.
+// copy: a streaming float4 copy (the HBM reference).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+template <int U>
+__global__ __launch_bounds__(256) void gather4_kernel(const float4* __restrict__ src,
+                                                      const int32_t* __restrict__ idx, int nbins,
+                                                      float4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * 4 + (threadIdx.x >> 6)) * U;
+  float4 v[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int b = min(wave + u, nbins - 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[u][c] = src[(size_t)idx[4 * b + c] * 64 + lane];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int b = wave + u;
+    if (b >= nbins) break;
+    float4 s;
+    s.x = (v[u][0].x + v[u][1].x) + (v[u][2].x + v[u][3].x);
+    s.y = (v[u][0].y + v[u][1].y) + (v[u][2].y + v[u][3].y);
+    s.z = (v[u][0].z + v[u][1].z) + (v[u][2].z + v[u][3].z);
+    s.w = (v[u][0].w + v[u][1].w) + (v[u][2].w + v[u][3].w);
+    out[(size_t)b * 64 + lane] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather1_kernel(const float4* __restrict__ src,
+                                                      const int32_t* __restrict__ idx, int n,
+                                                      float4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += gridDim.x * 4)
+    out[(size_t)r * 64 + lane] = src[(size_t)idx[r] * 64 + lane];
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const float4* __restrict__ src, long long n4,
+                                                   float4* __restrict__ out) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += gridDim.x * 256LL)
+    out[i] = src[i];
+}
+
+extern "C" int gc_gather4(const float* src, const int32_t* idx, int nbins, float* out, int u,
+                          void* stream) {
+  const int waves = (nbins + u - 1) / u;
+  const dim3 grid((waves + 3) / 4);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (u == 4)
+    hipLaunchKernelGGL(gather4_kernel<4>, grid, dim3(256), 0, st, (const float4*)src, idx, nbins,
+                       (float4*)out);
+  else if (u == 2)
+    hipLaunchKernelGGL(gather4_kernel<2>, grid, dim3(256), 0, st, (const float4*)src, idx, nbins,
+                       (float4*)out);
+  else
+    hipLaunchKernelGGL(gather4_kernel<1>, grid, dim3(256), 0, st, (const float4*)src, idx, nbins,
+                       (float4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int gc_gather1(const float* src, const int32_t* idx, int n, float* out, void* stream) {
+  const int grid = (int)((n + 3) / 4 < 65536 ? (n + 3) / 4 : 65536);
+  hipLaunchKernelGGL(gather1_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const float4*)src, idx, n, (float4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int gc_copy(const float* src, long long n4, float* out, void* stream) {
+  hipLaunchKernelGGL(copy_kernel, dim3(8192), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const float4*)src, n4, (float4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
