@@ -254,7 +254,8 @@ def scratch(nbytes, device):
 
 
 _ERR_BITS = {1: "box index out of range", 2: "NMS candidate capacity exceeded",
-             4: "top-k candidate capacity exceeded"}
+             4: "top-k candidate capacity exceeded",
+             8: "cooperative split-K conv: a tile's workgroups were not co-resident (timeout)"}
 
 
 def error_word(device=None):
