@@ -84,6 +84,9 @@ def parse():
     p.add_argument("--mask-format", default="conventional", choices=["conventional", "raw", "fixed"],
                    help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
+    p.add_argument("--graphs", type=int, default=0,
+                   help="train: replay the step from hipGraphs (engine/graphed.py; world size 1 "
+                        "-- other world sizes run the eager step); 0 = the eager Trainer.step")
     p.add_argument("--mask-fixed-rows", action="store_true",
                    help="train: the mask head on the fixed BATCH_SIZE_PER_IMAGE x "
                         "POSITIVE_FRACTION rows per image (128 at the defaults, "
@@ -535,8 +538,6 @@ def cpu_baseline(args, model, batch, cfg=None):
 
 def main():
     args = parse()
-    if args.model.startswith("retinanet") and args.mode == "train":
-        raise SystemExit("RetinaNet is benchmarked in --mode infer (config C4)")
     if args.model.startswith("solo") and args.mode == "train":
         raise SystemExit("SOLOv2 is benchmarked in --mode infer (config C5: the inference tail)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -568,12 +569,20 @@ def main():
         if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
             model.roi_heads.mask_compact_rows = False
             PMC_SKIP.update({"roi_align_fwd_mask", "roi_align_bwd"})
-        trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        if args.graphs:
+            from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
+            trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        else:
+            trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
+        # the kernel-timing step (HIP events around every launch) runs eagerly:
+        # a replayed graph has no per-launch events
+        timed_step = (lambda: trainer.eager_step(batch)) if args.graphs else step
         grad_ctx = torch.enable_grad
     else:
         fwd = model if is_single_stage(model) else model.inference
         step = lambda: fwd(batch)
+        timed_step = step
         grad_ctx = torch.no_grad
 
     with grad_ctx():
@@ -599,10 +608,11 @@ def main():
         t0 = time.perf_counter()
         reducer = trainer.reducer if args.mode == "train" else None
         for i in range(args.steps):
-            KernelTimer.enabled = (i == sample) and not args.no_kernel_timing
+            timing = (i == sample) and not args.no_kernel_timing
+            KernelTimer.enabled = timing
             if reducer is not None:  # per-bucket all-reduce events (world > 1)
-                reducer.timing = i == sample and not args.no_kernel_timing
-            out = step()
+                reducer.timing = timing
+            out = timed_step() if timing else step()
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -667,6 +677,10 @@ def main():
                                if args.mode == "train" else {}),
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
                             else f"{sample + 1}/{args.steps}",
+                            **({"step_launch": (f"hipGraph replays ({trainer.replays} in warmup + "
+                                                "timed; the kernel-timing step eager)")
+                                if getattr(trainer, "enabled", False) else "eager"}
+                               if args.mode == "train" else {}),
                             **({"mask_format": args.mask_format} if args.mode == "infer" else {})},
                        **extra),
             # the dominant hot-path kernel: the split-product conv (else f32)

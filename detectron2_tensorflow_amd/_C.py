@@ -145,6 +145,12 @@ _SIGS = {
     "d2mi_mask_loss_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, P, P]),
     "d2mi_sgd_table_sizes": (c_int, [P, P, P]),
     "d2mi_momentum_sgd": (c_int, [P, P, c_int, P, c_float, c_float, c_float, P]),
+    "d2mi_momentum_sgd_ex": (c_int, [P, P, c_int, P, c_float, c_float, c_float, P, P]),
+    "d2mi_retina_loss_blocks": (c_int, []),
+    "d2mi_retina_loss_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
+                                     c_float, c_float, c_float, P, P, P]),
+    "d2mi_retina_loss_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
+                                     P, c_float, c_float, c_float, P, P, P, P]),
     "d2mi_fold_many_sizes": (c_int, [P, P]),
     "d2mi_fold_frozen_bn_many": (c_int, [P, c_int, c_int, P]),
     "d2mi_fold_frozen_bn_bwd_many": (c_int, [P, c_int, c_int, c_int, P, P]),

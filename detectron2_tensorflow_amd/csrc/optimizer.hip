@@ -96,8 +96,10 @@ __global__ __launch_bounds__(256) void sgd_sumsq_kernel(const SgdTensor* __restr
 __global__ __launch_bounds__(256) void sgd_update_kernel(const SgdTensor* __restrict__ tensors,
                                                          const SgdChunk* __restrict__ chunks,
                                                          const float* __restrict__ partial,
-                                                         float clip, float momentum, float lr) {
+                                                         float clip, float momentum, float lr,
+                                                         const float* __restrict__ lr_dev) {
   __shared__ float scale_s;
+  if (lr_dev) lr = *lr_dev;  // (a captured graph's step: the LR lives on the device)
   const SgdChunk c = chunks[blockIdx.x];
   const SgdTensor t = tensors[c.tensor];
   if (threadIdx.x == 0) {
@@ -157,9 +159,12 @@ extern "C" int d2mi_sgd_table_sizes(int* tensor_bytes, int* chunk_bytes, int* ch
   return 0;
 }
 
-extern "C" int d2mi_momentum_sgd(const void* tensor_table, const void* chunk_table, int num_chunks,
-                                 float* partial, float clip_norm, float momentum, float lr,
-                                 void* stream) {
+// lr_dev: when non-null the learning rate is read from this device float at
+// run time (a step captured in a hipGraph replays with each step's LR, which
+// the host writes there); lr is then ignored.
+extern "C" int d2mi_momentum_sgd_ex(const void* tensor_table, const void* chunk_table,
+                                    int num_chunks, float* partial, float clip_norm,
+                                    float momentum, float lr, const float* lr_dev, void* stream) {
   D2MI_REQUIRE(num_chunks >= 0, "num_chunks < 0");
   if (num_chunks == 0) return 0;
   hipStream_t st = as_stream(stream);
@@ -170,7 +175,14 @@ extern "C" int d2mi_momentum_sgd(const void* tensor_table, const void* chunk_tab
     D2MI_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(sgd_update_kernel, dim3(num_chunks), dim3(256), 0, st, t, c, partial,
-                     clip_norm, momentum, lr);
+                     clip_norm, momentum, lr, lr_dev);
   D2MI_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int d2mi_momentum_sgd(const void* tensor_table, const void* chunk_table, int num_chunks,
+                                 float* partial, float clip_norm, float momentum, float lr,
+                                 void* stream) {
+  return d2mi_momentum_sgd_ex(tensor_table, chunk_table, num_chunks, partial, clip_norm, momentum,
+                              lr, nullptr, stream);
 }

@@ -1,0 +1,192 @@
+"""The data-parallel training step replayed from hipGraphs (lib/engine/trainer.py:116-199).
+
+The eager ``Trainer.step`` enqueues ~550 launches per iteration from Python
+(autograd engine, custom Functions, ctypes): on an MI355X that host work is
+0.6-0.75 of the step's wall time, so one faster kernel away from binding the
+step.  Here the same step is captured into hipGraphs once and replayed:
+
+* graph A: the forward (backbone, FPN, RPN + its losses, ROI sampling, box
+  branch + losses) up to the one value the host must read -- the number of
+  foreground proposals, which sizes the compacted mask branch (the
+  reference's ``select_foreground_proposals``, roi_heads.py:35-62);
+* graph B[R], one per possible mask-branch row count R (a multiple of 32:
+  8 graphs for 2 images x 128 foreground slots, all captured right after
+  A): the mask branch forward + loss, the total loss, the whole backward (through graph A's retained autograd graph), the all-reduce
+  (world size 1: none) and the fused Momentum-SGD update with the LR read
+  from the device (``d2mi_momentum_sgd_ex``).
+
+A step is then: copy the batch into the captured input tensors (when the
+caller passes others), write the LR, replay A, read the foreground count
+(the step's one host synchronisation, as in the eager step), replay B[R].
+The arithmetic is the eager step's: the same kernels with the same arguments in the same order, so the updated
+weights are bit-identical to ``Trainer.step`` on the same inputs (tests).
+
+Every B graph shares graph A's memory pool: A's outputs and saved tensors
+stay alive (the retained autograd graph and the deferred mask loss hold
+them), and the B graphs, never replayed concurrently, reuse each other's
+freed temporaries.  The caches keyed on parameter versions (folded /
+packed weights) are made stale before A is captured, so A re-folds and
+re-packs every trainable layer at each replay; nothing bumps a version while
+the graphs are in use, and an eager step (``eager_step``) marks them stale
+again first.  A multi-rank job runs the eager step unless ``dp_graphs``
+asks for the RCCL all-reduces to be captured too (gloo cannot be).
+"""
+import torch
+import torch.distributed as dist
+
+from ..modeling.roi_heads.roi_heads import DeferredMaskLoss, StandardROIHeads
+from ..utils import host_sync
+from .trainer import Trainer
+
+
+def _flatten(tree, prefix=()):
+    """(path, tensor) leaves of a nested dict of tensors, in key order."""
+    out = []
+    for k in sorted(tree):
+        v = tree[k]
+        if isinstance(v, dict):
+            out += _flatten(v, prefix + (k,))
+        elif torch.is_tensor(v):
+            out.append((prefix + (k,), v))
+    return out
+
+
+def _clone_tree(tree):
+    return {k: (_clone_tree(v) if isinstance(v, dict) else
+                v.clone() if torch.is_tensor(v) else v) for k, v in tree.items()}
+
+
+class GraphedTrainer(Trainer):
+    """``Trainer`` whose steps replay captured hipGraphs (see the module
+    docstring).  ``warmup``: eager steps before the capture (allocator,
+    workspaces, per-shape caches).  Falls back to the eager step when the
+    process group has more than one rank."""
+
+    def __init__(self, cfg, model, warmup=1, dp_graphs=False, **kwargs):
+        super().__init__(cfg, model, **kwargs)
+        self.warmup = int(warmup)
+        self.heads = [m for m in model.modules() if isinstance(m, StandardROIHeads)]
+        # dp_graphs: capture the bucketed all-reduce too (RCCL: "nccl" backend
+        # only; tested at world size 1 in tests/rccl_worker.py).  Off, a
+        # multi-rank job runs the eager step.
+        nccl = dist.is_initialized() and dist.get_backend() == "nccl"
+        self.enabled = (next(model.parameters()).is_cuda
+                        and ((self.world == 1 and not self.reducer.active)
+                             or (dp_graphs and nccl)))
+        self._eager = 0
+        self._pool = None
+        self._A = None
+        self._B = {}
+        self._static = None
+        self._leaves = None
+        self._losses = None
+        self._deferred = None
+        self._lr_dev = None
+        self.captures = 0
+        self.replays = 0
+
+    # ------------------------------------------------------------------ state
+    def _mark_stale(self):
+        """Make every version-keyed cache of a trainable layer (FrozenBN folds,
+        packed weights, the RPN head's fused 1x1 weights) miss once."""
+        torch.autograd.graph.increment_version(self.optimizer.params)
+
+    def eager_step(self, batched_inputs):
+        """One eager ``Trainer.step`` (e.g. with kernel timers on).  It reads
+        the current weights: the caches are marked stale before it, and it
+        leaves no state the graphs depend on."""
+        if self._A is not None:
+            self._mark_stale()
+        for h in self.heads:
+            h.defer_mask_loss = False
+        return Trainer.step(self, batched_inputs)
+
+    def _load(self, batched_inputs):
+        leaves = _flatten(batched_inputs)
+        if [p for p, _ in leaves] != [p for p, _ in self._leaves]:
+            raise ValueError("graphed step: the batch has other fields than the captured one")
+        for (path, v), (_, s) in zip(leaves, self._leaves):
+            if v.shape != s.shape or v.dtype != s.dtype:
+                raise ValueError(f"graphed step: {'/'.join(path)} is {tuple(v.shape)} "
+                                 f"{v.dtype}, the graphs were captured for {tuple(s.shape)} "
+                                 f"{s.dtype}")
+            if v.data_ptr() != s.data_ptr():
+                s.copy_(v, non_blocking=True)
+
+    # ---------------------------------------------------------------- capture
+    def _capture_forward(self, batched_inputs):
+        self._static = _clone_tree(batched_inputs)
+        self._leaves = _flatten(self._static)
+        dev = self._leaves[0][1].device
+        self._lr_dev = torch.zeros((), dtype=torch.float32, device=dev)
+        for h in self.heads:
+            h.defer_mask_loss = True
+        if not self.model.training:
+            self.model.train()
+        self.optimizer.zero_grad()
+        self.reducer.reset()
+        self._mark_stale()
+        torch.cuda.synchronize(dev)
+        self._pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+            losses = self.model(self._static)
+        deferred = [v for v in losses.values() if isinstance(v, DeferredMaskLoss)]
+        if len(deferred) > 1:
+            raise RuntimeError("graphed step: more than one deferred mask loss")
+        self._A = g
+        self._losses = losses
+        self._deferred = deferred[0] if deferred else None
+        self.captures += 1
+        # every B graph now, while the layers' cached packed weights are the
+        # ones graph A refreshes (a later eager step re-points those caches)
+        d = self._deferred
+        for rows in (sorted({d.rows_for(n) for n in range(d.slots + 1)}) if d else [None]):
+            self._capture_rest(rows)
+
+    def _capture_rest(self, rows):
+        """Graph B[rows]: mask branch, total loss, backward, update."""
+        self.optimizer.zero_grad()
+        keep = []
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+            out = {k: (v.compute(rows) if isinstance(v, DeferredMaskLoss) else v)
+                   for k, v in self._losses.items()}
+            total = torch.stack(self._loss_terms(out)).sum()
+            seed = self._seed
+            if seed is None or seed.device != total.device or seed.dtype != total.dtype:
+                seed = self._seed = torch.ones_like(total)
+            # retain graph A's autograd graph: a later row count is captured
+            # by another backward through it
+            total.backward(seed, retain_graph=True)
+            self.reducer.finish()
+            self.optimizer.step_captured(self._lr_dev, keep)
+            values = torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()])
+        self.optimizer.zero_grad()
+        keys = list(out) + ["total_loss"]
+        self._B[rows] = (g, values, keys, keep)
+        self.captures += 1
+
+    # ------------------------------------------------------------------- step
+    def step(self, batched_inputs):
+        if not self.enabled:
+            return Trainer.step(self, batched_inputs)
+        if self._A is None and self._eager < self.warmup:
+            self._eager += 1
+            return self.eager_step(batched_inputs)
+        if self._A is None:
+            self._capture_forward(batched_inputs)
+        self._load(batched_inputs)
+        self._lr_dev.fill_(float(self.lr(self.iter)))
+        self._A.replay()
+        rows = None
+        if self._deferred is not None:
+            nfg = host_sync.read_ints(self._deferred.count)[0]  # the step's one host read
+            rows = self._deferred.rows_for(nfg)
+            for h in self.heads:
+                h.last_mask_rows = rows
+        g, values, keys, _ = self._B[rows]
+        g.replay()
+        self.replays += 1
+        self.iter += 1
+        return {k: values[i] for i, k in enumerate(keys)}

@@ -12,13 +12,17 @@ def smooth_l1_loss(*, labels, predictions, beta, reduction="none"):
     return loss
 
 
-def sigmoid_focal_loss(*, labels, logits, alpha=-1, gamma=2, reduction="none"):
-    p = torch.sigmoid(logits)
-    ce = torch.nn.functional.binary_cross_entropy_with_logits(logits, labels, reduction="none")
-    p_t = p * labels + (1 - p) * (1 - labels)
+def sigmoid_focal_loss(*, predictions, targets, alpha=-1.0, gamma=2.0, reduction="none",
+                       scope=None):
+    """loss.py:59-101 (the reference's keyword names; scope is TF's name scope)."""
+    del scope
+    p = torch.sigmoid(predictions)
+    ce = torch.nn.functional.binary_cross_entropy_with_logits(predictions, targets,
+                                                              reduction="none")
+    p_t = p * targets + (1 - p) * (1 - targets)
     loss = ce * ((1 - p_t) ** gamma)
     if alpha >= 0:
-        loss = (alpha * labels + (1 - alpha) * (1 - labels)) * loss
+        loss = (alpha * targets + (1 - alpha) * (1 - targets)) * loss
     if reduction == "mean":
         return loss.mean()
     if reduction == "sum":

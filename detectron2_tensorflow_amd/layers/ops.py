@@ -1092,6 +1092,91 @@ def rpn_loss(logits, deltas, anchors, gt_boxes, matches, pos, sampled, weights, 
                             tuple(weights), float(beta), float(scale))
 
 
+class _RetinaLossFn(torch.autograd.Function):
+    """(focal loss sum, smooth-L1 sum) of RetinaNet.losses over the head's
+    per-level outputs (d2mi_retina_loss_fwd / _bwd, csrc/retina_loss.hip);
+    differentiable w.r.t. every level's class logits and box deltas."""
+
+    @staticmethod
+    def forward(ctx, conf, anchors, gt_boxes, gt_classes, matches, labels, *levels):
+        L = len(levels) // 2
+        cls, box = levels[:L], levels[L:]
+        N, K, A = cls[0].shape[0], conf[0], conf[1]
+        lvl = [int(c.shape[1] * c.shape[2] * A) for c in cls]
+        nb = _C.lib().d2mi_retina_loss_blocks()
+        dev = anchors.device
+        part = torch.empty((N * nb, 2), dtype=torch.float32, device=dev)
+        la = _C.host_array(_C.ctypes.c_longlong, lvl)
+        w = _C.host_array(_C.c_float, list(conf[5]))
+        cp = _C.host_array(_C.c_void_p, [c.data_ptr() for c in cls])
+        bp = _C.host_array(_C.c_void_p, [b.data_ptr() for b in box])
+        rc = _C.lib().d2mi_retina_loss_fwd(cp, bp, la, L, N, K, A, _C.ptr(anchors),
+                                           _C.ptr(gt_boxes), _C.ptr(gt_classes),
+                                           gt_boxes.shape[1], _C.ptr(matches), _C.ptr(labels),
+                                           conf[2], conf[3], conf[4], w, _C.ptr(part),
+                                           _C.stream_of(dev))
+        _C.check(rc, "d2mi_retina_loss_fwd")
+        ctx.save_for_backward(anchors, gt_boxes, gt_classes, matches, labels, *levels)
+        ctx.conf = (conf, lvl)
+        ctx.set_materialize_grads(False)  # a missing gradient is a zero one (null pointer)
+        out = part.sum(0)  # fixed-size reduction of the partials: deterministic order
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_cls, g_box):
+        anchors, gt_boxes, gt_classes, matches, labels, *levels = ctx.saved_tensors
+        conf, lvl = ctx.conf
+        L = len(levels) // 2
+        cls, box = levels[:L], levels[L:]
+        N, K, A = cls[0].shape[0], conf[0], conf[1]
+        d = [torch.empty_like(t) for t in levels]
+        nul = _C.c_void_p(None)
+        g_cls = _f32c(g_cls) if g_cls is not None else None
+        g_box = _f32c(g_box) if g_box is not None else None
+        rc = _C.lib().d2mi_retina_loss_bwd(
+            _C.host_array(_C.c_void_p, [c.data_ptr() for c in cls]),
+            _C.host_array(_C.c_void_p, [b.data_ptr() for b in box]),
+            _C.host_array(_C.c_void_p, [t.data_ptr() for t in d[:L]]),
+            _C.host_array(_C.c_void_p, [t.data_ptr() for t in d[L:]]),
+            _C.host_array(_C.ctypes.c_longlong, lvl), L, N, K, A, _C.ptr(anchors),
+            _C.ptr(gt_boxes), _C.ptr(gt_classes), gt_boxes.shape[1], _C.ptr(matches),
+            _C.ptr(labels), conf[2], conf[3], conf[4], _C.host_array(_C.c_float, list(conf[5])),
+            _C.ptr(g_cls) if g_cls is not None else nul,
+            _C.ptr(g_box) if g_box is not None else nul, _C.stream_of(anchors.device))
+        _C.check(rc, "d2mi_retina_loss_bwd")
+        return (None,) * 6 + tuple(d)
+
+
+def retina_loss(cls_levels, box_levels, anchors, gt_boxes, gt_classes, matches, labels,
+                num_classes, num_anchors, alpha, gamma, beta, weights):
+    """Fused RetinaNet losses (retinanet.py:147-210, before the normaliser):
+    cls_levels [N, H, W, A*K] / box_levels [N, H, W, A*4] per level, anchors
+    [R, 4] (levels concatenated, (h, w, a) order), gt_boxes [N, G, 4],
+    gt_classes [N, G], matches / labels [N, R] (the Matcher's; labels 1 fg,
+    0 bg, -1 ignore) -> (sum of sigmoid_focal_loss over every valid anchor and
+    class, sum of smooth_l1 over the foreground anchors' deltas)."""
+    cls_levels = [_f32c(c) for c in cls_levels]
+    box_levels = [_f32c(b) for b in box_levels]
+    anchors, gt_boxes = _f32c(anchors), _f32c(gt_boxes)
+    gt_classes = gt_classes.to(torch.int64).contiguous()
+    matches = matches.to(torch.int64).contiguous()
+    labels = labels.to(torch.int64).contiguous()
+    _C.require_device(anchors, gt_boxes, gt_classes, matches, labels, *cls_levels, *box_levels)
+    for c, b in zip(cls_levels, box_levels):
+        if c.shape[-1] != num_anchors * num_classes or b.shape[-1] != num_anchors * 4 \
+                or c.shape[:3] != b.shape[:3]:
+            raise ValueError(f"retina loss: level outputs {tuple(c.shape)} / {tuple(b.shape)} do "
+                             f"not match A={num_anchors}, K={num_classes}")
+    R = sum(int(c.shape[1] * c.shape[2]) * num_anchors for c in cls_levels)
+    if anchors.shape[0] != R or labels.shape[-1] != R:
+        raise ValueError(f"retina loss: {anchors.shape[0]} anchors / {labels.shape[-1]} labels "
+                         f"for {R} head outputs")
+    conf = (int(num_classes), int(num_anchors), float(alpha), float(gamma), float(beta),
+            tuple(float(v) for v in weights))
+    return _RetinaLossFn.apply(conf, anchors, gt_boxes, gt_classes, matches, labels,
+                               *cls_levels, *box_levels)
+
+
 def stem_conv_weights(w):
     """HWIO [7, 7, 3, Cout=64] -> the [3][64][160] bf16 planes d2mi_stem_conv
     takes (K = (kh * 7 + kw) * 3 + c, zero-padded to 160)."""

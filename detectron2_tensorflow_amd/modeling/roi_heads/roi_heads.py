@@ -126,6 +126,29 @@ class ROIHeads(Layer):
                 "is_valid": valid}
 
 
+class DeferredMaskLoss:
+    """The training mask loss of a StandardROIHeads forward, not yet run:
+    the foreground count is known only on the device (``count``), and the
+    compacted mask branch's row count depends on it.  A step captured into
+    hipGraphs (engine/graphed.py) replays the forward up to here, reads
+    ``count`` once, and replays the mask branch + backward graph captured for
+    that row count (``compute(rows)``, run once per distinct row count at
+    capture time).  The eager trainer never sees one (defer_mask_loss False)."""
+
+    def __init__(self, heads, feats, sampled, targets, share, fg):
+        self.heads, self.feats, self.sampled, self.targets = heads, feats, sampled, targets
+        self.share, self.fg = share, fg
+        self.count = fg.sum()
+        self.slots = fg.numel()
+
+    def rows_for(self, nfg):
+        return self.heads.mask_rows(int(nfg), self.slots)
+
+    def compute(self, rows):
+        return self.heads._mask_loss(self.feats, self.sampled, self.targets, self.share, None,
+                                     self.fg, rows=rows)
+
+
 @ROI_HEADS_REGISTRY.register()
 class StandardROIHeads(ROIHeads):
     MASK_ROW_BUCKET = 32
@@ -158,6 +181,9 @@ class StandardROIHeads(ROIHeads):
         # host sync per step); False: fixed [N, S*POSITIVE_FRACTION] rows with
         # a validity mask (no host sync, capturable).
         self.mask_compact_rows = True
+        # True (set by engine.graphed.GraphedTrainer): the training forward
+        # returns a DeferredMaskLoss instead of reading the foreground count
+        self.defer_mask_loss = False
         self.last_mask_rows = None
         scales = tuple(1.0 / self.feature_strides[k] for k in self.in_features)
         c = [self.feature_channels[f] for f in self.in_features][0]
@@ -179,10 +205,13 @@ class StandardROIHeads(ROIHeads):
             # is enqueued (the device never idles at the read)
             pending = None
             fg = self._mask_fg(sampled) if self.mask_on else None  # (once per step)
-            if self.mask_on and self.mask_compact_rows:
+            defer = self.mask_on and self.mask_compact_rows and self.defer_mask_loss
+            if self.mask_on and self.mask_compact_rows and not defer:
                 pending = host_sync.start_read(fg.sum())
             losses = self._box_losses(feats, sampled, share)
-            if self.mask_on:
+            if defer:
+                losses["loss_mask"] = DeferredMaskLoss(self, feats, sampled, targets, share, fg)
+            elif self.mask_on:
                 losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg)
             return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
@@ -231,7 +260,15 @@ class StandardROIHeads(ROIHeads):
         return (sampled["is_valid"][:, :F_]
                 & (sampled["gt_classes"][:, :F_] < self.num_classes)).reshape(-1)
 
-    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None):
+    def mask_rows(self, nfg, slots):
+        """Rows the compacted mask branch runs for nfg foreground proposals out
+        of ``slots``: nfg rounded up to a multiple of MASK_ROW_BUCKET (at least
+        one bucket, at most every slot) -- a handful of distinct shapes."""
+        b = self.MASK_ROW_BUCKET
+        return min(slots, max(b, -(-nfg // b) * b))
+
+    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None,
+                   rows=None):
         """_forward_mask training branch (roi_heads.py:594-600) over the first
         int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
         foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
@@ -252,10 +289,12 @@ class StandardROIHeads(ROIHeads):
             # host read of the foreground count; the rows are gathered fg-first
             # (image order kept) and padded to a multiple of MASK_ROW_BUCKET
             # with masked-out rows, which bounds the number of distinct shapes.
-            nfg = (host_sync.finish_read(pending) if pending is not None
-                   else host_sync.read_ints(fg.sum()))[0]
-            B = fg.numel()
-            R = min(B, max(self.MASK_ROW_BUCKET, -(-nfg // self.MASK_ROW_BUCKET) * self.MASK_ROW_BUCKET))
+            # (rows given: a deferred mask loss, DeferredMaskLoss.compute)
+            if rows is None:
+                nfg = (host_sync.finish_read(pending) if pending is not None
+                       else host_sync.read_ints(fg.sum()))[0]
+                rows = self.mask_rows(nfg, fg.numel())
+            R = rows
             # fg rows first, each group in index order (a stable sort of ~fg)
             rows = torch.argsort((~fg).to(torch.uint8), stable=True)[:R]
             boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))

@@ -1,10 +1,17 @@
-"""RetinaNetHead inference (lib/modeling/single_stage_heads/retinanet.py:60-450).
+"""RetinaNetHead (lib/modeling/single_stage_heads/retinanet.py:60-450).
 
 Box tower: NUM_CONVS x (3x3 conv + ReLU) per branch + cls_score / bbox_pred
 3x3 convs, all on the MFMA conv kernel.  Inference: d2mi_retinanet_inference —
 per level sigmoid + exact top-k(min(1000, HWA)) over up to 12.1 M scores, score
 threshold, decode of the chosen anchors with MODEL.RPN.BBOX_REG_WEIGHTS (as the
-reference, retinanet.py:87), class-offset NMS, pad to DETECTIONS_PER_IMAGE."""
+reference, retinanet.py:87), class-offset NMS, pad to DETECTIONS_PER_IMAGE.
+Training (retinanet.py:147-283): IoU(valid GT, every anchor) + Matcher
+(IOU_THRESHOLDS 0.4 / 0.5, low-quality matches) on the fused HIP matcher,
+then sigmoid focal loss over every non-ignored anchor x class and smooth-L1
+of the foreground deltas in one fused HIP pass over the head's per-level
+outputs (d2mi_retina_loss_fwd / _bwd), both divided by the EMA of the
+foreground count (the non-trainable loss_normalizer, momentum 0.9, init 100,
+updated on the device before it divides: no host synchronisation)."""
 import math
 
 import torch
@@ -15,8 +22,14 @@ from ...layers import ops
 from ...structures import BoxList
 from ...utils.arg_scope import arg_scope
 from ..anchor_generator import build_anchor_generator
+from ...layers.loss import sigmoid_focal_loss, smooth_l1_loss
 from ..box_regression import Box2BoxTransform
+from ..matcher import Matcher, match_boxes
 from .build import SINGLE_STAGE_HEADS_REGISTRY
+
+
+# the fused HIP losses on the GPU (False: the tensor formulation; tests compare)
+FUSED_LOSSES = True
 
 
 class RetinaNetBoxTower(Layer):
@@ -70,13 +83,85 @@ class RetinaNetHead(Layer):
         self.anchor_generator = build_anchor_generator(cfg, shapes)
         self.head = RetinaNetBoxTower(cfg, shapes, self.anchor_generator.num_cell_anchors, scope="head")
         self.box2box_transform = Box2BoxTransform(weights=cfg.MODEL.RPN.BBOX_REG_WEIGHTS)
+        # training (retinanet.py:70-108)
+        self.focal_loss_alpha = r.FOCAL_LOSS_ALPHA
+        self.focal_loss_gamma = r.FOCAL_LOSS_GAMMA
+        self.smooth_l1_loss_beta = r.SMOOTH_L1_LOSS_BETA
+        s = cfg.MODEL.SINGLE_STAGE_HEAD
+        self.matcher = Matcher(s.IOU_THRESHOLDS, s.IOU_LABELS, allow_low_quality_matches=True)
+        self.register_buffer("loss_normalizer", torch.tensor(100.0))
+        self.loss_normalizer_momentum = 0.9
 
     def call(self, images, features, targets=None):
         feats = [features[f] for f in self.in_features]
         box_cls, box_delta = self.head(feats)
         if self.training:
-            raise NotImplementedError("RetinaNet training (focal loss, matcher) is a later round")
+            if targets is None:
+                raise ValueError("RetinaNet training needs targets")
+            return None, self.losses(feats, box_cls, box_delta, targets)
         return self.inference(box_cls, box_delta), {}
+
+    def _all_anchors(self, feats):
+        """Level-major concatenation of the grid anchors (box_list_ops.concatenate
+        of anchor_generator(features), retinanet.py:232), cached per grid."""
+        key = tuple((f.shape[1], f.shape[2]) for f in feats) + (str(feats[0].device),)
+        if getattr(self, "_anchor_key", None) != key:
+            grids = [(f.shape[1], f.shape[2]) for f in feats]
+            self._anchors = torch.cat(self.anchor_generator.grid_anchors(grids, feats[0].device))
+            self._anchor_key = key
+        return self._anchors
+
+    def losses(self, feats, box_cls, box_delta, gt):
+        """get_ground_truth + losses (retinanet.py:147-283) on dense [N, R]
+        anchor rows: the GT matched against are the valid ones
+        (boolean_mask(is_valid)); labels 1 -> the matched GT's class, 0 -> K
+        (background), -1 -> ignored; the two sums over the whole batch are
+        divided by the updated loss-normaliser EMA of max(1, #foreground)."""
+        anchors = self._all_anchors(feats)
+        gt_boxes, valid = gt["gt_boxes"], gt["is_valid"].bool()
+        gt_classes = gt["gt_classes"]
+        matches, labels = match_boxes(self.matcher, gt_boxes, valid, anchors)
+        K = self.num_classes
+        A = self.anchor_generator.num_cell_anchors[0]
+        if anchors.is_cuda and FUSED_LOSSES:
+            cls_sum, box_sum = ops.retina_loss(
+                box_cls, box_delta, anchors, gt_boxes, gt_classes, matches, labels, K, A,
+                self.focal_loss_alpha, self.focal_loss_gamma, self.smooth_l1_loss_beta,
+                self.box2box_transform.weights)
+        else:
+            cls_sum, box_sum = self._losses_dense(box_cls, box_delta, anchors, gt_boxes,
+                                                  gt_classes, matches, labels)
+        with torch.no_grad():
+            # moving_averages.assign_moving_average(zero_debias=False):
+            # v -= (v - value) * (1 - momentum), value = max(1, #foreground)
+            nfg = (labels == 1).sum().to(torch.float32).clamp(min=1.0)
+            v = self.loss_normalizer
+            v.sub_((v - nfg) * (1.0 - self.loss_normalizer_momentum))
+        norm = self.loss_normalizer.clone()  # (the next step's update stays out of this graph)
+        return {"loss_cls": cls_sum / norm, "loss_box_reg": box_sum / norm}
+
+    def _losses_dense(self, box_cls, box_delta, anchors, gt_boxes, gt_classes, matches, labels):
+        """The tensor formulation of the two sums (CPU, and the tests'
+        reference for the fused kernel): reshape_to_N_HWA_K + concat, the
+        one-hot targets of the valid anchors, sigmoid_focal_loss "sum", and
+        smooth_l1_loss "sum" of the foreground rows (retinanet.py:160-198)."""
+        N, K = box_cls[0].shape[0], self.num_classes
+        cls = torch.cat([c.reshape(N, -1, K) for c in box_cls], 1)
+        dl = torch.cat([d.reshape(N, -1, 4) for d in box_delta], 1)
+        gcls = torch.gather(gt_classes.to(torch.int64), 1, matches)
+        tgt = torch.where(labels == 1, gcls, torch.where(labels == 0, torch.full_like(gcls, K),
+                                                         torch.full_like(gcls, -1)))
+        valid, fg = tgt >= 0, labels == 1
+        onehot = torch.nn.functional.one_hot(tgt.clamp(min=0), K + 1)[..., :K].to(cls.dtype)
+        focal = sigmoid_focal_loss(predictions=cls, targets=onehot, alpha=self.focal_loss_alpha,
+                                   gamma=self.focal_loss_gamma)
+        cls_sum = torch.where(valid[..., None], focal, torch.zeros_like(focal)).sum()
+        gtb = torch.gather(gt_boxes, 1, matches[..., None].expand(-1, -1, 4))
+        src = anchors[None].expand(N, -1, -1).reshape(-1, 4)
+        target = self.box2box_transform.get_deltas(src, gtb.reshape(-1, 4)).reshape(N, -1, 4)
+        l1 = smooth_l1_loss(labels=target, predictions=dl, beta=self.smooth_l1_loss_beta)
+        box_sum = torch.where(fg[..., None], l1, torch.zeros_like(l1)).sum()
+        return cls_sum, box_sum
 
     def inference(self, box_cls, box_delta):
         ob, os_, oc, ov = ops.retinanet_inference(

@@ -114,6 +114,34 @@ class MomentumSGD:
         # and fused-head caches key on them)
         torch.autograd.graph.increment_version(self.params)
 
+    def step_captured(self, lr_dev, keep):
+        """The fused update for a training step being captured into a hipGraph
+        (engine/graphed.py): the table of this capture's gradient pointers goes
+        to its OWN pinned host buffer (appended to ``keep``, which the graph
+        holder owns: the captured upload re-reads it at every replay), and the
+        learning rate is read from the device float ``lr_dev`` at run time
+        (d2mi_momentum_sgd_ex).  No version bump: nothing runs at capture time,
+        and the packed-weight caches must keep the keys the captured forward
+        was recorded with."""
+        from .. import _C
+        if getattr(self, "_tab", None) is None:
+            self._fused_init()
+        tab = self._tab.copy()
+        for i, p in enumerate(self.params):
+            g = p.grad
+            if g is not None and not g.is_contiguous():
+                raise RuntimeError("captured Momentum-SGD needs contiguous gradients")
+            tab["g"][i] = 0 if g is None else g.data_ptr()
+        host = torch.from_numpy(tab.view(np.uint8).copy()).pin_memory()
+        dev_tab = torch.empty(tab.nbytes, dtype=torch.uint8, device=self._tab_dev.device)
+        dev_tab.copy_(host, non_blocking=True)
+        keep += [host, dev_tab]
+        rc = self._lib.d2mi_momentum_sgd_ex(_C.ptr(dev_tab), _C.ptr(self._chunks_dev), self._nchunks,
+                                            _C.ptr(self._partial), float(self.clip_norm),
+                                            float(self.momentum), 0.0, _C.ptr(lr_dev),
+                                            _C.stream_of(dev_tab.device))
+        _C.check(rc, "d2mi_momentum_sgd_ex")
+
     def zero_grad(self):
         for p in self.params:
             p.grad = None

@@ -754,6 +754,37 @@ int d2mi_stride_scatter(const float* g, const float* add, int N, int H, int W, i
 int d2mi_stride_scatter_ex(const float* g, const float* add, const float* add2, const float* gate,
                            int N, int H, int W, int C, int stride, float* out, void* stream);
 
+/* ------------------------------------------------------ RetinaNet losses
+ * Replaces RetinaNet.losses (lib/modeling/single_stage_heads/retinanet.py:
+ * 147-210) up to the loss normaliser: sigmoid_focal_loss (lib/layers/
+ * loss.py:59-104, alpha / gamma, reduction "sum") over every anchor whose
+ * label is not "ignore" and every class (target 1 at the matched GT's class
+ * for foreground anchors), and smooth_l1_loss (loss.py:9-58, beta, "sum")
+ * of the foreground anchors' deltas against get_deltas(anchor, matched GT)
+ * (lib/modeling/box_regression.py:38-74, weights[4] = wy, wx, wh, ww).
+ * cls[l] / box[l]: level l's head outputs [N, H_l, W_l, A*K] / [N, H_l, W_l,
+ * A*4] f32 (16-byte aligned), level_anchors[l] = H_l * W_l * A; anchors [R, 4]
+ * (levels concatenated, (h, w, a) order, R = sum of level_anchors); gt_boxes
+ * [N, G, 4]; gt_classes [N, G] int64; matches / labels [N, R] int64 (the
+ * Matcher's: labels 1 fg, 0 bg, -1 ignore).  K % 4 == 0.  fwd: partial
+ * [N * d2mi_retina_loss_blocks()][2] (cls, box) per-workgroup sums, to be
+ * added in a fixed order.  bwd: d_cls / d_box levels (every element written),
+ * scaled by the device scalars *g_cls / *g_box (null: zero). */
+int d2mi_retina_loss_blocks(void);
+int d2mi_retina_loss_fwd(const float* const* cls, const float* const* box,
+                         const long long* level_anchors, int L, int N, int K, int A,
+                         const float* anchors, const float* gt_boxes, const long long* gt_classes,
+                         int G, const long long* matches, const long long* labels, float alpha,
+                         float gamma, float beta, const float* weights, float* partial,
+                         void* stream);
+int d2mi_retina_loss_bwd(const float* const* cls, const float* const* box, float* const* d_cls,
+                         float* const* d_box, const long long* level_anchors, int L, int N, int K,
+                         int A, const float* anchors, const float* gt_boxes,
+                         const long long* gt_classes, int G, const long long* matches,
+                         const long long* labels, float alpha, float gamma, float beta,
+                         const float* weights, const float* g_cls, const float* g_box,
+                         void* stream);
+
 /* ------------------------------------------------------ Momentum-SGD step
  * Replaces the update of lib/engine/trainer.py:116-139 for every trainable
  * tensor in two launches: g' = g + wd * w (slim.l2_regularizer gradient,
@@ -769,6 +800,13 @@ int d2mi_stride_scatter_ex(const float* g, const float* add, const float* add2, 
 int d2mi_sgd_table_sizes(int* tensor_bytes, int* chunk_bytes, int* chunk_elems);
 int d2mi_momentum_sgd(const void* tensor_table, const void* chunk_table, int num_chunks,
                       float* partial, float clip_norm, float momentum, float lr, void* stream);
+/* The same step with the learning rate read from the device float *lr_dev at
+ * run time when lr_dev is non-null (lr ignored): a training step captured in
+ * a hipGraph (engine/graphed.py) replays with each iteration's LR of
+ * lib/solver/learning_rate.py, which the host writes to lr_dev. */
+int d2mi_momentum_sgd_ex(const void* tensor_table, const void* chunk_table, int num_chunks,
+                         float* partial, float clip_norm, float momentum, float lr,
+                         const float* lr_dev, void* stream);
 
 #ifdef __cplusplus
 }

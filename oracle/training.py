@@ -111,6 +111,63 @@ def rpn_losses(labels, gt_deltas, pred_logits, pred_deltas, num_images, batch_si
     return obj * norm, loc * norm
 
 
+def retinanet_targets(anchors, gt_boxes, gt_classes, is_valid, num_classes, weights,
+                      thresholds=(0.4, 0.5), labels=(0, -1, 1)):
+    """RetinaNet.get_ground_truth, one image (retinanet.py:212-283): the
+    valid GT (boolean_mask) against every anchor, Matcher with low-quality
+    matches; classes = matched GT class (label 1), K (label 0), -1 (ignored);
+    deltas = get_deltas(anchor, matched GT) for the positives, else 0."""
+    valid = np.asarray(is_valid, bool)
+    vgt = np.asarray(gt_boxes, F32)[valid]
+    vcls = np.asarray(gt_classes, np.int64)[valid]
+    iou = pairwise_iou(vgt, anchors)
+    matches, lab = matcher(iou, thresholds, labels, True)
+    cls = np.full(len(anchors), -1, np.int64)
+    pos = np.nonzero(lab > 0)[0]
+    cls[lab == 0] = num_classes
+    cls[pos] = vcls[matches[pos]]
+    deltas = np.zeros((len(anchors), 4), F32)
+    if len(pos):
+        deltas[pos] = get_deltas(anchors[pos], vgt[matches[pos]], weights)
+    return cls, deltas
+
+
+def sigmoid_focal_loss(x, t, alpha, gamma):
+    """loss.py:59-101 elementwise, float64."""
+    x = np.asarray(x, np.float64)
+    t = np.asarray(t, np.float64)
+    p = 1.0 / (1.0 + np.exp(-x))
+    ce = np.maximum(x, 0) - x * t + np.log1p(np.exp(-np.abs(x)))
+    p_t = p * t + (1 - p) * (1 - t)
+    loss = ce * (1 - p_t) ** gamma
+    if alpha >= 0:
+        loss = (alpha * t + (1 - alpha) * (1 - t)) * loss
+    return loss
+
+
+def retinanet_losses(gt_classes, gt_deltas, logits, deltas, num_classes, alpha, gamma, beta,
+                     normalizer, momentum=0.9):
+    """RetinaNet.losses (retinanet.py:147-210) over the batch's [N*R] anchor
+    rows: focal "sum" over the valid rows' one-hot targets, smooth-L1 "sum"
+    over the foreground rows, both / the normaliser EMA after its update
+    (assign_moving_average, zero_debias=False).  Returns (cls, box, new
+    normaliser), float64."""
+    gt_classes = np.asarray(gt_classes).reshape(-1)
+    logits = np.asarray(logits).reshape(-1, num_classes)
+    deltas = np.asarray(deltas).reshape(-1, 4)
+    gt_deltas = np.asarray(gt_deltas).reshape(-1, 4)
+    valid = gt_classes >= 0
+    fg = valid & (gt_classes < num_classes)
+    onehot = np.zeros_like(logits, dtype=np.float64)
+    onehot[np.nonzero(fg)[0], gt_classes[fg]] = 1.0
+    cls = sigmoid_focal_loss(logits[valid], onehot[valid], alpha, gamma).sum()
+    n = np.abs(gt_deltas[fg].astype(np.float64) - deltas[fg].astype(np.float64))
+    l1 = n if beta < 1e-5 else np.where(n < beta, 0.5 * n ** 2 / beta, n - 0.5 * beta)
+    nfg = max(1.0, float(fg.sum()))
+    norm = normalizer - (normalizer - nfg) * (1 - momentum)
+    return cls / norm, l1.sum() / norm, norm
+
+
 def label_proposals(proposals, p_valid, gt_boxes, gt_classes, is_valid, is_crowd, difficult,
                     num_classes, iou_threshold, append_gt=True):
     """label_and_sample_proposals before sampling, one image (roi_heads.py:130-180).

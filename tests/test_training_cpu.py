@@ -431,3 +431,48 @@ def test_trainer_loss_terms_cast_and_reject():
         Trainer._loss_terms({"a": torch.tensor(1.0), "bad": torch.ones(2)})
     with pytest.raises(TypeError, match="'n'"):
         Trainer._loss_terms({"n": torch.tensor(3)})
+
+
+def test_retinanet_dense_losses_match_oracle():
+    """RetinaNetHead's tensor formulation of the training losses (the GPU
+    kernel's reference in tests/test_retinanet.py) on the CPU Matcher, against
+    the per-image restatement of get_ground_truth + losses
+    (retinanet.py:147-283): targets, focal loss, smooth-L1, normaliser EMA."""
+    import oracle
+    from detectron2_tensorflow_amd.config import finalize, get_cfg
+    from detectron2_tensorflow_amd.layers import ShapeSpec
+    from detectron2_tensorflow_amd.modeling.matcher import match_boxes
+    from detectron2_tensorflow_amd.modeling.single_stage_heads.retinanet import RetinaNetHead
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(root, "configs", "COCO-Detection", "retinanet_R_50_FPN_1x.yaml"))
+    cfg.MODEL.SINGLE_STAGE_HEAD.NUM_CLASSES = 8
+    finalize(cfg, True, 1, {"num_thing_classes": 8, "num_stuff_classes": 0, "stuff_ignore_value": 0})
+    feats = cfg.MODEL.SINGLE_STAGE_HEAD.IN_FEATURES
+    strides = {f: 2 ** int(f[1:]) for f in feats}
+    head = RetinaNetHead(cfg, {f: ShapeSpec(channels=16, stride=strides[f]) for f in feats})
+    rng = np.random.default_rng(0)
+    N, H, W, G, K = 2, 64, 96, 5, 8
+    A = head.anchor_generator.num_cell_anchors[0]
+    grids = [(-(-H // strides[f]), -(-W // strides[f])) for f in feats]
+    anchors = np.concatenate([oracle.grid_anchors(h, w, strides[f], c.numpy())
+                              for (h, w), f, c in zip(grids, feats, head.anchor_generator.cell_anchors)])
+    gt = np.stack([rand_boxes(rng, G, H, W, 8, 60) for _ in range(N)])
+    valid = np.array([[1, 1, 1, 0, 1], [1, 0, 0, 0, 0]], bool)
+    gcls = rng.integers(0, K, (N, G))
+    cls = [torch.from_numpy(rng.normal(0, 2, (N, h, w, A * K)).astype(np.float32)) for h, w in grids]
+    box = [torch.from_numpy(rng.normal(0, 0.3, (N, h, w, A * 4)).astype(np.float32)) for h, w in grids]
+    t = torch.from_numpy
+    m, lab = match_boxes(head.matcher, t(gt), t(valid), t(anchors))
+    cs, bs = head._losses_dense(cls, box, t(anchors), t(gt), t(gcls), m, lab)
+    tc, td = zip(*[otrain.retinanet_targets(anchors, gt[i], gcls[i], valid[i], K,
+                                                     head.box2box_transform.weights)
+                   for i in range(N)])
+    lg = np.concatenate([np.concatenate([c[i].numpy().reshape(-1, K) for c in cls]) for i in range(N)])
+    dl = np.concatenate([np.concatenate([b[i].numpy().reshape(-1, 4) for b in box]) for i in range(N)])
+    want_c, want_b, norm = otrain.retinanet_losses(
+        np.concatenate(tc), np.concatenate(td), lg, dl, K, head.focal_loss_alpha,
+        head.focal_loss_gamma, head.smooth_l1_loss_beta, 100.0)
+    assert (np.concatenate(tc) >= 0).sum() > 0 and (np.concatenate(tc) < K).any()
+    assert float(cs) / norm == pytest.approx(want_c, rel=1e-5)
+    assert float(bs) / norm == pytest.approx(want_b, rel=1e-5)

@@ -4,6 +4,8 @@
 # pass on gfx950), each with --kernel-trace only, as MI355X_MICROARCH.md's
 # HBM/rocprofv3 section prescribes; tools/pmc_summarize.py applies its gfx950
 # correction (FETCH_SIZE counts half the bytes of 16 B/lane reads).
+# (the eager step: the same kernels as the graph-replayed one, launched one
+# by one)
 # usage: tools/pmc_traffic.sh <tag> [bench args...]
 set -eo pipefail
 tag=$1; shift
@@ -12,7 +14,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   out=gpurun_out/pmc_${tag}_$c
   rm -rf "$out"
   timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$out" -o run \
-      -- python3 bench.py --cpu-baseline 0 --no-kernel-timing "$@" > "$out.log" 2>&1
+      -- python3 bench.py --cpu-baseline 0 --no-kernel-timing --graphs 0 "$@" > "$out.log" 2>&1
 done
 python3 tools/pmc_summarize.py gpurun_out/pmc_${tag}_FETCH_SIZE gpurun_out/pmc_${tag}_WRITE_SIZE \
     gpurun_out/${tag}_pmc.json
