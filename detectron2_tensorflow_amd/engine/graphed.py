@@ -82,6 +82,7 @@ class GraphedTrainer(Trainer):
         self._losses = None
         self._deferred = None
         self._lr_dev = None
+        self._stream = None
         self.captures = 0
         self.replays = 0
 
@@ -91,15 +92,31 @@ class GraphedTrainer(Trainer):
         packed weights, the RPN head's fused 1x1 weights) miss once."""
         torch.autograd.graph.increment_version(self.optimizer.params)
 
+    def _on_stream(self, fn, *args):
+        """fn(*args) on the trainer's own stream -- the eager warm-up steps, the
+        captures and the replays alike, so every autograd node (AccumulateGrad
+        included) lives on the stream the graphs are captured on -- ordered
+        after the caller's stream on entry and before it on exit."""
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=next(self.model.parameters()).device)
+        caller = torch.cuda.current_stream(self._stream.device)
+        self._stream.wait_stream(caller)
+        with torch.cuda.stream(self._stream):
+            out = fn(*args)
+        caller.wait_stream(self._stream)
+        return out
+
     def eager_step(self, batched_inputs):
         """One eager ``Trainer.step`` (e.g. with kernel timers on).  It reads
         the current weights: the caches are marked stale before it, and it
         leaves no state the graphs depend on."""
+        if not self.enabled:
+            return Trainer.step(self, batched_inputs)
         if self._A is not None:
             self._mark_stale()
         for h in self.heads:
             h.defer_mask_loss = False
-        return Trainer.step(self, batched_inputs)
+        return self._on_stream(Trainer.step, self, batched_inputs)
 
     def _load(self, batched_inputs):
         leaves = _flatten(batched_inputs)
@@ -129,7 +146,8 @@ class GraphedTrainer(Trainer):
         torch.cuda.synchronize(dev)
         self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+        with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
+                              capture_error_mode="thread_local"):
             losses = self.model(self._static)
         deferred = [v for v in losses.values() if isinstance(v, DeferredMaskLoss)]
         if len(deferred) > 1:
@@ -149,7 +167,8 @@ class GraphedTrainer(Trainer):
         self.optimizer.zero_grad()
         keep = []
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+        with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
+                              capture_error_mode="thread_local"):
             out = {k: (v.compute(rows) if isinstance(v, DeferredMaskLoss) else v)
                    for k, v in self._losses.items()}
             total = torch.stack(self._loss_terms(out)).sum()
@@ -162,6 +181,7 @@ class GraphedTrainer(Trainer):
             self.reducer.finish()
             self.optimizer.step_captured(self._lr_dev, keep)
             values = torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()])
+        self.optimizer.upload_captured()
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
         self._B[rows] = (g, values, keys, keep)
@@ -174,6 +194,9 @@ class GraphedTrainer(Trainer):
         if self._A is None and self._eager < self.warmup:
             self._eager += 1
             return self.eager_step(batched_inputs)
+        return self._on_stream(self._graph_step, batched_inputs)
+
+    def _graph_step(self, batched_inputs):
         if self._A is None:
             self._capture_forward(batched_inputs)
         self._load(batched_inputs)

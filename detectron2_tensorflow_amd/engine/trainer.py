@@ -94,6 +94,8 @@ class Trainer:
         self.reducer.finish()
         self.optimizer.step(self.lr(self.iter))
         self.iter += 1
-        losses = dict(losses)
+        # detached: a returned loss must not keep this step's autograd graph
+        # (and its AccumulateGrad nodes, bound to this step's stream) alive
+        losses = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in losses.items()}
         losses["total_loss"] = total.detach()
         return losses

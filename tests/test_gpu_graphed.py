@@ -34,11 +34,10 @@ def test_graphed_trainer_matches_eager_trainer(dev, monkeypatch):
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
     cfg, m_eager = _model(dev)
     _, m_graph = _model(dev)
-    m_graph.load_state_dict(m_eager.state_dict())
     batches = [synthetic_train_batch(2, 256, 320, s, dev) for s in (11, 12)]
     batches[1]["instances"]["is_valid"][:, 2:] = False  # fewer GT: other mask row counts
-    calibrate_rcnn_scores(m_eager, batches[0])
-    calibrate_rcnn_scores(m_graph, batches[0])
+    calibrate_rcnn_scores(m_eager, batches[0])  # (draws random logit scales: once)
+    m_graph.load_state_dict(m_eager.state_dict())
     eager = Trainer(cfg, m_eager)
     graphed = GraphedTrainer(cfg, m_graph, warmup=1)
     heads = graphed.heads[0]
