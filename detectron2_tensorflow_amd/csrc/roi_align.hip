@@ -327,6 +327,11 @@ constexpr int kLongTile = 4096;  // run elements per LDS tile of the long sort
 
 struct PixMap {
   long long base[D2MI_MAX_LEVELS + 1];  // first global pixel id per level
+  // the touched-pixel list, partitioned by level: level l's entries start at
+  // tbase[l] (capacity tbase[l + 1] - tbase[l] = min(samples x 4, its pixels)),
+  // so a level's pixel pass walks its own pixels only
+  int32_t tbase[D2MI_MAX_LEVELS + 1];
+  int L;
 };
 
 struct Contrib {
@@ -338,6 +343,30 @@ struct Contrib {
 // Device-side bookkeeping of one backward (cleared by the clear launch).
 struct BwdCounters {
   int32_t touched, segs, tasks, cursor;
+  int32_t touched_lv[D2MI_MAX_LEVELS];  // touched pixels per level
+};
+
+// The touched pixels of levels [lo, hi]: their count, and the t-th of them
+// (the level segments of the list in level order).
+struct TouchedRange {
+  int32_t pre[D2MI_MAX_LEVELS + 1];
+  int lo, hi;
+  __device__ __forceinline__ void init(const PixMap& pm, const BwdCounters* ctr, int lv_lo,
+                                       int lv_hi) {
+    lo = lv_lo;
+    hi = lv_hi;
+    pre[0] = 0;
+    for (int l = lo; l <= hi; ++l) pre[l - lo + 1] = pre[l - lo] + ctr->touched_lv[l];
+  }
+  __device__ __forceinline__ int total() const { return pre[hi - lo + 1]; }
+  // global pixel id and level of entry t < total()
+  __device__ __forceinline__ long long at(const PixMap& pm, const int32_t* touched, int t,
+                                          int& l) const {
+    int k = 0;
+    while (k < hi - lo && t >= pre[k + 1]) ++k;
+    l = lo + k;
+    return touched[pm.tbase[l] + (t - pre[k])];
+  }
 };
 
 // One launch clears every buffer the backward starts from (the per-level grad
@@ -491,7 +520,7 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
     const int32_t* __restrict__ count, long long total_pixels, int set_bits,
     int32_t* __restrict__ run_start, int32_t* __restrict__ seg_first,
     int32_t* __restrict__ seg_pixel, int2* __restrict__ tasks, int32_t* __restrict__ touched,
-    BwdCounters* __restrict__ ctr) {
+    BwdCounters* __restrict__ ctr, PixMap pm) {
   __shared__ int s_wave[16], s_base;
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = p < total_pixels;
@@ -507,7 +536,19 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
     }
   }
   const int pos = wg_alloc<1024>(tot, &ctr->cursor, s_wave, &s_base);
-  const int tix = wg_alloc<1024>(tot > 0 ? 1 : 0, &ctr->touched, s_wave, &s_base);
+  // the pixel's slot in its level's segment of the touched list (the
+  // workgroup's pixels span levels lf..ll: one allocation per level, uniform)
+  const long long p0 = (long long)blockIdx.x * blockDim.x;
+  const long long p1 = min(p0 + (long long)blockDim.x, total_pixels) - 1;
+  int lf = 0, ll = 0, lp = 0;
+  while (lf + 1 < pm.L && p0 >= pm.base[lf + 1]) ++lf;
+  while (ll + 1 < pm.L && p1 >= pm.base[ll + 1]) ++ll;
+  while (lp + 1 < pm.L && p >= pm.base[lp + 1]) ++lp;
+  int tix = 0;
+  for (int lv = lf; lv <= ll; ++lv) {
+    const int o = wg_alloc<1024>(tot > 0 && lp == lv ? 1 : 0, &ctr->touched_lv[lv], s_wave, &s_base);
+    if (lp == lv) tix = pm.tbase[lv] + o;
+  }
   const int sf = wg_alloc<1024>(nseg[0] + nseg[1], &ctr->segs, s_wave, &s_base);
   const int tf = wg_alloc<1024>(ntask[0] + ntask[1], &ctr->tasks, s_wave, &s_base);
   if (tot == 0) return;
@@ -699,19 +740,19 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
     RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
     int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, long long pix_lo,
-    long long pix_hi) {
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, int lv_lo,
+    int lv_hi) {
   __shared__ int32_t lds[4][2][kSeg];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int C = a.C;
   const int step = VEC4 ? 256 : 64;
-  const int nt = ctr->touched;
+  TouchedRange tr;
+  tr.init(pm, ctr, lv_lo, lv_hi);  // the levels of this pass (bwd2 phase 2: one)
+  const int nt = tr.total();
   const int nsets = 1 << set_bits;
   for (int t = blockIdx.x * 4 + w; t < nt; t += gridDim.x * 4) {
-    const long long pix = touched[t];
-    if (pix < pix_lo || pix >= pix_hi) continue;  // a level-range pass (bwd2 phase 2)
-    int l = 0;
-    while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
+    int l;
+    const long long pix = tr.at(pm, touched, t, l);
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C;
     const bool acc_lv = (a.acc_mask >> l) & 1;
     // each set's run in slot order once per pixel (the channel loop reuses it)
@@ -781,8 +822,8 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
     int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, long long pix_lo,
-    long long pix_hi) {
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, int lv_lo,
+    int lv_hi) {
   constexpr int C = 256;
   constexpr int LPP = 64 / PPW;     // lanes per pixel
   constexpr int F = C / LPP / 4;    // float4 per lane
@@ -790,7 +831,9 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane / LPP, sub = lane % LPP;
   const int c = sub * 4 * F;  // this lane's channels
-  const int nt = ctr->touched;
+  TouchedRange tr;
+  tr.init(pm, ctr, lv_lo, lv_hi);
+  const int nt = tr.total();
   const int nsets = 1 << set_bits;
   int32_t* lin = lds[w][grp][0];
   int32_t* lout = lds[w][grp][1];
@@ -798,10 +841,8 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
   for (int tb = wave * PPW; tb < nt; tb += gridDim.x * 4 * PPW) {
     const int t = tb + grp;
     if (t >= nt) continue;
-    const long long pix = touched[t];
-    if (pix < pix_lo || pix >= pix_hi) continue;  // a level-range pass (bwd2 phase 2)
-    int l = 0;
-    while (l + 1 < a.L && pix >= pm.base[l + 1]) ++l;
+    int l;
+    const long long pix = tr.at(pm, touched, t, l);
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
     float4 res[F];
     bool any = false;
@@ -996,14 +1037,21 @@ int bwd_plan_n(const int32_t* dims, int num_levels, long long n_samples, int set
     t += (long long)dims[3 * l] * dims[3 * l + 1] * dims[3 * l + 2];
   }
   p->pm.base[num_levels] = t;
+  p->pm.L = num_levels;
   p->total_pixels = t;
   p->pairs = t << set_bits;
   // every split run has > kSeg contributions: segments <= 2 * n / kSeg, and
   // long-sort tasks <= n / kLongTask + (number of long runs)
   p->max_segs = 2 * (p->n_keys / kSeg) + 1;
   p->max_tasks = p->n_keys / kLongTask + p->n_keys / (kSeg + 1) + 2;
-  p->max_touched = std::min(p->n_keys, t);
-  D2MI_REQUIRE(p->n_keys < (1LL << 31) && p->pairs < (1LL << 31), "ROIAlign backward too large");
+  p->pm.tbase[0] = 0;
+  for (int l = 0; l < num_levels; ++l)
+    p->pm.tbase[l + 1] =
+        p->pm.tbase[l] + (int32_t)std::min(p->n_keys, p->pm.base[l + 1] - p->pm.base[l]);
+  p->max_touched = p->pm.tbase[num_levels];
+  D2MI_REQUIRE(p->n_keys < (1LL << 31) && p->pairs < (1LL << 31) &&
+                   p->n_keys * num_levels < (1LL << 31),
+               "ROIAlign backward too large");
   return 0;
 }
 
@@ -1107,7 +1155,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   }
   hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.total_pixels + 1023) / 1024)),
                      dim3(1024), 0, st, count, p.total_pixels, sb, run_start, seg_first, seg_pixel,
-                     tasks, touched, ctr);
+                     tasks, touched, ctr, p.pm);
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
                      st, ent, p.n_keys, run_start, arrival);
@@ -1147,29 +1195,30 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     }
   }
   if (!(phase & 2) || p.n_keys == 0) return 0;
-  const long long pix_lo = p.pm.base[lv_lo], pix_hi = p.pm.base[lv_hi + 1];
-  // fixed grid (the touched count stays on the device): at most 8192
-  // workgroups x 4 waves = 32 waves per SIMD over 256 CUs x 4 SIMDs; waves
-  // beyond residency start as earlier ones retire (the kBatch sweep above)
-  const dim3 grid((unsigned)std::max(1LL, std::min((p.max_touched + 3) / 4, 8192LL)));
+  // fixed grid sized by the capacity of the pass's level segments (the
+  // touched counts stay on the device): at most 8192 workgroups x 4 waves =
+  // 32 waves per SIMD over 256 CUs x 4 SIMDs; waves beyond residency start
+  // as earlier ones retire (the kBatch sweep above)
+  const long long cap = p.pm.tbase[lv_hi + 1] - p.pm.tbase[lv_lo];
+  const dim3 grid((unsigned)std::max(1LL, std::min((cap + 3) / 4, 8192LL)));
   if (vec4 && C == 256) {
     static const int ppw = [] {
       const char* e = getenv("D2MI_ROI_BWD_PPW");
       return e && e[0] == '8' ? 8 : 4;
     }();
-    const dim3 g4((unsigned)std::max(1LL, std::min((p.max_touched + 4 * ppw - 1) / (4 * ppw), 8192LL)));
+    const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), 8192LL)));
     if (ppw == 8)
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
+                         sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
     else
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
+                         sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
   } else if (vec4) {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
-                       sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
+                       sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
   } else {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<false>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
-                       sb, count, run_start, seg_first, partial, touched, ctr, pix_lo, pix_hi);
+                       sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
   }
   D2MI_LAUNCH_CHECK();
   return 0;

@@ -28,14 +28,12 @@ freed temporaries.  The caches keyed on parameter versions (folded /
 packed weights) are made stale before A is captured, so A re-folds and
 re-packs every trainable layer at each replay; nothing bumps a version while
 the graphs are in use, and an eager step (``eager_step``) marks them stale
-again first.  A multi-rank job runs the eager step unless ``dp_graphs``
-asks for the RCCL all-reduces to be captured too (gloo cannot be).
+again first.  A multi-rank job runs the eager step (see __init__).
 """
 import torch
-import torch.distributed as dist
 
 from ..modeling.roi_heads.roi_heads import DeferredMaskLoss, StandardROIHeads
-from ..utils import host_sync
+from ..utils import capture, host_sync
 from .trainer import Trainer
 
 
@@ -58,21 +56,22 @@ def _clone_tree(tree):
 
 class GraphedTrainer(Trainer):
     """``Trainer`` whose steps replay captured hipGraphs (see the module
-    docstring).  ``warmup``: eager steps before the capture (allocator,
-    workspaces, per-shape caches).  Falls back to the eager step when the
+    docstring).  ``warmup``: eager steps before the capture (at least one:
+    allocator, workspaces, per-shape caches).  Falls back to the eager step when the
     process group has more than one rank."""
 
-    def __init__(self, cfg, model, warmup=1, dp_graphs=False, **kwargs):
+    def __init__(self, cfg, model, warmup=1, **kwargs):
         super().__init__(cfg, model, **kwargs)
-        self.warmup = int(warmup)
+        # >= 1: the first eager step makes the per-shape caches, workspaces and
+        # the optimizer / fold tables, none of which may be created in a capture
+        self.warmup = max(1, int(warmup))
         self.heads = [m for m in model.modules() if isinstance(m, StandardROIHeads)]
-        # dp_graphs: capture the bucketed all-reduce too (RCCL: "nccl" backend
-        # only; tested at world size 1 in tests/rccl_worker.py).  Off, a
-        # multi-rank job runs the eager step.
-        nccl = dist.is_initialized() and dist.get_backend() == "nccl"
-        self.enabled = (next(model.parameters()).is_cuda
-                        and ((self.world == 1 and not self.reducer.active)
-                             or (dp_graphs and nccl)))
+        # world size 1 only: capturing the bucketed all-reduce was tried over
+        # RCCL at world size 1 and fails (the process group's watchdog queries
+        # the events of collectives recorded inside the capture); gloo cannot
+        # be captured at all.  A multi-rank job runs the eager step.
+        self.enabled = (next(model.parameters()).is_cuda and self.world == 1
+                        and not self.reducer.active)
         self._eager = 0
         self._pool = None
         self._A = None
@@ -149,6 +148,8 @@ class GraphedTrainer(Trainer):
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             losses = self.model(self._static)
+        self._keep = []
+        capture.flush(self._keep)
         deferred = [v for v in losses.values() if isinstance(v, DeferredMaskLoss)]
         if len(deferred) > 1:
             raise RuntimeError("graphed step: more than one deferred mask loss")
@@ -179,9 +180,9 @@ class GraphedTrainer(Trainer):
             # by another backward through it
             total.backward(seed, retain_graph=True)
             self.reducer.finish()
-            self.optimizer.step_captured(self._lr_dev, keep)
+            self.optimizer.step_captured(self._lr_dev)
             values = torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()])
-        self.optimizer.upload_captured()
+        capture.flush(keep)
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
         self._B[rows] = (g, values, keys, keep)
@@ -198,7 +199,11 @@ class GraphedTrainer(Trainer):
 
     def _graph_step(self, batched_inputs):
         if self._A is None:
-            self._capture_forward(batched_inputs)
+            try:
+                self._capture_forward(batched_inputs)
+            except BaseException:
+                capture.discard()
+                raise
         self._load(batched_inputs)
         self._lr_dev.fill_(float(self.lr(self.iter)))
         self._A.replay()

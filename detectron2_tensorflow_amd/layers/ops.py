@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from .. import _C
-from ..utils import host_sync
+from ..utils import capture, host_sync
 from . import handoff
 
 _DEFAULT_SCALE_CLAMP = math.log(1000.0 / 16)  # lib/modeling/box_regression.py:10
@@ -1275,6 +1275,8 @@ class _HostTable:
         self.i = 0
 
     def upload(self, arr):
+        if capture.capturing():  # a per-graph table, filled after the capture
+            return capture.table(arr, self.dev.device)
         k = self.i
         self.i = (k + 1) % self.RING
         if self.events[k] is not None:

@@ -11,7 +11,7 @@ import torch
 
 from ...layers import ShapeSpec
 from ...structures import BoxList
-from ...utils import host_sync
+from ...utils import capture, host_sync
 from ...utils.registry import Registry
 from ..box_regression import Box2BoxTransform
 from ..poolers import ROIPooler
@@ -41,7 +41,10 @@ def _cached_index(kind, n, m, device):
             t = torch.arange(m, dtype=torch.int32, device=device).repeat(n)
         else:  # "base": arange(n)[:, None] * m, int64
             t = torch.arange(n, device=device)[:, None] * m
-        _INDEX_CACHE[key] = t
+        # (made inside a hipGraph capture, the tensor holds its values only
+        # once that graph has replayed: not cached for anything else)
+        if not capture.capturing():
+            _INDEX_CACHE[key] = t
     return t
 
 ROI_HEADS_REGISTRY = Registry("ROI_HEADS")

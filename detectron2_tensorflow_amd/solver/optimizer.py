@@ -114,17 +114,17 @@ class MomentumSGD:
         # and fused-head caches key on them)
         torch.autograd.graph.increment_version(self.params)
 
-    def step_captured(self, lr_dev, keep):
+    def step_captured(self, lr_dev):
         """The fused update for a training step being captured into a hipGraph
         (engine/graphed.py).  The table of this capture's gradient pointers is
         constant across replays: the captured launches read it from a device
-        buffer of their own (appended to ``keep``, which the graph holder owns)
-        that ``upload_captured`` fills once, after the capture -- no host
-        memory or copy node inside the graph.  The learning rate is read from
-        the device float ``lr_dev`` at run time (d2mi_momentum_sgd_ex).  No
-        version bump: nothing runs at capture time, and the packed-weight
+        buffer of their own that utils.capture fills after the capture (no
+        host memory or copy node inside the graph).  The learning rate is read
+        from the device float ``lr_dev`` at run time (d2mi_momentum_sgd_ex).
+        No version bump: nothing runs at capture time, and the packed-weight
         caches must keep the keys the captured forward was recorded with."""
         from .. import _C
+        from ..utils import capture
         if getattr(self, "_tab", None) is None:
             self._fused_init()
         tab = self._tab.copy()
@@ -133,21 +133,12 @@ class MomentumSGD:
             if g is not None and not g.is_contiguous():
                 raise RuntimeError("captured Momentum-SGD needs contiguous gradients")
             tab["g"][i] = 0 if g is None else g.data_ptr()
-        dev_tab = torch.empty(tab.nbytes, dtype=torch.uint8, device=self._tab_dev.device)
-        keep.append(dev_tab)
-        self._uploads = getattr(self, "_uploads", []) + [(dev_tab, tab.view(np.uint8).copy())]
+        dev_tab = capture.table(tab, self._tab_dev.device)
         rc = self._lib.d2mi_momentum_sgd_ex(_C.ptr(dev_tab), _C.ptr(self._chunks_dev), self._nchunks,
                                             _C.ptr(self._partial), float(self.clip_norm),
                                             float(self.momentum), 0.0, _C.ptr(lr_dev),
                                             _C.stream_of(dev_tab.device))
         _C.check(rc, "d2mi_momentum_sgd_ex")
-
-    def upload_captured(self):
-        """Fill the tables of the steps captured since the last call (outside
-        any capture; synchronous)."""
-        for dev_tab, host in getattr(self, "_uploads", []):
-            dev_tab.copy_(torch.from_numpy(host))
-        self._uploads = []
 
     def zero_grad(self):
         for p in self.params:

@@ -86,11 +86,6 @@ def test_rccl_backend_one_rank_runs_the_reducer(dev, tmp_path):
     assert res["backend"] == "nccl"
     assert torch.equal(res["rccl"], res["plain"]), float((res["rccl"] - res["plain"]).abs().max())
     assert res["rccl_losses"] == res["plain_losses"]
-    # the same steps replayed from hipGraphs with the RCCL all-reduces captured
-    assert res["graph_replays"] == 2
-    assert torch.equal(res["rccl_graphed"], res["plain"]), \
-        float((res["rccl_graphed"] - res["plain"]).abs().max())
-    assert res["rccl_graphed_losses"] == res["plain_losses"]
     tl = res["timeline"]
     print("rccl timeline:", tl)
     assert tl is not None and tl["buckets"] == res["buckets"] >= 5

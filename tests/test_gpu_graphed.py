@@ -72,7 +72,10 @@ def test_graphed_trainer_rejects_other_batch_shape(dev):
     from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
     from detectron2_tensorflow_amd.utils.synthetic import synthetic_train_batch
     cfg, model = _model(dev)
-    tr = GraphedTrainer(cfg, model, warmup=0)
-    tr.step(synthetic_train_batch(2, 256, 320, 3, dev))
+    tr = GraphedTrainer(cfg, model, warmup=1)
+    b = synthetic_train_batch(2, 256, 320, 3, dev)
+    tr.step(b)  # eager warm-up
+    tr.step(b)  # capture + replay
+    assert tr.replays == 1
     with pytest.raises(ValueError, match="captured for"):
         tr.step(synthetic_train_batch(2, 256, 384, 3, dev))
