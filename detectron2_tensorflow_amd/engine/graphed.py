@@ -84,6 +84,10 @@ class GraphedTrainer(Trainer):
         self._stream = None
         self.captures = 0
         self.replays = 0
+        # a directory: every captured graph is written there as a DOT file
+        # (hipGraphDebugDotPrint; tools/graph_dump.py) -- a diagnosis that
+        # replays nothing
+        self.debug_dump_dir = None
 
     # ------------------------------------------------------------------ state
     def _mark_stale(self):
@@ -130,6 +134,18 @@ class GraphedTrainer(Trainer):
                 s.copy_(v, non_blocking=True)
 
     # ---------------------------------------------------------------- capture
+    def _new_graph(self):
+        g = torch.cuda.CUDAGraph()
+        if self.debug_dump_dir:
+            g.enable_debug_mode()
+        return g
+
+    def _dump(self, g, name):
+        if self.debug_dump_dir:
+            import os
+            os.makedirs(self.debug_dump_dir, exist_ok=True)
+            g.debug_dump(os.path.join(self.debug_dump_dir, f"graph_{name}.dot"))
+
     def _capture_forward(self, batched_inputs):
         self._static = _clone_tree(batched_inputs)
         self._leaves = _flatten(self._static)
@@ -144,10 +160,11 @@ class GraphedTrainer(Trainer):
         self._mark_stale()
         torch.cuda.synchronize(dev)
         self._pool = torch.cuda.graph_pool_handle()
-        g = torch.cuda.CUDAGraph()
+        g = self._new_graph()
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             losses = self.model(self._static)
+        self._dump(g, "A")
         self._keep = []
         capture.flush(self._keep)
         deferred = [v for v in losses.values() if isinstance(v, DeferredMaskLoss)]
@@ -167,7 +184,7 @@ class GraphedTrainer(Trainer):
         """Graph B[rows]: mask branch, total loss, backward, update."""
         self.optimizer.zero_grad()
         keep = []
-        g = torch.cuda.CUDAGraph()
+        g = self._new_graph()
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             out = {k: (v.compute(rows) if isinstance(v, DeferredMaskLoss) else v)
@@ -183,6 +200,7 @@ class GraphedTrainer(Trainer):
             self.optimizer.step_captured(self._lr_dev)
             values = torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()])
         capture.flush(keep)
+        self._dump(g, f"B{rows}")
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
         self._B[rows] = (g, values, keys, keep)

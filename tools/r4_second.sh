@@ -6,7 +6,7 @@
 # the chain (a test assertion, rc 1, does not).
 set -o pipefail
 mkdir -p gpurun_out
-step() { local ok=$1 t=$2 name=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/${TAG:-r4b}_$name.log 2>&1; local rc=$?; tail -3 gpurun_out/r4b_$name.log; if [ $rc -ne 0 ] && [ $rc -ne $ok ]; then echo "$name rc=$rc: stopping"; exit $rc; fi; }
+step() { local ok=$1 t=$2 name=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/${TAG:-r4b}_$name.log 2>&1; local rc=$?; tail -3 gpurun_out/${TAG:-r4b}_$name.log; if [ $rc -ne 0 ] && [ $rc -ne $ok ]; then echo "$name rc=$rc: stopping"; exit $rc; fi; }
 step 1 500 newtests python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_graphed.py "tests/test_gpu_dp.py::test_rccl_backend_one_rank_runs_the_reducer" -k "graphed or rccl"
 step 1 400 nms python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_ops.py tests/test_gpu_geometry.py -k "nms or fast_rcnn or proposals or rpn"
 step 1 400 retina python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_retinanet.py -k "training or fused_loss"
