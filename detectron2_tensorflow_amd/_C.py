@@ -240,6 +240,12 @@ def workspace(nbytes, device):
 
 
 _scratch = {}
+# every scratch buffer ever handed out stays allocated: a launch captured into
+# a hipGraph keeps its buffer's address, so a buffer outgrown later (a larger
+# request, e.g. a graph of a larger mask-branch row count) must not be freed
+# -- torch.cuda.graph's empty_cache() would return it to the driver and the
+# earlier graphs' replays would fault on it
+_scratch_outgrown = []
 
 
 def scratch(nbytes, device):
@@ -254,14 +260,17 @@ def scratch(nbytes, device):
     buf = _scratch.get(key)
     n = max(int(nbytes), 1)
     if buf is None or buf.numel() < n:
-        buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=torch.device("cuda", idx))
+        if buf is not None:
+            _scratch_outgrown.append(buf)
+        # (grown geometrically: few outgrown buffers)
+        size = max(n, 1 << 20, 2 * buf.numel() if buf is not None else 0)
+        buf = torch.empty(size, dtype=torch.uint8, device=torch.device("cuda", idx))
         _scratch[key] = buf
     return buf
 
 
 _ERR_BITS = {1: "box index out of range", 2: "NMS candidate capacity exceeded",
-             4: "top-k candidate capacity exceeded",
-             8: "cooperative split-K conv: a tile's workgroups were not co-resident (timeout)"}
+             4: "top-k candidate capacity exceeded"}
 
 
 def error_word(device=None):

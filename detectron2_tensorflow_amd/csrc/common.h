@@ -39,7 +39,6 @@ enum ErrorBits : int32_t {
   kErrBoxInd = 1,
   kErrNmsCapacity = 2,
   kErrTopkCapacity = 4,
-  kErrCoopTimeout = 8,  // a cooperative split-K tile waited too long for its peers
 };
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

@@ -138,12 +138,6 @@ struct ConvArgs {
   int tdH, tdW;
   int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
   int xcd2;  // xcd_tile(): the 2-D XCD-contiguous remap (tuning conv_xcd, default 1)
-  // Cooperative split-K (splitk_coop, tuning conv_coop): per-tile arrival and
-  // departure counters of the stream's pool (zero between launches); null:
-  // the separate splitk_reduce4_kernel launch
-  unsigned* tile_cnt;
-  unsigned* tile_done;
-  int32_t* err;
   // Multi-level launch (d2mi_conv2d_nhwc_levels): nlev > 0 levels share the
   // weights; level l owns tiles [lv_tile0[l], lv_tile0[l + 1]) and its own
   // input / output / gate maps.  The kernel swaps them into the fields above
@@ -341,77 +335,6 @@ __device__ __forceinline__ void store_partial(const ConvArgs& a, const Geo& g,
       }
     }
   }
-}
-
-// Cooperative split-K fix-up (ConvArgs::tile_cnt).  Every workgroup of a
-// split tile has stored its raw partial slab; the S workgroups of the tile
-// meet at its arrival counter (all S are resident at once: the host plans
-// this only when the whole grid fits one round of resident workgroups), then
-// each sums its share of the tile's rows over the S slabs in split order
-// 0..S-1 -- splitk_reduce4_kernel's order, so the outputs are bit-identical
-// -- and applies the epilogue.  No reduce launch, and the reduction spread
-// over the tile's own S workgroups (r3's last-arriver form made one
-// workgroup sum all S slabs alone: 6 % slower in the step).  Agent-scope
-// release before the arrival, acquire after the wait: the slabs of other
-// XCDs' workgroups are visible.  The wait is bounded: a co-residency failure
-// raises kErrCoopTimeout in the device error word instead of hanging the GPU.
-// The departure counter puts both counters back to zero for the next launch
-// on this stream.  All NT threads call it; lds: >= 4 bytes of the kernel's LDS.
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void splitk_coop(const ConvArgs& a, const Geo& g, int tile, int split,
-                                            int m0, int n0, float* lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(a.tile_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    while (__hip_atomic_load(a.tile_cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           (unsigned)a.splits) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins == (1u << 24)) {
-        atomicOr(a.err, kErrCoopTimeout);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  constexpr int F4 = BN / 4;
-  const int rows = (BM + a.splits - 1) / a.splits;
-  const int r0 = split * rows, r1 = min(BM, r0 + rows);
-  const float4* p4 = reinterpret_cast<const float4*>(a.partial);
-  const size_t slab4 = (size_t)g.pstride * a.Cout / 4;
-  for (int idx = threadIdx.x; idx < (r1 - r0) * F4; idx += NT) {
-    const int r = r0 + idx / F4, c4 = idx - (idx / F4) * F4;
-    const int m = m0 + r, co = n0 + 4 * c4;
-    if (m >= g.M || co >= a.Cout) continue;
-    const size_t off = ((size_t)(m - g.prow0) * a.Cout + co) / 4;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < a.splits; ++s) {
-      const float4 v = p4[(size_t)s * slab4 + off];
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
-    }
-    float4 o;
-    o.x = epilogue(a, g, acc.x, m, co);
-    o.y = epilogue(a, g, acc.y, m, co + 1);
-    o.z = epilogue(a, g, acc.z, m, co + 2);
-    o.w = epilogue(a, g, acc.w, m, co + 3);
-    *reinterpret_cast<float4*>(g.y + (size_t)m * a.Cout + co) = o;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned d = __hip_atomic_fetch_add(a.tile_done + tile, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (unsigned)a.splits - 1) {  // the last one out: every peer is past the wait
-      __hip_atomic_store(a.tile_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.tile_done + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  (void)lds;
 }
 
 // LDS-staged epilogue (ConvArgs::lds_epi): the accumulators leave through
@@ -814,9 +737,6 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
   // none of its barriers) unless tuning conv_epi = 0
   if (a.splits > 1 && a.reg_partials) {
     store_outputs<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, true);
-    if constexpr (!ML) {
-      if (a.tile_cnt) splitk_coop<BM, BN, 256>(a, g, tile, split, m0, n0, &As[0][0]);
-    }
   } else if (WN * TN * 32 == 128 || a.lds_epi)  // 128-wide tiles: planned only with lds_epi
     store_outputs_lds<WM, WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
                                       &As[0][0]);
@@ -1086,7 +1006,6 @@ __global__ __launch_bounds__(1024, 1) void conv_ws_kernel(ConvArgs a) {
   if constexpr ((kAblate & 8) != 0) return;  // (ablation: no epilogue)
   if (a.splits > 1 && a.reg_partials) {  // partial slabs straight from the accumulators
     if (wave < 8) store_partial<WN, TM, TN>(a, g, acc, m0, n0, wr, wc, lane, split);
-    if (a.tile_cnt) splitk_coop<BM, BN, 1024>(a, g, tile, split, m0, n0, smem);
     return;
   }
   store_outputs_lds<WM, WN, TM, TN, 1024>(a, g, acc, m0, n0, wr, wc, lane, split, a.splits > 1,
@@ -1253,35 +1172,6 @@ struct Plan {
   int main_m_end;  // output rows of the main launch (its split-K partial rows)
   size_t ws_bytes;
 };
-
-// Tile counters of the cooperative split-K (splitk_coop): one pool of
-// arrival + departure counters per (device, stream), zeroed by a
-// stream-ordered memset when it is made.  Launches on one stream never
-// overlap and each leaves its counters zero, so one pool serves every launch
-// on its stream.  Null (allocation failed): the separate reduce launch.
-constexpr int kCoopCounters = 1 << 16;
-static unsigned* coop_counters(hipStream_t st) {
-  struct Pool {
-    int dev;
-    hipStream_t st;
-    unsigned* p;
-  };
-  static std::mutex mu;
-  static std::vector<Pool> pools;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const Pool& e : pools)
-    if (e.dev == dev && e.st == st) return e.p;
-  unsigned* p = nullptr;
-  if (hipMalloc(&p, 2 * kCoopCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(p, 0, 2 * kCoopCounters * sizeof(unsigned), st) != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
-  }
-  pools.push_back(Pool{dev, st, p});
-  return p;
-}
 
 // Resident workgroups of the 128-wide conv tiles: 2 per CU.
 // Resident workgroups per CU of a plan's kernel: the 128x128 split kernel
@@ -1581,27 +1471,14 @@ static int conv_core(const float* x, const float* w_packed, const float* bias,
   // tile, agent-scope release / acquire): bit-identical but 6 % slower in the
   // step -- one workgroup reads its tile's 64-128 KiB slabs at ~100 GB/s --
   // and r4 removed it.
-  // tuning conv_coop: the split tiles reduce cooperatively inside the conv
-  // launch (splitk_coop) -- only when every workgroup of the grid is resident
-  // at once (the plan's split target is one round: CUs for the WS kernel,
-  // 2 per CU for the others) and the float4 epilogue applies
-  const bool coop_ok = tuning(kTuneConvCoop) > 0 && a.reg_partials && Cout % 4 == 0 &&
-                       ((uintptr_t)y & 15) == 0 && ((uintptr_t)workspace & 15) == 0 &&
-                       a.nM * a.nN <= kCoopCounters;
-  unsigned* const coop = coop_ok ? coop_counters(st) : nullptr;
-  auto launch = [&](ConvArgs c) {
+  auto launch = [&](const ConvArgs& c) {
     const dim3 g(c.ntiles, c.splits);
-    const long long resident = (long long)wg_slots(p.cfg == 3 ? 3 : 1);
-    const bool cooperative = coop && c.splits > 1 && (long long)c.ntiles * c.splits <= resident;
-    c.tile_cnt = cooperative ? coop : nullptr;
-    c.tile_done = cooperative ? coop + kCoopCounters : nullptr;
-    c.err = error_word();
     if (flags & kSplit3)
       launch_conv<true>(p.cfg, db, g, st, c);
     else
       launch_conv<false>(p.cfg, db, g, st, c);
     D2MI_LAUNCH_CHECK();
-    if (c.splits > 1 && !cooperative) {
+    if (c.splits > 1) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
       if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
         const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);

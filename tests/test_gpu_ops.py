@@ -1460,46 +1460,3 @@ def test_fused_subsample_pairwise_co_inclusion(dev):
     assert np.all(np.abs(off - p2) < 5 * sd), (off.min(), off.max(), p2)
     near = np.array([co[i, i + 1] for i in range(n - 1)])
     assert abs(near.mean() - p2) < 5 * sd / math.sqrt(n - 1) + 1e-3, (near.mean(), p2)
-
-
-@pytest.mark.parametrize("shape,form", [
-    ((2, 25, 42, 512, 512, 3), ""),      # res5 3x3: WS kernel, 36 tiles x 7 splits
-    ((2, 50, 84, 256, 256, 3), "gf"),    # res4 3x3 dgrad: WS, 3 splits, flipped taps + gate
-    ((2, 50, 84, 1024, 256, 1), "r"),    # 1x1 1024 -> 256, residual + ReLU
-    ((1, 20, 30, 128, 128, 3), "t"),     # the 128x128 kernel's split-K, top-down add
-    ((2, 200, 336, 256, 256, 3), ""),    # FPN p2 3x3: full rounds + the tail split launch
-])
-def test_conv2d_cooperative_split_k_bit_identical(dev, shape, form):
-    """Tuning conv_coop: a split tile's workgroups meet at a per-tile counter
-    inside the conv launch and reduce their partial slabs cooperatively
-    (csrc/conv_mfma.hip splitk_coop) -- the separate reduce launch's split
-    order, so the outputs are bit-identical, with every epilogue form; three
-    launches in a row (the counters are left zero) and no device error
-    (co-residency held)."""
-    N, H, W, Cin, Cout, k = shape
-    pad = (k - 1) // 2
-    g = torch.Generator().manual_seed(31 + sum(shape))
-    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
-    w = (torch.randn(k, k, Cin, Cout, generator=g) / math.sqrt(k * k * Cin)).to(dev)
-    b = torch.randn(Cout, generator=g).to(dev)
-    kw = dict(math_mode="split", flip_taps="f" in form)
-    if "r" in form:
-        kw.update(residual=torch.randn(N, H, W, Cout, generator=g).to(dev), relu=True,
-                  relu_after_add=True)
-    if "g" in form:
-        kw.update(relu_gate=torch.randn(N, H, W, Cout, generator=g).to(dev))
-    if "t" in form:
-        kw.update(topdown=torch.randn(N, (H + 1) // 2, (W + 1) // 2, Cout, generator=g).to(dev))
-    wp = ops().pack_conv_weights(w)
-    run = lambda: ops().conv2d_nhwc(x, wp, b, 1, (pad, pad), **kw)  # noqa: E731
-    try:
-        ops().set_tuning("conv_coop", 0)
-        y0 = run()
-        ops().set_tuning("conv_coop", 1)
-        ys = [run() for _ in range(3)]
-    finally:
-        ops().set_tuning("conv_coop", 0)  # (the default)
-    from detectron2_tensorflow_amd import _C
-    _C.raise_on_errors(dev)
-    for y in ys:
-        assert torch.equal(y, y0), float((y - y0).abs().max())
