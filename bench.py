@@ -84,9 +84,6 @@ def parse():
     p.add_argument("--mask-format", default="conventional", choices=["conventional", "raw", "fixed"],
                    help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
-    p.add_argument("--graphs", type=int, default=0,
-                   help="train: replay the step from hipGraphs (engine/graphed.py; world size 1 "
-                        "-- other world sizes run the eager step); 0 = the eager Trainer.step")
     p.add_argument("--mask-fixed-rows", action="store_true",
                    help="train: the mask head on the fixed BATCH_SIZE_PER_IMAGE x "
                         "POSITIVE_FRACTION rows per image (128 at the defaults, "
@@ -569,15 +566,9 @@ def main():
         if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
             model.roi_heads.mask_compact_rows = False
             PMC_SKIP.update({"roi_align_fwd_mask", "roi_align_bwd"})
-        if args.graphs:
-            from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
-            trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
-        else:
-            trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
-        # the kernel-timing step (HIP events around every launch) runs eagerly:
-        # a replayed graph has no per-launch events
-        timed_step = (lambda: trainer.eager_step(batch)) if args.graphs else step
+        timed_step = step
         grad_ctx = torch.enable_grad
     else:
         fwd = model if is_single_stage(model) else model.inference
@@ -677,10 +668,7 @@ def main():
                                if args.mode == "train" else {}),
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
                             else f"{sample + 1}/{args.steps}",
-                            **({"step_launch": (f"hipGraph replays ({trainer.replays} in warmup + "
-                                                "timed; the kernel-timing step eager)")
-                                if getattr(trainer, "enabled", False) else "eager"}
-                               if args.mode == "train" else {}),
+
                             **({"mask_format": args.mask_format} if args.mode == "infer" else {})},
                        **extra),
             # the dominant hot-path kernel: the split-product conv (else f32)

@@ -1,4 +1,7 @@
-"""The data-parallel training step replayed from hipGraphs (lib/engine/trainer.py:116-199).
+"""EXPERIMENTAL (r4, not used by bench.py or the tests): the training step
+replayed from hipGraphs (lib/engine/trainer.py:116-199).  Status: graph A
+replays bit-exactly (tools/graph_bisect.py stages 0-8); the first replay of a
+backward graph B[R] faulted the GPU (twice, r4) and the cause is not found.
 
 The eager ``Trainer.step`` enqueues ~550 launches per iteration from Python
 (autograd engine, custom Functions, ctypes): on an MI355X that host work is
@@ -60,7 +63,13 @@ class GraphedTrainer(Trainer):
     allocator, workspaces, per-shape caches).  Falls back to the eager step when the
     process group has more than one rank."""
 
-    def __init__(self, cfg, model, warmup=1, **kwargs):
+    def __init__(self, cfg, model, warmup=1, experimental=False, **kwargs):
+        if not experimental:
+            raise RuntimeError(
+                "GraphedTrainer is experimental (r4): graph A (the forward) replays bit-exactly "
+                "stage by stage (tools/graph_bisect.py), but replaying a backward graph B[R] "
+                "faulted the GPU on its first replay and the cause is not found; pass "
+                "experimental=True only for that diagnosis")
         super().__init__(cfg, model, **kwargs)
         # >= 1: the first eager step makes the per-shape caches, workspaces and
         # the optimizer / fold tables, none of which may be created in a capture

@@ -51,7 +51,7 @@ def main():
     cfg, model = bench.build(args, dev)
     batch = bench.synthetic_batch(args, dev, 0)
     bench.calibrate_scores(model, batch)
-    tr = GraphedTrainer(cfg, model)
+    tr = GraphedTrainer(cfg, model, experimental=True)
     tr.debug_dump_dir = a.out
     tr.step(batch)  # eager warm-up
     torch.cuda.synchronize()

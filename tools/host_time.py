@@ -9,7 +9,7 @@ foreground count), waiting for the device to catch up; host_busy_ms =
 host_ms - blocked: the host's own enqueue work.  host_busy close to wall_ms
 means the step is launch-bound, not kernel-bound.
 
-usage: python tools/host_time.py [--mode train|infer] [--steps 5] [--graphs 0|1]
+usage: python tools/host_time.py [--mode train|infer] [--steps 5]
 """
 import argparse
 import os
@@ -26,8 +26,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="train")
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--graphs", type=int, default=0,
-                    help="train: the hipGraph-replayed step (engine/graphed.py), as bench.py; 0 = eager")
     ap.add_argument("--cprofile", type=int, default=0,
                     help="also cProfile this many steps and print the top host functions")
     a = ap.parse_args()
@@ -43,8 +41,7 @@ def main():
     bench.calibrate_scores(model, batch)
     if a.mode == "train":
         from detectron2_tensorflow_amd.engine import Trainer
-        from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
-        tr = GraphedTrainer(cfg, model) if a.graphs else Trainer(cfg, model)
+        tr = Trainer(cfg, model)
         step = lambda: tr.step(batch)
         ctx = torch.enable_grad
     else:

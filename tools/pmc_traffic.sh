@@ -14,7 +14,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   out=gpurun_out/pmc_${tag}_$c
   rm -rf "$out"
   timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$out" -o run \
-      -- python3 bench.py --cpu-baseline 0 --no-kernel-timing --graphs 0 "$@" > "$out.log" 2>&1
+      -- python3 bench.py --cpu-baseline 0 --no-kernel-timing "$@" > "$out.log" 2>&1
 done
 python3 tools/pmc_summarize.py gpurun_out/pmc_${tag}_FETCH_SIZE gpurun_out/pmc_${tag}_WRITE_SIZE \
     gpurun_out/${tag}_pmc.json

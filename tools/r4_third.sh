@@ -8,7 +8,7 @@ set -o pipefail
 mkdir -p gpurun_out
 T=${TAG:-r4d}
 step() { local ok=$1 t=$2 name=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > gpurun_out/${T}_$name.log 2>&1; local rc=$?; tail -3 gpurun_out/${T}_$name.log; if [ $rc -ne 0 ] && [ $rc -ne $ok ]; then echo "$name rc=$rc: stopping"; exit $rc; fi; }
-step 0 300 dump python3 -u tools/graph_dump.py --out gpurun_out/${T}_graphs
+
 step 1 500 roi python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_ops.py tests/test_gpu_train.py -k "roi or deferred or whole_training"
 step 0 300 bench python3 -u bench.py --cpu-baseline 0
 step 0 300 ab_coop python3 -u tools/ab_inproc.py --switch tune:conv_coop=1,0 --blocks 6
