@@ -98,98 +98,54 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    lo |= (uint32_t)__shfl_xor((int)lo, o, 64);
-    hi |= (uint32_t)__shfl_xor((int)hi, o, 64);
-  }
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// One workgroup of four waves per segment, one 64-row tile per iteration and
-// ONE barrier per tile, with no memory latency on the resolver's path:
-// * wave 0 resolves tile t serially (its diagonal words in registers,
-//   v_readlane), from removed[t] (LDS: the kept rows of tiles <= t - 2) OR
-//   carry (the kept rows of tile t - 1, folded by wave 0 itself from the
-//   words of column t it loaded one tile ahead); it then folds tile t's kept
-//   rows' column-(t + 1) words into the next carry (a wave OR) and publishes
-//   tile t's kept mask;
-// * waves 1-3 propagate tile t - 1's kept rows into the removal words of
-//   tiles >= t + 1 (LDS atomic OR, order-free: exact) from words they loaded
-//   during the previous iteration, then load tile t's rows for the next one.
-// The barrier is a raw s_barrier after the LDS traffic has drained, so the
-// global prefetches of both sides stay in flight across it (a __syncthreads
-// would wait for them).  Same greedy selection as TF's loop: the kept lists
-// are bit-identical.  (r3: resolve, then a propagation round trip, two
-// barriers per tile: 144 us per RPN training scan.)
+// One workgroup of four waves per segment; removed[] lives in LDS (T words).
+// Wave 0 resolves each 64-row tile serially (the diagonal words in scalar
+// registers via v_readlane); then all four waves propagate the kept rows
+// into the removal words of the later tiles, each wave a quarter of the rows
+// (16 mask loads in flight per lane: one round of load latency per tile
+// instead of four), combined with an LDS atomic OR (order-free: exact).
 constexpr int kScanWaves = 4;
-constexpr int kPropRows = 22;  // rows per propagation wave: 22 + 21 + 21
-
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 __global__ __launch_bounds__(64 * kScanWaves) void nms_scan_kernel(
     const uint64_t* __restrict__ mask, const int32_t* __restrict__ idx,
     const int32_t* __restrict__ count, int cap, int T, int max_out, int32_t* __restrict__ keep,
     int32_t* __restrict__ num_keep) {
   extern __shared__ uint64_t removed[];
-  __shared__ uint64_t s_keptm[2];
-  __shared__ int s_stop;
+  __shared__ uint64_t s_keptm;
   __shared__ int s_kept;
   const int s = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = count[s];
   const int nt = (n + 63) / 64;
   for (int t = threadIdx.x; t < nt; t += blockDim.x) removed[t] = 0;
-  if (threadIdx.x == 0) {
-    s_stop = max_out <= 0;
-    s_kept = 0;
-  }
   __syncthreads();
   const size_t base = (size_t)s * cap;
   int32_t* out = keep + (size_t)s * max_out;
-  const uint64_t* seg = mask + base * T;
-  // wave 0: tile t's diagonal word / output index / column-(t + 1) word per lane
   int kept = 0;
-  uint64_t diag = 0, nextc = 0, carry = 0;
-  int32_t myidx = 0;
-  if (wave == 0 && nt > 0 && lane < n) {
-    diag = seg[(size_t)lane * T];
-    myidx = idx[base + lane];
-    if (nt > 1) nextc = seg[(size_t)lane * T + 1];
+  constexpr int RW = 64 / kScanWaves;  // propagation rows per wave
+  const int r0 = wave * RW;
+  // wave 0 holds the next tile's diagonal words and output indices in flight
+  // while the current tile resolves and propagates (neither depends on
+  // removed[]).  (Issuing the propagation loads before the resolve too
+  // measured slower: 157 vs 144 us per RPN scan.)
+  uint64_t diag_next = 0;
+  int32_t idx_next = 0;
+  if (wave == 0 && nt > 0) {
+    diag_next = lane < n ? mask[(base + lane) * T] : 0ull;
+    idx_next = lane < n ? idx[base + lane] : 0;
   }
-  // waves 1-3: rows pr0 .. pr0 + npr - 1 of a tile, column (tile + 2 + lane)
-  const int pw = wave - 1;
-  const int pr0 = pw <= 0 ? 0 : (pw == 1 ? kPropRows : 2 * kPropRows - 1);
-  const int npr = pw <= 0 ? kPropRows : kPropRows - 1;
-  uint64_t v[kPropRows];
-  auto prop_load = [&](int tt) {
-    const int t2 = tt + 2 + lane;
-#pragma unroll
-    for (int r = 0; r < kPropRows; ++r) {
-      const int row = tt * 64 + pr0 + r;
-      v[r] = (r < npr && t2 < nt && row < n) ? seg[(size_t)row * T + t2] : 0ull;
-    }
-  };
-  if (wave > 0 && nt > 2) prop_load(0);
-  for (int t = 0; t < nt; ++t) {
+  for (int t = 0; t < nt && kept < max_out; ++t) {
+    const int t2a = t + 1 + lane;  // this lane's first later tile
     if (wave == 0) {
-      uint64_t diag_n = 0, nextc_n = 0;
-      int32_t idx_n = 0;
-      const int nrow = (t + 1) * 64 + lane;
-      if (t + 1 < nt && nrow < n) {  // tile t + 1, loaded under this tile's resolve
-        diag_n = seg[(size_t)nrow * T + t + 1];
-        idx_n = idx[base + nrow];
-        if (t + 2 < nt) nextc_n = seg[(size_t)nrow * T + t + 2];
+      const int row = t * 64 + lane;
+      const uint64_t diag = diag_next;
+      const int32_t my_idx = idx_next;
+      if (t + 1 < nt) {
+        const int nrow = row + 64;
+        diag_next = nrow < n ? mask[(base + nrow) * T + t + 1] : 0ull;
+        idx_next = nrow < n ? idx[base + nrow] : 0;
       }
-      uint64_t w = removed[t] | carry;
       const int rem = n - t * 64;
+      uint64_t w = removed[t];
       if (rem < 64) w |= ~((1ull << rem) - 1ull);
       uint64_t keptm = 0;
       for (int r = 0; r < 64; ++r) {
@@ -202,43 +158,34 @@ __global__ __launch_bounds__(64 * kScanWaves) void nms_scan_kernel(
       }
       if ((keptm >> lane) & 1ull) {
         const int pos = (kept - __popcll(keptm)) + __popcll(keptm & ((1ull << lane) - 1ull));
-        out[pos] = myidx;
+        out[pos] = my_idx;
       }
-      carry = wave_or64(((keptm >> lane) & 1ull) ? nextc : 0ull);
       if (lane == 0) {
-        s_keptm[t & 1] = keptm;
-        if (kept >= max_out) s_stop = 1;
+        s_keptm = keptm;
         s_kept = kept;
       }
-      diag = diag_n;
-      nextc = nextc_n;
-      myidx = idx_n;
-    } else if (t >= 1) {
-      // tile t - 1's kept rows -> removal words of tiles >= t + 1
-      const uint64_t mine = (s_keptm[(t - 1) & 1] >> pr0) & ((1ull << npr) - 1ull);
-      if (mine) {
+    }
+    __syncthreads();
+    const uint64_t keptm = s_keptm;
+    kept = s_kept;
+    if (kept >= max_out) break;  // uniform: every wave read the same s_kept
+    // propagate the kept rows of tile t (not the last, so all 64 rows exist)
+    // into the removal words of the later tiles: wave v takes rows 16v..16v+15
+    if ((keptm >> r0) & ((1ull << RW) - 1ull)) {
+      for (int t2 = t2a; t2 < nt; t2 += 64) {
+        const uint64_t* col = mask + (base + (size_t)t * 64 + r0) * T + t2;
+        uint64_t v[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) v[r] = col[(size_t)r * T];
         uint64_t acc = 0;
 #pragma unroll
-        for (int r = 0; r < kPropRows; ++r) acc |= ((mine >> r) & 1ull) ? v[r] : 0ull;
-        if (acc && t + 1 + lane < nt)
-          atomicOr(reinterpret_cast<unsigned long long*>(&removed[t + 1 + lane]),
-                   (unsigned long long)acc);
-        // segments of more than 65 tiles: the columns past the first 64, loaded here
-        for (int t2 = t + 65 + lane; t2 < nt; t2 += 64) {
-          uint64_t a2 = 0;
-          for (int r = 0; r < npr; ++r)
-            if ((mine >> r) & 1ull) a2 |= seg[(size_t)((t - 1) * 64 + pr0 + r) * T + t2];
-          if (a2) atomicOr(reinterpret_cast<unsigned long long*>(&removed[t2]),
-                           (unsigned long long)a2);
-        }
+        for (int r = 0; r < RW; ++r) acc |= ((keptm >> (r0 + r)) & 1ull) ? v[r] : 0ull;
+        if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&removed[t2]),
+                          (unsigned long long)acc);
       }
     }
-    if (wave > 0 && t + 2 < nt) prop_load(t);  // for the next iteration
-    lds_barrier();
-    if (s_stop) break;  // uniform: written by wave 0 before the barrier
+    __syncthreads();
   }
-  __syncthreads();
-  kept = s_kept;
   for (int i = kept + (int)threadIdx.x; i < max_out; i += blockDim.x) out[i] = -1;
   if (threadIdx.x == 0) num_keep[s] = kept;
 }

@@ -1199,14 +1199,16 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   // touched counts stay on the device): at most 8192 workgroups x 4 waves =
   // 32 waves per SIMD over 256 CUs x 4 SIMDs; waves beyond residency start
   // as earlier ones retire (the kBatch sweep above)
+  // (tuning roi_pix_grid: the workgroup cap; the waves grid-stride)
   const long long cap = p.pm.tbase[lv_hi + 1] - p.pm.tbase[lv_lo];
-  const dim3 grid((unsigned)std::max(1LL, std::min((cap + 3) / 4, 8192LL)));
+  const long long wg_max = std::max(1, tuning(kTuneRoiPixGrid));
+  const dim3 grid((unsigned)std::max(1LL, std::min((cap + 3) / 4, wg_max)));
   if (vec4 && C == 256) {
     static const int ppw = [] {
       const char* e = getenv("D2MI_ROI_BWD_PPW");
       return e && e[0] == '8' ? 8 : 4;
     }();
-    const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), 8192LL)));
+    const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), wg_max)));
     if (ppw == 8)
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
                          sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);

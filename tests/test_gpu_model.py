@@ -203,8 +203,11 @@ def test_faster_rcnn_c2_1333x800_vs_oracle_on_its_own_heads(dev):
     RPN-head outputs over all 268,569 anchors per image: scores and valid
     flags bit-exact, boxes within max(1e-4, 2 ulp); (3) the detections equal
     the oracle's fast_rcnn_inference (fast_rcnn.py:28-187) on the model's
-    OWN box-head outputs and proposals: classes, kept ROI rows and valid
-    flags bit-exact, scores within 2e-6 relative, boxes within max(1e-4, 2 ulp)."""
+    OWN box-head outputs and proposals: valid flags bit-exact, scores within
+    2e-6 relative, classes bit-exact and boxes within max(1e-4, 2 ulp) --
+    position by position, except among detections whose oracle scores tie
+    within that tolerance (compared as sets: their order follows ulp-level
+    softmax differences)."""
     import oracle
     from test_gpu_ops import assert_boxes_close
     from detectron2_tensorflow_amd.utils.synthetic import calibrate_rcnn_scores, synthetic_images
@@ -271,7 +274,22 @@ def test_faster_rcnn_c2_1333x800_vs_oracle_on_its_own_heads(dev):
     for n in range(N):
         wbx, wsc, wc, wvd, wroi = want[n]
         np.testing.assert_array_equal(h["is_valid"][n], wvd)
-        np.testing.assert_array_equal(h["classes"][n], wc)
         np.testing.assert_allclose(h["scores"][n], wsc, rtol=2e-6, atol=1e-7)
-        assert_boxes_close(h["boxes"][n], wbx)
-        assert int(wvd.sum()) >= 20  # a realistic survivor count (score injection)
+        k = int(wvd.sum())
+        # detections whose oracle scores lie within the score tolerance of each
+        # other form a tie group: their order follows ulp-level softmax
+        # differences (ocml vs libm expf), so each group is compared as a set
+        # of (class, box); everything else position by position
+        g0 = 0
+        for i in range(1, k + 1):
+            if i < k and wsc[g0] - wsc[i] <= 1e-7 + 2e-6 * abs(wsc[g0]):
+                continue
+            key = lambda c, b: np.lexsort((b[:, 3], b[:, 2], b[:, 1], b[:, 0], c))  # noqa: E731
+            gc, gb = h["classes"][n][g0:i], h["boxes"][n][g0:i]
+            oc, ob = wc[g0:i], wbx[g0:i]
+            og, oo = key(gc, np.round(gb, 2)), key(oc, np.round(ob, 2))
+            np.testing.assert_array_equal(gc[og], oc[oo])
+            assert_boxes_close(gb[og], ob[oo])
+            g0 = i
+        assert_boxes_close(h["boxes"][n][k:], wbx[k:])
+        assert k >= 20  # a realistic survivor count (score injection)
