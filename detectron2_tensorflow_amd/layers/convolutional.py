@@ -472,15 +472,25 @@ class Conv2D(Layer):
         return (x.is_cuda and self.num_groups == 1 and self.rate == 1
                 and (padded or self.in_channels % 4 == 0))
 
+    def _key_tensors(self):
+        """(weights, the other tensors the fold reads), looked up once (the
+        module attribute lookups are host time on every conv call)."""
+        kt = self.__dict__.get("_key_ts")
+        w = self.weights
+        # (re-looked up when the weights move: .to() / .cuda() also replace
+        # the normalizer's buffers)
+        if kt is None or kt[0] is not w or kt[2] != w.data_ptr():
+            rest = [self.bias] if self.bias is not None else []
+            if isinstance(self.normalizer_fn, BatchNorm):
+                n = self.normalizer_fn
+                rest += [t for t in (n.gamma, n.beta, n.moving_mean, n.moving_variance)
+                         if t is not None]
+            kt = self.__dict__["_key_ts"] = (w, tuple(rest), w.data_ptr())
+        return kt
+
     def _param_key(self):
-        key = [self.weights.data_ptr(), self.weights._version]
-        if self.bias is not None:
-            key.append(self.bias._version)
-        if isinstance(self.normalizer_fn, BatchNorm):
-            n = self.normalizer_fn
-            key += [t._version for t in (n.gamma, n.beta, n.moving_mean, n.moving_variance)
-                    if t is not None]
-        return tuple(key)
+        w, rest, _ = self._key_tensors()
+        return (w.data_ptr(), w._version) + tuple(t._version for t in rest)
 
     def _pack_key(self, w):
         return self._param_key() + (tuple(w.shape),)
@@ -515,9 +525,11 @@ class Conv2D(Layer):
 
     def fold_trainable(self):
         norm = self.normalizer_fn
-        ts = [self.weights, self.bias] + ([norm.gamma, norm.beta] if isinstance(norm, BatchNorm)
-                                          else [])
-        return any(t is not None and t.requires_grad for t in ts)
+        if self.weights.requires_grad or (self.bias is not None and self.bias.requires_grad):
+            return True
+        if isinstance(norm, BatchNorm):
+            return any(t is not None and t.requires_grad for t in (norm.gamma, norm.beta))
+        return False
 
     def wants_packed(self):
         return (self.impl in ("mfma", "auto") and self.num_groups == 1 and self.rate == 1

@@ -1308,16 +1308,67 @@ def _addr(t):
     return 0 if t is None else t.data_ptr()
 
 
+def _sole_owner(t):
+    """True when no tensor but ``t`` itself uses t's storage (no live view)."""
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2
+
+
+class _FoldPlan:
+    """The forward fold of one set of layers, kept across training steps: the
+    parameters are updated in place (same addresses every step), so the
+    entry table and the three flat output buffers are reused -- one launch
+    over a table already on the device, no host table rebuild or upload --
+    whenever none of last step's output views is still alive (the previous
+    step's graph is gone)."""
+
+    def __init__(self, flats, tab, fwd, shapes, dev):
+        self.flats, self.tab, self.fwd, self.shapes = flats, tab, fwd, shapes
+        self.dev_tab = torch.empty(tab.nbytes, dtype=torch.uint8, device=dev)
+        self.dev_tab.copy_(torch.from_numpy(tab.view(np.uint8)))
+
+    def reusable(self):
+        return all(_sole_owner(f) for f in self.flats)
+
+    def views(self):
+        sizes, couts, psz, shapes = self.shapes
+        w_effs = self.flats[0].split(sizes)
+        b_effs = self.flats[1].split(couts)
+        packs = self.flats[2].split(psz)
+        outs = []
+        for i, (KH, KW, Cin, Cout) in enumerate(shapes):
+            outs += [w_effs[i].view(KH, KW, Cin, Cout), b_effs[i],
+                     packs[i].view(KH, KW, Cout, Cin) if psz[i] else None]
+        return outs
+
+
+_fold_plans = {}
+
+
 class _FoldManyFn(torch.autograd.Function):
     """Every BN-conv of the network folded at once: d2mi_fold_frozen_bn_many
     (one launch) forward, d2mi_fold_frozen_bn_bwd_many (two launches)
     backward.  inputs: per entry (w, bias, gamma, beta, mean, var); outputs:
-    per entry (w_eff, b_eff, packed-or-None)."""
+    per entry (w_eff, b_eff, packed-or-None).  Repeated folds of the same
+    parameters run from a _FoldPlan."""
 
     @staticmethod
     def forward(ctx, spec, *ts):
         n = len(spec)
         dev = ts[0].device
+        key = (spec, dev, tuple(_addr(t) for t in ts), tuple(ts[6 * i].shape for i in range(n)))
+        plan = None if capture.capturing() else _fold_plans.get(key)
+        if plan is not None and plan.reusable():
+            outs = plan.views()
+            for i in range(n):
+                if outs[3 * i + 2] is not None:
+                    ctx.mark_non_differentiable(outs[3 * i + 2])
+            rc = _C.lib().d2mi_fold_frozen_bn_many(_C.ptr(plan.dev_tab), n, plan.fwd,
+                                                   _C.stream_of(dev))
+            _C.check(rc, "d2mi_fold_frozen_bn_many")
+            ctx.save_for_backward(*ts)
+            ctx.tab, ctx.sizes = plan.tab, plan.bwd_sizes
+            ctx.set_materialize_grads(False)
+            return tuple(outs)
         rows, outs = [], []
         fwd = bwd = cob = part = 0
         table, chunks = _fold_table("fwd", n, dev)
@@ -1328,10 +1379,14 @@ class _FoldManyFn(torch.autograd.Function):
         # the outputs are views of three flat buffers (3 allocations, not 3n)
         sizes = [w.numel() for w in ws_]
         couts = [w.shape[3] for w in ws_]
-        w_effs = torch.empty(sum(sizes), dtype=torch.float32, device=dev).split(sizes)
-        b_effs = torch.empty(sum(couts), dtype=torch.float32, device=dev).split(couts)
+        flats = (torch.empty(sum(sizes), dtype=torch.float32, device=dev),
+                 torch.empty(sum(couts), dtype=torch.float32, device=dev),
+                 torch.empty(max(sum(sz if sp[1] else 0 for sz, sp in zip(sizes, spec)), 1),
+                             dtype=torch.float32, device=dev))
+        w_effs = flats[0].split(sizes)
+        b_effs = flats[1].split(couts)
         psz = [sz if sp[1] else 0 for sz, sp in zip(sizes, spec)]
-        packs = torch.empty(max(sum(psz), 1), dtype=torch.float32, device=dev).split(psz)
+        packs = flats[2].split(psz)
         for i, (eps, want_packed) in enumerate(spec):
             w, bias, gamma, beta, mean, var = ts[6 * i:6 * i + 6]
             KH, KW, Cin, Cout = w.shape
@@ -1353,6 +1408,13 @@ class _FoldManyFn(torch.autograd.Function):
         rc = _C.lib().d2mi_fold_frozen_bn_many(_C.ptr(table.upload(tab)), n, fwd,
                                                _C.stream_of(dev))
         _C.check(rc, "d2mi_fold_frozen_bn_many")
+        if not capture.capturing():
+            if len(_fold_plans) > 16:
+                _fold_plans.clear()
+            plan = _FoldPlan(flats, tab.copy(), fwd,
+                             (sizes, couts, psz, [tuple(w.shape) for w in ws_]), dev)
+            plan.bwd_sizes = (bwd, cob, part)
+            _fold_plans[key] = plan
         ctx.save_for_backward(*ts)
         ctx.tab, ctx.sizes = tab, (bwd, cob, part)
         ctx.set_materialize_grads(False)
@@ -1368,6 +1430,7 @@ class _FoldManyFn(torch.autograd.Function):
         bwd, cob, part = ctx.sizes
         ret = [None]
         keep = []
+        cols = [[0] * n for _ in range(6)]  # gw_eff gb_eff gw gbias ggamma gbeta
         for i in range(n):
             w, bias, gamma, beta = ts[6 * i:6 * i + 4]
             gw_eff, gb_eff = grads[3 * i], grads[3 * i + 1]
@@ -1376,17 +1439,19 @@ class _FoldManyFn(torch.autograd.Function):
             if gb_eff is not None:
                 gb_eff = _f32c(gb_eff)
             keep += [gw_eff, gb_eff]
-            Cout = w.shape[-1]
-            mk = lambda cond, t: torch.empty_like(t) if cond and t is not None else None
-            gw, gbias = mk(need[6 * i], w), mk(need[6 * i + 1], bias)
-            ggamma, gbeta = mk(need[6 * i + 2], gamma), mk(need[6 * i + 3], beta)
-            e = tab[i]
-            e["gw_eff"], e["gb_eff"] = _addr(gw_eff), _addr(gb_eff)
-            e["gw"], e["gbias"] = _addr(gw), _addr(gbias)
-            e["ggamma"], e["gbeta"] = _addr(ggamma), _addr(gbeta)
+            k = 6 * i
+            gw = torch.empty_like(w) if need[k] else None
+            gbias = torch.empty_like(bias) if need[k + 1] and bias is not None else None
+            ggamma = torch.empty_like(gamma) if need[k + 2] and gamma is not None else None
+            gbeta = torch.empty_like(beta) if need[k + 3] and beta is not None else None
+            for c, t in enumerate((gw_eff, gb_eff, gw, gbias, ggamma, gbeta)):
+                if t is not None:
+                    cols[c][i] = t.data_ptr()
             ret += [gw, gbias, ggamma, gbeta, None, None]
+        for c, name in enumerate(("gw_eff", "gb_eff", "gw", "gbias", "ggamma", "gbeta")):
+            tab[name] = cols[c]
         table, _ = _fold_table("bwd", n, dev)
-        ws = _C.workspace(part * 4, dev)
+        ws = _C.scratch(part * 4, dev)
         rc = _C.lib().d2mi_fold_frozen_bn_bwd_many(_C.ptr(table.upload(tab)), n, bwd, cob,
                                                    _C.ptr(ws), _C.stream_of(dev))
         _C.check(rc, "d2mi_fold_frozen_bn_bwd_many")

@@ -67,14 +67,17 @@ def main():
             import cProfile
             import pstats
             pr = cProfile.Profile()
-            pr.enable()
-            for _ in range(a.cprofile):
-                step()
-            pr.disable()
+            # backward on this thread, so the profile sees the backward
+            # functions (the autograd engine's device thread is invisible to it)
+            with torch.autograd.set_multithreading_enabled(False):
+                pr.enable()
+                for _ in range(a.cprofile):
+                    step()
+                pr.disable()
             torch.cuda.synchronize()
             st = pstats.Stats(pr)
-            st.sort_stats("tottime").print_stats(45)
-            st.sort_stats("cumulative").print_stats(60)
+            st.sort_stats("tottime").print_stats(70)
+            st.sort_stats("cumulative").print_stats(120)
     med = lambda v: sorted(v)[len(v) // 2]
     busy = [h - b for h, b in zip(hs, bs)]
     print(f"host_ms median {med(hs):.2f}  blocked_in_syncs_ms {med(bs):.2f}  "
