@@ -4,8 +4,6 @@
 # pass on gfx950), each with --kernel-trace only, as MI355X_MICROARCH.md's
 # HBM/rocprofv3 section prescribes; tools/pmc_summarize.py applies its gfx950
 # correction (FETCH_SIZE counts half the bytes of 16 B/lane reads).
-# (the eager step: the same kernels as the graph-replayed one, launched one
-# by one)
 # usage: tools/pmc_traffic.sh <tag> [bench args...]
 set -eo pipefail
 tag=$1; shift
