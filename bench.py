@@ -182,6 +182,10 @@ TRAFFIC_SOURCE = ("builder-committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE p
 # kernels whose PMC-counted bytes belong to the default (foreground-row)
 # training workload only: --mask-fixed-rows changes their work
 PMC_SKIP = set()
+# groups whose PMC "launch" is one op call made of several HIP-event launches
+# (tools/pmc_summarize.py: the ROIAlign backward's main kernel is its one
+# roi_bwd_clear per backward): op calls per training step
+PMC_OPS_PER_STEP = {"roi_align_bwd": 1}
 
 
 def pmc_traffic(group, mode):
@@ -249,7 +253,14 @@ def kernel_report(summary, mode="infer", extras=None):
             r["achieved_d4"] = round(byts / sec / 1e9, 1)
             r["d4_per_launch"] = byts / n
         if traffic:
-            ac = traffic * n / sec / 1e9
+            # the PMC group's "launch" is one op call: for the ROIAlign
+            # backward that is the whole backward of the step (its phase-1
+            # launch and the deferred per-level pixel passes, n HIP-event
+            # launches together), so the counter bytes cover all n launches
+            units = PMC_OPS_PER_STEP.get(name, n)
+            if name in PMC_OPS_PER_STEP:
+                r["traffic_per"] = "backward op (all of its launches in the step)"
+            ac = traffic * units / sec / 1e9
             r["achieved_counter"] = round(ac, 1)
             r["frac_counter"] = round(ac / HBM_PEAK_GBPS, 4)
         rep[name] = r
