@@ -159,7 +159,11 @@ def calibrate_scores(model, batch):
 def synthetic_batch(args, device, rank):
     from detectron2_tensorflow_amd.utils.synthetic import synthetic_images, synthetic_train_batch
     if args.mode == "train":
-        return synthetic_train_batch(args.batch, args.height, args.width, 1000 + rank, device)
+        # SOLOv2 takes its GT masks at the padded image size (solo_v2.py:399-401)
+        full = ((-(-args.height // 32) * 32, -(-args.width // 32) * 32)
+                if args.model.startswith("solo") else None)
+        return synthetic_train_batch(args.batch, args.height, args.width, 1000 + rank, device,
+                                     full_mask_hw=full)
     return synthetic_images(args.batch, args.height, args.width, 1000 + rank, device)
 
 
@@ -546,8 +550,6 @@ def cpu_baseline(args, model, batch, cfg=None):
 
 def main():
     args = parse()
-    if args.model.startswith("solo") and args.mode == "train":
-        raise SystemExit("SOLOv2 is benchmarked in --mode infer (config C5: the inference tail)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -844,6 +844,16 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     int l;
     const long long pix = tr.at(pm, touched, t, l);
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    // accumulate: the map's old value is loaded first, its latency hidden
+    // behind the contribution sums (r4: the deferred per-level passes into
+    // the RPN head's dgrad output waited on it at the end)
+    const bool acc_lv = (a.acc_mask >> l) & 1;
+    float4 old[F];
+    if (acc_lv) {
+#pragma unroll
+      for (int k = 0; k < F; ++k) old[k] = d4[k];
+    }
     float4 res[F];
     bool any = false;
     for (int sidx = 0; sidx < nsets; ++sidx) {
@@ -901,12 +911,10 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
       any = true;
     }
     if (!any) continue;
-    const bool acc_lv = (a.acc_mask >> l) & 1;
-    float4* d4 = reinterpret_cast<float4*>(dst);
 #pragma unroll
     for (int k = 0; k < F; ++k) {
       if (acc_lv) {
-        const float4 o = d4[k];
+        const float4 o = old[k];
         res[k].x = o.x + res[k].x; res[k].y = o.y + res[k].y;
         res[k].z = o.z + res[k].z; res[k].w = o.w + res[k].w;
       }

@@ -19,7 +19,7 @@ def resize_images(images, size, method="bilinear", **kwargs):
     interpolate (half-pixel for bicubic / area; nearest is floor-indexed)."""
     x = images if images.dim() == 4 else images[None]
     if method == "bilinear":
-        y = ops.resize_bilinear(x, size)
+        y = ops.resize_bilinear_grad(x, size)
     else:
         mode = {"nearest": "nearest", "bicubic": "bicubic", "area": "area"}[method]
         kw = {"align_corners": False} if mode == "bicubic" else {}

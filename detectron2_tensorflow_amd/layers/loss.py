@@ -1,4 +1,4 @@
-"""smooth_l1_loss / sigmoid_focal_loss (lib/layers/loss.py:9-101)."""
+"""smooth_l1_loss / sigmoid_focal_loss / dice_loss (lib/layers/loss.py:9-136)."""
 import torch
 
 
@@ -23,6 +23,26 @@ def sigmoid_focal_loss(*, predictions, targets, alpha=-1.0, gamma=2.0, reduction
     loss = ce * ((1 - p_t) ** gamma)
     if alpha >= 0:
         loss = (alpha * targets + (1 - alpha) * (1 - targets)) * loss
+    if reduction == "mean":
+        return loss.mean()
+    if reduction == "sum":
+        return loss.sum()
+    return loss
+
+
+def dice_loss(*, predictions, targets, reduction="none", scope=None):
+    """loss.py:104-136: per row (everything after axis 0 flattened)
+    1 - 2 sum(p t) / (sum(p p) + sum(t t) + 1e-5); an empty input gives 0."""
+    del scope
+    if predictions.numel() == 0:
+        loss = predictions.new_zeros(())
+    else:
+        p = predictions.reshape(predictions.shape[0], -1)
+        t = targets.reshape(targets.shape[0], -1).to(p.dtype)
+        a = (p * t).sum(1)
+        b = (p * p).sum(1)
+        c = (t * t).sum(1)
+        loss = 1 - (2 * a) / (b + c + 1e-5)
     if reduction == "mean":
         return loss.mean()
     if reduction == "sum":

@@ -1552,6 +1552,33 @@ def group_norm_levels(xs, num_groups, gamma, beta, eps, relu=False):
 
 
 # ------------------------------------------------------------ resize / SOLOv2
+class _ResizeBilinearFn(torch.autograd.Function):
+    """The half-pixel ResizeBilinear with a gradient (SOLOv2 training: the
+    head's grid resamples of the FPN maps): forward on the HIP kernel, the
+    adjoint of the same bilinear weights (half-pixel centres, edge-clamped;
+    PyTorch's align_corners=False sampling is that rule) for the backward."""
+
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        ctx.in_shape = tuple(x.shape)
+        return resize_bilinear(x.detach(), (oh, ow))
+
+    @staticmethod
+    def backward(ctx, g):
+        N, H, W, C = ctx.in_shape
+        gi = torch.ops.aten.upsample_bilinear2d_backward(
+            g.permute(0, 3, 1, 2).contiguous(), [g.shape[1], g.shape[2]], [N, C, H, W], False,
+            None, None)
+        return gi.permute(0, 2, 3, 1), None, None
+
+
+def resize_bilinear_grad(x, size):
+    """resize_bilinear (half-pixel) that autograd can differentiate."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _ResizeBilinearFn.apply(x, int(size[0]), int(size[1]))
+    return resize_bilinear(x, size)
+
+
 def resize_bilinear(x, size, align_corners=False, half_pixel_centers=True):
     """TF ResizeBilinear on NHWC f32 (d2mi_resize_bilinear): x [N,H,W,C] ->
     [N, size[0], size[1], C]."""

@@ -22,7 +22,10 @@ from the masks.  Output masks are uint8 0/1 (the reference's float 0/1).
 Strides: the reference's split_features multiplies strides[0] by 2 and
 divides strides[-1] by 2 on EVERY call (:237-238, a bug not reproduced); the
 first call's values ([8, 8, 16, 32, 32] for p2..p6) are used.
-Training (dice + focal losses, :274-474) is outside the hot path: raises.
+Training (:274-474): get_ground_truth as batched tensor ops (solov2_targets)
+and the dice + focal losses (MaskKernelBranch.losses); the dynamic 1x1 conv
+runs only for the positive cells (the reference convolves every cell's
+kernel, then gathers the positives: the same products).
 """
 import numpy as np
 import torch
@@ -30,6 +33,7 @@ import torch
 from ...layers import Conv2D, GroupNorm, Layer, Sequential, Upsample
 from ...layers import initializers as init
 from ...layers import ops
+from ...layers.loss import dice_loss, sigmoid_focal_loss
 from ...layers.functional import resize_images
 from ...structures import BoxList
 from ...utils.arg_scope import arg_scope
@@ -66,6 +70,108 @@ def coord_channels(N, H, W, device):
     return torch.cat([xx, yy], dim=3)
 
 
+def tf_resize_bilinear(x, oh, ow):
+    """TF ResizeBilinear with half-pixel centres on [P, H, W] float32 in
+    torch, the TF arithmetic op for op (the oracle's resize_bilinear_tf):
+    the gt-mask resample of get_ground_truth (solo_v2.py:468-471), on any
+    device."""
+    P, H, W = x.shape
+    dev = x.device
+
+    def interp(o, i):
+        scale = torch.tensor(np.float32(i) / np.float32(o), device=dev)
+        v = (torch.arange(o, device=dev, dtype=torch.float32) + 0.5) * scale - 0.5
+        f = torch.floor(v)
+        lo = f.to(torch.int64).clamp(min=0)
+        hi = torch.ceil(v).to(torch.int64).clamp(max=i - 1)
+        return lo, hi, v - f
+
+    ylo, yhi, yl = interp(oh, H)
+    xlo, xhi, xl = interp(ow, W)
+    top_rows, bot_rows = x[:, ylo], x[:, yhi]
+    tl, tr = top_rows[:, :, xlo], top_rows[:, :, xhi]
+    bl, br = bot_rows[:, :, xlo], bot_rows[:, :, xhi]
+    xl_, yl_ = xl.view(1, 1, ow), yl.view(1, oh, 1)
+    top = tl + (tr - tl) * xl_
+    bottom = bl + (br - bl) * xl_
+    return top + (bottom - top) * yl_
+
+
+def _floordiv(x, g):
+    """TF FloorDiv of a float32 tensor by the Python float 1. / g (a float32
+    constant): floor(x / f32(1 / g))."""
+    return torch.floor(x / torch.tensor(np.float32(1.0 / g), device=x.device))
+
+
+def solov2_targets(gt_boxes, gt_classes, is_valid, gt_masks, mask_hw, num_grids, scale_ranges,
+                   sigma):
+    """get_ground_truth (solo_v2.py:373-474) on a dense batch: gt_boxes
+    [N, G, 4] yxyx image px, gt_classes [N, G], is_valid [N, G], gt_masks
+    [N, G, Hi, Wi] 0/1 at the padded image size, mask_hw the mask-feature
+    size.  Per level (classes [N, S, S] int64, 0 = no object; positives
+    [P, 2] = (image, cell) in tf.where order: GT, then row, then column;
+    target masks [P, Hm, Wm] float32).  center_of_mass is the reference's
+    mean of mask x coordinate over all pixels (:43-64), from exact sums;
+    a cell two GT of a level claim takes the later GT's class."""
+    dev = gt_boxes.device
+    N = gt_boxes.shape[0]
+    vb, vg = torch.nonzero(is_valid.bool(), as_tuple=True)
+    boxes = gt_boxes[vb, vg].float()
+    classes = gt_classes[vb, vg].long()
+    masks = gt_masks[vb, vg]
+    Hi, Wi = masks.shape[1:]
+    h, w = boxes[:, 2] - boxes[:, 0], boxes[:, 3] - boxes[:, 1]
+    area_sqrt = torch.sqrt(h * w)
+    sig = torch.tensor(np.float32(sigma), device=dev)
+    half_h, half_w = 0.5 * h * sig, 0.5 * w * sig
+    Hm, Wm = int(mask_hw[0]), int(mask_hw[1])
+    up_h = torch.tensor(np.float32(Hm * 4), device=dev)
+    up_w = torch.tensor(np.float32(Wm * 4), device=dev)
+    # exact coordinate sums (integers, float64), then the mean in float32
+    m64 = masks.to(torch.float64)
+    rows = m64.sum(2)                               # [V, Hi]
+    cols = m64.sum(1)                               # [V, Wi]
+    cy_all = ((rows * torch.arange(Hi, device=dev, dtype=torch.float64)).sum(1)
+              / (Hi * Wi)).float()
+    cx_all = ((cols * torch.arange(Wi, device=dev, dtype=torch.float64)).sum(1)
+              / (Hi * Wi)).float()
+    out = []
+    for (lo, hi), S in zip(scale_ranges, num_grids):
+        sel = torch.nonzero((area_sqrt >= np.float32(lo)) & (area_sqrt <= np.float32(hi)),
+                            as_tuple=True)[0]
+        ch, cw = cy_all[sel], cx_all[sel]
+        coord_h = _floordiv(ch / up_h, S)
+        coord_w = _floordiv(cw / up_w, S)
+        zero = torch.zeros_like(ch)
+        top = torch.maximum(coord_h - 1, torch.maximum(zero, _floordiv((ch - half_h[sel]) / up_h, S)))
+        down = torch.minimum(coord_h + 1, torch.minimum(zero + (S - 1),
+                                                        _floordiv((ch + half_h[sel]) / up_h, S)))
+        left = torch.maximum(coord_w - 1, torch.maximum(zero, _floordiv((cw - half_w[sel]) / up_w, S)))
+        right = torch.minimum(coord_w + 1, torch.minimum(zero + (S - 1),
+                                                         _floordiv((cw + half_w[sel]) / up_w, S)))
+        g = torch.arange(S, device=dev, dtype=torch.float32)
+        yy, xx = g.view(1, S, 1), g.view(1, 1, S)
+        pos = ((yy >= top.view(-1, 1, 1)) & (yy <= down.view(-1, 1, 1))
+               & (xx >= left.view(-1, 1, 1)) & (xx <= right.view(-1, 1, 1)))
+        k, py, px = torch.nonzero(pos, as_tuple=True)
+        b = vb[sel][k]
+        cell = py * S + px
+        cls_map = torch.zeros(N * S * S, dtype=torch.int64, device=dev)
+        if k.numel():
+            # the later positive of a cell wins (a scatter of the ordinal, max)
+            flat = b * S * S + cell
+            order = torch.arange(k.numel(), device=dev)
+            win = torch.full((N * S * S,), -1, dtype=torch.int64, device=dev)
+            win.scatter_reduce_(0, flat, order, reduce="amax")
+            hit = win >= 0
+            cls_map[hit] = classes[sel][k[win[hit]]]
+            tm = torch.round(tf_resize_bilinear(masks[sel].float(), Hm, Wm))[k]
+        else:
+            tm = torch.zeros((0, Hm, Wm), dtype=torch.float32, device=dev)
+        out.append((cls_map.view(N, S, S), torch.stack([b, cell], 1), tm))
+    return out
+
+
 def _gn_params():
     return {"num_groups": 32, "scope": "norm"}
 
@@ -81,6 +187,11 @@ class MaskKernelBranch(Layer):
         strides[-1] /= 2
         self.strides = strides
         self.num_grids = list(s.NUM_GRIDS)
+        self.scale_ranges = [tuple(r) for r in s.SCALE_RANGES]
+        self.sigma = s.SIGMA
+        self.focal_loss_alpha = s.FOCAL_LOSS_ALPHA
+        self.focal_loss_gamma = s.FOCAL_LOSS_GAMMA
+        self.ins_loss_weight = s.INS_LOSS_WEIGHT
         self.mask_kernel_size = s.MASK_KERNEL_SIZE
         self.mask_feature_out_dims = s.MASK_FEATURE_OUT_DIMS
         self.score_threshold = s.SCORE_THRESH_TEST
@@ -149,6 +260,44 @@ class MaskKernelBranch(Layer):
         for layer in self.kernel_layers:
             k = layer.call_levels(k)
         return self.solo_cate.call_levels(c), self.solo_kernel.call_levels(k)
+
+    def losses(self, pred_classes, pred_kernels, mask_feats, targets):
+        """MaskKernelBranch.losses (solo_v2.py:274-371): dice ("mean") x
+        INS_LOSS_WEIGHT over the positive cells' dynamic-conv masks, focal
+        ("sum") over every cell against one_hot(class, K + 1)[:, 1:] -- the
+        reference's class 0 is "no object" here (so a 0-based label L trains
+        category channel L - 1, as the reference computes it) -- divided by
+        (positives + 1)."""
+        N, Hm, Wm, E = mask_feats.shape
+        tg = solov2_targets(targets["gt_boxes"], targets["gt_classes"], targets["is_valid"],
+                            targets["gt_masks"], (Hm, Wm), self.num_grids, self.scale_ranges,
+                            self.sigma)
+        feats = mask_feats.reshape(N, Hm * Wm, E)
+        kern, pos, gts, offset = [], [], [], 0
+        for (cls_map, p, tm), pk in zip(tg, pred_kernels):
+            S = cls_map.shape[1]
+            kern.append(pk.reshape(N, S * S, E))
+            pos.append(torch.stack([p[:, 0], p[:, 1] + offset], 1))
+            gts.append(tm)
+            offset += S * S
+        kern = torch.cat(kern, 1)
+        pos = torch.cat(pos, 0)
+        gts = torch.cat(gts, 0)
+        masks = mask_feats.new_zeros((pos.shape[0], Hm * Wm))
+        for b in range(N):  # one GEMM per image: its positive cells' kernels x its features
+            rows = torch.nonzero(pos[:, 0] == b, as_tuple=True)[0]
+            if rows.numel():
+                masks = masks.index_copy(0, rows, kern[b, pos[rows, 1]] @ feats[b].t())
+        loss_ins = dice_loss(predictions=torch.sigmoid(masks), targets=gts.reshape(-1, Hm * Wm),
+                             reduction="mean") * self.ins_loss_weight
+        K = self.num_classes
+        logits = torch.cat([pc.reshape(-1, K) for pc in pred_classes], 0)
+        labels = torch.cat([c.reshape(-1) for c, _, _ in tg], 0)
+        onehot = torch.nn.functional.one_hot(labels, K + 1)[:, 1:].to(logits.dtype)
+        loss_cls = sigmoid_focal_loss(predictions=logits, targets=onehot,
+                                      alpha=self.focal_loss_alpha, gamma=self.focal_loss_gamma,
+                                      reduction="sum")
+        return {"loss_ins": loss_ins, "loss_cls": loss_cls / (pos.shape[0] + 1)}
 
 
 class MaskFeatureBranch(Layer):
@@ -222,12 +371,14 @@ class SOLOv2Head(Layer):
         self.mask_feature_branch = MaskFeatureBranch(cfg, input_shape, scope="mask_feature")
 
     def call(self, images, features, targets=None):
-        if self.training:
-            raise NotImplementedError("SOLOv2 training (dice + focal losses) is outside the hot "
-                                      "path: BASELINE config C5 is the inference tail")
-        image_hw = images.tensor.shape[1:3]
         pred_cls, pred_kernels = self.mask_kernel_branch(features)
         mask_feats = self.mask_feature_branch(features)
+        if self.training:
+            if targets is None:
+                raise ValueError("SOLOv2 training needs targets")
+            return None, self.mask_kernel_branch.losses(pred_cls, pred_kernels, mask_feats,
+                                                        targets)
+        image_hw = images.tensor.shape[1:3]
         return self.inference(pred_cls, pred_kernels, mask_feats, image_hw), {}
 
     def inference(self, pred_cls, pred_kernels, mask_feats, image_hw, debug=None):

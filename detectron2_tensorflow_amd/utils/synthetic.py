@@ -19,7 +19,10 @@ def synthetic_images(batch, height, width, seed, device):
 
 
 def synthetic_instances(batch, height, width, seed, device, num_gt=7, num_classes=80,
-                        mask_size=56, sqrt_area=(32.0, 512.0)):
+                        mask_size=56, sqrt_area=(32.0, 512.0), full_mask_hw=None):
+    """full_mask_hw: (H, W) -- image-size box-filled masks [batch, num_gt, H, W]
+    instead of the mini masks (SOLOv2 training: get_ground_truth takes the
+    masks at the padded image size, solo_v2.py:399-401)."""
     rng = np.random.default_rng(seed)
     n = batch * num_gt
     s = np.exp(rng.uniform(np.log(sqrt_area[0]), np.log(sqrt_area[1]), n))
@@ -39,6 +42,15 @@ def synthetic_instances(batch, height, width, seed, device, num_gt=7, num_classe
         "gt_difficult": torch.zeros(batch, num_gt, dtype=torch.bool),
         "gt_masks": torch.ones(batch, num_gt, mask_size, mask_size, dtype=torch.uint8),
     }
+    if full_mask_hw is not None:
+        H, W = full_mask_hw
+        yy = torch.arange(H).view(1, 1, H, 1).float()
+        xx = torch.arange(W).view(1, 1, 1, W).float()
+        b = inst["gt_boxes"]
+        # pixel (y, x) inside when its centre is: y + 0.5 in (y1, y2)
+        inst["gt_masks"] = (((yy + 0.5) > b[..., 0, None, None]) & ((yy + 0.5) < b[..., 2, None, None])
+                            & ((xx + 0.5) > b[..., 1, None, None])
+                            & ((xx + 0.5) < b[..., 3, None, None])).to(torch.uint8)
     return {k: v.to(device) for k, v in inst.items()}
 
 

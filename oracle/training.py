@@ -242,3 +242,116 @@ def sgd_step(params, grads, accums, lr, momentum, weight_decays, clip_norm):
         out_a.append(a)
         out_p.append(p - lr * a)
     return out_p, out_a
+
+
+def _floordiv_f32(x, g):
+    """TF FloorDiv of a float32 tensor by the Python float 1. / g (converted
+    to float32): floor(x / f32(1 / g)) in float32 (solo_v2.py:402-435)."""
+    q = (np.asarray(x, F32) / F32(1.0 / g)).astype(F32)
+    return np.floor(q).astype(F32)
+
+
+def solov2_targets(gt_boxes, gt_classes, is_valid, gt_masks, mask_hw, num_grids, scale_ranges,
+                   sigma):
+    """MaskKernelBranch.get_ground_truth (solo_v2.py:373-474) for a dense
+    batch: gt_boxes [N, G, 4] yxyx image px, gt_classes [N, G], is_valid
+    [N, G], gt_masks [N, G, Hi, Wi] 0/1 at the padded image size, mask_hw the
+    mask-feature size.  The valid GT in batch-major order (SparseBoxList.from_dense).
+    Per level: (grid classes [N, S, S] int64 with 0 = no object, positive
+    (batch, cell) pairs [P, 2] in tf.where order -- GT, then row, then column --
+    and their target masks [P, Hm, Wm] float32).
+
+    center_of_mass is the reference's (:43-64): the MEAN of mask * coordinate
+    over every pixel (not divided by the mask area), here from exact sums
+    (float64) rounded to float32 -- TF's float32 reduce_mean over ~1 M pixels
+    depends on its summation order.  A cell claimed by two GT of one level
+    takes the later GT's class (tf.sparse.reorder + to_dense keep one of the
+    duplicates; which one is unpinned)."""
+    gt_boxes = np.asarray(gt_boxes, F32)
+    N, G = gt_boxes.shape[:2]
+    vb, vg = np.nonzero(np.asarray(is_valid, bool))
+    boxes = gt_boxes[vb, vg]
+    classes = np.asarray(gt_classes)[vb, vg].astype(np.int64)
+    masks = np.asarray(gt_masks)[vb, vg].astype(F32)
+    h = (boxes[:, 2] - boxes[:, 0]).astype(F32)
+    w = (boxes[:, 3] - boxes[:, 1]).astype(F32)
+    area_sqrt = np.sqrt((h * w).astype(F32)).astype(F32)
+    half_h = (F32(0.5) * h * F32(sigma)).astype(F32)
+    half_w = (F32(0.5) * w * F32(sigma)).astype(F32)
+    Hm, Wm = mask_hw
+    up_h, up_w = F32(Hm * 4), F32(Wm * 4)
+    Hi, Wi = masks.shape[1:] if len(masks) else (Hm * 4, Wm * 4)
+    out = []
+    for (lo, hi), S in zip(scale_ranges, num_grids):
+        li = np.nonzero((area_sqrt >= F32(lo)) & (area_sqrt <= F32(hi)))[0]
+        cls_map = np.zeros((N, S, S), np.int64)
+        pos, tmasks = [], []
+        if len(li):
+            m = masks[li]
+            yy = np.arange(Hi, dtype=np.float64)[None, :, None]
+            xx = np.arange(Wi, dtype=np.float64)[None, None, :]
+            ch = ((m.astype(np.float64) * yy).sum((1, 2)) / (Hi * Wi)).astype(F32)
+            cw = ((m.astype(np.float64) * xx).sum((1, 2)) / (Hi * Wi)).astype(F32)
+            coord_h = _floordiv_f32(ch / up_h, S)
+            coord_w = _floordiv_f32(cw / up_w, S)
+            top = np.maximum(coord_h - 1, np.maximum(F32(0), _floordiv_f32((ch - half_h[li]) / up_h, S)))
+            down = np.minimum(coord_h + 1, np.minimum(F32(S - 1), _floordiv_f32((ch + half_h[li]) / up_h, S)))
+            left = np.maximum(coord_w - 1, np.maximum(F32(0), _floordiv_f32((cw - half_w[li]) / up_w, S)))
+            right = np.minimum(coord_w + 1, np.minimum(F32(S - 1), _floordiv_f32((cw + half_w[li]) / up_w, S)))
+            rs = oracle_resize_masks(m, Hm, Wm)
+            for k, gi in enumerate(li):
+                for y in range(S):
+                    for x in range(S):
+                        if top[k] <= y <= down[k] and left[k] <= x <= right[k]:
+                            b = vb[gi]
+                            pos.append((b, y * S + x))
+                            tmasks.append(rs[k])
+                            cls_map[b, y, x] = classes[gi]
+        out.append((cls_map, np.asarray(pos, np.int64).reshape(-1, 2),
+                    np.asarray(tmasks, F32).reshape(-1, Hm, Wm)))
+    return out
+
+
+def oracle_resize_masks(m, Hm, Wm):
+    """resize_images(masks[..., None], pred_mask_size) then tf.round
+    (solo_v2.py:466-471): TF ResizeBilinear, half-pixel centres (the
+    reference's kwargs filter drops align_corners), round half to even."""
+    from solo import resize_bilinear_tf
+    r = resize_bilinear_tf(np.asarray(m, F32)[..., None], Hm, Wm)[..., 0]
+    return np.round(r).astype(F32)
+
+
+def solov2_losses(pred_classes, pred_kernels, mask_feats, targets, num_classes, alpha, gamma,
+                  ins_loss_weight):
+    """MaskKernelBranch.losses (solo_v2.py:274-371): the dynamic 1x1 conv of
+    every positive cell's kernel over its image's mask features, dice loss
+    ("mean") x INS_LOSS_WEIGHT, and the focal loss ("sum") over every cell of
+    every level against one_hot(class, K + 1)[:, 1:] (class 0 = no object),
+    divided by (positives + 1).  Returns (loss_ins, loss_cls), float64."""
+    feats = np.asarray(mask_feats, np.float64)
+    N, Hm, Wm, E = feats.shape
+    pred_masks, gt_masks = [], []
+    logits, onehots = [], []
+    num_ins = 0
+    for (cls_map, pos, tm), pc, pk in zip(targets, pred_classes, pred_kernels):
+        S = cls_map.shape[1]
+        pk = np.asarray(pk, np.float64).reshape(N, S * S, E)
+        for (b, j), t in zip(pos, tm):
+            pred_masks.append(feats[b].reshape(-1, E) @ pk[b, j])
+            gt_masks.append(t.reshape(-1))
+        num_ins += len(pos)
+        logits.append(np.asarray(pc, np.float64).reshape(-1, num_classes))
+        oh = np.zeros((N * S * S, num_classes + 1))
+        oh[np.arange(N * S * S), cls_map.reshape(-1)] = 1.0
+        onehots.append(oh[:, 1:])
+    if pred_masks:
+        p = 1.0 / (1.0 + np.exp(-np.stack(pred_masks)))
+        t = np.stack(gt_masks).astype(np.float64)
+        a = (p * t).sum(1)
+        bb = (p * p).sum(1)
+        c = (t * t).sum(1)
+        loss_ins = (1.0 - 2 * a / (bb + c + 1e-5)).mean()
+    else:
+        loss_ins = 0.0
+    cls = sigmoid_focal_loss(np.concatenate(logits), np.concatenate(onehots), alpha, gamma).sum()
+    return ins_loss_weight * loss_ins, cls / (num_ins + 1)

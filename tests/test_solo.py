@@ -490,3 +490,61 @@ def test_group_norm_hip_vs_float64(dev, C, G, relu, up2, acc):
                          torch.from_numpy(beta).to(dev), 1e-5, relu, up2,
                          torch.from_numpy(base).to(dev) if acc else None)
     np.testing.assert_allclose(out.cpu().numpy(), want, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_solo_training_steps(dev):
+    """SOLOv2 R50-FPN training through the Trainer at 256x320
+    (solo_v2.py:274-474: dice + focal losses, get_ground_truth): the losses
+    of the first step equal the oracle's on the model's own head outputs,
+    every trainable parameter gets a finite gradient, and over-fitting one
+    batch lowers the loss."""
+    import training as otrain
+    from detectron2_tensorflow_amd import _C
+    from detectron2_tensorflow_amd.engine import Trainer
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.utils.synthetic import synthetic_train_batch
+    cfg = _cfg()
+    cfg.defrost()
+    cfg.SOLVER.BASE_LR = 0.005
+    cfg.SOLVER.WARMUP_ITERS = 0
+    cfg.freeze()
+    torch.manual_seed(0)
+    model = build_model(cfg).to(dev).train()
+    batch = synthetic_train_batch(2, 256, 320, 5, dev, num_classes=80, sqrt_area=(24.0, 200.0),
+                                  full_mask_hw=(256, 320))
+    head = model.detector
+    got = {}
+    orig = head.mask_kernel_branch.losses
+
+    def spy(pc, pk, mf, tg):
+        got["args"] = ([t.detach().cpu().numpy() for t in pc], [t.detach().cpu().numpy() for t in pk],
+                       mf.detach().cpu().numpy())
+        return orig(pc, pk, mf, tg)
+    head.mask_kernel_branch.losses = spy
+    try:
+        losses = model(batch)
+    finally:
+        del head.mask_kernel_branch.losses
+    assert set(losses) == {"loss_ins", "loss_cls"}
+    sum(losses.values()).backward()
+    bad = [n for n, p in model.named_parameters()
+           if p.requires_grad and (p.grad is None or not torch.isfinite(p.grad).all())]
+    assert not bad, bad[:5]
+    inst = {k: v.cpu().numpy() for k, v in batch["instances"].items()}
+    pc, pk, mf = got["args"]
+    b = head.mask_kernel_branch
+    tg = otrain.solov2_targets(inst["gt_boxes"], inst["gt_classes"], inst["is_valid"],
+                               inst["gt_masks"], mf.shape[1:3], b.num_grids, b.scale_ranges,
+                               b.sigma)
+    assert sum(len(p) for _, p, _ in tg) > 5
+    ins, cls = otrain.solov2_losses(pc, pk, mf, tg, b.num_classes, b.focal_loss_alpha,
+                                    b.focal_loss_gamma, b.ins_loss_weight)
+    assert float(losses["loss_ins"]) == pytest.approx(ins, rel=1e-4)
+    assert float(losses["loss_cls"]) == pytest.approx(cls, rel=1e-4)
+    model.zero_grad(set_to_none=True)
+    tr = Trainer(cfg, model)
+    hist = [float(tr.step(batch)["total_loss"]) for _ in range(10)]
+    assert all(np.isfinite(hist)), hist
+    assert np.mean(hist[-3:]) < 0.9 * np.mean(hist[:3]), hist
+    _C.raise_on_errors(dev)

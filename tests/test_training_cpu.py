@@ -476,3 +476,75 @@ def test_retinanet_dense_losses_match_oracle():
     assert (np.concatenate(tc) >= 0).sum() > 0 and (np.concatenate(tc) < K).any()
     assert float(cs) / norm == pytest.approx(want_c, rel=1e-5)
     assert float(bs) / norm == pytest.approx(want_b, rel=1e-5)
+
+
+def _solo_batch(seed, N=2, G=6, H=128, W=160):
+    """Dense SOLOv2 targets: boxes across the scale ranges, box-filled masks
+    at the padded image size, an invalid GT and a duplicated GT (two GT of one
+    level claiming the same cells)."""
+    rng = np.random.default_rng(seed)
+    s = np.exp(rng.uniform(np.log(12), np.log(150), (N, G)))
+    r = np.exp(rng.uniform(np.log(0.5), np.log(2.0), (N, G)))
+    h, w = s * np.sqrt(r), s / np.sqrt(r)
+    cy, cx = rng.uniform(0, H, (N, G)), rng.uniform(0, W, (N, G))
+    boxes = np.stack([np.clip(cy - h / 2, 0, H - 4), np.clip(cx - w / 2, 0, W - 4),
+                      np.clip(cy + h / 2, 4, H), np.clip(cx + w / 2, 4, W)], -1)
+    boxes = np.round(boxes).astype(np.float32)
+    boxes[..., 2] = np.maximum(boxes[..., 2], boxes[..., 0] + 4)
+    boxes[..., 3] = np.maximum(boxes[..., 3], boxes[..., 1] + 4)
+    boxes[0, 1] = boxes[0, 0]  # a duplicate: same box, another class
+    classes = rng.integers(0, 5, (N, G))
+    valid = np.ones((N, G), bool)
+    valid[1, -1] = False
+    masks = np.zeros((N, G, H, W), np.uint8)
+    for b in range(N):
+        for g in range(G):
+            y1, x1, y2, x2 = boxes[b, g].astype(int)
+            masks[b, g, y1:y2, x1:x2] = 1
+    return boxes, classes, valid, masks
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_solov2_targets_match_oracle(seed):
+    from detectron2_tensorflow_amd.modeling.single_stage_heads.solo_v2 import solov2_targets
+    boxes, classes, valid, masks = _solo_batch(seed)
+    grids, ranges = [40, 36, 24, 16, 12], [(1, 96), (48, 192), (96, 384), (192, 768), (384, 2048)]
+    want = otrain.solov2_targets(boxes, classes, valid, masks, (32, 40), grids, ranges, 0.2)
+    got = solov2_targets(torch.from_numpy(boxes), torch.from_numpy(classes),
+                         torch.from_numpy(valid), torch.from_numpy(masks), (32, 40), grids, ranges,
+                         0.2)
+    npos = 0
+    for (wc, wp, wm), (gc, gp, gm) in zip(want, got):
+        np.testing.assert_array_equal(gc.numpy(), wc)
+        np.testing.assert_array_equal(gp.numpy(), wp)
+        np.testing.assert_array_equal(gm.numpy(), wm)
+        npos += len(wp)
+    assert npos > 10
+
+
+def test_solov2_losses_match_oracle():
+    from types import SimpleNamespace
+
+    from detectron2_tensorflow_amd.modeling.single_stage_heads.solo_v2 import MaskKernelBranch
+    boxes, classes, valid, masks = _solo_batch(7)
+    grids, ranges = [40, 36, 24, 16, 12], [(1, 96), (48, 192), (96, 384), (192, 768), (384, 2048)]
+    N, K, E, Hm, Wm = 2, 5, 8, 32, 40
+    g = torch.Generator().manual_seed(0)
+    pc = [torch.randn(N, S, S, K, generator=g) - 2 for S in grids]
+    pk = [torch.randn(N, S, S, E, generator=g) * 0.3 for S in grids]
+    mf = torch.randn(N, Hm, Wm, E, generator=g)
+    me = SimpleNamespace(num_grids=grids, scale_ranges=ranges, sigma=0.2, num_classes=K,
+                         focal_loss_alpha=0.25, focal_loss_gamma=2.0, ins_loss_weight=3.0)
+    tg = {"gt_boxes": torch.from_numpy(boxes), "gt_classes": torch.from_numpy(classes),
+          "is_valid": torch.from_numpy(valid), "gt_masks": torch.from_numpy(masks)}
+    for t in pc + pk + [mf]:
+        t.requires_grad_(True)
+    got = MaskKernelBranch.losses(me, pc, pk, mf, tg)
+    want_t = otrain.solov2_targets(boxes, classes, valid, masks, (Hm, Wm), grids, ranges, 0.2)
+    ins, cls = otrain.solov2_losses([t.detach().numpy() for t in pc],
+                                    [t.detach().numpy() for t in pk], mf.detach().numpy(), want_t,
+                                    K, 0.25, 2.0, 3.0)
+    np.testing.assert_allclose(float(got["loss_ins"].detach()), ins, rtol=1e-5)
+    np.testing.assert_allclose(float(got["loss_cls"].detach()), cls, rtol=1e-5)
+    (got["loss_ins"] + got["loss_cls"]).backward()
+    assert all(t.grad is not None and torch.isfinite(t.grad).all() for t in pk[:2] + [mf])
