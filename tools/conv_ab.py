@@ -26,6 +26,13 @@ SETS = {
     "wgrad": ["2,200,336,256,256,3,1,w", "2,100,168,256,256,3,1,w", "2,50,84,256,256,3,1,w",
               "2,100,168,128,128,3,1,w", "2,25,42,512,512,3,1,w", "32,14,14,256,256,3,1,w",
               "2,50,84,1024,256,1,1,w", "2,50,84,256,1024,1,1,w", "2,200,336,64,64,3,1,w"],
+    # the res4 / res5 / p4-p6 shapes: few output tiles, split K
+    "small_m": ["2,50,84,1024,256,1,1,plain", "2,50,84,1024,256,1,1,g", "2,50,84,256,1024,1,1,r",
+                "2,50,84,256,1024,1,1,gr", "2,50,84,256,256,3,1,plain", "2,25,42,2048,512,1,1,plain",
+                "2,25,42,2048,512,1,1,g", "2,25,42,512,2048,1,1,r", "2,25,42,512,512,3,1,plain",
+                "2,25,42,256,256,3,1,plain", "2,13,21,256,256,3,1,plain",
+                "2,50,84,256,1024,1,1,w", "2,50,84,1024,256,1,1,w", "2,25,42,512,512,3,1,w",
+                "2,25,42,2048,512,1,1,w", "2,25,42,512,2048,1,1,w"],
     "kxk": ["2,200,336,256,256,3,1,plain", "2,50,84,256,256,3,1,plain",
             "2,100,168,128,128,3,1,plain", "2,25,42,512,512,3,1,plain",
             "2,200,336,64,64,3,1,plain", "32,14,14,256,256,3,1,plain"],
