@@ -231,6 +231,62 @@ __global__ __launch_bounds__(256) void fold_bn_many_kernel(const d2mi_fold_entry
   const int cit = local % nci;
   const int tap = local / nci;
   const int co0 = cot * 64, ci0 = cit * 64;
+  // float4 form (Cin, Cout multiples of 4, 16-B aligned tensors: every ResNet
+  // conv): 16 threads per 64-channel row, 16-B loads and stores, the same
+  // per-element product (bit-identical)
+  const bool al = ((reinterpret_cast<uintptr_t>(e.w) | reinterpret_cast<uintptr_t>(e.w_eff) |
+                    reinterpret_cast<uintptr_t>(e.w_packed)) & 15) == 0;
+  if (Cout % 4 == 0 && Cin % 4 == 0 && al) {
+    const int t = threadIdx.x;
+    const int cq = t & 15, ri = t >> 4;  // channel quad, row phase
+    const int c4 = co0 + 4 * cq;
+    const bool live4 = c4 < Cout;        // (Cout % 4 == 0: the quad is whole)
+    float sc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float inv = bn_inv(e.var, e.eps, c4 + q);
+        sc[q] = e.gamma ? inv * e.gamma[c4 + q] : inv;
+      }
+      if (cit == 0 && tap == 0 && ri == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float shift = -e.mean[c4 + q] * sc[q];
+          if (e.beta) shift = shift + e.beta[c4 + q];
+          e.b_eff[c4 + q] = e.bias ? e.bias[c4 + q] * sc[q] + shift : shift;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = ri + 16 * k;
+      const bool row = ci0 + i < Cin;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (live4 && row) {
+        const size_t o = ((size_t)tap * Cin + ci0 + i) * Cout + c4;
+        const float4 w4 = *reinterpret_cast<const float4*>(e.w + o);
+        v = make_float4(w4.x * sc[0], w4.y * sc[1], w4.z * sc[2], w4.w * sc[3]);
+        if (e.w_eff) *reinterpret_cast<float4*>(e.w_eff + o) = v;
+      }
+      tile[i][4 * cq] = v.x;
+      tile[i][4 * cq + 1] = v.y;
+      tile[i][4 * cq + 2] = v.z;
+      tile[i][4 * cq + 3] = v.w;
+    }
+    if (!e.w_packed) return;
+    __syncthreads();
+    const int ciq = t & 15, cj = t >> 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = cj + 16 * k;
+      const int ci = ci0 + 4 * ciq;
+      if (co0 + j < Cout && ci < Cin)
+        *reinterpret_cast<float4*>(e.w_packed + ((size_t)tap * Cout + co0 + j) * Cin + ci) =
+            make_float4(tile[4 * ciq][j], tile[4 * ciq + 1][j], tile[4 * ciq + 2][j],
+                        tile[4 * ciq + 3][j]);
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int co = co0 + lane;
   const bool live = co < Cout;
@@ -279,6 +335,8 @@ __global__ __launch_bounds__(256) void fold_bn_bwd_many_kernel(
   }
   float s = 0.f;
   if (live) {
+    // unrolled: eight rows' loads in flight per lane (the sum keeps its order)
+#pragma unroll 8
     for (int r = r0 + wv; r < r1; r += 4) {
       const float g = e.gw_eff ? e.gw_eff[(size_t)r * Cout + co] : 0.f;
       s += g * e.w[(size_t)r * Cout + co];
