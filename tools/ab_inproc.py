@@ -74,7 +74,15 @@ def _defer_pixels(on):
     ops.DEFER_PIXELS = on
 
 
-SWITCHES = {"defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+def _gc_off(on):
+    import gc
+    if on:
+        gc.disable()
+    else:
+        gc.enable()
+
+
+SWITCHES = {"gc_off": _gc_off, "defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 

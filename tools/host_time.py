@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="train")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--gc-off", action="store_true",
+                    help="Python's cyclic garbage collector disabled for the timed steps")
     ap.add_argument("--cprofile", type=int, default=0,
                     help="also cProfile this many steps and print the top host functions")
     a = ap.parse_args()
@@ -52,6 +54,10 @@ def main():
         for _ in range(3):
             step()
         torch.cuda.synchronize()
+        if a.gc_off:
+            import gc
+            gc.collect()
+            gc.disable()
         hs, ws, bs = [], [], []
         for _ in range(a.steps):
             host_sync.reset()
