@@ -155,6 +155,9 @@ class DeferredMaskLoss:
 @ROI_HEADS_REGISTRY.register()
 class StandardROIHeads(ROIHeads):
     MASK_ROW_BUCKET = 32
+    # the mask branch's fg-first ordering and per-slot gathers issued before
+    # the foreground-count read, so less host work follows it
+    MASK_PREP_EARLY = True
 
     def __init__(self, cfg, input_shape, **kwargs):
         super().__init__(cfg, input_shape, **kwargs)
@@ -209,13 +212,16 @@ class StandardROIHeads(ROIHeads):
             pending = None
             fg = self._mask_fg(sampled) if self.mask_on else None  # (once per step)
             defer = self.mask_on and self.mask_compact_rows and self.defer_mask_loss
+            prep = None
             if self.mask_on and self.mask_compact_rows and not defer:
                 pending = host_sync.start_read(fg.sum())
+                prep = self._mask_prep(sampled, targets, fg) if self.MASK_PREP_EARLY else None
             losses = self._box_losses(feats, sampled, share)
             if defer:
                 losses["loss_mask"] = DeferredMaskLoss(self, feats, sampled, targets, share, fg)
             elif self.mask_on:
-                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg)
+                losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg,
+                                                      prep=prep)
             return sampled, losses
         pred = self._forward_box(feats, proposals, images.image_shapes)
         pred = self.forward_with_given_boxes(features, pred)
@@ -270,11 +276,11 @@ class StandardROIHeads(ROIHeads):
         b = self.MASK_ROW_BUCKET
         return min(slots, max(b, -(-nfg // b) * b))
 
-    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None,
-                   rows=None):
-        """_forward_mask training branch (roi_heads.py:594-600) over the first
-        int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
-        foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
+    def _mask_prep(self, sampled, targets, fg=None):
+        """The mask branch's per-slot inputs over the first int(S *
+        POSITIVE_FRACTION) slots per image, and (compact rows) the slots in
+        fg-first order -- everything that does not need the foreground count,
+        so the host issues it before the count's read."""
         F_ = int(self.batch_size_per_image * self.positive_sample_fraction)
         boxes = sampled["boxes"][:, :F_].reshape(-1, 4)
         N = sampled["boxes"].shape[0]
@@ -286,6 +292,20 @@ class StandardROIHeads(ROIHeads):
         G = gm.shape[1]
         mind = (sampled["gt_index"][:, :F_] + _cached_index("base", N, G, dev)).reshape(-1)
         gt_boxes = sampled["gt_boxes"][:, :F_].reshape(-1, 4)
+        ts = (boxes, cls, fg, img, mind, gt_boxes)
+        if self.mask_compact_rows:
+            # fg rows first, each group in index order (a stable sort of ~fg);
+            # the count only decides how many of them run (a view)
+            order = torch.argsort((~fg).to(torch.uint8), stable=True)
+            ts = tuple(t[order] for t in ts)
+        return ts, gm.reshape(N * G, *gm.shape[2:]), fg
+
+    def _mask_loss(self, feats, sampled, targets, grad_share=None, pending=None, fg=None,
+                   rows=None, prep=None):
+        """_forward_mask training branch (roi_heads.py:594-600) over the first
+        int(S * POSITIVE_FRACTION) slots per image, which hold every sampled
+        foreground proposal (select_foreground_proposals, roi_heads.py:35-62)."""
+        ts, gm, fg_all = prep if prep is not None else self._mask_prep(sampled, targets, fg)
         if self.mask_compact_rows:
             # The reference runs the mask head on the foreground proposals only
             # (select_foreground_proposals, roi_heads.py:35-62 + :594-600).  One
@@ -295,19 +315,17 @@ class StandardROIHeads(ROIHeads):
             # (rows given: a deferred mask loss, DeferredMaskLoss.compute)
             if rows is None:
                 nfg = (host_sync.finish_read(pending) if pending is not None
-                       else host_sync.read_ints(fg.sum()))[0]
-                rows = self.mask_rows(nfg, fg.numel())
+                       else host_sync.read_ints(fg_all.sum()))[0]
+                rows = self.mask_rows(nfg, fg_all.numel())
             R = rows
-            # fg rows first, each group in index order (a stable sort of ~fg)
-            rows = torch.argsort((~fg).to(torch.uint8), stable=True)[:R]
-            boxes, cls, fg, img, mind, gt_boxes = (t[rows] for t in (boxes, cls, fg, img, mind, gt_boxes))
+            ts = tuple(t[:R] for t in ts)
             self.last_mask_rows = R
         else:
-            self.last_mask_rows = int(boxes.shape[0])
+            self.last_mask_rows = int(ts[0].shape[0])
+        boxes, cls, fg, img, mind, gt_boxes = ts
         x = self.mask_pooler.pool(feats, boxes.contiguous(), img, grad_share=grad_share)
         _, logits = self.mask_head(x)
-        return mask_rcnn_loss(logits, boxes, gt_boxes, cls, gm.reshape(N * G, *gm.shape[2:]), mind,
-                              fg, self.use_mini_masks)
+        return mask_rcnn_loss(logits, boxes, gt_boxes, cls, gm, mind, fg, self.use_mini_masks)
 
     def forward_with_given_boxes(self, features, instances, image_shape=None):
         assert not self.training

@@ -82,7 +82,12 @@ def _gc_off(on):
         gc.enable()
 
 
-SWITCHES = {"gc_off": _gc_off, "defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+def _mask_prep_early(on):
+    from detectron2_tensorflow_amd.modeling.roi_heads.roi_heads import StandardROIHeads
+    StandardROIHeads.MASK_PREP_EARLY = on
+
+
+SWITCHES = {"mask_prep_early": _mask_prep_early, "gc_off": _gc_off, "defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
