@@ -117,6 +117,9 @@ _SIGS = {
     "d2mi_wgrad_skinny_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "d2mi_wgrad_skinny": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "d2mi_wgrad_skinny_ex": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, P, c_size_t, P]),
+    "d2mi_wgrad_skinny_levels_workspace_size": (c_size_t, [P, c_int, c_int, c_int]),
+    "d2mi_wgrad_skinny_levels": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P, c_size_t,
+                                         P]),
     "d2mi_column_sum_workspace_size": (c_size_t, [ctypes.c_longlong, c_int]),
     "d2mi_column_sum": (c_int, [P, ctypes.c_longlong, c_int, P, P, c_size_t, P]),
     "d2mi_upsample2x_grad": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),

@@ -10,6 +10,8 @@
 // pixel for Cin = 256), the chunk's G rows staged in LDS and broadcast, 16
 // f32 accumulators per thread; per-chunk partials then reduced in chunk
 // order by a second kernel (deterministic, no atomics).
+#include <algorithm>
+
 #include "common.h"
 #include "internal.h"
 
@@ -73,14 +75,11 @@ __global__ __launch_bounds__(256) void wgrad_skinny_partial_kernel(
 // chunk partial is written.  kChunk4 pixels per workgroup.
 constexpr int kChunk4 = 128;
 
-__global__ __launch_bounds__(256, 2) void wgrad_skinny_partial4_kernel(
-    const float* __restrict__ x, const float* __restrict__ g, int P, int Cin, int Cout,
-    float* __restrict__ partial /* [chunks][Cin + 1][Cout] */) {
-  // gs: the chunk's G rows (16 KiB); reused for the wave combine (3 x 64
-  // lanes x 64 floats = 48 KiB)
-  __shared__ float4 lds[3 * 64 * 16];
+__device__ __forceinline__ void skinny_partial4(const float* __restrict__ x,
+                                                const float* __restrict__ g, int P, int Cin,
+                                                int Cout, int chunk,
+                                                float* __restrict__ partial, float4* lds) {
   float* gs = reinterpret_cast<float*>(lds);
-  const int chunk = blockIdx.x;
   const int p0 = chunk * kChunk4;
   const int np = min(kChunk4, P - p0);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -164,6 +163,36 @@ __global__ __launch_bounds__(256, 2) void wgrad_skinny_partial4_kernel(
   }
 }
 
+__global__ __launch_bounds__(256, 2) void wgrad_skinny_partial4_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, int P, int Cin, int Cout,
+    float* __restrict__ partial /* [chunks][Cin + 1][Cout] */) {
+  // the chunk's G rows (16 KiB); reused for the wave combine (3 x 64 lanes x
+  // 64 floats = 48 KiB)
+  __shared__ float4 lds[3 * 64 * 16];
+  skinny_partial4(x, g, P, Cin, Cout, blockIdx.x, partial, lds);
+}
+
+// Several calls' (levels') passes in one launch: the levels' chunks one
+// after another, level l's partials at chunk offset cb[l] (each level's
+// chunk partials exactly the single-level kernel's).
+constexpr int kSkinnyMaxLevels = 8;
+struct SkinnyLevels {
+  const float* x[kSkinnyMaxLevels];
+  const float* g[kSkinnyMaxLevels];
+  int P[kSkinnyMaxLevels];
+  int cb[kSkinnyMaxLevels + 1];
+  int L;
+};
+
+__global__ __launch_bounds__(256, 2) void wgrad_skinny_partial4_levels_kernel(
+    SkinnyLevels lv, int Cin, int Cout, float* __restrict__ partial) {
+  __shared__ float4 lds[3 * 64 * 16];
+  int l = 0;
+  while (l + 1 < lv.L && (int)blockIdx.x >= lv.cb[l + 1]) ++l;
+  skinny_partial4(lv.x[l], lv.g[l], lv.P[l], Cin, Cout, blockIdx.x - lv.cb[l],
+                  partial + (size_t)lv.cb[l] * (Cin + 1) * Cout, lds);
+}
+
 // Sum the chunk partials (gw rows, then the gb row) in a fixed order: 16
 // outputs per workgroup, 16 chunk segments per output summed in chunk order
 // by 16 threads, then the 16 segment sums in segment order (one thread per
@@ -191,6 +220,44 @@ __global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
     // accumulate: old + new, the rounding of autograd's sum of two gradients
     if (o < Cin * Cout) gw[o] = accumulate ? gw[o] + t : t;
     else if (gb) gb[o - Cin * Cout] = accumulate ? gb[o - Cin * Cout] + t : t;
+  }
+}
+
+// The levels' reduces in one launch: per output, each level's chunk partials
+// summed exactly as wgrad_skinny_reduce_kernel sums one call's (16 ordered
+// segments, then the segments in order), and the levels added in launch
+// order -- the rounding of one call per level with accumulate (old + new).
+__global__ __launch_bounds__(256) void wgrad_skinny_reduce_levels_kernel(
+    const float* __restrict__ partial, SkinnyLevels lv, int Cin, int Cout,
+    float* __restrict__ gw, float* __restrict__ gb, int accumulate) {
+  __shared__ float red[kRedSeg][kRedOut];
+  const int n = (Cin + 1) * Cout;
+  const int ol = threadIdx.x % kRedOut, sg = threadIdx.x / kRedOut;
+  const int o = blockIdx.x * kRedOut + ol;
+  // accumulate: start from the old value (old + t0, then + t1 ...)
+  float acc = 0.f;
+  if (accumulate && sg == 0 && o < n) acc = o < Cin * Cout ? gw[o] : (gb ? gb[o - Cin * Cout] : 0.f);
+  for (int l = 0; l < lv.L; ++l) {
+    const int chunks = lv.cb[l + 1] - lv.cb[l];
+    const float* part = partial + (size_t)lv.cb[l] * n;
+    const int per = (chunks + kRedSeg - 1) / kRedSeg;
+    const int k0 = sg * per, k1 = min(chunks, k0 + per);
+    float s = 0.f;
+    if (o < n)
+      for (int k = k0; k < k1; ++k) s += part[(size_t)k * n + o];
+    __syncthreads();  // (the previous level's red reads are done)
+    red[sg][ol] = s;
+    __syncthreads();
+    if (sg == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < kRedSeg; ++j) t += red[j][ol];
+      acc = (l == 0 && !accumulate) ? t : acc + t;
+    }
+  }
+  if (sg == 0 && o < n) {
+    if (o < Cin * Cout) gw[o] = acc;
+    else if (gb) gb[o - Cin * Cout] = acc;
   }
 }
 
@@ -283,6 +350,48 @@ extern "C" int d2mi_wgrad_skinny_ex(const float* x, const float* g, int P, int C
   const int n = (Cin + 1) * Cout;
   hipLaunchKernelGGL(wgrad_skinny_reduce_kernel, dim3((n + kRedOut - 1) / kRedOut), dim3(256), 0,
                      st, partial, chunks, Cin, Cout, gw, gb, accumulate);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t d2mi_wgrad_skinny_levels_workspace_size(const int* P, int L, int Cin, int Cout) {
+  if (!P || L <= 0 || L > kSkinnyMaxLevels || Cin <= 0 || Cout <= 0) return 0;
+  size_t chunks = 0;
+  for (int l = 0; l < L; ++l) chunks += ((size_t)std::max(P[l], 0) + kChunk4 - 1) / kChunk4;
+  return chunks * (size_t)(Cin + 1) * Cout * sizeof(float);
+}
+
+extern "C" int d2mi_wgrad_skinny_levels(const float* const* x, const float* const* g, const int* P,
+                                        int L, int Cin, int Cout, float* gw, float* gb,
+                                        int accumulate, void* workspace, size_t workspace_bytes,
+                                        void* stream) {
+  D2MI_REQUIRE(x && g && P && L > 0 && L <= kSkinnyMaxLevels,
+               "wgrad_skinny_levels: 1..%d levels", kSkinnyMaxLevels);
+  D2MI_REQUIRE(Cin > 0 && Cin % 4 == 0 && Cout > 0 && Cout <= kMaxCout,
+               "wgrad_skinny_levels: Cin=%d (a multiple of 4) Cout=%d (1..%d)", Cin, Cout,
+               kMaxCout);
+  SkinnyLevels lv = {};
+  lv.L = L;
+  lv.cb[0] = 0;
+  for (int l = 0; l < L; ++l) {
+    D2MI_REQUIRE(P[l] > 0 && x[l] && g[l] && ((uintptr_t)x[l] & 15) == 0,
+                 "wgrad_skinny_levels: level %d (P=%d) needs 16-B aligned x", l, P[l]);
+    lv.x[l] = x[l];
+    lv.g[l] = g[l];
+    lv.P[l] = P[l];
+    lv.cb[l + 1] = lv.cb[l] + (P[l] + kChunk4 - 1) / kChunk4;
+  }
+  const size_t need = d2mi_wgrad_skinny_levels_workspace_size(P, L, Cin, Cout);
+  D2MI_REQUIRE(workspace && workspace_bytes >= need,
+               "wgrad_skinny_levels workspace too small: %zu < %zu", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  float* partial = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(wgrad_skinny_partial4_levels_kernel, dim3(lv.cb[L]), dim3(256), 0, st, lv,
+                     Cin, Cout, partial);
+  D2MI_LAUNCH_CHECK();
+  const int n = (Cin + 1) * Cout;
+  hipLaunchKernelGGL(wgrad_skinny_reduce_levels_kernel, dim3((n + kRedOut - 1) / kRedOut),
+                     dim3(256), 0, st, partial, lv, Cin, Cout, gw, gb, accumulate);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

@@ -1961,6 +1961,42 @@ def wgrad_skinny(x, g, with_bias=True, accumulate_into=None):
     return gw, gb
 
 
+def wgrad_skinny_levels(xs, gs, with_bias=True):
+    """wgrad_skinny of several calls sharing one weight, summed in list order
+    (d2mi_wgrad_skinny_levels: one partial launch + one reduce; bit-identical
+    to the calls one by one with accumulate_into after the first).  xs[l]
+    [..., Cin] 16-B aligned with Cin % 4 == 0, gs[l] [..., Cout]."""
+    xs = [_f32c(x) for x in xs]
+    gs = [_f32c(g) for g in gs]
+    _C.require_device(*xs, *gs)
+    Cin, Cout = xs[0].shape[-1], gs[0].shape[-1]
+    Ps = [x.numel() // Cin for x in xs]
+    for x, g, P in zip(xs, gs, Ps):
+        if x.shape[-1] != Cin or g.numel() != P * Cout:
+            raise ValueError(f"wgrad_skinny_levels: {tuple(x.shape)} vs {tuple(g.shape)}")
+    dev = xs[0].device
+    gw = torch.empty((1, 1, Cin, Cout), dtype=torch.float32, device=dev)
+    gb = torch.empty((Cout,), dtype=torch.float32, device=dev) if with_bias else None
+    Pa = _C.host_array(_C.ctypes.c_int32, Ps)
+    lib = _C.lib()
+    wsb = lib.d2mi_wgrad_skinny_levels_workspace_size(Pa, len(xs), Cin, Cout)
+    ws = _C.scratch(wsb, dev)
+    ev = KernelTimer.start()
+    rc = lib.d2mi_wgrad_skinny_levels(_C.host_array(_C.c_void_p, [x.data_ptr() for x in xs]),
+                                      _C.host_array(_C.c_void_p, [g.data_ptr() for g in gs]), Pa,
+                                      len(xs), Cin, Cout, _C.ptr(gw), _C.ptr(gb), 0, _C.ptr(ws),
+                                      wsb, _C.stream_of(dev))
+    KernelTimer.stop(ev, "wgrad_skinny", 4 * sum(Ps) * (Cin + Cout))
+    _C.check(rc, "d2mi_wgrad_skinny_levels")
+    return gw, gb
+
+
+def skinny_levels_ok(x):
+    """Whether a level's input can join wgrad_skinny_levels."""
+    return x.dtype == torch.float32 and x.is_contiguous() and x.shape[-1] % 4 == 0 \
+        and x.data_ptr() % 16 == 0
+
+
 def column_sum(x):
     """Sum over every leading dim of x [..., C] -> [C] (fixed order)."""
     x = _f32c(x)

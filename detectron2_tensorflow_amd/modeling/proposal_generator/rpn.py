@@ -182,6 +182,9 @@ class _RPNHead1x1Fn(torch.autograd.Function):
     # weight gradient, the last one the in-order sum -- autograd's
     # ((g1 + g2) + g3) ... of the per-level gradients, without its adds
     ACC_LEVELS = True
+    # True: the levels' skinny wgrads as ONE multi-level launch pair at the
+    # last level's backward (d2mi_wgrad_skinny_levels, bit-identical sums)
+    LEVELS_ONE_LAUNCH = True
 
     @staticmethod
     def forward(ctx, share, wo, bo, wd, bd, w16, wp, b16, wacc=None):
@@ -218,13 +221,29 @@ class _RPNHead1x1Fn(torch.autograd.Function):
                 # weight gradient (returned by the last level) never leaves
                 # and a stale buffer would poison a later backward
                 handoff.expect_complete(acc, lambda a: a["k"] == 0,
-                                        lambda a: (a.pop("buf", None), a.__setitem__("k", 0)),
+                                        lambda a: (a.pop("buf", None), a.pop("lv", None),
+                                                   a.__setitem__("k", 0)),
                                         "RPN head 1x1 weight-gradient levels")
-            acc["buf"] = ops.wgrad_skinny(share, g16, with_bias=True,
-                                          accumulate_into=acc.get("buf"))
+            if _RPNHead1x1Fn.LEVELS_ONE_LAUNCH:
+                # the levels' (input, gradient) pairs in backward order, one
+                # multi-level skinny wgrad at the last (the same sums)
+                acc.setdefault("lv", []).append((share, g16))
+            else:
+                acc["buf"] = ops.wgrad_skinny(share, g16, with_bias=True,
+                                              accumulate_into=acc.get("buf"))
             if acc["k"] < acc["n"]:
                 return gx, None, None, None, None, None, None, None, None
-            gw, gb = acc.pop("buf")
+            if _RPNHead1x1Fn.LEVELS_ONE_LAUNCH:
+                lv = acc.pop("lv")
+                if len(lv) <= 8 and all(ops.skinny_levels_ok(x) for x, _ in lv):
+                    gw, gb = ops.wgrad_skinny_levels([x for x, _ in lv], [g for _, g in lv])
+                else:
+                    buf = None
+                    for x, g in lv:
+                        buf = ops.wgrad_skinny(x, g, with_bias=True, accumulate_into=buf)
+                    gw, gb = buf
+            else:
+                gw, gb = acc.pop("buf")
             acc["k"] = 0  # (a second backward of the same graph starts over)
         else:
             gw, gb = ops.wgrad_skinny(share, g16, with_bias=True)

@@ -613,6 +613,18 @@ int d2mi_wgrad_skinny(const float* x, const float* g, int P, int Cin, int Cout, 
 int d2mi_wgrad_skinny_ex(const float* x, const float* g, int P, int Cin, int Cout, float* gw,
                          float* gb, int accumulate, void* workspace, size_t workspace_bytes,
                          void* stream);
+/* d2mi_wgrad_skinny_levels: the skinny wgrad of L <= 8 calls sharing one
+ * weight (the RPN head's fused 1x1 over the FPN levels, rpn.py:31-96: one
+ * weight applied per level, its gradient the sum over levels) in one partial
+ * launch and one reduce: x[l] [P[l], Cin] (16-B aligned, Cin % 4 == 0),
+ * g[l] [P[l], Cout]; each level summed exactly as one d2mi_wgrad_skinny call
+ * and the levels added in array order (accumulate != 0: after the old gw /
+ * gb) -- bit-identical to the per-level calls with accumulate after the
+ * first.  workspace >= d2mi_wgrad_skinny_levels_workspace_size. */
+size_t d2mi_wgrad_skinny_levels_workspace_size(const int* P, int L, int Cin, int Cout);
+int d2mi_wgrad_skinny_levels(const float* const* x, const float* const* g, const int* P, int L,
+                             int Cin, int Cout, float* gw, float* gb, int accumulate,
+                             void* workspace, size_t workspace_bytes, void* stream);
 /* Column sums of a row-major [rows, cols] f32 matrix (a conv's bias gradient,
  * TF BiasAddGrad, when its weight gradient runs as a library GEMM): out[cols],
  * fixed-order two-level reduction; workspace from

@@ -552,12 +552,14 @@ def test_fpn_join_engages_and_matches_plain_step(dev, monkeypatch):
         assert torch.equal(grads[True][n], grads[False][n]), n
 
 
-def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch):
+@pytest.mark.parametrize("one_launch", [True, False])
+def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch, one_launch):
     """The RPN head's fused 1x1 and its shared 3x3 accumulate their weight /
     bias gradients over the FPN levels in one buffer each
-    (d2mi_wgrad_skinny_ex accumulate; d2mi_conv2d_wgrad_ex bit 3, levels with
-    one split included): the model's gradients equal those of per-level
-    gradients summed by autograd, bit for bit."""
+    (d2mi_wgrad_skinny_levels -- one launch pair at the last level -- or
+    d2mi_wgrad_skinny_ex accumulate per level; d2mi_conv2d_wgrad_ex bit 3,
+    levels with one split included): the model's gradients equal those of
+    per-level gradients summed by autograd, bit for bit."""
     from detectron2_tensorflow_amd.modeling import build_model
     from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import (StandardRPNHead,
                                                                            _RPNHead1x1Fn)
@@ -569,6 +571,7 @@ def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch):
     batch = synthetic_train_batch(2, 256, 320, 6, dev)
     calibrate_rcnn_scores(model, batch)
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(_RPNHead1x1Fn, "LEVELS_ONE_LAUNCH", one_launch)
     grads = {}
     for acc in (True, False):
         monkeypatch.setattr(_RPNHead1x1Fn, "ACC_LEVELS", acc)

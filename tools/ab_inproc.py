@@ -87,7 +87,12 @@ def _mask_prep_early(on):
     StandardROIHeads.MASK_PREP_EARLY = on
 
 
-SWITCHES = {"mask_prep_early": _mask_prep_early, "gc_off": _gc_off, "defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
+def _skinny_levels(on):
+    from detectron2_tensorflow_amd.modeling.proposal_generator.rpn import _RPNHead1x1Fn
+    _RPNHead1x1Fn.LEVELS_ONE_LAUNCH = on
+
+
+SWITCHES = {"skinny_levels": _skinny_levels, "mask_prep_early": _mask_prep_early, "gc_off": _gc_off, "defer_pixels": _defer_pixels, "rpn_concat": _rpn_concat, "rpn_conv_acc": _rpn_conv_acc, "fpn_join": _fpn_join, "pack_group": _pack_group, "rpn_acc": _rpn_acc,
             "conv_ws": _conv_ws, "conv_epi": _conv_epi,
             "wgrad_ws1": _wgrad_ws1, "stem_mfma": _stem_mfma, "fused_sample": _fused_sample}
 
