@@ -1,4 +1,5 @@
 // Thread-local host error string + the device error word (see include/d2mi.h).
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,6 +46,38 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+namespace {
+__global__ void fill_u32_words_kernel(uint32_t* __restrict__ p, size_t n, uint32_t v) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+__global__ void fill_u8_kernel(uint8_t* __restrict__ p, size_t n, uint8_t v) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+}  // namespace
+
+// A byte fill as a kernel on ``st`` (in place of hipMemsetAsync, r5): inside
+// a captured hipGraph a memset becomes a memset node, and the graphed
+// training step's replays diverged from the eager step only where a buffer
+// zeroed by one fed an atomic accumulation (the matcher's per-GT best IoU)
+// and only when the batch changed -- the node's ordering against the
+// kernels around it is not what the stream order was.  A kernel node is
+// ordered like every other launch of the capture.
+int fill_bytes(void* p, size_t nbytes, uint8_t value, hipStream_t st) {
+  if (nbytes == 0) return 0;
+  if (((uintptr_t)p & 3) == 0 && (nbytes & 3) == 0) {
+    const size_t n = nbytes / 4;
+    const uint32_t v = 0x01010101u * value;
+    hipLaunchKernelGGL(fill_u32_words_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)),
+                       dim3(256), 0, st, (uint32_t*)p, n, v);
+  } else {
+    hipLaunchKernelGGL(fill_u8_kernel, dim3((unsigned)std::min<size_t>((nbytes + 255) / 256, 4096)),
+                       dim3(256), 0, st, (uint8_t*)p, nbytes, value);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int32_t* error_word() {
   void* p = nullptr;
   if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_error_word)) != hipSuccess) return nullptr;
@@ -85,7 +118,8 @@ int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }
 int d2mi_clear_errors(void* stream) {
   int32_t* w = d2mi::error_word();
   D2MI_REQUIRE(w != nullptr, "cannot resolve the device error word");
-  D2MI_HIP(hipMemsetAsync(w, 0, sizeof(int32_t), d2mi::as_stream(stream)));
+  D2MI_REQUIRE(d2mi::fill_bytes(w, sizeof(int32_t), 0, d2mi::as_stream(stream)) == 0,
+               "error word clear failed");
   return 0;
 }
 

@@ -52,4 +52,8 @@ enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi 
                kTuneConvWSMinK = 8, kTuneRoiPixGrid = 9, kTuneCount };
 int tuning(TuneKey k);
 
+// Byte fill by a kernel launch on st (never hipMemsetAsync: errors.hip).
+// 0 on success.
+int fill_bytes(void* p, size_t nbytes, uint8_t value, hipStream_t st);
+
 }  // namespace d2mi

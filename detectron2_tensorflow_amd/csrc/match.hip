@@ -15,6 +15,7 @@
 // same, inter = ih * iw, union = (area_a + area_b) - inter, inter / union
 // (0 when union == 0): the tensor code's order, so labels are identical.
 #include "common.h"
+#include "internal.h"
 
 namespace d2mi {
 namespace {
@@ -224,7 +225,7 @@ static int match_core(const float* gt_boxes, FlagSrc gt_flags, const float* boxe
   if (c.allow_low) {
     D2MI_REQUIRE(workspace && workspace_bytes >= d2mi_match_workspace_size(N, G),
                  "match workspace too small");
-    D2MI_HIP(hipMemsetAsync(best, 0, d2mi_match_workspace_size(N, G), st));
+    D2MI_REQUIRE(fill_bytes(best, d2mi_match_workspace_size(N, G), 0, st) == 0, "fill failed");
     hipLaunchKernelGGL(best_gt_kernel, dim3((P + 1023) / 1024, N), dim3(256), 0, st,
                        reinterpret_cast<const float4*>(gt_boxes), gt_flags,
                        reinterpret_cast<const float4*>(boxes), bstride, G, P, best);

@@ -205,8 +205,9 @@ int nms_sorted(const float4* sboxes, const int32_t* sidx, const int32_t* count, 
   if (S == 0) return 0;
   D2MI_REQUIRE(max_out >= 0, "max_output_size must be >= 0");
   if (cap == 0 || max_out == 0) {
-    D2MI_HIP(hipMemsetAsync(num_keep, 0, S * sizeof(int32_t), stream));
-    if (max_out > 0) D2MI_HIP(hipMemsetAsync(keep, 0xff, (size_t)S * max_out * 4, stream));
+    D2MI_REQUIRE(fill_bytes(num_keep, S * sizeof(int32_t), 0, stream) == 0, "fill failed");
+    if (max_out > 0)
+      D2MI_REQUIRE(fill_bytes(keep, (size_t)S * max_out * 4, 0xff, stream) == 0, "fill failed");
     return 0;
   }
   const int T = (cap + 63) / 64;

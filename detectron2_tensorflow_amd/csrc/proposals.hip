@@ -705,8 +705,8 @@ extern "C" int d2mi_fast_rcnn_inference(const float* logits, const float* deltas
   frcnn_layout(w, &o, N, P, K, cap, max_det);
   D2MI_REQUIRE(w.ok(), "fast_rcnn workspace too small (%zu < %zu)", workspace_bytes, w.off);
   int32_t* err = error_word();
-  D2MI_HIP(hipMemsetAsync(o.slot2roi, 0xff, (size_t)N * P * 4, st));
-  D2MI_HIP(hipMemsetAsync(o.cnt, 0, N * 4, st));
+  D2MI_REQUIRE(fill_bytes(o.slot2roi, (size_t)N * P * 4, 0xff, st) == 0, "fill failed");
+  D2MI_REQUIRE(fill_bytes(o.cnt, (size_t)N * 4, 0, st) == 0, "fill failed");
   hipLaunchKernelGGL(fill_u32_kernel, dim3((N + 255) / 256), dim3(256), 0, st, o.maxc, N,
                      0x80000000u /* orderable(+0.0f) */);
   D2MI_LAUNCH_CHECK();

@@ -11,6 +11,7 @@
 // Three launches per call (block counts, selection + selected counts, order)
 // replace ~50 small torch / top-k launches per training step.
 #include "common.h"
+#include "internal.h"
 
 namespace d2mi {
 namespace {
@@ -256,8 +257,8 @@ extern "C" int d2mi_subsample(const int64_t* labels, int N, int P, long long bg_
   hipStream_t st = as_stream(stream);
   if (P == 0) {
     if (order_out && S > 0) {
-      D2MI_HIP(hipMemsetAsync(order_out, 0, (size_t)N * S * sizeof(int64_t), st));
-      D2MI_HIP(hipMemsetAsync(order_valid, 0, (size_t)N * S, st));
+      D2MI_REQUIRE(fill_bytes(order_out, (size_t)N * S * sizeof(int64_t), 0, st) == 0, "fill failed");
+      D2MI_REQUIRE(fill_bytes(order_valid, (size_t)N * S, 0, st) == 0, "fill failed");
     }
     return 0;
   }

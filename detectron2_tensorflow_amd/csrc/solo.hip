@@ -861,7 +861,7 @@ extern "C" int d2mi_solo_select(const float* probs, const int32_t* live_row,
   const size_t tk_bytes = topk_workspace_size(N, k);
   void* tk_ws = w.take<char>(tk_bytes);
   D2MI_REQUIRE(w.ok(), "SOLO select workspace too small (%zu < %zu)", workspace_bytes, w.off);
-  D2MI_HIP(hipMemsetAsync(valid, 0, sizeof(int32_t) * N, st));
+  D2MI_REQUIRE(fill_bytes(valid, sizeof(int32_t) * N, 0, st) == 0, "fill failed");
   const size_t total = (size_t)N * T * K;
   hipLaunchKernelGGL(solo_cand_kernel, dim3(grid_for(std::max(total, (size_t)N), 256)),
                      dim3(256), 0, st, lv, probs, live_row, row_off, sum_masks, sum_scores, N, K,
@@ -897,7 +897,7 @@ extern "C" int d2mi_solo_matrix_nms(const uint64_t* mask_bits, const int64_t* cl
   int32_t* inter = w.take<int32_t>((size_t)N * k * k);
   float* comp = w.take<float>((size_t)N * k);
   D2MI_REQUIRE(w.ok(), "SOLO Matrix-NMS workspace too small (%zu < %zu)", workspace_bytes, w.off);
-  D2MI_HIP(hipMemsetAsync(inter, 0, sizeof(int32_t) * (size_t)N * k * k, st));
+  D2MI_REQUIRE(fill_bytes(inter, sizeof(int32_t) * (size_t)N * k * k, 0, st) == 0, "fill failed");
   const int tiles = (k + kMT - 1) / kMT;
   // word slices: enough workgroups to fill the chip (>= ~4 per CU over the
   // upper-triangle tiles), at least one LDS stage each

@@ -170,6 +170,7 @@ class GraphedTrainer(Trainer):
         torch.cuda.synchronize(dev)
         self._pool = torch.cuda.graph_pool_handle()
         g = self._new_graph()
+        capture.begin(dev)  # (outside the capture: see utils/capture.py)
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             losses = self.model(self._static)
@@ -194,6 +195,13 @@ class GraphedTrainer(Trainer):
         self.optimizer.zero_grad()
         keep = []
         g = self._new_graph()
+        dev = self._lr_dev.device
+        # the loss values land in a buffer of the ordinary pool: no later
+        # capture's temporary (the shared pool) can overwrite them before the
+        # host reads them
+        nvals = len(self._losses) + 1
+        vals = torch.empty(nvals, dtype=torch.float32, device=dev)
+        capture.begin(dev)
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             out = {k: (v.compute(rows) if isinstance(v, DeferredMaskLoss) else v)
@@ -207,8 +215,9 @@ class GraphedTrainer(Trainer):
             total.backward(seed, retain_graph=True)
             self.reducer.finish()
             self.optimizer.step_captured(self._lr_dev)
-            values = torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()])
+            vals.copy_(torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()]))
         capture.flush(keep)
+        values = vals
         self._dump(g, f"B{rows}")
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
@@ -244,4 +253,6 @@ class GraphedTrainer(Trainer):
         g.replay()
         self.replays += 1
         self.iter += 1
+        # (a copy: the next replay rewrites ``values``)
+        values = values.clone()
         return {k: values[i] for i, k in enumerate(keys)}

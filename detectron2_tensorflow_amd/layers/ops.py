@@ -1268,7 +1268,8 @@ class _HostTable:
     buffers (each slot reused once its previous copy has left, by event)."""
     RING = 4
 
-    def __init__(self, nbytes, device):
+    def __init__(self, nbytes, device, what="table"):
+        self.what = what
         self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
         self.ring = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(self.RING)]
         self.events = [None] * self.RING
@@ -1276,7 +1277,7 @@ class _HostTable:
 
     def upload(self, arr):
         if capture.capturing():  # a per-graph table, filled after the capture
-            return capture.table(arr, self.dev.device)
+            return capture.table(arr, self.dev.device, self.what)
         k = self.i
         self.i = (k + 1) % self.RING
         if self.events[k] is not None:
@@ -1300,7 +1301,8 @@ def _fold_table(kind, n, device):
         _C.lib().d2mi_fold_many_sizes(_C.ctypes.byref(sz), _C.ctypes.byref(chunks))
         if sz.value != _FOLD_DT.itemsize:
             raise RuntimeError("d2mi_fold_entry layout mismatch")
-        t = _fold_tables[key] = (_HostTable(n * _FOLD_DT.itemsize, device), chunks.value)
+        t = _fold_tables[key] = (_HostTable(n * _FOLD_DT.itemsize, device, f"fold {kind}"),
+                                 chunks.value)
     return t
 
 

@@ -133,7 +133,7 @@ class MomentumSGD:
             if g is not None and not g.is_contiguous():
                 raise RuntimeError("captured Momentum-SGD needs contiguous gradients")
             tab["g"][i] = 0 if g is None else g.data_ptr()
-        dev_tab = capture.table(tab, self._tab_dev.device)
+        dev_tab = capture.table(tab, self._tab_dev.device, "momentum-sgd")
         rc = self._lib.d2mi_momentum_sgd_ex(_C.ptr(dev_tab), _C.ptr(self._chunks_dev), self._nchunks,
                                             _C.ptr(self._partial), float(self.clip_norm),
                                             float(self.momentum), 0.0, _C.ptr(lr_dev),
