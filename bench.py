@@ -35,6 +35,11 @@ import os
 import sys
 import time
 
+# before the HIP runtime starts: the hipGraph-replayed step (--graphs) needs
+# the runtime's graph packet capture off (engine/graphed.py); eager steps
+# launch no graphs
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -73,7 +78,11 @@ def parse():
     p.add_argument("--width", type=int, default=1333)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
     p.add_argument("--cpu-images", type=int, default=2, help="images per CPU iteration (<= batch)")
-    p.add_argument("--cpu-iters", type=int, default=3, help="timed CPU iterations (median)")
+    p.add_argument("--cpu-iters", type=int, default=5,
+                   help="timed CPU iterations (median).  BASELINE.md section 2 asks 3 warm-ups + "
+                        "the median of 20 per OP (cpu_per_op_c2 does that); a whole training "
+                        "iteration takes ~4 s on 16 threads, so the step-level sample is bounded "
+                        "to 1 warm-up + the median of 5 (~25 s, the CPU-sample budget)")
     p.add_argument("--cpu-one-core", type=int, default=1, help="also time 1 image on 1 core")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--no-calibration", action="store_true",
@@ -84,6 +93,13 @@ def parse():
     p.add_argument("--mask-format", default="conventional", choices=["conventional", "raw", "fixed"],
                    help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
+    p.add_argument("--graphs", type=int, default=1,
+                   help="train: replay the step from hipGraphs (engine/graphed.py; world size 1 "
+                        "-- other world sizes run the eager step); 0 = the eager Trainer.step")
+    p.add_argument("--fixed-rows-steps", type=int, default=10,
+                   help="train (default run): after the main timed region, also time this many "
+                        "steps with the fixed 256-row mask branch (a second object in the "
+                        "line); 0 = skip")
     p.add_argument("--mask-fixed-rows", action="store_true",
                    help="train: the mask head on the fixed BATCH_SIZE_PER_IMAGE x "
                         "POSITIVE_FRACTION rows per image (128 at the defaults, "
@@ -534,6 +550,9 @@ def cpu_baseline(args, model, batch, cfg=None):
         med, ts = _median_time(lambda: run(n, cores), iters)
     out = {"value": round(n / med, 4), "unit": "img/s", "cores": cores, "kind": "port",
            "cpu_model": cpu_model_name(),
+           "protocol": (f"1 warm-up iteration (256x320) + the median of {iters} timed iterations "
+                        "(BASELINE.md section 2's 3 + 20 applies per op: per_op_c2; a whole "
+                        "iteration is seconds long, so the step-level sample is bounded)"),
            "sample": f"median of {iters} x {n} image(s) {args.height}x{args.width} "
                      f"({', '.join(f'{t:.2f}' for t in ts)} s), {args.model} {what}, "
                      f"TF-1.15-semantics CPU restatement (oracle/: C kernels + torch-CPU "
@@ -546,6 +565,45 @@ def cpu_baseline(args, model, batch, cfg=None):
         out["sample_1core"] = f"1 x 1 image, 1 thread (threadpoolctl + torch), {t1:.1f} s"
     out.update(extra)
     return out
+
+
+def fixed_rows_region(args, trainer, batch, rh, world, device):
+    """The training step with the mask branch on the fixed BATCH_SIZE_PER_IMAGE
+    x POSITIVE_FRACTION slots per image (mask_compact_rows False: 256 rows at
+    bs 2), timed like the main region (warm-up, barrier + synchronize on both
+    sides, max over ranks) right after it, on the same model and batch: the
+    heavier mask branch a trained model's foreground count approaches."""
+    rh.mask_compact_rows = False
+    # (a graphed trainer's graphs are captured for the compacted branch: the
+    # fixed-rows steps run its eager step)
+    step = getattr(trainer, "eager_step", trainer.step)
+    try:
+        with torch.enable_grad():
+            for _ in range(max(1, args.warmup)):
+                step(batch)
+            torch.cuda.synchronize()
+            if world > 1:
+                torch.distributed.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.fixed_rows_steps):
+                step(batch)
+            torch.cuda.synchronize()
+            if world > 1:
+                torch.distributed.barrier()
+            el = time.perf_counter() - t0
+        rows = rh.last_mask_rows
+    finally:
+        rh.mask_compact_rows = True
+    if world > 1:
+        t = torch.tensor([el], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return {"value": round(world * args.batch * args.fixed_rows_steps / el, 3), "unit": "img/s",
+            "ms_per_step": round(1e3 * el / args.fixed_rows_steps, 3),
+            "steps": args.fixed_rows_steps, "mask_head_rows": rows,
+            "step_launch": "eager",
+            "note": "same process, model and batch as the main line, timed after it; mask head "
+                    "on every sampled foreground slot (roi_heads.mask_compact_rows = False)"}
 
 
 def main():
@@ -579,9 +637,16 @@ def main():
         if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
             model.roi_heads.mask_compact_rows = False
             PMC_SKIP.update({"roi_align_fwd_mask", "roi_align_bwd"})
-        trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        if args.graphs and world == 1:
+            from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
+            trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+        else:
+            trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
-        timed_step = step
+        # the kernel-timing step (HIP events around every launch) runs eagerly:
+        # a replayed graph has no per-launch events
+        timed_step = (lambda: trainer.eager_step(batch)) if getattr(trainer, "enabled",
+                                                                    False) else step
         grad_ctx = torch.enable_grad
     else:
         fwd = model if is_single_stage(model) else model.inference
@@ -630,6 +695,12 @@ def main():
         t = torch.tensor([elapsed], device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    fixed_rows = None
+    rh = getattr(model, "roi_heads", None)
+    main_rows = getattr(rh, "last_mask_rows", None)
+    if (args.mode == "train" and args.fixed_rows_steps > 0 and not args.mask_fixed_rows
+            and getattr(rh, "mask_on", False)):
+        fixed_rows = fixed_rows_region(args, trainer, batch, rh, world, device)
     _C.raise_on_errors(device)
     in_sync = None
     if world > 1 and args.mode == "train":
@@ -648,11 +719,10 @@ def main():
             # when its all-reduce completed, relative to the end of backward;
             # exposed_ms = the all-reduce time the backward did not hide
             extra["allreduce_rank0"] = tl
-        rh = getattr(model, "roi_heads", None)
-        if getattr(rh, "last_mask_rows", None) is not None:
-            # mask head rows of the last step: the foreground ROIs (as the
+        if main_rows is not None:
+            # mask head rows of the last timed step: the foreground ROIs (as the
             # reference) padded to a multiple of MASK_ROW_BUCKET
-            extra["mask_head_rows_last_step_rank0"] = rh.last_mask_rows
+            extra["mask_head_rows_last_step_rank0"] = main_rows
     else:
         extra = {"detections_per_step_rank0": int(out["instances"]["is_valid"].sum().item())}
 
@@ -681,9 +751,16 @@ def main():
                                if args.mode == "train" else {}),
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
                             else f"{sample + 1}/{args.steps}",
-
+                            **({"step_launch": (f"hipGraph replays ({trainer.replays} in warmup + "
+                                                "timed; the kernel-timing step eager)")
+                                if getattr(trainer, "enabled", False) else "eager"}
+                               if args.mode == "train" else {}),
                             **({"mask_format": args.mask_format} if args.mode == "infer" else {})},
                        **extra),
+            # the same workload with the mask head on every sampled foreground
+            # slot (256 rows: the reference's ceiling, defaults.py:413-415),
+            # timed after the main region in the same process
+            **({"fixed_mask_rows": fixed_rows} if fixed_rows is not None else {}),
             # the dominant hot-path kernel: the split-product conv (else f32)
             "roofline": kernels.get("conv2d_split", kernels.get("conv2d_mfma")),
             **({"replicas_in_sync": in_sync} if in_sync is not None else {}),

@@ -30,6 +30,13 @@ def read_tensor_file(path):
     raise ValueError(f"unsupported checkpoint format {ext!r} (use .npz, .safetensors, .pth)")
 
 
+OPTIONAL_STATE = ("loss_normalizer",)
+
+
+def _optional_state(name):
+    return name.rsplit("/", 1)[-1] in OPTIONAL_STATE
+
+
 @torch.no_grad()
 def load_reference_weights(model, tensors, strict=True):
     """Copy {reference variable name: array} into the model's parameters and
@@ -37,7 +44,9 @@ def load_reference_weights(model, tensors, strict=True):
     norm/gamma).  Returns (missing, unexpected) name lists; strict raises on
     either, and on any shape mismatch."""
     own = dict(model.reference_variables(include_scope=False))
-    missing = [k for k in own if k not in tensors]
+    # training-only state no detectron2 checkpoint carries (the RetinaNet
+    # loss-normaliser EMA): optional, keeps its initial value when absent
+    missing = [k for k in own if k not in tensors and not _optional_state(k)]
     unexpected = [k for k in tensors if k not in own]
     if strict and (missing or unexpected):
         raise KeyError(f"missing {missing[:5]}... ({len(missing)}), "
@@ -56,4 +65,13 @@ def load_detectron2_checkpoint(model, path_or_dict, cfg, strict=True):
     """detectron2 weights (file or {name: array}) -> convert_weights
     (lib/convert_models/convert_d2.py) -> the model."""
     d = read_tensor_file(path_or_dict) if isinstance(path_or_dict, str) else dict(path_or_dict)
-    return load_reference_weights(model, convert_weights(d, cfg), strict=strict)
+    tensors = convert_weights(d, cfg)
+    # The reference converter names the RetinaNet tower "head/<conv>"
+    # (convert_d2.py:77-81), its model scopes it "head/head/<conv>" (the
+    # detector's "head" scope around RetinaNetHead's "head", retinanet.py:83,
+    # single_stage_detector.py:26): a converted name the model lacks is looked
+    # up under the tower scope too.
+    own = {k for k, _ in model.reference_variables(include_scope=False)}
+    tensors = {(("head/" + k) if k not in own and k.startswith("head/") and "head/" + k in own
+                else k): v for k, v in tensors.items()}
+    return load_reference_weights(model, tensors, strict=strict)

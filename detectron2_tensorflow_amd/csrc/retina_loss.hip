@@ -73,9 +73,10 @@ __device__ __forceinline__ float focal_grad(float x, float t, float alpha, float
   const float q = 1.f - pt;
   const float dp = p * (1.f - p);
   const float dpt = dp * t - dp * (1.f - t);
-  // d(q^gamma)/dx = gamma q^(gamma - 1) * (-d p_t)
-  const float dmod = gamma * powf(q, gamma - 1.f) * -dpt;
-  float g = (p - t) * powf(q, gamma) + ce * dmod;
+  // d(q^gamma)/dx = gamma q^(gamma - 1) * (-d p_t); 0 for gamma = 0 (plain
+  // BCE: torch's pow backward for a zero exponent) -- q^(-1) is inf at q = 0
+  const float dmod = gamma == 0.f ? 0.f : gamma * powf(q, gamma - 1.f) * -dpt;
+  float g = (p - t) * (gamma == 0.f ? 1.f : powf(q, gamma)) + ce * dmod;
   if (alpha >= 0.f) g = (alpha * t + (1.f - alpha) * (1.f - t)) * g;
   return g;
 }

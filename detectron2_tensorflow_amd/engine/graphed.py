@@ -1,7 +1,24 @@
-"""EXPERIMENTAL (r4, not used by bench.py or the tests): the training step
-replayed from hipGraphs (lib/engine/trainer.py:116-199).  Status: graph A
-replays bit-exactly (tools/graph_bisect.py stages 0-8); the first replay of a
-backward graph B[R] faulted the GPU (twice, r4) and the cause is not found.
+"""The training step replayed from hipGraphs (lib/engine/trainer.py:116-199).
+
+Status (r5): bit-identical to ``Trainer.step`` over steps that change the
+batch and the mask-branch row count (tests/test_gpu_graphed.py).  Two causes
+of the r4 failures were found and fixed:
+
+* the replay FAULTS: host-filled launch tables (fold / optimizer pointer
+  tables) were allocated inside the capture, from the graph pool, where a
+  captured temporary could share their bytes and overwrite them at replay
+  (utils/capture.py; tools/graph_audit.py proves it from the allocator trace:
+  15 of 17 tables overlapped captured allocations, 0 with the fix);
+* the replay DIVERGENCE once the batch changes: memset nodes are not ordered
+  against the kernel nodes around them when the HIP runtime pre-records the
+  graph's kernels as AQL packets (its graph "packet capture"): the matcher's
+  zeroed per-GT best IoU (an atomic max) and torch's global-reduction
+  semaphores (the box head's bias gradient) kept a previous replay's values
+  (tools/graph_diff.py: eager-exact with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0,
+  divergent with it on).  The library now fills with kernels instead of
+  hipMemsetAsync, and the graphed step requires
+  DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before the HIP runtime
+  starts (torch's own memsets remain in the graphs).
 
 The eager ``Trainer.step`` enqueues ~550 launches per iteration from Python
 (autograd engine, custom Functions, ctypes): on an MI355X that host work is
@@ -33,6 +50,8 @@ re-packs every trainable layer at each replay; nothing bumps a version while
 the graphs are in use, and an eager step (``eager_step``) marks them stale
 again first.  A multi-rank job runs the eager step (see __init__).
 """
+import os
+
 import torch
 
 from ..modeling.roi_heads.roi_heads import DeferredMaskLoss, StandardROIHeads
@@ -64,12 +83,13 @@ class GraphedTrainer(Trainer):
     process group has more than one rank."""
 
     def __init__(self, cfg, model, warmup=1, experimental=False, **kwargs):
-        if not experimental:
+        """experimental: accepted for the r4 call sites (no longer needed)."""
+        if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
             raise RuntimeError(
-                "GraphedTrainer is experimental (r4): graph A (the forward) replays bit-exactly "
-                "stage by stage (tools/graph_bisect.py), but replaying a backward graph B[R] "
-                "faulted the GPU on its first replay and the cause is not found; pass "
-                "experimental=True only for that diagnosis")
+                "GraphedTrainer needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before "
+                "the HIP runtime starts: with the runtime's graph packet capture on, memset "
+                "nodes are not ordered against the kernels around them and replays diverge "
+                "(see engine/graphed.py)")
         super().__init__(cfg, model, **kwargs)
         # >= 1: the first eager step makes the per-shape caches, workspaces and
         # the optimizer / fold tables, none of which may be created in a capture

@@ -32,6 +32,11 @@ from .build import SINGLE_STAGE_HEADS_REGISTRY
 FUSED_LOSSES = True
 
 
+def _world():
+    d = torch.distributed
+    return d.get_world_size() if d.is_available() and d.is_initialized() else 1
+
+
 class RetinaNetBoxTower(Layer):
     def __init__(self, cfg, input_shape, num_anchors, **kwargs):
         super().__init__(**kwargs)
@@ -123,7 +128,9 @@ class RetinaNetHead(Layer):
         matches, labels = match_boxes(self.matcher, gt_boxes, valid, anchors)
         K = self.num_classes
         A = self.anchor_generator.num_cell_anchors[0]
-        if anchors.is_cuda and FUSED_LOSSES:
+        # the fused kernels read the logits as float4 class quads (K % 4 == 0,
+        # e.g. COCO's 80); any other class count takes the tensor formulation
+        if anchors.is_cuda and FUSED_LOSSES and K % 4 == 0:
             cls_sum, box_sum = ops.retina_loss(
                 box_cls, box_delta, anchors, gt_boxes, gt_classes, matches, labels, K, A,
                 self.focal_loss_alpha, self.focal_loss_gamma, self.smooth_l1_loss_beta,
@@ -135,6 +142,13 @@ class RetinaNetHead(Layer):
             # moving_averages.assign_moving_average(zero_debias=False):
             # v -= (v - value) * (1 - momentum), value = max(1, #foreground)
             nfg = (labels == 1).sum().to(torch.float32).clamp(min=1.0)
+            world = _world()
+            if world > 1:
+                # one normaliser for every replica (the reference's single
+                # shared variable): the mean of the ranks' max(1, #fg), so the
+                # replicas scale their losses alike and stay in sync
+                torch.distributed.all_reduce(nfg)
+                nfg = nfg / world
             v = self.loss_normalizer
             v.sub_((v - nfg) * (1.0 - self.loss_normalizer_momentum))
         norm = self.loss_normalizer.clone()  # (the next step's update stays out of this graph)

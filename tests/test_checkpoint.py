@@ -11,6 +11,7 @@ tests/golden/convert_d2_golden.npz (five layouts, bit-equal arrays).  No
 real detectron2 checkpoint is here, so the AP of converted weights is
 unmeasured."""
 import os
+import re
 
 import numpy as np
 import pytest
@@ -44,6 +45,8 @@ def _export_d2(model, cfg):
     ren = {"gamma": "norm.weight", "beta": "norm.bias", "moving_mean": "norm.running_mean",
            "moving_variance": "norm.running_var"}
     for name, t in model.reference_variables(include_scope=False):
+        if name.endswith("/loss_normalizer"):  # training state: in no detectron2 checkpoint
+            continue
         v = t.detach().numpy().copy()
         parts = name.split("/")
         leaf = parts[-1]
@@ -56,7 +59,9 @@ def _export_d2(model, cfg):
             else:
                 src = f"backbone.bottom_up.{p[0]}.{int(p[1].split('_')[1]) - 1}.{p[2]}"
         elif path.startswith("neck/"):
-            src = "backbone." + mod[1]
+            src = "backbone." + ".".join(mod[1:])  # (neck/top_block/p6 -> backbone.top_block.p6)
+        elif path.startswith("head/head/"):  # the RetinaNet tower (cls_subnet0 -> cls_subnet.0)
+            src = "head." + re.sub(r"(subnet)(\d+)$", r"\1.\2", mod[2])
         elif path.startswith("proposal_generator/rpn_head"):
             src = "proposal_generator.rpn_head." + {"share": "conv"}.get(mod[2], mod[2])
         elif path.startswith("roi_heads/box_predictor"):
@@ -67,7 +72,7 @@ def _export_d2(model, cfg):
         if leaf in ren:
             d[f"{src}.{ren[leaf]}"] = v
             continue
-        is_box = mod[-1] in ("anchor_deltas", "box_deltas")
+        is_box = mod[-1] in ("anchor_deltas", "box_deltas", "bbox_pred")
         if leaf == "bias":
             d[src + ".bias"] = v[_box_indices(v.shape[0] // 4)] if is_box else v
             continue
@@ -96,17 +101,29 @@ def test_reference_variable_names_follow_the_reference_scopes():
         assert want in names, want
 
 
-def test_detectron2_round_trip_loads_every_variable():
+@pytest.mark.parametrize("yaml", ["COCO-InstanceSegmentation/mask_rcnn_R_50_FPN_1x.yaml",
+                                  "COCO-Detection/retinanet_R_50_FPN_1x.yaml"])
+def test_detectron2_round_trip_loads_every_variable(yaml):
+    """Export -> convert -> strict load.  RetinaNet: its
+    loss-normaliser EMA is training state no checkpoint carries -- the strict
+    load must not ask for it, and it keeps its initial 100."""
     from detectron2_tensorflow_amd.checkpoint import load_detectron2_checkpoint
-    cfg, a = _model(0)
-    _, b = _model(1)
+    cfg, a = _model(0, yaml)
+    _, b = _model(1, yaml)
     d = _export_d2(a, cfg)
     assert len(d) > 300 and "backbone.bottom_up.res2.0.conv1.norm.running_var" in d
+    if "retinanet" in yaml:
+        assert "head.cls_subnet.0.weight" in d and "backbone.top_block.p6.weight" in d
+        with torch.no_grad():
+            b.detector.loss_normalizer.fill_(100.0)
     missing, unexpected = load_detectron2_checkpoint(b, d, cfg)
     assert not missing and not unexpected
     for (na, ta), (nb, tb) in zip(a.reference_variables(include_scope=False),
                                   b.reference_variables(include_scope=False)):
         assert na == nb
+        if na.endswith("/loss_normalizer"):
+            assert float(tb) == 100.0
+            continue
         torch.testing.assert_close(tb, ta, rtol=0, atol=0, msg=na)
 
 

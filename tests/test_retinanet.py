@@ -208,7 +208,8 @@ def _train_cfg(depth=50):
 
 
 @pytest.mark.gpu
-def test_retina_fused_loss_matches_dense_formulation(dev):
+@pytest.mark.parametrize("gamma", [None, 0.0])
+def test_retina_fused_loss_matches_dense_formulation(dev, gamma):
     """d2mi_retina_loss_fwd / _bwd (csrc/retina_loss.hip) against the tensor
     formulation of RetinaNet.losses (retinanet.py:147-210: one-hot targets,
     sigmoid_focal_loss "sum" over the valid anchors, smooth-L1 "sum" over the
@@ -222,6 +223,8 @@ def test_retina_fused_loss_matches_dense_formulation(dev):
     feats = cfg.MODEL.SINGLE_STAGE_HEAD.IN_FEATURES
     strides = {f: 2 ** int(f[1:]) for f in feats}
     head = RetinaNetHead(cfg, {f: ShapeSpec(channels=16, stride=strides[f]) for f in feats}).to(dev)
+    if gamma is not None:  # plain BCE (q^(gamma-1) at a saturated logit)
+        head.focal_loss_gamma = gamma
     rng = np.random.default_rng(1)
     N, H, W, G, K = 2, 256, 320, 7, 80
     A = head.anchor_generator.num_cell_anchors[0]
@@ -237,7 +240,9 @@ def test_retina_fused_loss_matches_dense_formulation(dev):
     gcls = t(rng.integers(0, K, (N, G)))
     m, lab = match_boxes(head.matcher, t(gt), t(valid), anchors)
     assert int((lab == 1).sum()) > 10 and int((lab == -1).sum()) > 10
-    cls = [t(rng.normal(-3, 1.5, (N, h, w, A * K)).astype(F32)).requires_grad_() for h, w in grids]
+    cls = [rng.normal(-3, 1.5, (N, h, w, A * K)).astype(F32) for h, w in grids]
+    cls[0][..., :7] = -30.0  # saturated: q = 1 - p_t rounds to 0 on the negatives
+    cls = [t(c).requires_grad_() for c in cls]
     box = [t(rng.normal(0, 0.3, (N, h, w, A * 4)).astype(F32)).requires_grad_() for h, w in grids]
     got = ops.retina_loss(cls, box, anchors, t(gt), gcls, m, lab, K, A, head.focal_loss_alpha,
                           head.focal_loss_gamma, head.smooth_l1_loss_beta,
@@ -248,7 +253,35 @@ def test_retina_fused_loss_matches_dense_formulation(dev):
     for a, b in zip(got, want):
         assert float(a) == pytest.approx(float(b), rel=1e-5)
     for a, b in zip(gg, gw):
+        assert torch.isfinite(a).all()
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_retinanet_odd_class_count_takes_the_tensor_losses(dev):
+    """NUM_CLASSES % 4 != 0: the fused kernels read float4 class
+    quads, so such a head takes the tensor formulation on the GPU instead of
+    raising (both losses finite)."""
+    from detectron2_tensorflow_amd.layers import ShapeSpec
+    from detectron2_tensorflow_amd.modeling.single_stage_heads.retinanet import RetinaNetHead
+    cfg = _train_cfg()
+    cfg.defrost()
+    cfg.MODEL.SINGLE_STAGE_HEAD.NUM_CLASSES = 3
+    cfg.freeze()
+    feats = cfg.MODEL.SINGLE_STAGE_HEAD.IN_FEATURES
+    strides = {f: 2 ** int(f[1:]) for f in feats}
+    torch.manual_seed(0)
+    head = RetinaNetHead(cfg, {f: ShapeSpec(channels=16, stride=strides[f]) for f in feats}).to(dev)
+    head.train()
+    assert head.num_classes == 3
+    H, W = 128, 160
+    fm = [torch.randn(1, -(-H // strides[f]), -(-W // strides[f]), 16, device=dev) for f in feats]
+    box_cls, box_delta = head.head(fm)
+    gt = {"gt_boxes": torch.tensor([[[10., 12., 90., 120.], [40., 50., 70., 100.]]], device=dev),
+          "gt_classes": torch.tensor([[1, 2]], device=dev),
+          "is_valid": torch.ones(1, 2, dtype=torch.bool, device=dev)}
+    out = head.losses(fm, box_cls, box_delta, gt)
+    assert torch.isfinite(out["loss_cls"]) and torch.isfinite(out["loss_box_reg"])
 
 
 @pytest.mark.gpu

@@ -22,6 +22,10 @@ import argparse
 import os
 import sys
 
+# before the HIP runtime starts: the graphed step needs the runtime's graph
+# packet capture off (engine/graphed.py); nothing else launches graphs
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,6 +58,9 @@ def main():
     ap.add_argument("--no-arena", action="store_true",
                     help="tables from the capture pool (the r4 code path)")
     ap.add_argument("--expect-clean", action="store_true")
+    ap.add_argument("--ops", action="store_true",
+                    help="also list the aten ops issued inside the captures (a census of the "
+                         "ops that can put memset / memcpy nodes into the graphs)")
     a = ap.parse_args()
     from detectron2_tensorflow_amd import _C
     from detectron2_tensorflow_amd.engine import graphed
@@ -93,9 +100,25 @@ def main():
     capture.issued.clear()
     torch.cuda.memory._record_memory_history(enabled="all", context=None, stacks="python",
                                              max_entries=20_000_000)
+    import collections
+    from torch.utils._python_dispatch import TorchDispatchMode
+    census = collections.Counter()
+
+    class Census(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            if capture.capturing():
+                shapes = [tuple(a.shape) for a in args if torch.is_tensor(a)][:2]
+                census[(str(func), str(shapes))] += 1
+            return func(*args, **(kwargs or {}))
+
+    mode = Census() if a.ops else None
     try:
         # A and every B[R]: captured, tables flushed -- nothing replayed
-        tr._on_stream(tr._capture_forward, batch)
+        if mode is not None:
+            with mode:
+                tr._on_stream(tr._capture_forward, batch)
+        else:
+            tr._on_stream(tr._capture_forward, batch)
         torch.cuda.synchronize()
         snap = torch.cuda.memory._snapshot()
     finally:
@@ -141,6 +164,10 @@ def main():
     print(f"audit: {bad} of {len(capture.issued)} tables share memory with captured "
           f"temporaries ({'tables from the capture pool (r4)' if a.no_arena else 'table arena (r5)'})",
           flush=True)
+    if a.ops:
+        print("aten ops inside the captures (op, first shapes): count", flush=True)
+        for (op, sh), c in sorted(census.items(), key=lambda kv: -kv[1]):
+            print(f"  {c:5d}  {op}  {sh}", flush=True)
     if a.expect_clean and bad:
         sys.exit(1)
 

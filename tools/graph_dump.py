@@ -64,8 +64,8 @@ def main():
         for n, c in names.most_common(80):
             print(f"  {c:4d}  {n}")
         for line in txt.splitlines():
-            if re.search(r"(?i)memcpy|host", line):
-                print("  MEMCPY/HOST:", line[:300])
+            if re.search(r"(?i)memcpy|memset|host", line):
+                print("  MEMCPY/MEMSET/HOST:", line[:300])
 
 
 if __name__ == "__main__":
