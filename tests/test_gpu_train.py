@@ -367,21 +367,9 @@ def test_fused_rpn_loss_matches_tensor_formulation(dev):
     assert ds.grad is not None and not ds.grad.any()
 
 
-def test_whole_training_step_matches_cpu_restatement(dev):
-    """One HIP Trainer.step vs oracle/cpu_train.py's CPUTrainStep.step on
-    identical weights and batch (lib/engine/trainer.py:116-139,
-    model_deploy.py:203-205), with EVERY candidate sampled: the RPN and ROI
-    batch sizes exceed the candidate counts (2^20 anchors per image at
-    positive fraction 0.5; 200 train proposals + GT per image under 512 at
-    fraction 1.0), so the random subsampling is a permutation and every loss
-    is order-invariant.  Pins A14 (RPN losses), A18 (label + sample), A19
-    (box losses), A20 (mask loss) and A23 (clip_by_norm + Momentum-SGD)
-    together: losses to 1e-4 relative, the updated FPN / RPN / ROI-head
-    weights to 1e-4 of their scale, and their updates w1 - w0 to 5e-3 of the
-    update's scale per tensor plus 4 ulp of the weight (an f32 weight of 0.03
-    rounds its update to ~2e-9; ReLU units within f32 noise of zero pass or
-    block their gradient differently: the box head's updates differ by
-    ~1.5e-3), for the tensors whose update exceeds 100 such ulps."""
+def _whole_step_vs_cpu(dev, height, width, post_topk, roi_batch, seed=3):
+    """One HIP Trainer.step vs oracle/cpu_train.py at height x width (see the
+    callers), every RPN anchor and ROI candidate sampled."""
     import cpu_train
     from detectron2_tensorflow_amd.config import finalize, get_cfg
     from detectron2_tensorflow_amd.engine import Trainer
@@ -396,14 +384,15 @@ def test_whole_training_step_matches_cpu_restatement(dev):
     cfg.SOLVER.WARMUP_ITERS = 0
     cfg.SOLVER.IMS_PER_BATCH_BASE = 2
     cfg.MODEL.RPN.BATCH_SIZE_PER_IMAGE = 1 << 20
-    cfg.MODEL.RPN.POST_NMS_TOPK_TRAIN = 200
-    cfg.MODEL.ROI_HEADS.BATCH_SIZE_PER_IMAGE = 512
+    if post_topk is not None:
+        cfg.MODEL.RPN.POST_NMS_TOPK_TRAIN = post_topk
+    cfg.MODEL.ROI_HEADS.BATCH_SIZE_PER_IMAGE = roi_batch
     cfg.MODEL.ROI_HEADS.POSITIVE_FRACTION = 1.0
     finalize(cfg, True, 1, CATS)
     torch.manual_seed(0)
     model = build_model(cfg).to(dev)
     model.train()
-    batch = synthetic_train_batch(2, 256, 320, 3, dev)
+    batch = synthetic_train_batch(2, height, width, seed, dev)
     calibrate_rcnn_scores(model, batch)               # BASELINE.md logit scales
     cpu = cpu_train.CPUTrainStep(model, cfg)          # deep copy of the same weights
     names = [n for n, p in model.named_parameters() if p.requires_grad
@@ -437,6 +426,41 @@ def test_whole_training_step_matches_cpu_restatement(dev):
     print(f"losses gpu {g_losses}\nlosses cpu {c_losses}\nworst weight rel diff {worst_w:.3g}, "
           f"worst update rel diff {worst_d:.3g} over {checked} tensors")
     assert checked > 25, checked
+    return g_losses, c_losses, trainer
+
+
+
+
+def test_whole_training_step_matches_cpu_restatement(dev):
+    """One HIP Trainer.step vs oracle/cpu_train.py's CPUTrainStep.step on
+    identical weights and batch (lib/engine/trainer.py:116-139,
+    model_deploy.py:203-205), with EVERY candidate sampled: the RPN and ROI
+    batch sizes exceed the candidate counts (2^20 anchors per image at
+    positive fraction 0.5; 200 train proposals + GT per image under 512 at
+    fraction 1.0), so the random subsampling is a permutation and every loss
+    is order-invariant.  Pins A14 (RPN losses), A18 (label + sample), A19
+    (box losses), A20 (mask loss) and A23 (clip_by_norm + Momentum-SGD)
+    together: losses to 1e-4 relative, the updated FPN / RPN / ROI-head
+    weights to 1e-4 of their scale, and their updates w1 - w0 to 5e-3 of the
+    update's scale per tensor plus 4 ulp of the weight (an f32 weight of 0.03
+    rounds its update to ~2e-9; ReLU units within f32 noise of zero pass or
+    block their gradient differently: the box head's updates differ by
+    ~1.5e-3), for the tensors whose update exceeds 100 such ulps."""
+    _whole_step_vs_cpu(dev, 256, 320, post_topk=200, roi_batch=512)
+
+
+def test_whole_training_step_1333x800_matches_cpu_restatement(dev):
+    """The headline config itself (BASELINE C3: Mask R-CNN R50-FPN training,
+    2 images at 1333x800 padded to 1344x800, the config's 1,000 post-NMS
+    training proposals per image) against oracle/cpu_train.py with every
+    candidate sampled: RPN batch 2^20 >= the 268,569 anchors per image, ROI
+    batch 1,024 >= 1,000 proposals + 7 GT at fraction 1.0.  Same bars as the
+    256x320 test (losses 1e-4 relative; weights and updates per tensor).
+    Reference: lib/engine/trainer.py:116-139, lib/engine/model_deploy.py:203-205."""
+    g, c, trainer = _whole_step_vs_cpu(dev, 800, 1333, post_topk=None, roi_batch=1024, seed=1000)
+    rows = trainer.model.roi_heads.last_mask_rows
+    print(f"1333x800: mask-branch rows {rows}")
+    assert rows >= 32
 
 
 @pytest.mark.parametrize("nreg", [80, 1])
