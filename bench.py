@@ -252,6 +252,31 @@ def kernel_report(summary, mode="infer", extras=None):
                      "traffic": pmc_traffic(pmc_group, mode), "traffic_source": TRAFFIC_SOURCE,
                      "launches": n,
                      "avg_us": round(ms * 1e3 / n, 2), "algorithmic_per_launch": flops / n}
+    # the same conv launches split by their own bound (ops.bound_of: flop/B
+    # against the product form's ridge): MFMA-bound shapes against the MFMA
+    # peak, memory-bound shapes (the short-K residual 1x1s, ...) against HBM
+    for base, peak in (("conv2d_split", MFMA_SPLIT_PEAK_TFLOPS),
+                       ("conv2d_wgrad_split", MFMA_SPLIT_PEAK_TFLOPS),
+                       ("conv2d_mfma", MFMA_F32_PEAK_TFLOPS)):
+        for bound in ("mfma", "hbm"):
+            name = f"{base}_{bound}_bound"
+            if name not in summary:
+                continue
+            n, ms, flops = summary[name]
+            sec = ms * 1e-3
+            byts = extras.get(name, {}).get("bytes", 0.0)
+            tf = flops / sec / 1e12
+            gbs = byts / sec / 1e9
+            r = {"bound": bound, "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                 "ms_per_step": round(ms, 3), "achieved_tflops": round(tf, 2),
+                 "achieved_gbs": round(gbs, 1), "flop_per_byte": round(flops / max(byts, 1.0), 1),
+                 "bytes_model": "every operand read once + the output written once"}
+            if bound == "mfma":
+                r.update(achieved=round(tf, 2), peak=peak, unit="TFLOP/s", frac=round(tf / peak, 4))
+            else:
+                r.update(achieved=round(gbs, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
+                         frac=round(gbs / HBM_PEAK_GBPS, 4))
+            rep[name] = r
     for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_postprocess",
                  "solo_mask_stats",
                  "solo_matrix_nms", "solo_paste"):

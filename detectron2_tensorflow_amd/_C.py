@@ -27,6 +27,7 @@ _SIGS = {
     "d2mi_version": (c_int, []),
     "d2mi_source_hash": (c_char_p, []),
     "d2mi_set_tuning": (c_int, [c_char_p, c_int]),
+    "d2mi_get_tuning": (c_int, [c_char_p]),
     "d2mi_last_error": (c_char_p, []),
     "d2mi_error_word_dev": (c_void_p, []),
     "d2mi_clear_errors": (c_int, [P]),

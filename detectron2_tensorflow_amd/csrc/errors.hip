@@ -1,5 +1,6 @@
 // Thread-local host error string + the device error word (see include/d2mi.h).
 #include <algorithm>
+#include <climits>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,13 +20,14 @@ namespace {
 const char* const kTuneNames[kTuneCount] = {"conv_ws",   "roi_fwd",  "wgrad_ws",
                                             "conv_epi",  "wgrad_ws1", "wgrad_xcd",
                                             "conv_xcd",  "wgrad_inc", "conv_ws_mink",
-                                            "roi_pix_grid"};
+                                            "roi_pix_grid", "conv_stream"};
 const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D2MI_WGRAD_WS",
                                           "D2MI_CONV_EPI",  "D2MI_WGRAD_WS1", "D2MI_WGRAD_XCD",
                                           "D2MI_CONV_XCD",  "D2MI_WGRAD_INC", "D2MI_CONV_WS_MINK",
-                                          "D2MI_ROI_PIX_GRID"};
+                                          "D2MI_ROI_PIX_GRID", "D2MI_CONV_STREAM"};
 // defaults: measured per shape and in the training step
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192};
+// conv_stream: 0 = off until the r5 A/B (tools/conv_ab.py) sets its threshold
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 0};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace
@@ -111,6 +113,13 @@ int d2mi_set_tuning(const char* key, int value) {
   }
   D2MI_REQUIRE(false, "unknown tuning key '%s'", key);
   return -1;
+}
+
+int d2mi_get_tuning(const char* key) {
+  if (key == nullptr) return INT32_MIN;
+  for (int k = 0; k < d2mi::kTuneCount; ++k)
+    if (strcmp(key, d2mi::kTuneNames[k]) == 0) return d2mi::tuning((d2mi::TuneKey)k);
+  return INT32_MIN;
 }
 
 int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }

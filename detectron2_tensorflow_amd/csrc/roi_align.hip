@@ -340,6 +340,17 @@ struct Contrib {
   int32_t set;  // ROI set (0 / 1) of a merged backward
 };
 
+// A contribution in its run's arrival order (r5): the place launch writes
+// the slot AND the sample's record next to each other, so the C = 256 pixel
+// pass reads a run's records in one coalesced load round instead of a slot
+// and then a record per contribution (one dependent load fewer per
+// contribution, and the row addresses of a run all known after its slot sort).
+struct RunRec {
+  int32_t slot;  // ((sample) << 2) | corner
+  int32_t row;   // grad_out row of the sample's bin (its set's grad_out)
+  float yl, xl;
+};
+
 // Device-side bookkeeping of one backward (cleared by the clear launch).
 struct BwdCounters {
   int32_t touched, segs, tasks, cursor;
@@ -569,17 +580,25 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
   }
 }
 
-// One thread per contribution: its slot at its arrival rank in its pair's range.
+// One thread per contribution: its slot at its arrival rank in its pair's
+// range, and (runrec non-null) its run record there too.
 __global__ __launch_bounds__(256) void roi_bwd_place_kernel(const uint64_t* __restrict__ ent,
                                                             long long n,
                                                             const int32_t* __restrict__ run_start,
-                                                            int32_t* __restrict__ arrival) {
+                                                            int32_t* __restrict__ arrival,
+                                                            const Contrib* __restrict__ rec,
+                                                            RunRec* __restrict__ runrec) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t e = ent[i];
   if (e == ~0ull) return;
   const int q = (int)(e >> 32);
-  arrival[run_start[q] + (int)(uint32_t)e] = (int32_t)i;
+  const int pos = run_start[q] + (int)(uint32_t)e;
+  arrival[pos] = (int32_t)i;
+  if (runrec) {
+    const Contrib c = rec[i >> 2];
+    runrec[pos] = RunRec{(int32_t)i, c.row, c.yl, c.xl};
+  }
 }
 
 // Long runs (> kSeg contributions) in slot order: a task ranks kLongTask of a
@@ -815,19 +834,27 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
 
 // C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
 // once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
-// independent load chains (run bounds -> slots -> records -> grad_out rows)
-// in flight per wave instead of one, the same per-pixel order and rounding.
+// independent load chains (run bounds -> run records -> grad_out rows) in
+// flight per wave instead of one, the same per-pixel order and rounding.
+// r5: a short run's records come from runrec in one coalesced round (each
+// lane kSeg / 16 of them), are put in slot order in LDS, and their grad_out
+// rows are then loaded kRowBatch at a time (the row addresses are all known
+// after the sort) and summed in that order -- the slot -> record -> row chain
+// per contribution of r4 (one dependent global load per step) is gone.
+constexpr int kRowBatch = 4;
 template <int PPW>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
-    RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
-    int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
+    RoiArgs a, PixMap pm, const RunRec* __restrict__ runrec, int set_bits,
+    const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
     const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
     const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, int lv_lo,
     int lv_hi) {
   constexpr int C = 256;
   constexpr int LPP = 64 / PPW;     // lanes per pixel
   constexpr int F = C / LPP / 4;    // float4 per lane
-  __shared__ int32_t lds[4][PPW][2][kSeg];
+  constexpr int KR = kSeg / LPP;    // run records per lane
+  __shared__ int32_t lslot[4][PPW][kSeg];
+  __shared__ int4 lrec[4][PPW][kSeg];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane / LPP, sub = lane % LPP;
   const int c = sub * 4 * F;  // this lane's channels
@@ -835,8 +862,8 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
   tr.init(pm, ctr, lv_lo, lv_hi);
   const int nt = tr.total();
   const int nsets = 1 << set_bits;
-  int32_t* lin = lds[w][grp][0];
-  int32_t* lout = lds[w][grp][1];
+  int32_t* lin = lslot[w][grp];
+  int4* lout = lrec[w][grp];
   const int wave = blockIdx.x * 4 + w;
   for (int tb = wave * PPW; tb < nt; tb += gridDim.x * 4 * PPW) {
     const int t = tb + grp;
@@ -865,28 +892,59 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
 #pragma unroll
       for (int k = 0; k < F; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (n <= kSeg) {
-        order_run<LPP>(arrival, i0, n, sub, lin, lout);
-        for (int i = 0; i < n; ++i) {
-          const int slot = lout[i];
-          const int corner = slot & 3;
-          const Contrib e = rec[slot >> 2];
-          const float4* src =
-              reinterpret_cast<const float4*>(a.gout_s[e.set] + (size_t)e.row * C + c);
-          float4 v[F];
+        // the run's records (arrival order), ranked by slot: the TF loop order
+        int4 v[KR];
 #pragma unroll
-          for (int k = 0; k < F; ++k) v[k] = src[k];
-          const int sr = a.sr_s[e.set];
-          const float inv = (float)(sr * sr);
+        for (int k = 0; k < KR; ++k) {
+          const int idx = sub + k * LPP;
+          v[k] = idx < n ? *reinterpret_cast<const int4*>(runrec + i0 + idx)
+                         : make_int4(INT_MAX, 0, 0, 0);
+          if (idx < n) lin[idx] = v[k].x;
+        }
+        __builtin_amdgcn_wave_barrier();
+        int rank[KR] = {};
+        for (int j = 0; j < n; ++j) {
+          const int o = lin[j];
 #pragma unroll
-          for (int k = 0; k < F; ++k) {
-            float4 g = v[k];
-            if (sr > 0) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
-            acc[k].x += weigh(corner, e.yl, e.xl, g.x);
-            acc[k].y += weigh(corner, e.yl, e.xl, g.y);
-            acc[k].z += weigh(corner, e.yl, e.xl, g.z);
-            acc[k].w += weigh(corner, e.yl, e.xl, g.w);
+          for (int k = 0; k < KR; ++k) rank[k] += o < v[k].x ? 1 : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < KR; ++k)
+          if (sub + k * LPP < n) lout[rank[k]] = v[k];
+        __builtin_amdgcn_wave_barrier();
+        const float* gout = a.gout_s[sidx];
+        const int sr = a.sr_s[sidx];
+        const float inv = (float)(sr * sr);
+        for (int i = 0; i < n; i += kRowBatch) {
+          int4 e[kRowBatch];
+          float4 vv[kRowBatch][F];
+#pragma unroll
+          for (int u = 0; u < kRowBatch; ++u) {
+            if (i + u < n) {
+              e[u] = lout[i + u];
+              const float4* src = reinterpret_cast<const float4*>(gout + (size_t)e[u].y * C + c);
+#pragma unroll
+              for (int k = 0; k < F; ++k) vv[u][k] = src[k];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kRowBatch; ++u) {
+            if (i + u < n) {
+              const int corner = e[u].x & 3;
+              const float yl = __int_as_float(e[u].z), xl = __int_as_float(e[u].w);
+#pragma unroll
+              for (int k = 0; k < F; ++k) {
+                float4 g = vv[u][k];
+                if (sr > 0) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
+                acc[k].x += weigh(corner, yl, xl, g.x);
+                acc[k].y += weigh(corner, yl, xl, g.y);
+                acc[k].z += weigh(corner, yl, xl, g.z);
+                acc[k].w += weigh(corner, yl, xl, g.w);
+              }
+            }
           }
         }
+        __builtin_amdgcn_wave_barrier();  // (lin / lout reused by the next run)
       } else {
         const int f = seg_first[q];
         const int ns = (n + kSeg - 1) / kSeg;
@@ -1073,6 +1131,7 @@ template <class WS>
 void bwd_layout(WS& w, int C, const BwdPlan& p) {
   w.template take<uint64_t>((size_t)p.n_keys + 1);          // ent: pair << 32 | arrival rank
   w.template take<int32_t>((size_t)p.n_keys + 1);           // arrival-ordered slots
+  w.template take<RunRec>((size_t)p.n_keys + 1);            // arrival-ordered run records
   w.template take<int32_t>((size_t)p.n_keys + 1);           // long runs in slot order
   w.template take<Contrib>((size_t)p.n_samples + 1);        // records
   w.template take<int32_t>((size_t)p.pairs + 1);            // count
@@ -1122,6 +1181,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   Workspace w(workspace, workspace_bytes);
   uint64_t* ent = w.take<uint64_t>((size_t)p.n_keys + 1);
   int32_t* arrival = w.take<int32_t>((size_t)p.n_keys + 1);
+  RunRec* runrec = w.take<RunRec>((size_t)p.n_keys + 1);
   int32_t* sorted_long = w.take<int32_t>((size_t)p.n_keys + 1);
   Contrib* rec = w.take<Contrib>((size_t)p.n_samples + 1);
   int32_t* count = w.take<int32_t>((size_t)p.pairs + 1);
@@ -1166,7 +1226,8 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                      tasks, touched, ctr, p.pm);
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
-                     st, ent, p.n_keys, run_start, arrival);
+                     st, ent, p.n_keys, run_start, arrival, rec,
+                     (vec4 && C == 256) ? runrec : nullptr);
   D2MI_LAUNCH_CHECK();
   // long runs (degenerate piles of boxes) in slot order, then their segment
   // partials: grid-stride loops over the device-side task / segment counts
@@ -1218,11 +1279,11 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     }();
     const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), wg_max)));
     if (ppw == 8)
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, runrec, sb,
+                         count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
     else
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, arrival, rec,
-                         sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, runrec, sb,
+                         count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
   } else if (vec4) {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
                        sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);

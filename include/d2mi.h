@@ -44,23 +44,25 @@ int d2mi_version(void);
 const char* d2mi_source_hash(void);
 const char* d2mi_last_error(void);
 /* Process-wide kernel-selection knobs for in-process A/B timing (tools/);
- * each starts from its environment variable.  No reference counterpart (a
- * tuning hook of this implementation).  Keys:
- *   "conv_ws"  D2MI_CONV_WS  warp-specialised 256x128 split conv kernel for
- *                            the long-K convs: 0 off, else on (default 2);
- *   "roi_fwd"  D2MI_ROI_FWD  ROIAlign forward variant bits (-1 = default);
- *   "wgrad_ws" D2MI_WGRAD_WS warp-specialised 256x128 split weight-gradient
- *                            kernel for KxK convs (Cin % 256 == 0,
- *                            Cout % 128 == 0): 0 off, 1 (default) on;
- *   "conv_epi" D2MI_CONV_EPI split-K partial slabs stored from the MFMA
- *                            accumulators (1, default) or through the LDS
- *                            epilogue (0);
- *   "conv_sk"  D2MI_CONV_SK  stream-K plans for the WS conv where its cost
- *                            model wins (1) or never (0, default: faster per
- *                            shape, +0.9 % on the training step);
- *   "wgrad_ws1" D2MI_WGRAD_WS1 the warp-specialised weight-gradient kernel
- *                            on 1x1 convs of >= 6 GFLOP too (1, default). */
+ * each starts from its environment variable (D2MI_<KEY in capitals>).  No
+ * reference counterpart (a tuning hook of this implementation).  Keys:
+ *   "conv_ws"      warp-specialised 256x128 split conv for the long-K convs:
+ *                  0 off, else on (default 2);
+ *   "roi_fwd"      ROIAlign forward variant bits (-1 = default);
+ *   "wgrad_ws"     warp-specialised split weight gradient for KxK convs
+ *                  (Cin % 256 == 0, Cout % 128 == 0): 0 off, 1 (default) on;
+ *   "conv_epi"     split-K partials stored from the accumulators (1, default)
+ *                  or through the LDS epilogue (0);
+ *   "wgrad_ws1"    the WS weight gradient on 1x1 convs of >= N GFLOP (6);
+ *   "wgrad_xcd" / "conv_xcd"  XCD-contiguous grid remaps (1 on);
+ *   "wgrad_inc"    incremental pixel cursor in the WS weight gradient (1 on);
+ *   "conv_ws_mink" fewest k-steps that go to the WS conv (16);
+ *   "roi_pix_grid" ROIAlign backward pixel-pass grid (8192);
+ *   "conv_stream"  streaming short-K 1x1 conv (r5) for stride-1 1x1 launches
+ *                  of at least this many output pixels; 0 = off. */
 int d2mi_set_tuning(const char* key, int value);
+/* Current value of a d2mi_set_tuning key (INT32_MIN for an unknown key). */
+int d2mi_get_tuning(const char* key);
 /* Device int32 error word. Bits: 1 = box_ind out of range (CropAndResize),
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
 int32_t* d2mi_error_word_dev(void);

@@ -582,6 +582,51 @@ def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
         assert es <= 4 * ef + 1e-6, (es, ef)
 
 
+@pytest.mark.parametrize("shape,form", [
+    ((2, 40, 52, 64, 256), "r"), ((2, 40, 52, 64, 256), "plain"), ((1, 37, 41, 64, 96), "g"),
+    ((2, 33, 40, 128, 512), "gr"), ((2, 33, 40, 128, 128), "plain"), ((1, 29, 31, 128, 192), "r"),
+    ((2, 20, 24, 256, 1024), "gr"), ((2, 20, 24, 256, 256), "g"), ((1, 21, 23, 256, 64), "plain"),
+])
+def test_conv1x1_stream_kernel_matches_tiled_and_float64(dev, shape, form):
+    """conv1x1_stream_kernel (r5, tuning "conv_stream": the streaming short-K
+    1x1 for the memory-bound stride-1 1x1s; weights resident in LDS, pixels
+    as the MFMA B operand, float4 epilogue) against float64 (the split
+    conv's 1e-4 bar) and against the tiled split kernel on the same launch
+    (the same K order and per-accumulator product sequence: equal to the
+    tiled kernel's result); ragged pixel strips, Cout not a multiple of the
+    slice width, and every epilogue form (bias, residual + ReLU after, ReLU
+    gate, gate + residual)."""
+    N, H, W, Cin, Cout = shape
+    g = torch.Generator().manual_seed(5 + sum(shape))
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(1, 1, Cin, Cout, generator=g) / math.sqrt(Cin)
+    b = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(N, H, W, Cout, generator=g) if "r" in form else None
+    gate = torch.randn(N, H, W, Cout, generator=g) if "g" in form else None
+    ref = torch.einsum("nhwc,cd->nhwd", x.double(), w[0, 0].double()) + b.double()
+    if form == "r":
+        ref = torch.relu(ref + res.double())
+    elif form == "gr":
+        ref = torch.where(gate > 0, ref + res.double(), torch.zeros_like(ref))
+    elif form == "g":
+        ref = torch.where(gate > 0, ref, torch.zeros_like(ref))
+    kw = dict(residual=None if res is None else res.to(dev),
+              relu_gate=None if gate is None else gate.to(dev),
+              relu_after_add=form == "r", relu=form == "r")
+    wp = ops().pack_conv_weights(w.to(dev))
+    outs = {}
+    old = ops().get_tuning("conv_stream")
+    try:
+        for v in (0, 1):
+            ops().set_tuning("conv_stream", v)
+            outs[v] = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), 1, (0, 0), math_mode="split",
+                                        **kw).cpu()
+    finally:
+        ops().set_tuning("conv_stream", old)
+    np.testing.assert_allclose(outs[1].double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_split_bf16x3_is_exact(dev):
     """h + m + l == x bit for bit (evaluated in float64), each term a bf16.
     Exact wherever the residuals stay normal f32 (|x| >= 2^-110 or so); below

@@ -30,7 +30,8 @@ LIB = os.path.join(ROOT, "tools", "libgather_ceiling.so")
 
 
 def load_lib():
-    if not os.path.exists(LIB):
+    src = os.path.join(ROOT, "tools", "gather_ceiling.hip")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
         subprocess.check_call(["hipcc", "-O3", "-std=c++17", "-fPIC", "-shared",
                                "--offload-arch=gfx950", os.path.join(ROOT, "tools", "gather_ceiling.hip"),
                                "-o", LIB])
@@ -39,6 +40,8 @@ def load_lib():
     lib.gc_gather4.argtypes = [P, P, I, P, I, P]
     lib.gc_gather1.argtypes = [P, P, I, P, P]
     lib.gc_copy.argtypes = [P, ctypes.c_longlong, P, P]
+    lib.gc_copy_u.argtypes = [P, ctypes.c_longlong, P, I, I, P]
+    lib.gc_gather1_u.argtypes = [P, P, I, P, I, I, P]
     return lib
 
 
@@ -145,6 +148,11 @@ def main():
         "gather1_unique": lambda: lib.gc_gather1(src.data_ptr(), uniq.data_ptr(), uniq.numel(),
                                                  out1.data_ptr(), st),
         "copy_unique_bytes": lambda: lib.gc_copy(cp_src.data_ptr(), cb // 16, cp_out.data_ptr(), st),
+        # r5: unrolled forms (U loads in flight per lane, persistent grid)
+        "gather1_unique_u8": lambda: lib.gc_gather1_u(src.data_ptr(), uniq.data_ptr(), uniq.numel(),
+                                                      out1.data_ptr(), 8, 2048, st),
+        "copy_unique_u8": lambda: lib.gc_copy_u(cp_src.data_ptr(), cb // 16, cp_out.data_ptr(), 8,
+                                                2048, st),
     }
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)  # > the 256 MiB MALL
 
@@ -160,6 +168,7 @@ def main():
             tot += e0.elapsed_time(e1)
         return tot / a.iters * 1e3
 
+    copy_validation(lib, dev, st)
     t = {k: [] for k in arms}
     for _ in range(a.rounds):
         for k, fn in arms.items():
@@ -168,9 +177,35 @@ def main():
     print(f"box pooler of the step: {y.shape[0]} ROIs x 49 bins, {uniq.numel()} distinct rows "
           f"({cb / 1e6:.1f} MB), unique-bytes model {ub / 1e6:.1f} MB; cold caches per launch")
     for k, us in med.items():
-        by = cb * 2 if k == "copy_unique_bytes" else (cb + uniq.numel() * C * 4 if k == "gather1_unique" else ub)
+        by = (cb * 2 if k.startswith("copy_unique") else
+              cb + uniq.numel() * C * 4 if k.startswith("gather1_unique") else ub)
         print(f"{k:18s} {us:8.1f} us  {by / us / 1e3:7.1f} GB/s ({by / us / 1e3 / 8000:.3f} of 8 TB/s)"
               f"  roi_align / this = {med['roi_align'] / us:.3f}", flush=True)
+
+
+def copy_validation(lib, dev, st, iters=20):
+    """The unrolled copy on a 1 GiB buffer (the guide's streaming-copy
+    measurement, MI355X_MICROARCH.md: 6.29 TB/s) and at the pooler's size:
+    validates the ceiling kernel itself before it is used as one."""
+    for mb in (1024, 134):
+        n4 = (mb << 20) // 16
+        a_ = torch.empty(n4 * 4, device=dev)
+        b_ = torch.empty_like(a_)
+        for name, fn in (("copy (r4, 1 float4 / iteration)", lambda: lib.gc_copy(a_.data_ptr(), n4, b_.data_ptr(), st)),
+                         ("copy_u8 (r5)", lambda: lib.gc_copy_u(a_.data_ptr(), n4, b_.data_ptr(), 8, 2048, st)),
+                         ("copy_u4 (r5)", lambda: lib.gc_copy_u(a_.data_ptr(), n4, b_.data_ptr(), 4, 4096, st))):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) / iters * 1e3
+            print(f"validation {mb:5d} MiB {name:34s} {us:9.1f} us  "
+                  f"{2 * (mb << 20) / us / 1e3:7.1f} GB/s (read + write)", flush=True)
+        del a_, b_
 
 
 if __name__ == "__main__":
