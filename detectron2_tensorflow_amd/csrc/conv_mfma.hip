@@ -817,31 +817,45 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs 
   // row-contiguous epilogue positions of this lane: q-th float4 at pixel row
   // (lane >> 4) + 4 q, channel chunk lane & 15 of the half
   const int erow = lane >> 4, ec4 = lane & 15;
-  for (int s = grp * WAVES + wave; s < nstrips; s += ngrp * WAVES) {
-    const int m0 = s * 32;
-    const int arow = min(m0 + li, a.M - 1);
+  // Software-pipelined over the wave's strips: the next strip's A fragments
+  // are issued as soon as this strip's MFMAs have consumed theirs (under this
+  // strip's epilogue), and its epilogue operands as soon as this strip's
+  // epilogue has used its own (under the next strip's MFMAs) -- the same
+  // registers, one strip ahead.
+  const int sstep = ngrp * WAVES;
+  float4 ra[K / 16][2];
+  float4 res[RES ? NH : 1][8], gt[GATE ? NH : 1][8];
+  auto load_a = [&](int strip) {
+    const int arow = min(strip * 32 + li, a.M - 1);
     const float* xr = a.x + (size_t)arow * K + lh * 8;
-    // the whole strip's A fragments in flight at once
-    float4 ra[K / 16][2];
 #pragma unroll
     for (int j = 0; j < K / 16; ++j) {
       ra[j][0] = *reinterpret_cast<const float4*>(xr + j * 16);
       ra[j][1] = *reinterpret_cast<const float4*>(xr + j * 16 + 4);
     }
-    // epilogue operands (row-contiguous float4s), issued before the MFMAs
-    float4 res[RES ? NH : 1][8], gt[GATE ? NH : 1][8];
+  };
+  auto load_e = [&](int strip) {  // the epilogue operands, row-contiguous float4s
     if constexpr (RES || GATE) {
 #pragma unroll
       for (int h = 0; h < NH; ++h)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int m = m0 + erow + 4 * q, co = n0 + h * 64 + ec4 * 4;
+          const int m = strip * 32 + erow + 4 * q, co = n0 + h * 64 + ec4 * 4;
           const bool ok = m < a.M && co < a.Cout;
           const size_t o = (size_t)m * a.Cout + co;
           if constexpr (RES) res[h][q] = ok ? ld4(a.residual + o) : make_float4(0.f, 0.f, 0.f, 0.f);
           if constexpr (GATE) gt[h][q] = ok ? ld4(a.gate + o) : make_float4(1.f, 1.f, 1.f, 1.f);
         }
     }
+  };
+  int s = grp * WAVES + wave;
+  if (s < nstrips) {
+    load_a(s);
+    load_e(s);
+  }
+  for (; s < nstrips; s += sstep) {
+    const int m0 = s * 32;
+    const bool more = s + sstep < nstrips;
     // The MFMAs take the weights as the A operand and the pixels as B
     // (C^T = W X^T): lane li holds pixel m0 + li and, per 32-channel tile t,
     // the channels 32 t + 8 g + 4 lh + {0..3} in acc[t][4 g .. 4 g + 3]
@@ -881,6 +895,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs 
       __builtin_amdgcn_sched_barrier(0);
     }
     if (kPrioMfma) __builtin_amdgcn_s_setprio(0);
+    if (more) load_a(s + sstep);  // ra is free: the next strip's A under this epilogue
     // epilogue, one 64-channel half at a time through the wave's slab;
     // epilogue() order: conv + bias, ReLU (before), + residual, ReLU (after), gate
 #pragma unroll
@@ -919,6 +934,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs 
           *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+    if (more) load_e(s + sstep);  // res / gt are free: the next strip's, under its MFMAs
   }
 }
 
@@ -1581,7 +1597,14 @@ static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
   if (a.Cout % 4 != 0 || !al16(a.x) || !al16(a.w) || !al16(a.y) || !al16(a.residual) ||
       !al16(a.gate) || !al16(a.bias))
     return 0;
-  return a.Cin == 64 ? 1 : (a.Cin == 128 ? 2 : 3);
+  if (a.Cin == 256 && a.residual && a.gate) return 0;  // (its registers spill)
+  // where it measured faster than the tiled kernel (tools/stream_ab.py,
+  // profiles/r5_stream_ab.log): every K = 64 launch; K = 128 into >= 256
+  // channels; K = 256 into <= 64 channels.  Elsewhere (128 -> 128, the
+  // 256 -> 256 / 1024 shapes) the tiled kernel's 3 workgroups per CU win.
+  if (a.Cin == 64) return 1;
+  if (a.Cin == 128) return a.Cout >= 256 ? 2 : 0;
+  return a.Cout <= 64 ? 3 : 0;
 }
 
 template <int TN, int KMAX>
@@ -1614,9 +1637,10 @@ static int launch_stream1x1(int variant, const ConvArgs& a, void* stream) {
   const int BN = 32 * TN;
   const int nslices = (a.Cout + BN - 1) / BN;
   const int nstrips = (a.M + 31) / 32;
-  // about two workgroups per CU over all slices, whole XCD rounds, and no
-  // group without a strip for each of its waves
-  int groups = std::max(1, 2 * wg_slots(3) / nslices / 8);
+  // one resident workgroup per CU (LDS: the weight slice + the slabs) over
+  // all slices, whole XCD rounds, and no group without a strip for each of
+  // its waves
+  int groups = std::max(1, wg_slots(3) / nslices / 8);
   groups = std::min(groups, std::max(1, nstrips / WAVES / 8));
   const dim3 grid(8 * groups * nslices);
   hipStream_t st = as_stream(stream);

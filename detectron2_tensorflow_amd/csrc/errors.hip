@@ -20,14 +20,15 @@ namespace {
 const char* const kTuneNames[kTuneCount] = {"conv_ws",   "roi_fwd",  "wgrad_ws",
                                             "conv_epi",  "wgrad_ws1", "wgrad_xcd",
                                             "conv_xcd",  "wgrad_inc", "conv_ws_mink",
-                                            "roi_pix_grid", "conv_stream"};
+                                            "roi_pix_grid", "conv_stream", "roi_bwd_rec"};
 const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D2MI_WGRAD_WS",
                                           "D2MI_CONV_EPI",  "D2MI_WGRAD_WS1", "D2MI_WGRAD_XCD",
                                           "D2MI_CONV_XCD",  "D2MI_WGRAD_INC", "D2MI_CONV_WS_MINK",
-                                          "D2MI_ROI_PIX_GRID", "D2MI_CONV_STREAM"};
+                                          "D2MI_ROI_PIX_GRID", "D2MI_CONV_STREAM",
+                                          "D2MI_ROI_BWD_REC"};
 // defaults: measured per shape and in the training step
 // conv_stream: 0 = off until the r5 A/B (tools/conv_ab.py) sets its threshold
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 0};
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 0, 1};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

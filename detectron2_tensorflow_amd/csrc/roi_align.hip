@@ -832,6 +832,118 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_kernel(
   }
 }
 
+// r4 form of roi_bwd_pixel_c256_kernel (tuning "roi_bwd_rec" = 0, A/B): the
+// run's slots ordered in LDS, then a record and a row per contribution.
+// C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
+// once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
+// independent load chains (run bounds -> slots -> records -> grad_out rows)
+// in flight per wave instead of one, the same per-pixel order and rounding.
+template <int PPW>
+__global__ __launch_bounds__(256) void roi_bwd_pixel_c256_slots_kernel(
+    RoiArgs a, PixMap pm, const int32_t* __restrict__ arrival, const Contrib* __restrict__ rec,
+    int set_bits, const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
+    const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
+    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, int lv_lo,
+    int lv_hi) {
+  constexpr int C = 256;
+  constexpr int LPP = 64 / PPW;     // lanes per pixel
+  constexpr int F = C / LPP / 4;    // float4 per lane
+  __shared__ int32_t lds[4][PPW][2][kSeg];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane / LPP, sub = lane % LPP;
+  const int c = sub * 4 * F;  // this lane's channels
+  TouchedRange tr;
+  tr.init(pm, ctr, lv_lo, lv_hi);
+  const int nt = tr.total();
+  const int nsets = 1 << set_bits;
+  int32_t* lin = lds[w][grp][0];
+  int32_t* lout = lds[w][grp][1];
+  const int wave = blockIdx.x * 4 + w;
+  for (int tb = wave * PPW; tb < nt; tb += gridDim.x * 4 * PPW) {
+    const int t = tb + grp;
+    if (t >= nt) continue;
+    int l;
+    const long long pix = tr.at(pm, touched, t, l);
+    float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    // accumulate: the map's old value is loaded first, its latency hidden
+    // behind the contribution sums (r4: the deferred per-level passes into
+    // the RPN head's dgrad output waited on it at the end)
+    const bool acc_lv = (a.acc_mask >> l) & 1;
+    float4 old[F];
+    if (acc_lv) {
+#pragma unroll
+      for (int k = 0; k < F; ++k) old[k] = d4[k];
+    }
+    float4 res[F];
+    bool any = false;
+    for (int sidx = 0; sidx < nsets; ++sidx) {
+      const long long q = (pix << set_bits) | sidx;
+      const int n = count[q];
+      if (n == 0) continue;
+      const int i0 = run_start[q];
+      float4 acc[F];
+#pragma unroll
+      for (int k = 0; k < F; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n <= kSeg) {
+        order_run<LPP>(arrival, i0, n, sub, lin, lout);
+        for (int i = 0; i < n; ++i) {
+          const int slot = lout[i];
+          const int corner = slot & 3;
+          const Contrib e = rec[slot >> 2];
+          const float4* src =
+              reinterpret_cast<const float4*>(a.gout_s[e.set] + (size_t)e.row * C + c);
+          float4 v[F];
+#pragma unroll
+          for (int k = 0; k < F; ++k) v[k] = src[k];
+          const int sr = a.sr_s[e.set];
+          const float inv = (float)(sr * sr);
+#pragma unroll
+          for (int k = 0; k < F; ++k) {
+            float4 g = v[k];
+            if (sr > 0) { g.x = g.x / inv; g.y = g.y / inv; g.z = g.z / inv; g.w = g.w / inv; }
+            acc[k].x += weigh(corner, e.yl, e.xl, g.x);
+            acc[k].y += weigh(corner, e.yl, e.xl, g.y);
+            acc[k].z += weigh(corner, e.yl, e.xl, g.z);
+            acc[k].w += weigh(corner, e.yl, e.xl, g.w);
+          }
+        }
+      } else {
+        const int f = seg_first[q];
+        const int ns = (n + kSeg - 1) / kSeg;
+        for (int j = 0; j < ns; ++j) {
+          const float4* src = reinterpret_cast<const float4*>(partial + (size_t)(f + j) * C + c);
+#pragma unroll
+          for (int k = 0; k < F; ++k) {
+            const float4 v = src[k];
+            acc[k].x += v.x; acc[k].y += v.y; acc[k].z += v.z; acc[k].w += v.w;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < F; ++k) {
+        if (any) {
+          res[k].x = res[k].x + acc[k].x; res[k].y = res[k].y + acc[k].y;
+          res[k].z = res[k].z + acc[k].z; res[k].w = res[k].w + acc[k].w;
+        } else {
+          res[k] = acc[k];
+        }
+      }
+      any = true;
+    }
+    if (!any) continue;
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      if (acc_lv) {
+        const float4 o = old[k];
+        res[k].x = o.x + res[k].x; res[k].y = o.y + res[k].y;
+        res[k].z = o.z + res[k].z; res[k].w = o.w + res[k].w;
+      }
+      d4[k] = res[k];
+    }
+  }
+}
+
 // C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
 // once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
 // independent load chains (run bounds -> run records -> grad_out rows) in
@@ -1192,6 +1304,10 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
   int2* tasks = w.take<int2>((size_t)p.max_tasks);
   BwdCounters* ctr = w.take<BwdCounters>(1);
+  // r5: the C = 256 pixel pass reads run records (tuning "roi_bwd_rec", 1);
+  // 0 = the r4 slot pass (A/B).  Phase 1 and phase 2 of one backward must
+  // see the same value (a deferred pass reads what the prepare wrote).
+  const bool use_runrec = vec4 && C == 256 && tuning(kTuneRoiBwdRec) != 0;
   if (phase & 1) {
   ClearList cl = {};
   long long clear_words = 0;
@@ -1226,8 +1342,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                      tasks, touched, ctr, p.pm);
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
-                     st, ent, p.n_keys, run_start, arrival, rec,
-                     (vec4 && C == 256) ? runrec : nullptr);
+                     st, ent, p.n_keys, run_start, arrival, rec, use_runrec ? runrec : nullptr);
   D2MI_LAUNCH_CHECK();
   // long runs (degenerate piles of boxes) in slot order, then their segment
   // partials: grid-stride loops over the device-side task / segment counts
@@ -1278,7 +1393,11 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
       return e && e[0] == '8' ? 8 : 4;
     }();
     const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), wg_max)));
-    if (ppw == 8)
+    if (!use_runrec)  // the r4 pixel pass (A/B)
+      hipLaunchKernelGGL(roi_bwd_pixel_c256_slots_kernel<4>, g4, dim3(256), 0, st, a, p.pm,
+                         arrival, rec, sb, count, run_start, seg_first, partial, touched, ctr,
+                         lv_lo, lv_hi);
+    else if (ppw == 8)
       hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, runrec, sb,
                          count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
     else

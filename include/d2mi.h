@@ -59,7 +59,9 @@ const char* d2mi_last_error(void);
  *   "conv_ws_mink" fewest k-steps that go to the WS conv (16);
  *   "roi_pix_grid" ROIAlign backward pixel-pass grid (8192);
  *   "conv_stream"  streaming short-K 1x1 conv (r5) for stride-1 1x1 launches
- *                  of at least this many output pixels; 0 = off. */
+ *                  of at least this many output pixels; 0 = off;
+ *   "roi_bwd_rec"  ROIAlign backward pixel pass over run records (r5, 1) or
+ *                  the r4 slot pass (0). */
 int d2mi_set_tuning(const char* key, int value);
 /* Current value of a d2mi_set_tuning key (INT32_MIN for an unknown key). */
 int d2mi_get_tuning(const char* key);
