@@ -27,8 +27,9 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
                                           "D2MI_ROI_PIX_GRID", "D2MI_CONV_STREAM",
                                           "D2MI_ROI_BWD_REC"};
 // defaults: measured per shape and in the training step
-// conv_stream: 0 = off until the r5 A/B (tools/conv_ab.py) sets its threshold
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 0, 1};
+// conv_stream: the streaming 1x1 for launches of >= 8192 output pixels (r5 in-step A/B:
+// -0.85 %, profiles/r5_ab_inproc_conv_stream.log); roi_bwd_rec: run records (-0.41 %)
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace
