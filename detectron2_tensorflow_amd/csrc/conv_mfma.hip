@@ -1589,8 +1589,10 @@ extern "C" size_t d2mi_conv2d_workspace_size(int N, int H, int W, int Cin, int C
 // == 0, 16-B aligned operands, and enough pixel strips to fill the chip
 // (tuning "conv_stream": 0 off; else the fewest output pixels).
 static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
-  const int minM = tuning(kTuneConvStream);
-  if (minM <= 0 || !(flags & kSplit3) || a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad != 0 ||
+  const int tv = tuning(kTuneConvStream);
+  const bool force = tv < 0;  // (A/B: every eligible shape of >= -tv pixels)
+  const int minM = force ? -tv : tv;
+  if (tv == 0 || !(flags & kSplit3) || a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad != 0 ||
       a.topdown || !(a.Cin == 64 || a.Cin == 128 || a.Cin == 256) || a.M < minM)
     return 0;
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
@@ -1599,12 +1601,13 @@ static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
     return 0;
   if (a.Cin == 256 && a.residual && a.gate) return 0;  // (its registers spill)
   // where it measured faster than the tiled kernel (tools/stream_ab.py,
-  // profiles/r5_stream_ab.log): every K = 64 launch; K = 128 into >= 256
-  // channels; K = 256 into <= 64 channels.  Elsewhere (128 -> 128, the
-  // 256 -> 256 / 1024 shapes) the tiled kernel's 3 workgroups per CU win.
-  if (a.Cin == 64) return 1;
-  if (a.Cin == 128) return a.Cout >= 256 ? 2 : 0;
-  return a.Cout <= 64 ? 3 : 0;
+  // profiles/r5_stream_ab_force_tn_rule.log, with TN 2 when 128-wide slices
+  // leave too few strip tasks): every K = 64 and K = 128 launch; K = 256 into
+  // <= 64 channels, or into >= 512 over >= 16 K pixels.  Elsewhere (256 ->
+  // 256, 256 -> 1024 at 8,400 pixels) the tiled kernel's 3 workgroups per CU
+  // win.
+  if (a.Cin == 64 || a.Cin == 128) return a.Cin == 64 ? 1 : 2;
+  return (force || a.Cout <= 64 || (a.Cout >= 512 && a.M >= 16384)) ? 3 : 0;
 }
 
 template <int TN, int KMAX>
@@ -1633,7 +1636,11 @@ static void launch_stream1x1_t(dim3 grid, hipStream_t st, const ConvArgs& a, int
 static int launch_stream1x1(int variant, const ConvArgs& a, void* stream) {
   constexpr int WAVES = 8;
   const bool both = a.residual && a.gate;
-  const int TN = (variant == 3 || both) ? 2 : 4;
+  // TN 2 also when 128-wide slices leave fewer strip tasks than the chip has
+  // waves (one 8-wave workgroup per CU)
+  const int strips = (a.M + 31) / 32;
+  const bool few = (long long)strips * ((a.Cout + 127) / 128) < 8LL * wg_slots(3);
+  const int TN = (variant == 3 || both || few) ? 2 : 4;
   const int BN = 32 * TN;
   const int nslices = (a.Cout + BN - 1) / BN;
   const int nstrips = (a.M + 31) / 32;

@@ -12,38 +12,10 @@
 // 1333x800) and then keeps <= 1000 per level; decoding is elementwise, so
 // selecting first and decoding only the selected anchors (regenerated from
 // the flat index) gives identical results for a fraction of the traffic.
-#include "internal.h"
+#include "detect.h"
 
 namespace d2mi {
 namespace {
-
-constexpr int kMaxA = 12;
-
-struct Levels {
-  int64_t off_a[D2MI_MAX_LEVELS];  // element offset of level l's tensor from base_a
-  int64_t off_b[D2MI_MAX_LEVELS];  // element offset of level l's tensor from base_b
-  // image strides of level l's tensors (a: elements per K, b: float4s); by
-  // default H * W * A (each level a dense [N, H, W, A(*K)] tensor)
-  int64_t img_a[D2MI_MAX_LEVELS];
-  int64_t img_b[D2MI_MAX_LEVELS];
-  int H[D2MI_MAX_LEVELS], W[D2MI_MAX_LEVELS];
-  int stride[D2MI_MAX_LEVELS];
-  float cell[D2MI_MAX_LEVELS][kMaxA][4];
-  int L, A;
-};
-
-__device__ __forceinline__ float4 anchor_at(const Levels& lv, int l, int hw, int a) {
-  const int h = hw / lv.W[l], w = hw - h * lv.W[l];
-  // tf.range(0, H*stride, stride) cast to float32, then + cell anchor (float32)
-  const float sy = (float)(h * lv.stride[l]);
-  const float sx = (float)(w * lv.stride[l]);
-  return make_float4(sy + lv.cell[l][a][0], sx + lv.cell[l][a][1], sy + lv.cell[l][a][2],
-                     sx + lv.cell[l][a][3]);
-}
-
-struct DeltaCfg {
-  float wy, wx, wh, ww, clamp;
-};
 
 __device__ __forceinline__ void atomic_max_ordered(uint32_t* p, float v) {
   atomicMax(p, orderable(v));
@@ -418,6 +390,18 @@ __global__ void retina_output_kernel(const int32_t* __restrict__ keep,
   }
 }
 
+inline int grid1(size_t n, int block = 256, int cap = 4096) {
+  return (int)std::max<size_t>(1, std::min<size_t>((n + block - 1) / block, cap));
+}
+
+int frcnn_cap(int P, int K, float thresh) {
+  int per = K;
+  if (thresh > 0.f) per = std::min(K, (int)std::ceil(1.0 / (double)thresh) + 1);
+  return std::max(1, P * per);
+}
+
+}  // namespace
+
 int make_levels(Levels& lv, const float* const* a_ptrs, const float* const* b_ptrs,
                 const int32_t* level_hw, const float* strides, const float* cell, int L, int A) {
   D2MI_REQUIRE(L >= 1 && L <= D2MI_MAX_LEVELS, "L=%d out of range", L);
@@ -450,17 +434,6 @@ DeltaCfg make_dc(const float* w4, float clamp) {
   return d;
 }
 
-inline int grid1(size_t n, int block = 256, int cap = 4096) {
-  return (int)std::max<size_t>(1, std::min<size_t>((n + block - 1) / block, cap));
-}
-
-int frcnn_cap(int P, int K, float thresh) {
-  int per = K;
-  if (thresh > 0.f) per = std::min(K, (int)std::ceil(1.0 / (double)thresh) + 1);
-  return std::max(1, P * per);
-}
-
-}  // namespace
 }  // namespace d2mi
 
 using namespace d2mi;
@@ -809,12 +782,12 @@ void retina_layout(WS& w, RetinaWs* o, int N, int L, int k, int max_det) {
 
 extern "C" size_t d2mi_retinanet_workspace_size(int N, int L, const int32_t* level_hw, int A,
                                                 int K, int topk_candidates) {
-  (void)level_hw;
-  (void)A;
-  (void)K;
   SizerPtr s;
   retina_layout(s, nullptr, N, L, std::max(1, topk_candidates), 1000);
-  return s.z.off;
+  size_t z = s.z.off;
+  if (retina_fused_eligible(L, topk_candidates, 1000))
+    z = std::max(z, retina_fused_workspace_size(N, L, level_hw, A, K, topk_candidates));
+  return z;
 }
 
 extern "C" int d2mi_retinanet_inference(const float* const* cls, const float* const* box,
@@ -836,6 +809,11 @@ extern "C" int d2mi_retinanet_inference(const float* const* cls, const float* co
   int64_t maxlen = 0;
   for (int l = 0; l < L; ++l) maxlen = std::max<int64_t>(maxlen, (int64_t)lv.H[l] * lv.W[l] * A * K);
   D2MI_REQUIRE(maxlen < (1ll << 31), "level too large");
+  const int mode = tuning(kTuneRetinaFused);
+  if (mode != 0 && retina_fused_eligible(L, k, max_det))
+    return retinanet_fused(cls, box, lv, level_hw, K, N, k, score_thresh, nms_thresh, max_det,
+                           make_dc(weights4_host, scale_clamp), out_boxes, out_scores, out_classes,
+                           out_valid, workspace, workspace_bytes, st, mode == 2);
   const int S = N * L, cap = L * k;
   Workspace w(workspace, workspace_bytes);
   RetinaWs o;

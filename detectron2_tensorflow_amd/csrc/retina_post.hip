@@ -1,0 +1,1089 @@
+// RetinaNet inference (retinanet.py:285-387) in four launches on gfx950:
+// per level the exact top_k(sigmoid(logits), topk_candidates, sorted=True)
+// (TF TopKV2: value desc, ties lowest index first), the score threshold, the
+// box decode, then per image the class-offset NMS (NonMaxSuppressionV3) over
+// the concatenated levels and the zero padding.
+//
+//   floor    one workgroup per (image, level) segment: samples one 1,024-key
+//            run out of every 128 K keys, takes the sampled key that about
+//            4 k keys of the segment reach (bitonic sort of the threads'
+//            sample maxima) and lowers it to the lowest raw key with the same
+//            sigmoid.  Segments of <= 8,192 keys take every key.
+//   collect  one pass over every score (the only full read: 4 B per score),
+//            a persistent grid with the next chunk's loads in flight while
+//            the current one is tested.  No atomics: each wave of each chunk
+//            owns 8 candidate slots and a count it always writes; only the
+//            hits past a wave's 8 slots take an atomic on the segment's
+//            overflow buffer (device-scope atomics on one address serialize
+//            across the 8 XCDs: one per hitting wave cost 350 us here).
+//   finish   one workgroup per segment: gathers the slots; they are exact
+//            when at least k of them lie at or above the floor's sigmoid edge
+//            (every key below the floor then has a smaller sigmoid) and
+//            nothing overflowed; otherwise the workgroup selects exactly
+//            (radix passes over the segment, then the sigmoid tie group in
+//            index order).  Sort keys (sigmoid desc, index asc); the k-th
+//            smallest by a radix select in registers, the <= 1,024 keys at or
+//            below it bitonic-sorted with in-wave exchanges; threshold,
+//            decode of the kept top-k, the per-image max coordinate.
+//   nms      one workgroup per image: merge rank of the per-level sorted
+//            lists (binary searches in lockstep; the concat position breaks
+//            ties), then greedy NMS of the class-offset boxes in 64-candidate
+//            tiles against the kept list, stopping at max_detections -- the
+//            full candidate x candidate mask of nms.hip is never built.
+//
+// Exact in every case (the floor only decides how often the in-workgroup
+// select runs); the tie rules, sigmoid, IoU and decode expressions are those
+// of the unfused pipeline (topk.hip, nms.hip, proposals.hip), which stays
+// selectable with the tuning key "retina_fused" = 0.
+#include "detect.h"
+
+namespace d2mi {
+namespace {
+
+constexpr int kWG = 1024;                 // per-segment / per-image workgroups
+constexpr int kCap = kLdsSortCap;         // candidates per segment
+constexpr int kRun = 1024;                // sampled run (keys)
+constexpr int kRunStride = 131072;        // one run per 128 K keys
+constexpr int kCT = 256;                  // collect threads
+constexpr int kCW = kCT / 64;             // collect waves
+constexpr int kCV = 4;                    // float4 per collect thread per chunk
+constexpr int kChunk4 = kCT * kCV;        // float4 per chunk (16 KB)
+constexpr int kWaveSlots = 8;             // candidate slots per (chunk, wave)
+constexpr int kTile = 64;                 // NMS tile
+
+struct SegInfo {
+  uint32_t floor;     // collect keys >= floor
+  uint32_t exact_lo;  // keys >= exact_lo have a larger sigmoid than any key < floor
+  int32_t k;          // effective k: min(topk_candidates, anchors, keys)
+  int32_t exact;      // 1: skip the floor, select in the workgroup (tests)
+  int32_t novf;       // collect's overflow appends (counted past kCap)
+  int32_t pad;
+  uint64_t ts[10];    // wall-clock stamps of the phases (tools/retina_post_ab.py --debug)
+  uint64_t cyc[10];   // shader-clock stamps at the same points (the clock the phases ran at)
+};
+
+struct RetinaGeo {
+  int32_t len[D2MI_MAX_LEVELS];         // keys per image and level (H W A K)
+  int32_t anchors[D2MI_MAX_LEVELS];     // H W A
+  int32_t chunk0[D2MI_MAX_LEVELS + 1];  // per-image prefix of collect chunks
+  int32_t L, N, K;
+};
+
+__device__ __forceinline__ const float* seg_ptr(const float* base, const Levels& lv, int n, int l,
+                                                int K) {
+  return base + lv.off_a[l] + (int64_t)n * lv.img_a[l] * K;
+}
+
+__device__ __forceinline__ uint64_t stamp() { return (uint64_t)wall_clock64(); }
+__device__ __forceinline__ uint64_t cycles() { return (uint64_t)clock64(); }
+
+// Wave-aggregated append: one atomic per wave with hits.  Returns the slot
+// of this lane's hit (or -1).  Lanes outside the branch do not take part.
+__device__ __forceinline__ int wave_append(bool hit, int* counter) {
+  const uint64_t b = __ballot(hit);
+  if (!b) return -1;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)b) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(b));
+  base = __shfl(base, leader);
+  return hit ? base + __popcll(b & ((1ull << lane) - 1ull)) : -1;
+}
+
+// Inclusive scan of one value per thread over the workgroup (part: 16 words).
+__device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t* part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) part[w] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int j = 0; j < w; ++j) before += part[j];
+  __syncthreads();
+  return before + incl;
+}
+
+// Bitonic sort of 1,024 keys, one per thread; returns the key at the thread's
+// position in ascending order.  Exchanges at strides < 64 stay in the wave
+// (cross-lane), the 10 larger ones go through lds (2 x 1,024 words, used in
+// turn: one barrier per exchange).
+__device__ uint64_t bitonic1024(uint64_t v, uint64_t* lds) {
+  const int t = threadIdx.x;
+  int buf = 0;
+  for (int size = 2; size <= kWG; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      uint64_t o;
+      if (stride < 64) {
+        o = (uint64_t)__shfl_xor((unsigned long long)v, stride);
+      } else {
+        uint64_t* b = lds + buf * kWG;
+        b[t] = v;
+        __syncthreads();
+        o = b[t ^ stride];
+        buf ^= 1;
+      }
+      const bool up = (t & size) == 0, low = (t & stride) == 0;
+      const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
+      v = (low == up) ? mn : mx;
+    }
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ floor
+__global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restrict__ base,
+                                                           Levels lv, RetinaGeo g, int topk,
+                                                           int force_exact,
+                                                           SegInfo* __restrict__ info,
+                                                           uint32_t* __restrict__ maxc) {
+  const uint64_t t_start = stamp(), c_start = cycles();
+  const int s = blockIdx.x, n = s / g.L, l = s - n * g.L;
+  const int len = g.len[l];
+  const int kk = max(0, min(min(topk, g.anchors[l]), len));
+  const int t = threadIdx.x;
+  __shared__ uint64_t xch[kWG];
+  __shared__ uint32_t s_floor;
+  if (l == 0 && t == 0) maxc[n] = kKeyNegInf;
+  if (kk == 0 || len <= kCap || force_exact) {
+    if (t == 0) {
+      info[s].floor = kk == 0 ? 0xffffffffu : 0u;
+      info[s].exact_lo = 0u;
+      info[s].k = kk;
+      info[s].exact = (kk > 0 && len > kCap && force_exact) ? 1 : 0;
+      info[s].novf = 0;
+      info[s].ts[0] = t_start;
+      info[s].ts[1] = stamp();
+      info[s].cyc[0] = c_start;
+      info[s].cyc[1] = cycles();
+    }
+    return;
+  }
+  const float* p = seg_ptr(base, lv, n, l, g.K);
+  const int nruns = (len + kRunStride - 1) / kRunStride;
+  uint32_t best = 0;
+  if ((((uintptr_t)p) & 15) == 0 && nruns >= 8) {
+    // every run but the last is whole: thread t takes float4 (t & 255) of runs
+    // (t >> 8) + 4 u, 24 loads in flight (one round for up to 96 runs)
+    constexpr int U = 24;
+    const int q = t & 255, full = nruns - 1;
+    for (int r0 = t >> 8; r0 < full; r0 += 4 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = r0 + 4 * u;
+        v[u] = r < full ? *reinterpret_cast<const float4*>(p + (int64_t)r * kRunStride + 4 * q)
+                        : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        best = max(best, max(max(orderable(v[u].x), orderable(v[u].y)),
+                             max(orderable(v[u].z), orderable(v[u].w))));
+    }
+    const int64_t e = (int64_t)full * kRunStride + t;  // the last run, one key per thread
+    if (e < len) best = max(best, orderable(p[e]));
+  } else {  // (few runs: one sample per thread and run, so the maxima are the samples)
+    for (int r = 0; r < nruns; ++r) {
+      const int64_t e = (int64_t)r * kRunStride + t;
+      if (e < len) best = max(best, orderable(p[e]));
+    }
+  }
+  int64_t nsamp = 0;
+  for (int r = 0; r < nruns; ++r) nsamp += min<int64_t>(kRun, len - (int64_t)r * kRunStride);
+  // keys of the whole segment at the floor: about 4 k (never past the
+  // candidate buffer's middle ground), as a count of sampled keys
+  const int target = min(4 * kk, (kk + kCap) / 2);
+  const int ts = (int)max<int64_t>(1, min<int64_t>(kWG, (int64_t)target * nsamp / len));
+  // the ts-th largest thread maximum, bit by bit from the top (the largest
+  // value that at least ts maxima reach), by wave 0 alone: ballot counts, no
+  // further barriers
+  __shared__ uint32_t mx[kWG];
+  mx[t] = best;
+  __syncthreads();
+  uint32_t f0 = 0;
+  if (t < 64) {
+    uint32_t vals[kWG / 64];
+#pragma unroll
+    for (int j = 0; j < kWG / 64; ++j) vals[j] = mx[j * 64 + t];
+    for (int b = 31; b >= 0; --b) {
+      const uint32_t cand = f0 | (1u << b);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < kWG / 64; ++j) c += __popcll(__ballot(vals[j] >= cand));
+      if (c >= ts) f0 = cand;
+    }
+  }
+  if (t == 0) {
+    uint32_t floor = f0, exact_lo = f0;
+    if (f0 > kKeyNegInf && f0 <= kKeyPosInf) {  // no sigmoid tie across exact_lo
+      const uint32_t lb = lower_bound_sig(kKeyNegInf, f0, sigmoidf_tf(from_orderable(f0)));
+      exact_lo = lb;
+      floor = lb > kKeyNegInf + kWindowMargin ? lb - kWindowMargin : kKeyNegInf;
+    }
+    info[s].floor = floor;
+    info[s].exact_lo = exact_lo;
+    info[s].k = kk;
+    info[s].exact = 0;
+    info[s].novf = 0;
+    info[s].ts[0] = t_start;
+    info[s].ts[1] = stamp();
+    info[s].cyc[0] = c_start;
+    info[s].cyc[1] = cycles();
+  }
+}
+
+// ---------------------------------------------------------------- collect
+struct ChunkAt {
+  const float4* p4;
+  int s, h, len, q0, n4;
+  uint32_t floor;
+  bool on;
+};
+
+__device__ __forceinline__ ChunkAt locate_chunk(int c, const float* base, const Levels& lv,
+                                                const RetinaGeo& g, const SegInfo* info) {
+  const int cpi = g.chunk0[g.L];
+  const int n = c / cpi, r = c - n * cpi;
+  int l = 0;
+  while (l + 1 < g.L && g.chunk0[l + 1] <= r) ++l;
+  ChunkAt a;
+  a.s = n * g.L + l;
+  const float* p = seg_ptr(base, lv, n, l, g.K);
+  a.h = (int)(((uintptr_t)p >> 2) & 3);
+  a.p4 = reinterpret_cast<const float4*>(p - a.h);
+  a.len = g.len[l];
+  a.n4 = (a.h + a.len + 3) >> 2;
+  a.q0 = (r - g.chunk0[l]) * kChunk4;
+  a.floor = info[a.s].floor;
+  a.on = info[a.s].k > 0 && !info[a.s].exact && a.q0 < a.n4;
+  return a;
+}
+
+typedef float nv4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void load_chunk(const ChunkAt& a, float4 (&v)[kCV]) {
+  const nv4* p = reinterpret_cast<const nv4*>(a.p4);
+#pragma unroll
+  for (int u = 0; u < kCV; ++u) {
+    const int q = a.q0 + u * kCT + threadIdx.x;
+    nv4 x = {0.f, 0.f, 0.f, 0.f};
+    if (a.on && q < a.n4) x = __builtin_nontemporal_load(&p[q]);  // read once: no reuse
+    v[u] = make_float4(x.x, x.y, x.z, x.w);
+  }
+}
+
+__global__ __launch_bounds__(kCT) void retina_collect_kernel(
+    const float* __restrict__ base, Levels lv, RetinaGeo g, SegInfo* __restrict__ info,
+    int32_t* __restrict__ wcount, uint64_t* __restrict__ wslot, uint64_t* __restrict__ ovf) {
+  const int total = g.N * g.chunk0[g.L];
+  int c = blockIdx.x;
+  if (c >= total) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  ChunkAt cur = locate_chunk(c, base, lv, g, info);
+  float4 v[kCV];
+  load_chunk(cur, v);
+  for (; c < total; c += gridDim.x) {
+    const int cn = c + gridDim.x;
+    ChunkAt nxt = cur;
+    float4 w[kCV];
+    if (cn < total) {
+      nxt = locate_chunk(cn, base, lv, g, info);
+      load_chunk(nxt, w);
+    }
+    auto hit = [&](int q, int i, float e) {
+      return cur.on && q < cur.n4 && i >= 0 && i < cur.len && orderable(e) >= cur.floor;
+    };
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kCV; ++u) {
+      const int q = cur.q0 + u * kCT + threadIdx.x;
+      const int i0 = 4 * q - cur.h;
+      cnt += (hit(q, i0, v[u].x) ? 1 : 0) + (hit(q, i0 + 1, v[u].y) ? 1 : 0) +
+             (hit(q, i0 + 2, v[u].z) ? 1 : 0) + (hit(q, i0 + 3, v[u].w) ? 1 : 0);
+    }
+    const size_t slot = (size_t)c * kCW + wv;
+    if (__ballot(cnt > 0)) {
+      int incl = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const int wtot = __shfl(incl, 63);
+      int ob = 0;  // this wave's first overflow position (hits past its 8 slots)
+      if (wtot > kWaveSlots) {
+        if (lane == 0) ob = atomicAdd(&info[cur.s].novf, wtot - kWaveSlots);
+        ob = __shfl(ob, 0);
+      }
+      if (lane == 0) wcount[slot] = wtot;
+      int pos = incl - cnt;
+      // entry-major: entry j of every slot in one row (the gather reads first
+      // entries contiguously)
+      const size_t nslots = (size_t)total * kCW;
+      uint64_t* dst = wslot + slot;
+      uint64_t* odst = ovf + (size_t)cur.s * kCap;
+#pragma unroll
+      for (int u = 0; u < kCV; ++u) {
+        const int q = cur.q0 + u * kCT + threadIdx.x;
+        const int i0 = 4 * q - cur.h;
+        const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (hit(q, i0 + j, e[j])) {
+            const uint64_t ent = ((uint64_t)__float_as_uint(e[j]) << 32) | (uint32_t)(i0 + j);
+            if (pos < kWaveSlots) dst[(size_t)pos * nslots] = ent;
+            else if (ob + pos - kWaveSlots < kCap) odst[ob + pos - kWaveSlots] = ent;
+            ++pos;
+          }
+        }
+      }
+    } else if (lane == 0) {
+      wcount[slot] = 0;
+    }
+    cur = nxt;
+#pragma unroll
+    for (int u = 0; u < kCV; ++u) v[u] = w[u];
+  }
+}
+
+// ----------------------------------------------------------------- finish
+// f(index, value) over a segment by the whole workgroup: aligned float4 body
+// (8 loads in flight per thread), scalar head and tail.
+template <typename F>
+__device__ __forceinline__ void wg_visit(const float* __restrict__ p, int len, F f) {
+  const int h = min(len, (int)((4 - (((uintptr_t)p >> 2) & 3)) & 3));
+  if ((int)threadIdx.x < h) f((int)threadIdx.x, p[threadIdx.x]);
+  const float4* p4 = reinterpret_cast<const float4*>(p + h);
+  const int n4 = (len - h) >> 2;
+  constexpr int U = 8;
+  for (int q0 = 0; q0 < n4; q0 += U * kWG) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * kWG + threadIdx.x;
+      v[u] = q < n4 ? p4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * kWG + threadIdx.x;
+      if (q < n4) {
+        const int i = h + 4 * q;
+        f(i, v[u].x);
+        f(i + 1, v[u].y);
+        f(i + 2, v[u].z);
+        f(i + 3, v[u].w);
+      }
+    }
+  }
+  const int t0 = h + 4 * n4;
+  if (t0 + (int)threadIdx.x < len) f(t0 + (int)threadIdx.x, p[t0 + threadIdx.x]);
+}
+
+// The exact top-k set of p[0, len) by (sigmoid desc, index asc) into sk as
+// raw entries (value bits << 32 | index); returns their count (k, or more
+// when the tie group fits: the sort orders ties by index).  Radix select of
+// the k-th largest raw key u (12 + 12 + 8 bits), then keys above u's sigmoid
+// tie group and the group itself (keys of equal sigmoid, tested exactly in a
+// window below it), the group in index order when it does not fit.
+__device__ int exact_select(const float* __restrict__ p, int len, int k, uint64_t* sk,
+                            uint32_t* hist, uint32_t* part, int32_t* err) {
+  __shared__ int s_bin;
+  __shared__ uint32_t s_gt;
+  __shared__ int s_above, s_tie;
+  __shared__ uint32_t s_tie_hi, s_win_lo;
+  __shared__ float s_sig;
+  __shared__ int s_sigmode;
+  const int t = threadIdx.x;
+  uint32_t prefix = 0;
+  int krem = k;
+  for (int pass = 0; pass < 3; ++pass) {
+    const int nbits = pass < 2 ? 12 : 8;
+    const int shift = pass == 0 ? 20 : (pass == 1 ? 8 : 0);
+    const int hs = shift + nbits;
+    const uint32_t mask = (1u << nbits) - 1u;
+    for (int i = t; i < 4096; i += kWG) hist[i] = 0;
+    if (t == 0) s_bin = -1;
+    __syncthreads();
+    wg_visit(p, len, [&](int, float v) {
+      const uint32_t key = orderable(v);
+      if (hs == 32 || (key >> hs) == prefix) atomicAdd(&hist[(key >> shift) & mask], 1u);
+    });
+    __syncthreads();
+    // thread t owns 4 bins from the top: 4095 - 4t .. 4092 - 4t
+    uint32_t c4[4], loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c4[j] = hist[4095 - (4 * t + j)];
+      loc += c4[j];
+    }
+    const uint32_t incl = wg_inclusive_scan(loc, part);
+    const uint32_t before = incl - loc;
+    if ((uint32_t)krem > before && (uint32_t)krem <= incl) {
+      uint32_t acc = before;
+      for (int j = 0; j < 4; ++j) {
+        if ((uint32_t)krem <= acc + c4[j]) {
+          s_bin = 4095 - (4 * t + j);
+          s_gt = acc;
+          break;
+        }
+        acc += c4[j];
+      }
+    }
+    __syncthreads();
+    if (s_bin < 0) {  // counts inconsistent (cannot happen)
+      if (t == 0) atomicOr(err, kErrTopkCapacity);
+      return 0;
+    }
+    prefix = (prefix << nbits) | (uint32_t)s_bin;
+    krem -= (int)s_gt;
+    __syncthreads();
+  }
+  const uint32_t u = prefix;
+  if (t == 0) {
+    s_above = 0;
+    s_tie = 0;
+    if (u > kKeyNegInf && u <= kKeyPosInf) {
+      const float su = sigmoidf_tf(from_orderable(u));
+      const uint32_t lo = lower_bound_sig(kKeyNegInf, u, su);
+      s_sig = su;
+      s_sigmode = 1;
+      s_win_lo = lo > kKeyNegInf + kWindowMargin ? lo - kWindowMargin : kKeyNegInf;
+      s_tie_hi = upper_bound_sig(u, kKeyPosInf, su);
+    } else {
+      s_sig = 0.f;
+      s_sigmode = 0;
+      s_win_lo = u;
+      s_tie_hi = u;
+    }
+  }
+  __syncthreads();
+  const uint32_t tie_hi = s_tie_hi, win_lo = s_win_lo;
+  const float su = s_sig;
+  const bool sigmode = s_sigmode != 0;
+  const int room = kCap - k;  // tie slots after the k "above" slots
+  auto is_tie = [&](uint32_t key, float v) {
+    return key >= win_lo && key <= tie_hi && (sigmode ? sigmoidf_tf(v) == su : key == u);
+  };
+  wg_visit(p, len, [&](int i, float v) {
+    const uint32_t key = orderable(v);
+    const uint64_t e = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)i;
+    const bool above = key > tie_hi;
+    const int pa = wave_append(above, &s_above);
+    if (pa >= 0 && pa < k) sk[pa] = e;
+    const int pt = wave_append(!above && is_tie(key, v), &s_tie);
+    if (pt >= 0 && pt < room) sk[k + pt] = e;
+  });
+  __syncthreads();
+  const int G = min(s_above, k), T = s_tie;
+  if (T <= room) {  // every tied key fits: shift them down behind the above keys
+    for (int c0 = 0; c0 < T; c0 += kWG) {
+      const int i = c0 + t;
+      const uint64_t e = i < T ? sk[k + i] : 0ull;
+      __syncthreads();
+      if (i < T) sk[G + i] = e;
+      __syncthreads();
+    }
+    return G + T;
+  }
+  // the tie group in index order until k: blocks of 4 keys per thread
+  const int need = k - G;
+  int found = 0;
+  for (int b0 = 0; b0 < len && found < need; b0 += 4 * kWG) {
+    const int i0 = b0 + 4 * t;
+    bool hit[4];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j;
+      hit[j] = false;
+      if (i < len) {
+        const float v = p[i];
+        hit[j] = is_tie(orderable(v), v);
+      }
+      c += hit[j] ? 1u : 0u;
+    }
+    const uint32_t incl = wg_inclusive_scan(c, part);
+    uint32_t pos = incl - c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (hit[j]) {
+        if (found + (int)pos < need)
+          sk[G + found + pos] = ((uint64_t)__float_as_uint(p[i0 + j]) << 32) | (uint32_t)(i0 + j);
+        ++pos;
+      }
+    }
+    if (t == kWG - 1) s_bin = (int)incl;  // block total
+    __syncthreads();
+    found += s_bin;
+    __syncthreads();
+  }
+  return G + min(found, need);
+}
+
+// The k-th smallest (1-based) of the valid values, 8 per thread: radix
+// select, 12 + 12 + 8 bits, histograms in LDS.
+__device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8], int k,
+                                    uint32_t* hist, uint32_t* part) {
+  __shared__ int s_bin;
+  __shared__ uint32_t s_lt;
+  const int t = threadIdx.x;
+  uint32_t prefix = 0;
+  int krem = k;
+  for (int pass = 0; pass < 3; ++pass) {
+    const int nbits = pass < 2 ? 12 : 8;
+    const int shift = pass == 0 ? 20 : (pass == 1 ? 8 : 0);
+    const int hs = shift + nbits;
+    const uint32_t mask = (1u << nbits) - 1u;
+    for (int i = t; i < 4096; i += kWG) hist[i] = 0;
+    if (t == 0) {
+      s_bin = 0;
+      s_lt = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (ok[j] && (hs == 32 || (h[j] >> hs) == prefix))
+        atomicAdd(&hist[(h[j] >> shift) & mask], 1u);
+    __syncthreads();
+    uint32_t c4[4], loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c4[j] = hist[4 * t + j];
+      loc += c4[j];
+    }
+    const uint32_t incl = wg_inclusive_scan(loc, part);
+    const uint32_t before = incl - loc;
+    if ((uint32_t)krem > before && (uint32_t)krem <= incl) {
+      uint32_t acc = before;
+      for (int j = 0; j < 4; ++j) {
+        if ((uint32_t)krem <= acc + c4[j]) {
+          s_bin = 4 * t + j;
+          s_lt = acc;
+          break;
+        }
+        acc += c4[j];
+      }
+    }
+    __syncthreads();
+    prefix = (prefix << nbits) | (uint32_t)s_bin;
+    krem -= (int)s_lt;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(kWG) void retina_finish_kernel(
+    const float* __restrict__ base_a, const float* __restrict__ base_b, Levels lv, RetinaGeo g,
+    int topk, float thresh, DeltaCfg dc, SegInfo* __restrict__ info,
+    const int32_t* __restrict__ wcount, const uint64_t* __restrict__ wslot,
+    const uint64_t* __restrict__ ovf, float* __restrict__ cscore, float4* __restrict__ cbox,
+    int32_t* __restrict__ ccls, int32_t* __restrict__ lvl_cnt, uint32_t* __restrict__ maxc,
+    int32_t* __restrict__ err) {
+  extern __shared__ uint64_t sk[];  // kCap entries
+  __shared__ uint32_t hist[4096];
+  __shared__ uint32_t part[kWG / 64];
+  __shared__ int s_n, s_m, s_cnt, s_le;
+  const uint64_t t_start = stamp(), c_start = cycles();
+  const int s = blockIdx.x, n = s / g.L, l = s - n * g.L;
+  const int t = threadIdx.x;
+  const int xk = info[s].k, xexact = info[s].exact, xnovf = info[s].novf;
+  const uint32_t xlo = info[s].exact_lo;
+  if (xk == 0) {
+    if (t == 0) lvl_cnt[s] = 0;
+    return;
+  }
+  if (t == 0) {
+    s_n = 0;
+    s_m = 0;
+    s_cnt = 0;
+    s_le = 0;
+  }
+  __syncthreads();
+  // gather the wave slots of the segment's chunks (order is irrelevant: sorted
+  // below): every count in one round of loads, then the first two entries of
+  // each hit slot in a second, further entries (rare) after
+  const int cpi = g.chunk0[g.L];
+  const int w0 = (n * cpi + g.chunk0[l]) * kCW;
+  const int nw = (g.chunk0[l + 1] - g.chunk0[l]) * kCW;
+  const size_t nslots = (size_t)g.N * cpi * kCW;
+  bool ok = !xexact && xnovf <= kCap;
+  int m = 0;
+  auto put = [&](int p, uint64_t ent) {
+    if (p < kCap) sk[p] = ent;
+    m += orderable(__uint_as_float((uint32_t)(ent >> 32))) >= xlo ? 1 : 0;
+  };
+  if (ok) {
+    constexpr int U = 8;  // wave slots per thread per batch (1333x800 P3: 11,812 in two)
+    for (int e0 = 0; e0 < nw; e0 += U * kWG) {
+      int cc[U], pos[U];
+      uint64_t e1[U], e2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * kWG + t;
+        cc[u] = e < nw ? min(wcount[w0 + e], kWaveSlots) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t* src = wslot + (size_t)(w0 + e0 + u * kWG + t);
+        e1[u] = cc[u] > 0 ? src[0] : 0ull;
+        e2[u] = cc[u] > 1 ? src[nslots] : 0ull;
+      }
+      // positions: per wave one LDS atomic per batch row (wave prefix of the counts)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int incl = cc[u];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(incl, o);
+          if ((t & 63) >= o) incl += y;
+        }
+        const int wtot = __shfl(incl, 63);
+        int b = 0;
+        if ((t & 63) == 63 && wtot) b = atomicAdd(&s_n, wtot);
+        pos[u] = __shfl(b, 63) + incl - cc[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (cc[u] > 0) put(pos[u], e1[u]);
+        if (cc[u] > 1) put(pos[u] + 1, e2[u]);
+        for (int j = 2; j < cc[u]; ++j)
+          put(pos[u] + j, wslot[(size_t)j * nslots + (w0 + e0 + u * kWG + t)]);
+      }
+    }
+    __syncthreads();
+    const int nreg = s_n;
+    const uint64_t* osrc = ovf + (size_t)s * kCap;
+    for (int i = t; i < xnovf; i += kWG)
+      if (nreg + i < kCap) put(nreg + i, osrc[i]);
+    if (m) atomicAdd(&s_m, m);
+  }
+  __syncthreads();
+  const int nreg = s_n;
+  ok = ok && nreg + xnovf <= kCap;
+  ok = ok && s_m >= xk;
+  const uint64_t t_gather = stamp(), c_gather = cycles();
+  int nc = nreg + xnovf;
+  if (!ok) {
+    __syncthreads();
+    nc = exact_select(seg_ptr(base_a, lv, n, l, g.K), g.len[l], xk, sk, hist, part, err);
+  }
+  __syncthreads();
+  const uint64_t t_cand = stamp(), c_cand = cycles();
+  // sort keys (~orderable(sigmoid) << 32 | index), 8 per thread in registers
+  uint64_t kv[8];
+  uint32_t hi[8];
+  bool valid[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = j * kWG + t;
+    valid[j] = i < nc;
+    kv[j] = ~0ull;
+    if (valid[j]) {
+      const uint64_t e = sk[i];
+      const float sc = sigmoidf_tf(__uint_as_float((uint32_t)(e >> 32)));
+      kv[j] = ((uint64_t)(~orderable(sc)) << 32) | (uint32_t)e;
+    }
+    hi[j] = (uint32_t)(kv[j] >> 32);
+  }
+  const int kk = min(xk, nc);
+  __syncthreads();
+  // the kk smallest keys: all keys whose score word is <= the kk-th smallest
+  // one, when at most 1,024 (ties beyond that: the general sort)
+  const uint32_t thr32 = nc <= kWG ? 0xffffffffu : wg_kth_smallest(hi, valid, kk, hist, part);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int pos = wave_append(valid[j] && hi[j] <= thr32, &s_le);
+    if (pos >= 0 && pos < kWG) sk[pos] = kv[j];
+  }
+  __syncthreads();
+  const int nle = s_le;
+  if (nle <= kWG) {
+    const uint64_t v = t < nle ? sk[t] : ~0ull;
+    __syncthreads();
+    const uint64_t sv = bitonic1024(v, sk + kWG);
+    sk[t] = sv;
+  } else {  // more than 1,024 keys tie at the k-th score: bitonic over all of them
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sk[j * kWG + t] = kv[j];
+    int npad = 2;
+    while (npad < nc) npad <<= 1;
+    __syncthreads();
+    for (int size = 2; size <= npad; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const int lg = 31 - __clz(stride);
+        for (int i = t; i < (npad >> 1); i += kWG) {
+          const int lo = ((i >> lg) << (lg + 1)) + (i & (stride - 1));
+          const int hi2 = lo + stride;
+          const uint64_t a = sk[lo], b = sk[hi2];
+          const bool asc = (lo & size) == 0;
+          if ((a > b) == asc) {
+            sk[lo] = b;
+            sk[hi2] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t t_sorted = stamp(), c_sorted = cycles();
+  // top-k, threshold (a prefix: sorted by score), decode
+  const int capimg = g.L * topk;
+  const size_t o0 = (size_t)n * capimg + (size_t)l * topk;
+  const float4* d4 = reinterpret_cast<const float4*>(base_b + lv.off_b[l]) + (size_t)n * lv.img_b[l];
+  uint32_t mymax = 0;
+  bool any = false;
+  int kept = 0;
+  for (int j = t; j < kk; j += kWG) {
+    const uint64_t key = sk[j];
+    const float score = from_orderable(~(uint32_t)(key >> 32));
+    if (score > thresh) {
+      const int id = (int)(uint32_t)key;
+      const int aidx = id / g.K, cls = id - aidx * g.K;
+      const int hw = aidx / lv.A, a = aidx - hw * lv.A;
+      const float4 anc = anchor_at(lv, l, hw, a);
+      const float4 b = apply_delta(anc, d4[aidx], dc.wy, dc.wx, dc.wh, dc.ww, dc.clamp);
+      cscore[o0 + j] = score;
+      cbox[o0 + j] = b;
+      ccls[o0 + j] = cls;
+      const uint32_t bm = orderable(fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w)));
+      mymax = any ? max(mymax, bm) : bm;
+      any = true;
+      ++kept;
+    }
+  }
+  // per-wave max, one atomic per wave with a kept box
+  const int lane = t & 63;
+  uint32_t wm = any ? mymax : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, o));
+  if (__ballot(any) != 0 && lane == 0) atomicMax(&maxc[n], wm);
+  if (kept) atomicAdd(&s_cnt, kept);
+  __syncthreads();
+  if (t == 0) {
+    lvl_cnt[s] = s_cnt;
+    info[s].ts[2] = t_start;
+    info[s].ts[3] = t_gather;
+    info[s].ts[4] = t_cand;
+    info[s].ts[5] = t_sorted;
+    info[s].ts[6] = stamp();
+    info[s].cyc[2] = c_start;
+    info[s].cyc[3] = c_gather;
+    info[s].cyc[4] = c_cand;
+    info[s].cyc[5] = c_sorted;
+    info[s].cyc[6] = cycles();
+  }
+}
+
+// -------------------------------------------------------------------- nms
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Merge rank of the per-level sorted candidate lists of one image, many
+// workgroups per image (one candidate per thread): position = own rank +
+// earlier levels' scores >= s + later levels' scores > s (the concat
+// position breaks ties).  ord[image][position] = level * topk + rank.
+constexpr int kRankT = 256;
+__global__ __launch_bounds__(kRankT) void retina_rank_kernel(
+    RetinaGeo g, int topk, const float* __restrict__ cscore, const int32_t* __restrict__ lvl_cnt,
+    uint16_t* __restrict__ ord) {
+  extern __shared__ float sc[];  // [capimg]
+  __shared__ int cnt[D2MI_MAX_LEVELS], cum[D2MI_MAX_LEVELS + 1];
+  const int n = blockIdx.y, t = threadIdx.x;
+  const int L = g.L, capimg = L * topk;
+  const size_t o0 = (size_t)n * capimg;
+  if (t == 0) {
+    int acc = 0;
+    for (int l = 0; l < L; ++l) {
+      cnt[l] = lvl_cnt[n * L + l];
+      cum[l] = acc;
+      acc += cnt[l];
+    }
+    cum[L] = acc;
+  }
+  {
+    constexpr int U = 8 * kWG / kRankT / 4;  // float4 per thread: capimg <= 8 * kWG
+    float4 v[U];
+    const float4* src = reinterpret_cast<const float4*>(cscore + o0);  // capimg % 4 == 0
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q4 = u * kRankT + t;
+      v[u] = 4 * q4 < capimg ? src[q4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q4 = u * kRankT + t;
+      if (4 * q4 < capimg) reinterpret_cast<float4*>(sc)[q4] = v[u];
+    }
+  }
+  __syncthreads();
+  const int r = blockIdx.x * kRankT + t;
+  if (r >= cum[L]) return;
+  int l = 0;
+  while (l + 1 < L && cum[l + 1] <= r) ++l;
+  const int j = r - cum[l];
+  const float sv = sc[l * topk + j];
+  int lo[D2MI_MAX_LEVELS], hi[D2MI_MAX_LEVELS];
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+    lo[m] = 0;
+    hi[m] = (m < L && m != l) ? cnt[m] : 0;
+  }
+  // every level's search advances each step: D2MI_MAX_LEVELS probes in flight
+  for (int step = 0; step < 14; ++step) {
+    float pv[D2MI_MAX_LEVELS];
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m)
+      pv[m] = m < L ? sc[m * topk + min((lo[m] + hi[m]) >> 1, topk - 1)] : 0.f;
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+      if (lo[m] < hi[m]) {
+        const int mid = (lo[m] + hi[m]) >> 1;
+        if (m < l ? pv[m] >= sv : pv[m] > sv) lo[m] = mid + 1;
+        else hi[m] = mid;
+      }
+    }
+  }
+  int pos = j;
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) pos += lo[m];
+  ord[o0 + pos] = (uint16_t)(l * topk + j);
+}
+
+__global__ __launch_bounds__(kWG) void retina_nms_kernel(
+    RetinaGeo g, int topk, const float* __restrict__ cscore, const float4* __restrict__ cbox,
+    const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
+    const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
+    SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
+    int32_t* __restrict__ oc, uint8_t* __restrict__ ov) {
+  extern __shared__ float4 dyn[];
+  const uint64_t t_start = stamp(), c_start = cycles();
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int L = g.L, capimg = L * topk;
+  // LDS: kept (offset box, box, score, class) [max_det], the window's
+  // (offset box, box, score, class) [kWG]
+  float4* kept_obox = dyn;
+  float4* kept_box = kept_obox + max_det;
+  float4* wobox = kept_box + max_det;
+  float4* wbox = wobox + kWG;
+  float* kept_sc = reinterpret_cast<float*>(wbox + kWG);
+  int32_t* kept_cl = reinterpret_cast<int32_t*>(kept_sc + max_det);
+  float* wsc = reinterpret_cast<float*>(kept_cl + max_det);
+  int32_t* wcl = reinterpret_cast<int32_t*>(wsc + kWG);
+  __shared__ uint64_t diag[kTile], wsup[kWG / 64];
+  __shared__ int s_total, s_nk;
+  const size_t o0 = (size_t)n * capimg;
+  if (t == 0) {
+    int acc = 0;
+    for (int l = 0; l < L; ++l) acc += lvl_cnt[n * L + l];
+    s_total = acc;
+    s_nk = 0;
+  }
+  __syncthreads();
+  const uint64_t t_ranked = stamp(), c_ranked = cycles();
+  const int total = s_total;
+  const float off1 = from_orderable(maxc[n]) + 1.f;
+  int nk = 0;
+  for (int w0 = 0; w0 < total && nk < max_det; w0 += kWG) {
+    // window: the next 1,024 candidates in score order
+    const int wn = min(kWG, total - w0);
+    if (t < wn) {
+      const int q = ord[o0 + w0 + t];
+      const float4 c = cbox[o0 + q];
+      const int cl = ccls[o0 + q];
+      const float off = (float)cl * off1;
+      wobox[t] = make_float4(c.x + off, c.y + off, c.z + off, c.w + off);
+      wbox[t] = c;
+      wsc[t] = cscore[o0 + q];
+      wcl[t] = cl;
+    }
+    __syncthreads();
+    for (int t0 = 0; t0 < wn && nk < max_det; t0 += kTile) {
+      const int rem = wn - t0;
+      const float4 cb = lane < rem ? wobox[t0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      bool sup = false;
+      for (int i = w; i < nk; i += kWG / 64) sup = sup || (tf_iou(kept_obox[i], cb) > thr);
+      const uint64_t ws = __ballot(sup);
+      if (lane == 0) wsup[w] = ws;
+      constexpr int RPW = kTile / (kWG / 64);  // tile rows per wave
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int r = w * RPW + rr;
+        const bool live = r < rem && lane > r && lane < rem;
+        const uint64_t d = __ballot(live && tf_iou(wobox[t0 + r], cb) > thr);
+        if (lane == 0) diag[r] = d;
+      }
+      __syncthreads();
+      if (w == 0) {
+        uint64_t removed = 0;
+#pragma unroll
+        for (int vv = 0; vv < kWG / 64; ++vv) removed |= wsup[vv];
+        if (rem < 64) removed |= ~((1ull << rem) - 1ull);
+        const uint64_t my_diag = diag[lane];
+        uint64_t keptm = 0;
+        int k2 = nk;
+        for (int r = 0; r < kTile; ++r) {
+          if (k2 >= max_det) break;
+          if (!((removed >> r) & 1ull)) {
+            keptm |= 1ull << r;
+            ++k2;
+            removed |= readlane64(my_diag, r);
+          }
+        }
+        if ((keptm >> lane) & 1ull) {
+          const int pos = nk + __popcll(keptm & ((1ull << lane) - 1ull));
+          kept_obox[pos] = wobox[t0 + lane];
+          kept_box[pos] = wbox[t0 + lane];
+          kept_sc[pos] = wsc[t0 + lane];
+          kept_cl[pos] = wcl[t0 + lane];
+        }
+        if (lane == 0) s_nk = k2;
+      }
+      __syncthreads();
+      nk = s_nk;
+    }
+  }
+  for (int i = t; i < max_det; i += kWG) {
+    const size_t o = (size_t)n * max_det + i;
+    const bool k = i < nk;
+    ob[o] = k ? kept_box[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    os[o] = k ? kept_sc[i] : 0.f;
+    oc[o] = k ? kept_cl[i] : 0;
+    ov[o] = k ? 1 : 0;
+  }
+  if (t == 0) {
+    info[n * L].ts[7] = t_start;
+    info[n * L].ts[8] = t_ranked;
+    info[n * L].ts[9] = stamp();
+    info[n * L].cyc[7] = c_start;
+    info[n * L].cyc[8] = c_ranked;
+    info[n * L].cyc[9] = cycles();
+  }
+}
+
+struct FusedWs {
+  SegInfo* info;
+  int32_t* wcount;
+  uint64_t* wslot;
+  uint64_t* ovf;
+  float* cscore;
+  float4* cbox;
+  int32_t* ccls;
+  int32_t* lvl_cnt;
+  uint32_t* maxc;
+  uint16_t* ord;
+};
+template <typename WS>
+void fused_layout(WS& w, FusedWs* o, int N, int L, int k, int chunks) {
+  const int S = N * L;
+  const size_t C = (size_t)N * L * k;
+  auto a0 = w.template take<SegInfo>(S);
+  auto a1 = w.template take<int32_t>((size_t)chunks * kCW);
+  auto a2 = w.template take<uint64_t>((size_t)chunks * kCW * kWaveSlots);
+  auto a3 = w.template take<uint64_t>((size_t)S * kCap);
+  auto a4 = w.template take<float>(C);
+  auto a5 = w.template take<float4>(C);
+  auto a6 = w.template take<int32_t>(C);
+  auto a7 = w.template take<int32_t>(S);
+  auto a8 = w.template take<uint32_t>(N);
+  auto a9 = w.template take<uint16_t>(C);
+  if (o)
+    *o = FusedWs{(SegInfo*)a0, (int32_t*)a1, (uint64_t*)a2, (uint64_t*)a3, (float*)a4,
+                 (float4*)a5, (int32_t*)a6, (int32_t*)a7, (uint32_t*)a8, (uint16_t*)a9};
+}
+struct SizerP {
+  WorkspaceSizer z;
+  template <typename T>
+  T* take(size_t n) {
+    z.take<T>(n);
+    return nullptr;
+  }
+};
+
+// per-level geometry; false when a level does not fit the int32 indexing
+bool make_geo(RetinaGeo& g, const int32_t* level_hw, int L, int A, int K, int N) {
+  g = RetinaGeo{};
+  g.L = L;
+  g.N = N;
+  g.K = K;
+  g.chunk0[0] = 0;
+  for (int l = 0; l < L; ++l) {
+    const int64_t anchors = (int64_t)level_hw[2 * l] * level_hw[2 * l + 1] * A;
+    const int64_t len = anchors * K;
+    if (len >= (1ll << 31) - 8) return false;
+    g.len[l] = (int32_t)len;
+    g.anchors[l] = (int32_t)anchors;
+    const int64_t c = g.chunk0[l] + (len + 3 + 4LL * kChunk4 - 1) / (4LL * kChunk4);
+    if (c * N >= (1ll << 31) / kCW) return false;
+    g.chunk0[l + 1] = (int32_t)c;
+  }
+  return true;
+}
+}  // namespace
+
+bool retina_fused_eligible(int L, int k, int max_det) {
+  return L >= 1 && L <= D2MI_MAX_LEVELS && k >= 1 && k <= kCap && (int64_t)L * k <= 8 * kWG &&
+         (L * k) % 4 == 0 && max_det >= 1 && max_det <= 1000;
+}
+
+size_t retina_fused_workspace_size(int N, int L, const int32_t* level_hw, int A, int K, int k) {
+  RetinaGeo g;
+  if (!make_geo(g, level_hw, L, A, K, N)) return 0;
+  SizerP s;
+  fused_layout(s, nullptr, N, L, k, N * g.chunk0[L]);
+  return s.z.off;
+}
+
+int retinanet_fused(const float* const* cls, const float* const* box, const Levels& lv,
+                    const int32_t* level_hw, int K, int N, int k, float score_thresh,
+                    float nms_thresh, int max_det, DeltaCfg dc, float* out_boxes,
+                    float* out_scores, int32_t* out_classes, uint8_t* out_valid, void* workspace,
+                    size_t workspace_bytes, hipStream_t st, bool force_exact) {
+  const int L = lv.L, S = N * L;
+  D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
+  RetinaGeo g;
+  D2MI_REQUIRE(make_geo(g, level_hw, L, lv.A, K, N), "RetinaNet level too large");
+  const int chunks = N * g.chunk0[L];
+  Workspace w(workspace, workspace_bytes);
+  FusedWs o;
+  fused_layout(w, &o, N, L, k, chunks);
+  D2MI_REQUIRE(w.ok(), "retinanet workspace too small (%zu < %zu)", workspace_bytes, w.off);
+  hipLaunchKernelGGL(retina_floor_kernel, dim3(S), dim3(kWG), 0, st, cls[0], lv, g, k,
+                     force_exact ? 1 : 0, o.info, o.maxc);
+  D2MI_LAUNCH_CHECK();
+  // persistent collect grid: the workgroups the device holds at once
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    D2MI_HIP(hipGetDevice(&dev));
+    D2MI_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    D2MI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, retina_collect_kernel, kCT, 0));
+    resident = std::max(1, cus * std::max(1, per));
+  }
+  hipLaunchKernelGGL(retina_collect_kernel, dim3(std::min(chunks, resident)), dim3(kCT), 0, st, cls[0],
+                     lv, g, o.info, o.wcount, o.wslot, o.ovf);
+  D2MI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(retina_finish_kernel, dim3(S), dim3(kWG), kCap * sizeof(uint64_t), st, cls[0],
+                     box[0], lv, g, k, score_thresh, dc, o.info, o.wcount, o.wslot, o.ovf,
+                     o.cscore, o.cbox, o.ccls, o.lvl_cnt, o.maxc, error_word());
+  D2MI_LAUNCH_CHECK();
+  const int capimg = L * k;
+  hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
+                     (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);
+  D2MI_LAUNCH_CHECK();
+  const size_t lds = (size_t)(max_det + kWG) * (2 * sizeof(float4) + sizeof(float) + sizeof(int32_t));
+  hipLaunchKernelGGL(retina_nms_kernel, dim3(N), dim3(kWG), lds, st, g, k, o.cscore, o.cbox,
+                     o.ccls, o.lvl_cnt, o.ord, o.maxc, nms_thresh, max_det, o.info,
+                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace d2mi

@@ -52,7 +52,7 @@
 //            sigmoid) -> straight to rank; otherwise back to the radix passes,
 //            which then run exactly as without the floor.
 // Exact either way; the sample only decides how often the fallback runs.
-#include "internal.h"
+#include "detect.h"
 
 namespace d2mi {
 namespace {
@@ -78,8 +78,6 @@ struct SegState {
   uint32_t floor_key;
   int32_t nF[16];    // sampled floor: candidates per spread slot (fcollect)
 };
-
-__device__ __forceinline__ float sigmoidf_tf(float v) { return 1.f / (1.f + expf(-v)); }
 
 __device__ __forceinline__ float key_value(float v, int key_mode) {
   return key_mode == 1 ? sigmoidf_tf(v) : v;
@@ -208,32 +206,6 @@ __global__ __launch_bounds__(kThreads) void topk_hist_kernel(
     if (h[i]) atomicAdd(&g[i], h[i]);
 }
 
-// sigmoid(from_orderable(u)) over a key range, as a function of the key:
-// monotone non-decreasing (sigmoid is).  Smallest key in [lo, hi] whose
-// sigmoid is >= s, or hi + 1.
-__device__ uint32_t lower_bound_sig(uint32_t lo, uint32_t hi, float s) {
-  uint32_t a = lo, b = hi + 1;  // search [a, b)
-  while (a < b) {
-    const uint32_t m = a + ((b - a) >> 1);
-    if (sigmoidf_tf(from_orderable(m)) >= s) b = m;
-    else a = m + 1;
-  }
-  return a;
-}
-// Largest key in [lo, hi] whose sigmoid is <= s (lo's sigmoid must be <= s).
-__device__ uint32_t upper_bound_sig(uint32_t lo, uint32_t hi, float s) {
-  uint32_t a = lo, b = hi;
-  while (a < b) {
-    const uint32_t m = a + ((b - a + 1) >> 1);
-    if (sigmoidf_tf(from_orderable(m)) <= s) a = m;
-    else b = m - 1;
-  }
-  return a;
-}
-
-constexpr uint32_t kKeyNegInf = 0x007fffffu;  // orderable(-inf)
-constexpr uint32_t kKeyPosInf = 0xff800000u;  // orderable(+inf)
-constexpr uint32_t kWindowMargin = 256;       // keys below the solved tie edge still tested
 
 __device__ void finish_state(SegState& x, int key_mode) {
   // x.edge: lowest key of the prefix bin (mode 1) or the resolved key (mode 3)

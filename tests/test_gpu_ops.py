@@ -469,12 +469,26 @@ def _retina_logits(rng, shape, dist):
     return x.astype(F32)
 
 
+@pytest.mark.parametrize("path", ["fused", "fused_exact_select", "unfused"])
 @pytest.mark.parametrize("dist", ["normal", "quantized", "saturated", "sparse"])
-def test_retinanet_inference_vs_oracle(dev, dist):
+def test_retinanet_inference_vs_oracle(dev, dist, path):
     """Dense top-k + decode + NMS vs the oracle.  The distributions drive the
     top-k down both of its paths: the sampled floor (normal, quantized, sparse)
-    and the radix passes it falls back to (saturated: the tie group of
-    sigmoid == 1 overflows the candidate buffer)."""
+    and the exact select it falls back to (saturated: the tie group of
+    sigmoid == 1 overflows the candidate buffer).  ``path``: the four-launch
+    pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
+    its in-workgroup exact select forced on every level (2), and the unfused
+    top-k / sort / mask NMS pipeline (0)."""
+    from detectron2_tensorflow_amd.layers import ops as lops
+    old = lops.get_tuning("retina_fused")
+    lops.set_tuning("retina_fused", {"fused": 1, "fused_exact_select": 2, "unfused": 0}[path])
+    try:
+        _retinanet_inference_vs_oracle(dev, dist)
+    finally:
+        lops.set_tuning("retina_fused", old)
+
+
+def _retinanet_inference_vs_oracle(dev, dist):
     rng = np.random.default_rng(41)
     N, IH, IW, A, K = 2, 320, 320, 9, 80
     strides = [8, 16, 32, 64, 128]

@@ -32,7 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--min-m", type=int, default=1, help="conv_stream value of the stream arm")
+    ap.add_argument("--min-m", type=int, default=-1,
+                    help="conv_stream value of the stream arm (< 0: every eligible shape)")
     ap.add_argument("--shapes", default=None)
     a = ap.parse_args()
     shapes = a.shapes.split(";") if a.shapes else SHAPES
