@@ -360,6 +360,8 @@ struct BwdCounters {
 // The touched pixels of levels [lo, hi]: their count, and the t-th of them
 // (the level segments of the list in level order).
 struct TouchedRange {
+  // (every index below is a compile-time constant after unrolling: a
+  // dynamically indexed register array lives in scratch memory)
   int32_t pre[D2MI_MAX_LEVELS + 1];
   int lo, hi;
   __device__ __forceinline__ void init(const PixMap& pm, const BwdCounters* ctr, int lv_lo,
@@ -367,16 +369,32 @@ struct TouchedRange {
     lo = lv_lo;
     hi = lv_hi;
     pre[0] = 0;
-    for (int l = lo; l <= hi; ++l) pre[l - lo + 1] = pre[l - lo] + ctr->touched_lv[l];
+#pragma unroll
+    for (int j = 0; j < D2MI_MAX_LEVELS; ++j)
+      pre[j + 1] = pre[j] + (j <= hi - lo ? ctr->touched_lv[lo + j] : 0);
   }
-  __device__ __forceinline__ int total() const { return pre[hi - lo + 1]; }
+  __device__ __forceinline__ int total() const {
+    int v = 0;
+#pragma unroll
+    for (int j = 0; j <= D2MI_MAX_LEVELS; ++j) v = j == hi - lo + 1 ? pre[j] : v;
+    return v;
+  }
   // global pixel id and level of entry t < total()
   __device__ __forceinline__ long long at(const PixMap& pm, const int32_t* touched, int t,
                                           int& l) const {
-    int k = 0;
-    while (k < hi - lo && t >= pre[k + 1]) ++k;
+    return touched[index(pm, t, l)];
+  }
+  // the touched-list index of entry t < total(), and its level
+  __device__ __forceinline__ int index(const PixMap& pm, int t, int& l) const {
+    int k = 0, base = 0;
+#pragma unroll
+    for (int j = 1; j < D2MI_MAX_LEVELS; ++j)
+      if (j <= hi - lo && t >= pre[j]) {
+        k = j;
+        base = pre[j];
+      }
     l = lo + k;
-    return touched[pm.tbase[l] + (t - pre[k])];
+    return pm.tbase[l] + (t - base);
   }
 };
 
@@ -531,7 +549,7 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
     const int32_t* __restrict__ count, long long total_pixels, int set_bits,
     int32_t* __restrict__ run_start, int32_t* __restrict__ seg_first,
     int32_t* __restrict__ seg_pixel, int2* __restrict__ tasks, int32_t* __restrict__ touched,
-    BwdCounters* __restrict__ ctr, PixMap pm) {
+    int4* __restrict__ trun, BwdCounters* __restrict__ ctr, PixMap pm) {
   __shared__ int s_wave[16], s_base;
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = p < total_pixels;
@@ -567,6 +585,9 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
   int o = pos, so = sf, to = tf;
   for (int s = 0; s < nsets; ++s) {
     const int q = (int)((p << set_bits) | s);
+    // the touched entry's run of this set (pixel, count, start, first segment):
+    // the C = 256 pixel pass reads it with the entry, no count / start lookup
+    if (trun) trun[((long long)tix << set_bits) | s] = make_int4((int)p, c[s], o, nseg[s] ? so : -1);
     if (c[s] == 0) continue;
     run_start[q] = o;
     o += c[s];
@@ -953,14 +974,15 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_slots_kernel(
 // rows are then loaded kRowBatch at a time (the row addresses are all known
 // after the sort) and summed in that order -- the slot -> record -> row chain
 // per contribution of r4 (one dependent global load per step) is gone.
-constexpr int kRowBatch = 4;
-template <int PPW>
+// r5b: the touched entry carries each set's (pixel, count, run start, first
+// segment) (trun, written by the runs launch), so a pixel's chain is entry ->
+// run records -> rows; RB rows in flight per lane (tuning "roi_bwd_rec": 1 ->
+// 4, 2 -> 2: fewer VGPRs, more resident waves).
+template <int PPW, int kRowBatch>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     RoiArgs a, PixMap pm, const RunRec* __restrict__ runrec, int set_bits,
-    const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
-    const int32_t* __restrict__ seg_first, const float* __restrict__ partial,
-    const int32_t* __restrict__ touched, const BwdCounters* __restrict__ ctr, int lv_lo,
-    int lv_hi) {
+    const int4* __restrict__ trun, const float* __restrict__ partial,
+    const BwdCounters* __restrict__ ctr, int lv_lo, int lv_hi) {
   constexpr int C = 256;
   constexpr int LPP = 64 / PPW;     // lanes per pixel
   constexpr int F = C / LPP / 4;    // float4 per lane
@@ -981,7 +1003,10 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     const int t = tb + grp;
     if (t >= nt) continue;
     int l;
-    const long long pix = tr.at(pm, touched, t, l);
+    const int ti = tr.index(pm, t, l);
+    const int4 ru0 = trun[(long long)ti << set_bits];
+    const int4 ru1 = set_bits ? trun[((long long)ti << set_bits) | 1] : make_int4(0, 0, 0, -1);
+    const long long pix = ru0.x;
     float* dst = a.gfeat[l] + (size_t)(pix - pm.base[l]) * C + c;
     float4* d4 = reinterpret_cast<float4*>(dst);
     // accumulate: the map's old value is loaded first, its latency hidden
@@ -996,10 +1021,10 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     float4 res[F];
     bool any = false;
     for (int sidx = 0; sidx < nsets; ++sidx) {
-      const long long q = (pix << set_bits) | sidx;
-      const int n = count[q];
+      const int4 ru = sidx ? ru1 : ru0;  // (no dynamic register-array index: scratch)
+      const int n = ru.y;
       if (n == 0) continue;
-      const int i0 = run_start[q];
+      const int i0 = ru.z;
       float4 acc[F];
 #pragma unroll
       for (int k = 0; k < F; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1058,7 +1083,7 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
         }
         __builtin_amdgcn_wave_barrier();  // (lin / lout reused by the next run)
       } else {
-        const int f = seg_first[q];
+        const int f = ru.w;
         const int ns = (n + kSeg - 1) / kSeg;
         for (int j = 0; j < ns; ++j) {
           const float4* src = reinterpret_cast<const float4*>(partial + (size_t)(f + j) * C + c);
@@ -1252,6 +1277,7 @@ void bwd_layout(WS& w, int C, const BwdPlan& p) {
   w.template take<int32_t>((size_t)p.max_segs);             // seg_pixel
   w.template take<float>((size_t)p.max_segs * C);           // partial rows
   w.template take<int32_t>((size_t)p.max_touched + 1);      // touched pixels
+  w.template take<int4>(((size_t)p.max_touched + 1) * 2);   // their runs per set
   w.template take<int2>((size_t)p.max_tasks);               // long-sort tasks
   w.template take<BwdCounters>(1);
 }
@@ -1302,6 +1328,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   int32_t* seg_pixel = w.take<int32_t>((size_t)p.max_segs);
   float* partial = w.take<float>((size_t)p.max_segs * C);
   int32_t* touched = w.take<int32_t>((size_t)p.max_touched + 1);
+  int4* trun = w.take<int4>(((size_t)p.max_touched + 1) * 2);
   int2* tasks = w.take<int2>((size_t)p.max_tasks);
   BwdCounters* ctr = w.take<BwdCounters>(1);
   // r5: the C = 256 pixel pass reads run records (tuning "roi_bwd_rec", 1);
@@ -1339,7 +1366,7 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   }
   hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.total_pixels + 1023) / 1024)),
                      dim3(1024), 0, st, count, p.total_pixels, sb, run_start, seg_first, seg_pixel,
-                     tasks, touched, ctr, p.pm);
+                     tasks, touched, use_runrec ? trun : nullptr, ctr, p.pm);
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
                      st, ent, p.n_keys, run_start, arrival, rec, use_runrec ? runrec : nullptr);
@@ -1398,11 +1425,14 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                          arrival, rec, sb, count, run_start, seg_first, partial, touched, ctr,
                          lv_lo, lv_hi);
     else if (ppw == 8)
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<8>, g4, dim3(256), 0, st, a, p.pm, runrec, sb,
-                         count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
+      hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<8, 4>), g4, dim3(256), 0, st, a, p.pm, runrec,
+                         sb, trun, partial, ctr, lv_lo, lv_hi);
+    else if (tuning(kTuneRoiBwdRec) == 2)
+      hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<4, 2>), g4, dim3(256), 0, st, a, p.pm, runrec,
+                         sb, trun, partial, ctr, lv_lo, lv_hi);
     else
-      hipLaunchKernelGGL(roi_bwd_pixel_c256_kernel<4>, g4, dim3(256), 0, st, a, p.pm, runrec, sb,
-                         count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
+      hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<4, 4>), g4, dim3(256), 0, st, a, p.pm, runrec,
+                         sb, trun, partial, ctr, lv_lo, lv_hi);
   } else if (vec4) {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,
                        sb, count, run_start, seg_first, partial, touched, ctr, lv_lo, lv_hi);
