@@ -69,9 +69,12 @@ struct WorkspaceSizer {
   }
 };
 
-// float -> uint32 whose unsigned order equals the float order.
+// float -> uint32 whose unsigned order equals the float order.  -0.0 maps to
+// +0.0's word: TF's top_k / NMS compare the values, so the two zeros tie (and
+// the index decides), as in oracle/oracle.c's comparators.
 __device__ __forceinline__ uint32_t orderable(float f) {
   uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) == 0u) u = 0u;
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 __device__ __forceinline__ float from_orderable(uint32_t k) {

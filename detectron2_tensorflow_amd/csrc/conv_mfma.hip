@@ -1602,12 +1602,15 @@ static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
   if (a.Cin == 256 && a.residual && a.gate) return 0;  // (its registers spill)
   // where it measured faster than the tiled kernel (tools/stream_ab.py,
   // profiles/r5_stream_ab_force_tn_rule.log, with TN 2 when 128-wide slices
-  // leave too few strip tasks): every K = 64 and K = 128 launch; K = 256 into
-  // <= 64 channels, or into >= 512 over >= 16 K pixels.  Elsewhere (256 ->
-  // 256, 256 -> 1024 at 8,400 pixels) the tiled kernel's 3 workgroups per CU
-  // win.
+  // leave too few strip tasks): every K = 64 and K = 128 launch.  K = 256
+  // (1.12-1.17x into <= 64 or 512 channels) only under force: the tiled
+  // kernel splits the K of its tail tiles there (>= 8 k-steps), so the two
+  // kernels' results differ in the last bit, and a launch whose operands
+  // are not 16-B aligned (a gradient bucket view) would then round
+  // differently from an aligned one (tests/test_gpu_dp.py's one-rank RCCL
+  // equality).  For K <= 128 both kernels sum in the same order: bit-identical.
   if (a.Cin == 64 || a.Cin == 128) return a.Cin == 64 ? 1 : 2;
-  return (force || a.Cout <= 64 || (a.Cout >= 512 && a.M >= 16384)) ? 3 : 0;
+  return force ? 3 : 0;
 }
 
 template <int TN, int KMAX>

@@ -151,6 +151,91 @@ __global__ __launch_bounds__(1024) void rpn_merge_kernel(
   }
 }
 
+// r5: the same concat + top_k(post) as a merge rank over the per-level NMS
+// survivor lists, which are already in key order (score desc, keep position
+// asc): an entry's position = its own position + the earlier levels' entries
+// whose key is not above its own + the later levels' entries strictly above
+// it -- the desc_key(score, l * post + t) order of rpn_merge_kernel, scores
+// compared as orderable words (-0 < +0, as the key).  Many workgroups per
+// image (one entry per thread, every list's score words in LDS) instead of
+// one workgroup's bitonic sort of up to 8,192 keys (61 us per training step).
+constexpr int kMergeT = 256;
+__global__ __launch_bounds__(kMergeT) void rpn_merge_rank_kernel(
+    const float4* __restrict__ dec, const float* __restrict__ tvals,
+    const int32_t* __restrict__ keep, const int32_t* __restrict__ num_keep, int L, int k,
+    int post, float4* __restrict__ out_boxes, float* __restrict__ out_scores,
+    uint8_t* __restrict__ out_valid) {
+  extern __shared__ uint32_t sw[];  // [L * post] orderable score words
+  __shared__ int cnt[D2MI_MAX_LEVELS], cum[D2MI_MAX_LEVELS + 1];
+  const int n = blockIdx.y, t = threadIdx.x;
+  if (t == 0) {
+    int acc = 0;
+    for (int l = 0; l < L; ++l) {
+      cnt[l] = num_keep[n * L + l];
+      cum[l] = acc;
+      acc += cnt[l];
+    }
+    cum[L] = acc;
+  }
+  __syncthreads();
+  for (int q = t; q < L * post; q += kMergeT) {
+    const int l = q / post, i = q - l * post;
+    uint32_t w = 0;
+    if (i < cnt[l]) {
+      const int s = n * L + l;
+      w = orderable(tvals[(size_t)s * k + keep[(size_t)s * post + i]]);
+    }
+    sw[q] = w;
+  }
+  __syncthreads();
+  const int r = blockIdx.x * kMergeT + t;
+  const int total = cum[L];
+  if (r >= max(total, post)) return;
+  if (r >= total) {  // zero padding past the survivors
+    const size_t o = (size_t)n * post + r;
+    out_boxes[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    out_scores[o] = 0.f;
+    out_valid[o] = 0;
+    return;
+  }
+  int l = 0;
+  while (l + 1 < L && cum[l + 1] <= r) ++l;
+  const int i = r - cum[l];
+  const uint32_t me = sw[l * post + i];
+  int lo[D2MI_MAX_LEVELS], hi[D2MI_MAX_LEVELS];
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+    lo[m] = 0;
+    hi[m] = (m < L && m != l) ? cnt[m] : 0;
+  }
+  // earlier levels: entries with word >= mine come first; later: word > mine
+  for (int step = 0; step < 14; ++step) {
+    uint32_t pv[D2MI_MAX_LEVELS];
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m)
+      pv[m] = m < L ? sw[m * post + min((lo[m] + hi[m]) >> 1, post - 1)] : 0u;
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+      if (lo[m] < hi[m]) {
+        const int mid = (lo[m] + hi[m]) >> 1;
+        if (m < l ? pv[m] >= me : pv[m] > me) lo[m] = mid + 1;
+        else hi[m] = mid;
+      }
+    }
+  }
+  int pos = i;
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) pos += lo[m];
+  if (pos < post) {
+    const int s = n * L + l;
+    const int j = keep[(size_t)s * post + i];
+    const size_t o = (size_t)n * post + pos;
+    out_boxes[o] = dec[(size_t)s * k + j];
+    out_scores[o] = tvals[(size_t)s * k + j];
+    out_valid[o] = 1;
+  }
+}
+
 // --------------------------------------------------------- Fast R-CNN
 __global__ void slot_map_kernel(const int32_t* roi_img, const int32_t* roi_slot, int R, int P,
                                 int N, int32_t* slot2roi, int32_t* err) {
@@ -590,6 +675,16 @@ extern "C" int d2mi_rpn_proposals_ex(const float* const* logits, const float* co
   rc = nms_core(o.keys, o.lens, o.dec, nullptr, S, k, post_nms_topk, nms_thresh, o.keep,
                 o.num_keep, o.nms_ws, o.nms_bytes, st);
   if (rc) return rc;
+  // tuning "rpn_merge": 1 the merge rank (r5), 0 the one-workgroup bitonic sort (A/B)
+  if (tuning(kTuneRpnMerge) != 0) {
+    const int span = std::max(L * post_nms_topk, post_nms_topk);
+    hipLaunchKernelGGL(rpn_merge_rank_kernel, dim3((span + kMergeT - 1) / kMergeT, N),
+                       dim3(kMergeT), (size_t)L * post_nms_topk * sizeof(uint32_t), st, o.dec,
+                       o.tvals, o.keep, o.num_keep, L, k, post_nms_topk,
+                       reinterpret_cast<float4*>(out_boxes), out_scores, out_valid);
+    D2MI_LAUNCH_CHECK();
+    return 0;
+  }
   int m = 1;
   while (m < L * post_nms_topk) m <<= 1;
   hipLaunchKernelGGL(rpn_merge_kernel, dim3(N), dim3(1024), m * sizeof(uint64_t), st, o.dec,
