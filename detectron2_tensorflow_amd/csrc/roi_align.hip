@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
 //   4. a run's arrival order is not deterministic, its slot order (the TF
 //      loop order) is: runs up to kSeg are ranked by slot inside the pixel
 //      pass (a few LDS / shuffle compares per lane); longer runs are ranked by
-//      `roi_bwd_long_sort_kernel` (1,024 elements per task, each ranked
+//      `roi_bwd_long_kernel` (1,024 elements per task, each ranked
 //      against the whole run through LDS tiles) into sorted_long;
 //   5. segment partials of the long runs (one wave per kSeg slots), then the
 //      grad maps -- zero-filled by the clear launch -- get their touched
@@ -355,6 +355,7 @@ struct RunRec {
 struct BwdCounters {
   int32_t touched, segs, tasks, cursor;
   int32_t touched_lv[D2MI_MAX_LEVELS];  // touched pixels per level
+  int32_t lsdone;  // workgroups of the long-sort launch that finished
 };
 
 // The touched pixels of levels [lo, hi]: their count, and the t-th of them
@@ -454,14 +455,13 @@ __device__ __forceinline__ uint32_t arrival_rank(int32_t* __restrict__ count, ui
 // first (samples from sample_base on) with pairs pixel * 2 + set
 // (set_bits = 1): each set's contributions of a pixel form their own run.
 // ent[slot] = pair << 32 | arrival rank, ~0 for a contribution outside the map.
-__global__ __launch_bounds__(256) void roi_bwd_emit_kernel(RoiArgs a, PixMap pm, int set,
-                                                           int set_bits, long long sample_base,
-                                                           int32_t* __restrict__ count,
-                                                           uint64_t* __restrict__ ent,
-                                                           Contrib* __restrict__ rec) {
+__device__ __forceinline__ void emit_samples(const RoiArgs& a, const PixMap& pm, int set,
+                                             int set_bits, long long sample_base, long long tl,
+                                             int32_t* __restrict__ count,
+                                             uint64_t* __restrict__ ent,
+                                             Contrib* __restrict__ rec) {
   const int S = a.sr > 0 ? a.sr : 1;
   const long long nsamp = (long long)a.out_h * a.out_w * S * S;
-  const long long tl = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in_range = tl < (long long)a.R * nsamp;
   const int r = in_range ? (int)(tl / nsamp) : 0;
   const int s = in_range ? (int)(tl - (long long)r * nsamp) : 0;
@@ -507,6 +507,21 @@ __global__ __launch_bounds__(256) void roi_bwd_emit_kernel(RoiArgs a, PixMap pm,
     d[2] = e[2];
     d[3] = e[3];
   }
+}
+
+// Both ROI sets' samples in one launch (r5: a launch per set before): the
+// first nb0 workgroups take set 0, the rest set 1 (from sample ns0 on).
+__global__ __launch_bounds__(256) void roi_bwd_emit_kernel(RoiArgs a0, RoiArgs a1, int nb0,
+                                                           long long ns0, PixMap pm, int set_bits,
+                                                           int32_t* __restrict__ count,
+                                                           uint64_t* __restrict__ ent,
+                                                           Contrib* __restrict__ rec) {
+  if ((int)blockIdx.x < nb0)
+    emit_samples(a0, pm, 0, set_bits, 0, (long long)blockIdx.x * blockDim.x + threadIdx.x, count,
+                 ent, rec);
+  else
+    emit_samples(a1, pm, 1, set_bits, ns0,
+                 (long long)(blockIdx.x - nb0) * blockDim.x + threadIdx.x, count, ent, rec);
 }
 
 // Workgroup-aggregated allocation from a global counter: returns this
@@ -622,39 +637,6 @@ __global__ __launch_bounds__(256) void roi_bwd_place_kernel(const uint64_t* __re
   }
 }
 
-// Long runs (> kSeg contributions) in slot order: a task ranks kLongTask of a
-// run's elements against the whole run (slots are distinct), streamed through
-// LDS in kLongTile tiles.  O(len^2) compares per run, spread over len / 1024
-// workgroups; only degenerate piles of boxes make runs this long.
-__global__ __launch_bounds__(1024) void roi_bwd_long_sort_kernel(
-    const int32_t* __restrict__ arrival, const int32_t* __restrict__ count,
-    const int32_t* __restrict__ run_start, const int2* __restrict__ tasks,
-    const BwdCounters* __restrict__ ctr, int32_t* __restrict__ sorted_long) {
-  __shared__ int32_t tile[kLongTile];
-  const int ntasks = ctr->tasks;
-  for (int tk = blockIdx.x; tk < ntasks; tk += gridDim.x) {
-    const int2 task = tasks[tk];
-    const int i0 = run_start[task.x], len = count[task.x];
-    const int e = task.y * kLongTask + (int)threadIdx.x;
-    const int mine = e < len ? arrival[i0 + e] : INT_MAX;
-    int rank = 0;
-    for (int j0 = 0; j0 < len; j0 += kLongTile) {
-      const int m = min(kLongTile, len - j0);
-      __syncthreads();
-      for (int j = threadIdx.x; j < m; j += blockDim.x) tile[j] = arrival[i0 + j0 + j];
-      __syncthreads();
-      int j = 0;
-      for (; j + 8 <= m; j += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) rank += tile[j + u] < mine ? 1 : 0;
-      }
-      for (; j < m; ++j) rank += tile[j] < mine ? 1 : 0;
-    }
-    if (e < len) sorted_long[i0 + rank] = mine;
-    __syncthreads();
-  }
-}
-
 // TF order of operations: dtop = (1 - y_lerp) * g, dbot = y_lerp * g, then
 // (1 - x_lerp) * d or x_lerp * d.
 __device__ __forceinline__ float weigh(int corner, float yl, float xl, float v) {
@@ -741,17 +723,60 @@ __device__ __forceinline__ void order_run(const int32_t* __restrict__ arrival, i
   __builtin_amdgcn_wave_barrier();
 }
 
-// One wave per split segment: partial[seg] (C floats).
+// Long runs (> kSeg contributions), then their segment partials, in ONE
+// launch (r5; two before, each a dispatch that only reads zero counts and
+// exits in an ordinary step):
+//   1. a task ranks kLongTask of a run's elements against the whole run
+//      (slots are distinct), streamed through LDS in kLongTile tiles -- O(len^2)
+//      compares per run over len / 1024 workgroups; only degenerate piles of
+//      boxes make runs this long;
+//   2. the workgroup that finishes last (device counter, fences on both sides)
+//      writes every segment's partial[seg] (C floats, one wave per segment,
+//      slot order within it).
 template <bool VEC4>
-__global__ __launch_bounds__(256) void roi_bwd_segment_kernel(
-    RoiArgs a, const int32_t* __restrict__ sorted_long, const Contrib* __restrict__ rec,
-    const int32_t* __restrict__ count, const int32_t* __restrict__ run_start,
-    const int32_t* __restrict__ seg_first, const int32_t* __restrict__ seg_pixel,
-    const BwdCounters* __restrict__ ctr, float* __restrict__ partial) {
-  const int lane = threadIdx.x & 63;
+__global__ __launch_bounds__(1024) void roi_bwd_long_kernel(
+    RoiArgs a, const int32_t* __restrict__ arrival, const int32_t* __restrict__ count,
+    const int32_t* __restrict__ run_start, const int2* __restrict__ tasks,
+    BwdCounters* __restrict__ ctr, int32_t* __restrict__ sorted_long,
+    const Contrib* __restrict__ rec, const int32_t* __restrict__ seg_first,
+    const int32_t* __restrict__ seg_pixel, float* __restrict__ partial) {
+  __shared__ int32_t tile[kLongTile];
+  __shared__ int s_last;
+  const int ntasks = ctr->tasks;
+  for (int tk = blockIdx.x; tk < ntasks; tk += gridDim.x) {
+    const int2 task = tasks[tk];
+    const int i0 = run_start[task.x], len = count[task.x];
+    const int e = task.y * kLongTask + (int)threadIdx.x;
+    const int mine = e < len ? arrival[i0 + e] : INT_MAX;
+    int rank = 0;
+    for (int j0 = 0; j0 < len; j0 += kLongTile) {
+      const int m = min(kLongTile, len - j0);
+      __syncthreads();
+      for (int j = threadIdx.x; j < m; j += blockDim.x) tile[j] = arrival[i0 + j0 + j];
+      __syncthreads();
+      int j = 0;
+      for (; j + 8 <= m; j += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += tile[j + u] < mine ? 1 : 0;
+      }
+      for (; j < m; ++j) rank += tile[j] < mine ? 1 : 0;
+    }
+    if (e < len) sorted_long[i0 + rank] = mine;
+    __syncthreads();
+  }
+  // the last workgroup to finish computes the segment partials
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this workgroup's sorted_long stores before its arrival
+    s_last = atomicAdd(&ctr->lsdone, 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int nsegs = ctr->segs;
   const int step = VEC4 ? 256 : 64;
-  for (int seg = blockIdx.x * 4 + (threadIdx.x >> 6); seg < nsegs; seg += gridDim.x * 4) {
+  for (int seg = threadIdx.x >> 6; seg < nsegs; seg += nw) {
     const int q = seg_pixel[seg];
     const int k = seg - seg_first[q];
     const int i0 = run_start[q] + k * kSeg;
@@ -1355,14 +1380,13 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
                      dim3(256), 0, st, cl);
   D2MI_LAUNCH_CHECK();
   if (p.n_keys == 0) return 0;
-  long long base = 0;
-  for (int k = 0; k < nsets; ++k) {
-    if (ns[k] > 0) {
-      hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)((ns[k] + 255) / 256)), dim3(256), 0,
-                         st, sets[k], p.pm, k, sb, base, count, ent, rec);
+  {
+    const int nb0 = (int)((ns[0] + 255) / 256), nb1 = nsets > 1 ? (int)((ns[1] + 255) / 256) : 0;
+    if (nb0 + nb1 > 0) {
+      hipLaunchKernelGGL(roi_bwd_emit_kernel, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, st,
+                         sets[0], sets[nsets > 1 ? 1 : 0], nb0, ns[0], p.pm, sb, count, ent, rec);
       D2MI_LAUNCH_CHECK();
     }
-    base += ns[k];
   }
   hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.total_pixels + 1023) / 1024)),
                      dim3(1024), 0, st, count, p.total_pixels, sb, run_start, seg_first, seg_pixel,
@@ -1376,17 +1400,10 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   // (zero in an ordinary step: the launches exit at once)
   // (small grids: the dispatch of a large grid that only reads a zero count
   // and exits is most of these launches' cost in an ordinary step)
-  hipLaunchKernelGGL(roi_bwd_long_sort_kernel,
+  hipLaunchKernelGGL((vec4 ? roi_bwd_long_kernel<true> : roi_bwd_long_kernel<false>),
                      dim3((unsigned)std::max(1LL, std::min<long long>(p.max_tasks, 64LL))),
-                     dim3(1024), 0, st, arrival, count, run_start, tasks, ctr, sorted_long);
-  D2MI_LAUNCH_CHECK();
-  const dim3 sgrid((unsigned)std::max(1LL, std::min<long long>((p.max_segs + 3) / 4, 128LL)));
-  if (vec4)
-    hipLaunchKernelGGL(roi_bwd_segment_kernel<true>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
-                       count, run_start, seg_first, seg_pixel, ctr, partial);
-  else
-    hipLaunchKernelGGL(roi_bwd_segment_kernel<false>, sgrid, dim3(256), 0, st, a, sorted_long, rec,
-                       count, run_start, seg_first, seg_pixel, ctr, partial);
+                     dim3(1024), 0, st, a, arrival, count, run_start, tasks, ctr, sorted_long, rec,
+                     seg_first, seg_pixel, partial);
   D2MI_LAUNCH_CHECK();
   }  // phase 1
   if (phase == 2) {  // a pixel pass alone: its non-accumulated maps start from zero
