@@ -173,6 +173,30 @@ def test_roi_align_backward_raw_large_crops_and_ragged_channels(dev, C, crop, sr
         assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
 
 
+@pytest.mark.parametrize("C,sr", [(256, 2), (256, 3), (256, 1), (64, 2)])
+def test_roi_align_backward_sampled_bins_bit_exact(dev, C, sr):
+    """Sampling ratio > 0 (the poolers' mode): TF's backward is AvgPoolGrad
+    (each bin's gradient / sr^2 to its sr x sr samples) then
+    CropAndResizeGradImage over the sr-times-finer crop -- bit-exact, also
+    where sr^2 is a power of two and the kernels multiply by its reciprocal
+    instead of dividing (C = 256: the four-pixels-per-wave pass)."""
+    rng = np.random.default_rng(100 + sr)
+    img = rng.normal(size=(2, 23, 29, C)).astype(F32)
+    lo = rng.uniform(0.0, 0.3, size=(12, 2))
+    boxes = np.concatenate([lo, lo + rng.uniform(0.5, 0.7, size=(12, 2))], 1)[:, [0, 1, 2, 3]]
+    boxes = boxes.astype(F32)
+    bimg = rng.integers(0, 2, size=12).astype(np.int32)
+    x = torch.from_numpy(img).to(dev).requires_grad_(True)
+    out = ops().roi_align([x], torch.from_numpy(boxes).to(dev), torch.from_numpy(bimg).to(dev),
+                          (7, 7), [1.0], sr, pad_border=False, box_mode=ops().BOX_MODE_RAW)
+    g = rng.normal(size=tuple(out.shape)).astype(F32)
+    out.backward(torch.from_numpy(g).to(dev))
+    gs = (g / F32(sr * sr)).astype(F32)
+    up = np.repeat(np.repeat(gs, sr, axis=1), sr, axis=2)
+    want = oracle.crop_and_resize_grad_image(up, boxes, bimg, (2, 23, 29))
+    np.testing.assert_array_equal(x.grad.cpu().numpy(), want)
+
+
 def test_roi_align_backward_hot_pixels(dev):
     """Hundreds of ROIs collapsed onto the same pixels (degenerate proposals at
     the border): the split-segment path, against the TF scatter."""
@@ -255,8 +279,19 @@ def test_nms_golden_reference_vectors(dev):
         np.testing.assert_array_equal(keep.cpu().numpy(), d[f"c{i}_keep"], err_msg=f"case {i}")
 
 
+@pytest.fixture(params=[1, 0], ids=["scan_fixed_point", "scan_serial"])
+def nms_scan(request):
+    """Both NMS scans (tuning "nms_scan": 1 the r5 fixed-point tile resolve,
+    0 the serial one), restored after the test."""
+    from detectron2_tensorflow_amd.layers import ops as lops
+    old = lops.get_tuning("nms_scan")
+    lops.set_tuning("nms_scan", request.param)
+    yield request.param
+    lops.set_tuning("nms_scan", old)
+
+
 @pytest.mark.parametrize("thr", [0.0, 0.3, 0.5, 0.7, 1.0])
-def test_nms_segmented_vs_oracle_with_ties(dev, thr):
+def test_nms_segmented_vs_oracle_with_ties(dev, thr, nms_scan):
     rng = np.random.default_rng(int(thr * 10) + 7)
     lens = [0, 1, 5, 64, 65, 200, 1000, 2000, 777]
     boxes, scores, off = [], [], [0]
@@ -279,6 +314,34 @@ def test_nms_segmented_vs_oracle_with_ties(dev, thr):
                                   torch.from_numpy(off).to(dev), max_out, thr,
                                   seg_capacity=max(lens))
         np.testing.assert_array_equal(n.cpu().numpy(), want_n)
+        np.testing.assert_array_equal(k.cpu().numpy(), want_k)
+
+
+@pytest.mark.parametrize("cap", [2000, 4096, 4160])
+def test_nms_suppression_chains_and_truncation(dev, cap, nms_scan):
+    """Chains of boxes each overlapping the next above the threshold (the
+    greedy keeps every other one: the fixed-point resolve's worst case, one
+    round per row of a tile) next to clusters and random boxes; max_out cuts
+    inside a tile; capacity 4,096 is the fixed-point scan's largest (64 tiles),
+    4,160 falls back to the serial scan."""
+    rng = np.random.default_rng(cap)
+    segs = []
+    chain = np.array([[0, 10 * i, 100, 10 * i + 100] for i in range(cap // 2)], F32)
+    segs.append((chain, np.linspace(1, 0.1, len(chain)).astype(F32)))
+    n = cap
+    b = rand_boxes(rng, n, 600, 600, 4, 200)
+    b[: n // 4] = np.array([[5, 5, 105, 105]], F32) + rng.uniform(0, 8, size=(n // 4, 1)).astype(F32)
+    segs.append((b, rng.uniform(size=n).astype(F32)))
+    segs.append((rand_boxes(rng, 777, 300, 300, 4, 120), rng.uniform(size=777).astype(F32)))
+    boxes = np.concatenate([x for x, _ in segs])
+    scores = np.concatenate([y for _, y in segs])
+    off = np.cumsum([0] + [len(y) for _, y in segs]).astype(np.int32)
+    for thr, max_out in ((0.5, 1000), (0.5, 37), (0.7, 5000), (0.05, 99)):
+        want_k, want_n = oracle.nms_batched(boxes, scores, off, max_out, thr)
+        k, nk = ops().nms_segments(torch.from_numpy(boxes).to(dev),
+                                   torch.from_numpy(scores).to(dev), torch.from_numpy(off).to(dev),
+                                   max_out, thr, seg_capacity=cap)
+        np.testing.assert_array_equal(nk.cpu().numpy(), want_n)
         np.testing.assert_array_equal(k.cpu().numpy(), want_k)
 
 
