@@ -429,26 +429,6 @@ __global__ __launch_bounds__(256) void roi_bwd_clear_kernel(ClearList cl) {
   }
 }
 
-// Arrival rank of this lane's contribution to pair q (live lanes only).  When
-// every live lane of the wave hits the same pair -- degenerate boxes collapsed
-// onto one point, where hundreds of ROIs pile onto a pixel -- one atomic takes
-// the whole wave's ranks: same-address device atomics serialise.
-__device__ __forceinline__ uint32_t arrival_rank(int32_t* __restrict__ count, uint32_t q, bool live) {
-  const unsigned long long lm = __ballot(live);
-  if (lm == 0) return 0u;
-  const int lane = threadIdx.x & 63;
-  const int lead = __ffsll((long long)lm) - 1;
-  const uint32_t q0 = (uint32_t)__shfl((int)q, lead);
-  const unsigned long long same = __ballot(live && q == q0);
-  if (same == lm) {
-    uint32_t base = 0;
-    if (lane == lead) base = (uint32_t)atomicAdd(&count[q0], __popcll(lm));
-    base = (uint32_t)__shfl((int)base, lead);
-    return base + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
-  }
-  return live ? (uint32_t)atomicAdd(&count[q], 1) : 0u;
-}
-
 // The ROI geometry is recomputed per sample (a few dozen flops against the
 // 48 B the thread stores) rather than staged by a separate launch.
 // set / sample_base: a merged backward emits its second ROI set after the
@@ -494,12 +474,39 @@ __device__ __forceinline__ void emit_samples(const RoiArgs& a, const PixMap& pm,
     q[2] = (uint32_t)((img + (uint64_t)ty.r1 * g.W + tx.r0) << set_bits) | sb;
     q[3] = (uint32_t)((img + (uint64_t)ty.r1 * g.W + tx.r1) << set_bits) | sb;
   }
+  // the four corners' arrival ranks (live lanes only), all four atomics in
+  // flight before any result is used (r5; one round trip per corner before).
+  // When every live lane of the wave hits the same pair -- degenerate boxes
+  // collapsed onto one point, where hundreds of ROIs pile onto a pixel -- one
+  // atomic takes the whole wave's ranks: same-address device atomics serialise.
+  uint32_t rk[4] = {0u, 0u, 0u, 0u};
+  const unsigned long long lm = __ballot(ok);
+  if (lm != 0) {
+    const int lane = threadIdx.x & 63;
+    const int lead = __ffsll((long long)lm) - 1;
+    bool coll[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t q0 = (uint32_t)__shfl((int)q[k], lead);
+      coll[k] = __ballot(ok && q[k] == q0) == lm;  // the whole wave on one pair
+    }
+    uint32_t base[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (coll[k]) {
+        if (lane == lead) base[k] = (uint32_t)atomicAdd(&count[q[k]], __popcll(lm));
+      } else if (ok) {
+        rk[k] = (uint32_t)atomicAdd(&count[q[k]], 1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (coll[k])
+        rk[k] = (uint32_t)__shfl((int)base[k], lead) + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
+  }
   uint64_t e[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t rank = arrival_rank(count, q[k], ok);
-    e[k] = ok ? ((uint64_t)q[k] << 32) | rank : ~0ull;
-  }
+  for (int k = 0; k < 4; ++k) e[k] = ok ? ((uint64_t)q[k] << 32) | rk[k] : ~0ull;
   if (in_range) {
     uint64_t* d = ent + slot;
     d[0] = e[0];
@@ -555,6 +562,47 @@ __device__ __forceinline__ int wg_alloc(int want, int32_t* __restrict__ counter,
   return off;
 }
 
+// K allocations from K global counters in ONE workgroup round (r5): the K
+// wave scans run together, then K threads issue their atomics at once (one
+// round trip, two barriers) -- the runs launch made five wg_alloc rounds in a
+// row, each its own barriers and atomic latency.  Counter k's total is skipped
+// (no atomic) when it is zero; ctr[k] may be null when want[k] is always 0.
+template <int NT, int K>
+__device__ __forceinline__ void wg_alloc_multi(const int (&want)[K], int32_t* const (&ctr)[K],
+                                               int (&off)[K], int (*s_wave)[NT / 64],
+                                               int* s_base) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] = want[k];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int y = __shfl_up(x[k], d);
+      if (lane >= d) x[k] += y;
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) s_wave[k][w] = x[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    int tot = 0;
+    for (int j = 0; j < NT / 64; ++j) {
+      const int v = s_wave[k][j];
+      s_wave[k][j] = tot;
+      tot += v;
+    }
+    s_base[k] = tot ? atomicAdd(ctr[k], tot) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) off[k] = s_base[k] + s_wave[k][w] + x[k] - want[k];
+}
+
 // One thread per pixel: each touched (pixel, set) pair gets its range of the
 // arrival array, the pixel goes on the touched list, and a pair with more
 // than kSeg contributions gets its segment slots (owner = pair) and the tasks
@@ -566,6 +614,7 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
     int32_t* __restrict__ seg_pixel, int2* __restrict__ tasks, int32_t* __restrict__ touched,
     int4* __restrict__ trun, BwdCounters* __restrict__ ctr, PixMap pm) {
   __shared__ int s_wave[16], s_base;
+  __shared__ int s_wave5[5][16], s_base5[5];
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = p < total_pixels;
   const int nsets = 1 << set_bits;
@@ -579,22 +628,30 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
       ntask[s] = (c[s] + kLongTask - 1) / kLongTask;
     }
   }
-  const int pos = wg_alloc<1024>(tot, &ctr->cursor, s_wave, &s_base);
   // the pixel's slot in its level's segment of the touched list (the
-  // workgroup's pixels span levels lf..ll: one allocation per level, uniform)
+  // workgroup's pixels span levels lf..ll; the first two in the one round
+  // with the arrival range, the segments and the tasks, any further level --
+  // maps smaller than a workgroup -- one round each, uniform)
   const long long p0 = (long long)blockIdx.x * blockDim.x;
   const long long p1 = min(p0 + (long long)blockDim.x, total_pixels) - 1;
   int lf = 0, ll = 0, lp = 0;
   while (lf + 1 < pm.L && p0 >= pm.base[lf + 1]) ++lf;
   while (ll + 1 < pm.L && p1 >= pm.base[ll + 1]) ++ll;
   while (lp + 1 < pm.L && p >= pm.base[lp + 1]) ++lp;
-  int tix = 0;
-  for (int lv = lf; lv <= ll; ++lv) {
+  const int l2 = min(lf + 1, ll);
+  const int want[5] = {tot, tot > 0 && lp == lf ? 1 : 0, l2 > lf && tot > 0 && lp == l2 ? 1 : 0,
+                       nseg[0] + nseg[1], ntask[0] + ntask[1]};
+  int32_t* const ctrs[5] = {&ctr->cursor, &ctr->touched_lv[lf], &ctr->touched_lv[l2], &ctr->segs,
+                            &ctr->tasks};
+  int off[5];
+  wg_alloc_multi<1024, 5>(want, ctrs, off, s_wave5, s_base5);
+  const int pos = off[0], sf = off[3], tf = off[4];
+  int tix = lp == lf ? pm.tbase[lf] + off[1] : (lp == l2 ? pm.tbase[l2] + off[2] : 0);
+  for (int lv = l2 + 1; lv <= ll; ++lv) {
+    __syncthreads();  // (s_wave / s_base reused)
     const int o = wg_alloc<1024>(tot > 0 && lp == lv ? 1 : 0, &ctr->touched_lv[lv], s_wave, &s_base);
     if (lp == lv) tix = pm.tbase[lv] + o;
   }
-  const int sf = wg_alloc<1024>(nseg[0] + nseg[1], &ctr->segs, s_wave, &s_base);
-  const int tf = wg_alloc<1024>(ntask[0] + ntask[1], &ctr->tasks, s_wave, &s_base);
   if (tot == 0) return;
   touched[tix] = (int32_t)p;
   int o = pos, so = sf, to = tf;
@@ -1006,10 +1063,10 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_slots_kernel(
   }
 }
 
-// C == 256 form of roi_bwd_pixel_kernel: a wave sums FOUR touched pixels at
-// once, 16 lanes per pixel, 16 channels (4 float4) per lane -- four
-// independent load chains (run bounds -> run records -> grad_out rows) in
-// flight per wave instead of one, the same per-pixel order and rounding.
+// C == 256 form of roi_bwd_pixel_kernel: a wave sums PPW touched pixels at
+// once, 64 / PPW lanes per pixel -- PPW independent load chains (run bounds
+// -> run records -> grad_out rows) in flight per wave instead of one, the
+// same per-pixel order and rounding (r4: four pixels).
 // r5: a short run's records come from runrec in one coalesced round (each
 // lane kSeg / 16 of them), are put in slot order in LDS, and their grad_out
 // rows are then loaded kRowBatch at a time (the row addresses are all known
@@ -1017,8 +1074,15 @@ __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_slots_kernel(
 // per contribution of r4 (one dependent global load per step) is gone.
 // r5b: the touched entry carries each set's (pixel, count, run start, first
 // segment) (trun, written by the runs launch), so a pixel's chain is entry ->
-// run records -> rows; RB rows in flight per lane (tuning "roi_bwd_rec": 1 ->
-// 4, 2 -> 2: fewer VGPRs, more resident waves).
+// run records -> rows; RB rows in flight per lane.
+// r5c: TWO pixels per wave (32 lanes, 8 channels each), 4 rows in flight: a
+// launch's time is set by its longest runs' dependent row batches (a pixel
+// with n contributions waits n / RB load round trips; the widest launch of a
+// step ran 55 us against a 25 us mean), so a lane's registers buy more rows
+// of ONE pixel in flight instead of more pixels: 99.3 -> 85.2 us per step
+// (profiles/r5_roi_ppw2_timed_kernel_stats.csv), in-step -0.43 %
+// (profiles/r5_ab_roi_ppw2_rb4.log); one pixel per wave with 8 rows and two
+// with 2 rows measured the same (r5_ab_roi_ppw1_vs_ppw2.log, _rb2_vs_rb4.log).
 template <int PPW, int kRowBatch>
 __global__ __launch_bounds__(256) void roi_bwd_pixel_c256_kernel(
     RoiArgs a, PixMap pm, const RunRec* __restrict__ runrec, int set_bits,
@@ -1450,9 +1514,15 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   if (vec4 && C == 256) {
     static const int ppw = [] {
       const char* e = getenv("D2MI_ROI_BWD_PPW");
-      return e && e[0] == '8' ? 8 : 4;
+      return e && e[0] == '8' ? 8 : 0;
     }();
-    const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * ppw - 1) / (4 * ppw), wg_max)));
+    // tuning "roi_bwd_rec" (the run-record pass): 1 two pixels per wave, 4
+    // rows in flight per lane (r5c, default); 2 / 3 four pixels per wave with
+    // 2 / 4 rows (r5b: 4); 5 one pixel per wave, 8 rows; D2MI_ROI_BWD_PPW=8
+    // eight pixels per wave (A/B forms)
+    const int tv = tuning(kTuneRoiBwdRec);
+    const int pw = ppw == 8 ? 8 : tv == 5 ? 1 : (tv == 2 || tv == 3) ? 4 : 2;  // pixels per wave
+    const dim3 g4((unsigned)std::max(1LL, std::min((cap + 4 * pw - 1) / (4 * pw), wg_max)));
     if (!use_runrec)  // the r4 pixel pass (A/B)
       hipLaunchKernelGGL(roi_bwd_pixel_c256_slots_kernel<4>, g4, dim3(256), 0, st, a, p.pm,
                          arrival, rec, sb, count, run_start, seg_first, partial, touched, ctr,
@@ -1460,11 +1530,17 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
     else if (ppw == 8)
       hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<8, 4>), g4, dim3(256), 0, st, a, p.pm, runrec,
                          sb, trun, partial, ctr, lv_lo, lv_hi);
-    else if (tuning(kTuneRoiBwdRec) == 2)
+    else if (tv == 2)
       hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<4, 2>), g4, dim3(256), 0, st, a, p.pm, runrec,
                          sb, trun, partial, ctr, lv_lo, lv_hi);
-    else
+    else if (tv == 3)
       hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<4, 4>), g4, dim3(256), 0, st, a, p.pm, runrec,
+                         sb, trun, partial, ctr, lv_lo, lv_hi);
+    else if (tv == 5)
+      hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<1, 8>), g4, dim3(256), 0, st, a, p.pm, runrec,
+                         sb, trun, partial, ctr, lv_lo, lv_hi);
+    else
+      hipLaunchKernelGGL((roi_bwd_pixel_c256_kernel<2, 4>), g4, dim3(256), 0, st, a, p.pm, runrec,
                          sb, trun, partial, ctr, lv_lo, lv_hi);
   } else if (vec4) {
     hipLaunchKernelGGL(roi_bwd_pixel_kernel<true>, grid, dim3(256), 0, st, a, p.pm, arrival, rec,

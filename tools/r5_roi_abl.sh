@@ -8,7 +8,7 @@
 # grid and register counts from one kernel trace.
 set -eo pipefail
 mkdir -p gpurun_out
-for arm in ${ARMS:-1 3 4}; do
+for arm in ${ARMS-1 3 4}; do
   D2MI_ROI_BWD_REC=$arm bash tools/profile_bench.sh abl_$arm --steps 5 --warmup 3
   grep -h "roi_bwd_pixel" gpurun_out/abl_${arm}_timed_kernel_stats.csv | cut -c1-200
 done
@@ -23,11 +23,12 @@ rows = [r for r in csv.DictReader(open(f)) if "roi_bwd" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 with open("gpurun_out/r5_roi_bwd_calls.txt", "w") as out:
     for r in rows[-40:]:
-        n = r["Kernel_Name"].split("(")[0].replace("void d2mi::(anonymous namespace)::", "")
+        n = r["Kernel_Name"].replace("void ", "").replace("d2mi::(anonymous namespace)::", "").split("(")[0]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
-        out.write(f"{n[:48]:48s} {d:8.1f} us grid {r.get('Grid_Size', '?'):>9s} wg {r.get('Workgroup_Size', '?'):>5s} "
-                  f"vgpr {r.get('Arch_VGPR_Count', r.get('VGPR_Count', '?'))} lds {r.get('LDS_Block_Size', r.get('Lds_Size', '?'))} "
-                  f"scratch {r.get('Scratch_Size', '?')}\n")
+        grid = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
+        out.write(f"{n[:48]:48s} {d:8.1f} us grid {grid:>9s} "
+                  f"vgpr {r.get('Arch_VGPR_Count', r.get('VGPR_Count', '?'))} lds {r.get('LDS_Block_Size', r.get('Lds_Size', '?'))}\n")
+    out.write("columns: " + ",".join(rows[0].keys()) + "\n")
 print(open("gpurun_out/r5_roi_bwd_calls.txt").read())
 PY
 find gpurun_out/prof_roi_calls -name "*trace.csv" -delete
