@@ -50,7 +50,7 @@ int topk_core_ex(const float* values, const int64_t* seg_start, const int32_t* s
 enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi = 3,
                kTuneWgradWS1 = 4, kTuneWgradXCD = 5, kTuneConvXCD = 6, kTuneWgradInc = 7,
                kTuneConvWSMinK = 8, kTuneRoiPixGrid = 9, kTuneConvStream = 10,
-               kTuneRoiBwdRec = 11, kTuneRetinaFused = 12, kTuneRpnMerge = 13, kTuneNmsScan = 14,
+               kTuneRoiBwdRec = 11, kTuneRetinaFused = 12, kTuneRpnMerge = 13, kTuneNmsScan = 14, kTuneRoiHeavy = 15,
                kTuneCount };
 int tuning(TuneKey k);
 

@@ -354,16 +354,24 @@ struct RunRec {
 // Device-side bookkeeping of one backward (cleared by the clear launch).
 struct BwdCounters {
   int32_t touched, segs, tasks, cursor;
-  int32_t touched_lv[D2MI_MAX_LEVELS];  // touched pixels per level
+  int32_t touched_lv[D2MI_MAX_LEVELS];  // touched pixels per level (light: from the front)
+  int32_t touched_hv[D2MI_MAX_LEVELS];  // ... heavy (> roi_heavy contributions: from the back)
   int32_t lsdone;  // workgroups of the long-sort launch that finished
 };
 
 // The touched pixels of levels [lo, hi]: their count, and the t-th of them
 // (the level segments of the list in level order).
+// r5: a level's segment of the touched list holds its light pixels from the
+// front and its heavy ones (> roi_heavy contributions) from the back, and entry
+// order puts a level's heavy pixels first: the first waves of a pass take the
+// longest load chains, the light pixels fill in behind them (a pass's time was
+// its longest runs' row batches behind everything else).  The threshold is
+// tuning "roi_heavy" (default 16; 0: every pixel light, the r5b order).
 struct TouchedRange {
   // (every index below is a compile-time constant after unrolling: a
   // dynamically indexed register array lives in scratch memory)
   int32_t pre[D2MI_MAX_LEVELS + 1];
+  int32_t hv[D2MI_MAX_LEVELS];
   int lo, hi;
   __device__ __forceinline__ void init(const PixMap& pm, const BwdCounters* ctr, int lv_lo,
                                        int lv_hi) {
@@ -371,8 +379,11 @@ struct TouchedRange {
     hi = lv_hi;
     pre[0] = 0;
 #pragma unroll
-    for (int j = 0; j < D2MI_MAX_LEVELS; ++j)
-      pre[j + 1] = pre[j] + (j <= hi - lo ? ctr->touched_lv[lo + j] : 0);
+    for (int j = 0; j < D2MI_MAX_LEVELS; ++j) {
+      const bool in = j <= hi - lo;
+      hv[j] = in ? ctr->touched_hv[lo + j] : 0;
+      pre[j + 1] = pre[j] + (in ? ctr->touched_lv[lo + j] + hv[j] : 0);
+    }
   }
   __device__ __forceinline__ int total() const {
     int v = 0;
@@ -385,17 +396,20 @@ struct TouchedRange {
                                           int& l) const {
     return touched[index(pm, t, l)];
   }
-  // the touched-list index of entry t < total(), and its level
+  // the touched-list index of entry t < total(), and its level: a level's
+  // heavy pixels (its segment's back, last-allocated first) then its light ones
   __device__ __forceinline__ int index(const PixMap& pm, int t, int& l) const {
-    int k = 0, base = 0;
+    int k = 0, base = 0, h = hv[0];
 #pragma unroll
     for (int j = 1; j < D2MI_MAX_LEVELS; ++j)
       if (j <= hi - lo && t >= pre[j]) {
         k = j;
         base = pre[j];
+        h = hv[j];
       }
     l = lo + k;
-    return pm.tbase[l] + (t - base);
+    const int kk = t - base;
+    return kk < h ? pm.tbase[l + 1] - 1 - kk : pm.tbase[l] + (kk - h);
   }
 };
 
@@ -612,9 +626,9 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
     const int32_t* __restrict__ count, long long total_pixels, int set_bits,
     int32_t* __restrict__ run_start, int32_t* __restrict__ seg_first,
     int32_t* __restrict__ seg_pixel, int2* __restrict__ tasks, int32_t* __restrict__ touched,
-    int4* __restrict__ trun, BwdCounters* __restrict__ ctr, PixMap pm) {
+    int4* __restrict__ trun, BwdCounters* __restrict__ ctr, PixMap pm, int heavy_min) {
   __shared__ int s_wave[16], s_base;
-  __shared__ int s_wave5[5][16], s_base5[5];
+  __shared__ int s_wave7[7][16], s_base7[7];
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = p < total_pixels;
   const int nsets = 1 << set_bits;
@@ -639,18 +653,25 @@ __global__ __launch_bounds__(1024) void roi_bwd_runs_kernel(
   while (ll + 1 < pm.L && p1 >= pm.base[ll + 1]) ++ll;
   while (lp + 1 < pm.L && p >= pm.base[lp + 1]) ++lp;
   const int l2 = min(lf + 1, ll);
-  const int want[5] = {tot, tot > 0 && lp == lf ? 1 : 0, l2 > lf && tot > 0 && lp == l2 ? 1 : 0,
-                       nseg[0] + nseg[1], ntask[0] + ntask[1]};
-  int32_t* const ctrs[5] = {&ctr->cursor, &ctr->touched_lv[lf], &ctr->touched_lv[l2], &ctr->segs,
-                            &ctr->tasks};
-  int off[5];
-  wg_alloc_multi<1024, 5>(want, ctrs, off, s_wave5, s_base5);
+  const bool heavy = heavy_min > 0 && tot > heavy_min, light = tot > 0 && !heavy;
+  const int want[7] = {tot, light && lp == lf ? 1 : 0, l2 > lf && light && lp == l2 ? 1 : 0,
+                       nseg[0] + nseg[1], ntask[0] + ntask[1], heavy && lp == lf ? 1 : 0,
+                       l2 > lf && heavy && lp == l2 ? 1 : 0};
+  int32_t* const ctrs[7] = {&ctr->cursor, &ctr->touched_lv[lf], &ctr->touched_lv[l2], &ctr->segs,
+                            &ctr->tasks, &ctr->touched_hv[lf], &ctr->touched_hv[l2]};
+  int off[7];
+  wg_alloc_multi<1024, 7>(want, ctrs, off, s_wave7, s_base7);
   const int pos = off[0], sf = off[3], tf = off[4];
-  int tix = lp == lf ? pm.tbase[lf] + off[1] : (lp == l2 ? pm.tbase[l2] + off[2] : 0);
+  // light pixels from the level segment's front, heavy ones from its back
+  auto slot_of = [&](int lv, int o_light, int o_heavy) {
+    return heavy ? pm.tbase[lv + 1] - 1 - o_heavy : pm.tbase[lv] + o_light;
+  };
+  int tix = lp == lf ? slot_of(lf, off[1], off[5]) : (lp == l2 ? slot_of(l2, off[2], off[6]) : 0);
   for (int lv = l2 + 1; lv <= ll; ++lv) {
     __syncthreads();  // (s_wave / s_base reused)
-    const int o = wg_alloc<1024>(tot > 0 && lp == lv ? 1 : 0, &ctr->touched_lv[lv], s_wave, &s_base);
-    if (lp == lv) tix = pm.tbase[lv] + o;
+    const int ol = wg_alloc<1024>(light && lp == lv ? 1 : 0, &ctr->touched_lv[lv], s_wave, &s_base);
+    const int oh = wg_alloc<1024>(heavy && lp == lv ? 1 : 0, &ctr->touched_hv[lv], s_wave, &s_base);
+    if (lp == lv) tix = slot_of(lv, ol, oh);
   }
   if (tot == 0) return;
   touched[tix] = (int32_t)p;
@@ -1470,7 +1491,8 @@ int roi_bwd_core(const RoiArgs* sets, int nsets, const int32_t* dims, int num_le
   }
   hipLaunchKernelGGL(roi_bwd_runs_kernel, dim3((unsigned)((p.total_pixels + 1023) / 1024)),
                      dim3(1024), 0, st, count, p.total_pixels, sb, run_start, seg_first, seg_pixel,
-                     tasks, touched, use_runrec ? trun : nullptr, ctr, p.pm);
+                     tasks, touched, use_runrec ? trun : nullptr, ctr, p.pm,
+                     tuning(kTuneRoiHeavy));
   D2MI_LAUNCH_CHECK();
   hipLaunchKernelGGL(roi_bwd_place_kernel, dim3((unsigned)((p.n_keys + 255) / 256)), dim3(256), 0,
                      st, ent, p.n_keys, run_start, arrival, rec, use_runrec ? runrec : nullptr);

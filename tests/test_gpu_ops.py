@@ -173,13 +173,24 @@ def test_roi_align_backward_raw_large_crops_and_ragged_channels(dev, C, crop, sr
         assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
 
 
+@pytest.mark.parametrize("heavy", [16, 1, 0])
 @pytest.mark.parametrize("C,sr", [(256, 2), (256, 3), (256, 1), (64, 2)])
-def test_roi_align_backward_sampled_bins_bit_exact(dev, C, sr):
+def test_roi_align_backward_sampled_bins_bit_exact(dev, C, sr, heavy):
     """Sampling ratio > 0 (the poolers' mode): TF's backward is AvgPoolGrad
     (each bin's gradient / sr^2 to its sr x sr samples) then
     CropAndResizeGradImage over the sr-times-finer crop -- bit-exact, also
     where sr^2 is a power of two and the kernels multiply by its reciprocal
     instead of dividing (C = 256: the four-pixels-per-wave pass)."""
+    from detectron2_tensorflow_amd.layers import ops as lops
+    old_heavy = lops.get_tuning("roi_heavy")  # touched-list order: heavy pixels first (> heavy)
+    lops.set_tuning("roi_heavy", heavy)
+    try:
+        _sampled_bins_case(dev, C, sr)
+    finally:
+        lops.set_tuning("roi_heavy", old_heavy)
+
+
+def _sampled_bins_case(dev, C, sr):
     rng = np.random.default_rng(100 + sr)
     img = rng.normal(size=(2, 23, 29, C)).astype(F32)
     lo = rng.uniform(0.0, 0.3, size=(12, 2))
