@@ -85,6 +85,67 @@ __global__ void rpn_decode_kernel(const float* __restrict__ base_d, Levels lv, i
   }
 }
 
+// r5 (tuning "rpn_compact" = 1): decode AND the NMS input in one launch, one
+// workgroup per segment.  The top-k list is already in the NMS order (score
+// descending, list position ascending -- desc_key's order, -0.0 tied with
+// +0.0 in both), so the NMS's segmented sort is the identity on the valid
+// entries: a stable compaction of them (prune_small_boxes, NaN / -inf scores
+// dropped, as desc_key drops them) gives exactly the sorted boxes, positions
+// and count that keys -> sort -> gather produced (three launches, ~25 us per
+// RPN step).  dec keeps every decoded box at its list position for the merge.
+__global__ __launch_bounds__(1024) void rpn_decode_compact_kernel(
+    const float* __restrict__ base_d, Levels lv, int N, int k, const float* __restrict__ tvals,
+    const int32_t* __restrict__ tidx, const int32_t* __restrict__ tcount,
+    const int32_t* __restrict__ image_hw, DeltaCfg dc, float min_size, float4* __restrict__ dec,
+    float4* __restrict__ sboxes, int32_t* __restrict__ sidx, int32_t* __restrict__ scount) {
+  __shared__ int s_wave[16];
+  const int s = blockIdx.x;
+  const int n = s / lv.L, l = s - n * lv.L;
+  const int cnt = tcount[s];
+  const float hmax = (float)image_hw[2 * n], wmax = (float)image_hw[2 * n + 1];
+  const float4* d4 = reinterpret_cast<const float4*>(base_d + lv.off_b[l]);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int run = 0;
+  for (int j0 = 0; j0 < cnt; j0 += blockDim.x) {
+    const int j = j0 + (int)threadIdx.x;
+    const size_t o = (size_t)s * k + j;
+    bool valid = false;
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < cnt) {
+      const int id = tidx[o];
+      const int hw = id / lv.A, a = id - hw * lv.A;
+      const float4 anc = anchor_at(lv, l, hw, a);
+      const float4 d = d4[(size_t)n * lv.img_b[l] + (size_t)hw * lv.A + a];
+      b = apply_delta(anc, d, dc.wy, dc.wx, dc.wh, dc.ww, dc.clamp);
+      b = clip_box(b, hmax, wmax);
+      bool ok = true;
+      if (min_size > 0.f) {
+        const float bh = b.z - b.x, bw = b.w - b.y;
+        ok = (bw >= min_size) && (bh >= min_size);  // prune_small_boxes (box_list_ops.py:515)
+      }
+      dec[o] = b;
+      valid = ok && tvals[o] > -INFINITY;  // (desc_key: NaN / -inf never selected)
+    }
+    const unsigned long long bal = __ballot(valid);
+    if (lane == 0) s_wave[w] = __popcll(bal);
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int q = 0; q < nw; ++q) {
+      const int v = s_wave[q];
+      before += q < w ? v : 0;
+      tot += v;
+    }
+    if (valid) {
+      const int pos = run + before + __popcll(bal & ((1ull << lane) - 1ull));
+      sboxes[(size_t)s * k + pos] = b;
+      sidx[(size_t)s * k + pos] = j;
+    }
+    run += tot;
+    __syncthreads();  // (s_wave reused)
+  }
+  if (threadIdx.x == 0) scount[s] = run;
+}
+
 // One workgroup per image: concat the per-level NMS survivors, top_k(post,
 // sorted=True) with the concat position as tie-break, zero-pad.
 __global__ __launch_bounds__(1024) void rpn_merge_kernel(
@@ -668,13 +729,32 @@ extern "C" int d2mi_rpn_proposals_ex(const float* const* logits, const float* co
   rc = topk_core_ex(logits[0], o.seg_start, o.seg_len, nullptr, S, maxlen, k, 0, o.tvals, o.tidx,
                     o.tcount, o.topk_ws, o.topk_bytes, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(rpn_decode_kernel, dim3(grid1(k, 256, 64), S), dim3(256), 0, st, deltas[0], lv,
-                     N, k, o.tvals, o.tidx, o.tcount, image_hw, make_dc(weights4_host, scale_clamp),
-                     min_box_side_len, o.dec, o.keys, o.lens);
-  D2MI_LAUNCH_CHECK();
-  rc = nms_core(o.keys, o.lens, o.dec, nullptr, S, k, post_nms_topk, nms_thresh, o.keep,
-                o.num_keep, o.nms_ws, o.nms_bytes, st);
-  if (rc) return rc;
+  if (tuning(kTuneRpnCompact) != 0) {
+    // the NMS workspace carved as nms_core carves it (its sort keys unused)
+    Workspace nw(o.nms_ws, o.nms_bytes);
+    nw.take<uint64_t>((size_t)S * k);
+    float4* sboxes = nw.take<float4>((size_t)S * k);
+    int32_t* sidx = nw.take<int32_t>((size_t)S * k);
+    int32_t* scount = nw.take<int32_t>(S);
+    const size_t mask_bytes = nms_sorted_workspace_size(S, k);
+    void* mask_ws = nw.take<char>(mask_bytes);
+    D2MI_REQUIRE(nw.ok(), "RPN NMS workspace too small");
+    hipLaunchKernelGGL(rpn_decode_compact_kernel, dim3(S), dim3(1024), 0, st, deltas[0], lv, N, k,
+                       o.tvals, o.tidx, o.tcount, image_hw, make_dc(weights4_host, scale_clamp),
+                       min_box_side_len, o.dec, sboxes, sidx, scount);
+    D2MI_LAUNCH_CHECK();
+    rc = nms_sorted(sboxes, sidx, scount, S, k, post_nms_topk, nms_thresh, o.keep, o.num_keep,
+                    mask_ws, mask_bytes, st);
+    if (rc) return rc;
+  } else {  // decode -> keys -> nms_core's sort + gather (A/B)
+    hipLaunchKernelGGL(rpn_decode_kernel, dim3(grid1(k, 256, 64), S), dim3(256), 0, st, deltas[0],
+                       lv, N, k, o.tvals, o.tidx, o.tcount, image_hw,
+                       make_dc(weights4_host, scale_clamp), min_box_side_len, o.dec, o.keys, o.lens);
+    D2MI_LAUNCH_CHECK();
+    rc = nms_core(o.keys, o.lens, o.dec, nullptr, S, k, post_nms_topk, nms_thresh, o.keep,
+                  o.num_keep, o.nms_ws, o.nms_bytes, st);
+    if (rc) return rc;
+  }
   // tuning "rpn_merge": 1 the merge rank (r5), 0 the one-workgroup bitonic sort (A/B)
   if (tuning(kTuneRpnMerge) != 0) {
     const int span = std::max(L * post_nms_topk, post_nms_topk);

@@ -439,14 +439,17 @@ def _rpn_case(seed, N=2, IH=256, IW=320, A=3):
     return strides, hw, cells, logits, deltas, image_hw
 
 
-@pytest.mark.parametrize("merge", [1, 0])
+@pytest.mark.parametrize("merge,compact", [(1, 1), (0, 1), (1, 0)])
 @pytest.mark.parametrize("tied", [False, True])
 @pytest.mark.parametrize("pre,post,min_size", [(1000, 1000, 0.0), (300, 200, 0.0), (1000, 500, 8.0)])
-def test_rpn_proposals_vs_oracle(dev, pre, post, min_size, tied, merge):
+def test_rpn_proposals_vs_oracle(dev, pre, post, min_size, tied, merge, compact):
     """merge: the per-image concat + top-k as a merge rank over the per-level
     survivor lists (tuning "rpn_merge" 1, r5) or one workgroup's bitonic sort
-    (0).  tied: logits quantized to halves with signed zeros, so equal scores
-    across levels exercise the level-then-position tie rule (-0 below +0)."""
+    (0).  compact: decode + a stable compaction of the valid top-k entries as
+    the NMS input (tuning "rpn_compact" 1, r5) or decode -> keys -> the NMS's
+    own sort (0).  tied: logits quantized to halves with signed zeros, so
+    equal scores across levels exercise the level-then-position tie rule (-0
+    tied with +0: the index decides)."""
     from detectron2_tensorflow_amd.layers import ops as lops
     strides, hw, cells, logits, deltas, image_hw = _rpn_case(21)
     if tied:
@@ -454,13 +457,15 @@ def test_rpn_proposals_vs_oracle(dev, pre, post, min_size, tied, merge):
         for l in logits:
             l[..., 0][np.abs(l[..., 0]) < 0.25] = -0.0
         logits = [l.astype(F32) for l in logits]
-    old = lops.get_tuning("rpn_merge")
+    old = lops.get_tuning("rpn_merge"), lops.get_tuning("rpn_compact")
     lops.set_tuning("rpn_merge", merge)
+    lops.set_tuning("rpn_compact", compact)
     try:
         _rpn_proposals_vs_oracle(dev, pre, post, min_size, strides, hw, cells, logits, deltas,
                                  image_hw)
     finally:
-        lops.set_tuning("rpn_merge", old)
+        lops.set_tuning("rpn_merge", old[0])
+        lops.set_tuning("rpn_compact", old[1])
 
 
 def _rpn_proposals_vs_oracle(dev, pre, post, min_size, strides, hw, cells, logits, deltas,
