@@ -201,6 +201,16 @@ __device__ __forceinline__ Geo select_level(const ConvArgs& a, int& tile) {
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+typedef float ntv4 __attribute__((ext_vector_type(4)));
+// streaming (non-temporal) float4 load / store: data touched once
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const ntv4 v = __builtin_nontemporal_load(reinterpret_cast<const ntv4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+  ntv4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<ntv4*>(p));
+}
 
 __device__ __forceinline__ float epilogue(const ConvArgs& a, const Geo& g, float acc, int m,
                                           int co) {
@@ -769,7 +779,8 @@ __global__ __launch_bounds__(256, OCC) void conv_mfma_kernel(ConvArgs a) {
 // only then: 16 x TN floats per lane each).  LDS: the weight slice (K x BN x
 // 6 B) + 8 KiB per wave (<= 160 KiB: K 128 at BN 128, K 256 at BN 64).
 template <int TN, int KMAX, int WAVES, bool RES, bool GATE>
-__global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs a, int nslices) {
+__global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs a, int nslices,
+                                                                      int ntmode) {
   constexpr int BN = 32 * TN;
   static_assert(KMAX % 32 == 0, "K: whole 32-deep chunks");
   static_assert(TN == 2 || TN == 4, "64-column epilogue halves");
@@ -843,8 +854,13 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs 
           const int m = strip * 32 + erow + 4 * q, co = n0 + h * 64 + ec4 * 4;
           const bool ok = m < a.M && co < a.Cout;
           const size_t o = (size_t)m * a.Cout + co;
-          if constexpr (RES) res[h][q] = ok ? ld4(a.residual + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-          if constexpr (GATE) gt[h][q] = ok ? ld4(a.gate + o) : make_float4(1.f, 1.f, 1.f, 1.f);
+          const bool nt = ntmode & 1;  // (uniform)
+          if constexpr (RES)
+            res[h][q] = ok ? (nt ? ld4_nt(a.residual + o) : ld4(a.residual + o))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+          if constexpr (GATE)
+            gt[h][q] = ok ? (nt ? ld4_nt(a.gate + o) : ld4(a.gate + o))
+                          : make_float4(1.f, 1.f, 1.f, 1.f);
         }
     }
   };
@@ -930,8 +946,11 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv1x1_stream_kernel(ConvArgs 
             if (!(gg[e4] > 0.f)) v[e4] = 0.f;
           }
         }
-        if (m < a.M)
-          *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = make_float4(v[0], v[1], v[2], v[3]);
+        if (m < a.M) {
+          const float4 o4 = make_float4(v[0], v[1], v[2], v[3]);
+          if (ntmode & 2) st4_nt(a.y + (size_t)m * a.Cout + co, o4);
+          else *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o4;
+        }
       }
     }
     if (more) load_e(s + sstep);  // res / gt are free: the next strip's, under its MFMAs
@@ -1615,21 +1634,27 @@ static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
 
 template <int TN, int KMAX>
 static void launch_stream1x1_t(dim3 grid, hipStream_t st, const ConvArgs& a, int nslices) {
+  // tuning "conv_stream_nt": bit 0 streaming loads of the epilogue operands, bit 1
+  // streaming (non-temporal) stores of the output -- default 2: the stores
+  // alone (tools/stream_ab.py --nt, profiles/r5_stream_nt_*.log: 64 -> 256 +
+  // residual at 134 k pixels 82.2 -> 66.6 us, 0.58 of HBM; the loads alone
+  // lose on 128 -> 512; in-step -0.20 %, profiles/r5_ab_stream_nt.log)
+  const int nt = tuning(kTuneConvStreamNt);
   constexpr int W = 8;
   const bool r = a.residual != nullptr, g = a.gate != nullptr;
   if (r && g) {
     if constexpr (TN == 2)  // (both operands' registers: BN 64, launch_stream1x1)
       hipLaunchKernelGGL((conv1x1_stream_kernel<TN, KMAX, W, true, true>), grid, dim3(64 * W), 0,
-                         st, a, nslices);
+                         st, a, nslices, nt);
   } else if (r) {
     hipLaunchKernelGGL((conv1x1_stream_kernel<TN, KMAX, W, true, false>), grid, dim3(64 * W), 0,
-                       st, a, nslices);
+                       st, a, nslices, nt);
   } else if (g) {
     hipLaunchKernelGGL((conv1x1_stream_kernel<TN, KMAX, W, false, true>), grid, dim3(64 * W), 0,
-                       st, a, nslices);
+                       st, a, nslices, nt);
   } else {
     hipLaunchKernelGGL((conv1x1_stream_kernel<TN, KMAX, W, false, false>), grid, dim3(64 * W), 0,
-                       st, a, nslices);
+                       st, a, nslices, nt);
   }
 }
 

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--min-m", type=int, default=-1,
                     help="conv_stream value of the stream arm (< 0: every eligible shape)")
     ap.add_argument("--shapes", default=None)
+    ap.add_argument("--nt", type=int, default=None,
+                    help="compare the stream kernel with conv_stream_nt 0 (arm 0) and this value")
     a = ap.parse_args()
     shapes = a.shapes.split(";") if a.shapes else SHAPES
     _C.load()
@@ -54,14 +56,20 @@ def main():
                   relu=(form in ("r", "relu")))
         run = lambda: ops.conv2d_nhwc(x, wp, b, 1, (0, 0), math_mode="split", **kw)  # noqa: E731
         outs, times = {}, {0: [], 1: []}
+        def set_arm(arm):
+            if a.nt is None:
+                ops.set_tuning("conv_stream", a.min_m if arm else 0)
+            else:
+                ops.set_tuning("conv_stream", a.min_m)
+                ops.set_tuning("conv_stream_nt", a.nt if arm else 0)
         for arm in (0, 1):
-            ops.set_tuning("conv_stream", a.min_m if arm else 0)
+            set_arm(arm)
             outs[arm] = run()
         torch.cuda.synchronize()
         same = torch.equal(outs[0], outs[1])
         for _ in range(a.rounds):
             for arm in (0, 1):
-                ops.set_tuning("conv_stream", a.min_m if arm else 0)
+                set_arm(arm)
                 run()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -72,6 +80,7 @@ def main():
                 e1.synchronize()
                 times[arm].append(e0.elapsed_time(e1) / a.iters * 1e3)
         ops.set_tuning("conv_stream", 0)
+        ops.set_tuning("conv_stream_nt", 0)
         med = {k: statistics.median(v) for k, v in times.items()}
         y = outs[0]
         byts = ops.conv_bytes(x, wp, y, b, None, res, gate)
