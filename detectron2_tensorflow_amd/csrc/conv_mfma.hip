@@ -134,6 +134,7 @@ struct ConvArgs {
   // last round would run mostly empty, see conv_core)
   int tile_base, m_base, m_end;
   int lds_epi;  // store_outputs_lds usable (Cout % 4 == 0, 16-B aligned operands)
+  int nt_store;  // final outputs of the LDS epilogue / split-K reduce stored non-temporally
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB)
   int tdH, tdW;
   int reg_partials;  // split-K partials stored from the accumulators (tuning conv_epi)
@@ -422,7 +423,8 @@ __device__ __forceinline__ void store_outputs_lds(const ConvArgs& a, const Geo& 
           vv[e] = x;
         }
       }
-      *reinterpret_cast<float4*>(dst + (size_t)(m - mrow0) * a.Cout + co) = v;
+      if (!part && a.nt_store) st4_nt(dst + (size_t)(m - mrow0) * a.Cout + co, v);
+      else *reinterpret_cast<float4*>(dst + (size_t)(m - mrow0) * a.Cout + co) = v;
     }
     __syncthreads();
   }
@@ -1276,7 +1278,8 @@ __global__ void splitk_reduce4_kernel(ConvArgs a) {
     o.y = epilogue(a, g, acc.y, m, co + 1);
     o.z = epilogue(a, g, acc.z, m, co + 2);
     o.w = epilogue(a, g, acc.w, m, co + 3);
-    *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
+    if (a.nt_store) st4_nt(a.y + (size_t)m * a.Cout + co, o);
+    else *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
   }
 }
 
@@ -1731,6 +1734,7 @@ static int conv_core(const float* x, const float* w_packed, const float* bias,
   }
   a.reg_partials = tuning(kTuneConvEpi) != 0;
   a.xcd2 = tuning(kTuneConvXCD) != 0;
+  a.nt_store = tuning(kTuneConvNt) != 0;  // (tuning "conv_nt", A/B)
   Plan p = make_plan(a.M, Cout, KH, KW, Cin, a.lds_epi != 0, (flags & kSplit3) != 0);
   if (p.ws_bytes > workspace_bytes || workspace == nullptr) {  // no workspace: no split-K
     p.splits = 1;
