@@ -190,10 +190,18 @@ class GraphedTrainer(Trainer):
         torch.cuda.synchronize(dev)
         self._pool = torch.cuda.graph_pool_handle()
         g = self._new_graph()
+        # r5: graph A ends with the foreground count's copy into pinned host
+        # memory, so the host's one read is a wait on the replay alone (before:
+        # wait for A, then enqueue a device-to-host copy and wait for it -- the
+        # copy started ~60-140 us after A's last kernel, the device idle)
+        self._count_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         capture.begin(dev)  # (outside the capture: see utils/capture.py)
         with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
                               capture_error_mode="thread_local"):
             losses = self.model(self._static)
+            for v in losses.values():
+                if isinstance(v, DeferredMaskLoss):
+                    self._count_host.copy_(v.count.reshape(1).to(torch.int64), non_blocking=True)
         self._dump(g, "A")
         self._keep = []
         capture.flush(self._keep)
@@ -262,10 +270,12 @@ class GraphedTrainer(Trainer):
                 raise
         self._load(batched_inputs)
         self._lr_dev.fill_(float(self.lr(self.iter)))
+        if self._deferred is not None:
+            host_sync.arm_pinned(self._count_host)
         self._A.replay()
         rows = None
         if self._deferred is not None:
-            nfg = host_sync.read_ints(self._deferred.count)[0]  # the step's one host read
+            nfg = host_sync.read_pinned(self._count_host)[0]  # the step's one host read
             rows = self._deferred.rows_for(nfg)
             for h in self.heads:
                 h.last_mask_rows = rows

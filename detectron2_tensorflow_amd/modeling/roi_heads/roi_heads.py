@@ -138,9 +138,9 @@ class DeferredMaskLoss:
     that row count (``compute(rows)``, run once per distinct row count at
     capture time).  The eager trainer never sees one (defer_mask_loss False)."""
 
-    def __init__(self, heads, feats, sampled, targets, share, fg):
+    def __init__(self, heads, feats, sampled, targets, share, fg, prep=None):
         self.heads, self.feats, self.sampled, self.targets = heads, feats, sampled, targets
-        self.share, self.fg = share, fg
+        self.share, self.fg, self.prep = share, fg, prep
         self.count = fg.sum()
         self.slots = fg.numel()
 
@@ -149,7 +149,7 @@ class DeferredMaskLoss:
 
     def compute(self, rows):
         return self.heads._mask_loss(self.feats, self.sampled, self.targets, self.share, None,
-                                     self.fg, rows=rows)
+                                     self.fg, rows=rows, prep=self.prep)
 
 
 @ROI_HEADS_REGISTRY.register()
@@ -213,12 +213,17 @@ class StandardROIHeads(ROIHeads):
             fg = self._mask_fg(sampled) if self.mask_on else None  # (once per step)
             defer = self.mask_on and self.mask_compact_rows and self.defer_mask_loss
             prep = None
-            if self.mask_on and self.mask_compact_rows and not defer:
-                pending = host_sync.start_read(fg.sum())
+            if self.mask_on and self.mask_compact_rows:
+                if not defer:
+                    pending = host_sync.start_read(fg.sum())
+                # (deferred too, r5: in a replayed step these small gathers are
+                # issued inside graph A, under the box branch's kernels, not at
+                # graph B's head where the host's per-node submission outran them)
                 prep = self._mask_prep(sampled, targets, fg) if self.MASK_PREP_EARLY else None
             losses = self._box_losses(feats, sampled, share)
             if defer:
-                losses["loss_mask"] = DeferredMaskLoss(self, feats, sampled, targets, share, fg)
+                losses["loss_mask"] = DeferredMaskLoss(self, feats, sampled, targets, share, fg,
+                                                       prep)
             elif self.mask_on:
                 losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg,
                                                       prep=prep)

@@ -25,6 +25,30 @@ def read_ints(t):
     return [int(v) for v in t.reshape(-1).cpu().tolist()]
 
 
+def arm_pinned(host):
+    """Mark a pinned int64 host buffer unwritten (-1) before the work that
+    writes it is queued (read_pinned spins on it)."""
+    host.fill_(-1)
+
+
+def read_pinned(host, spin_s=0.005):
+    """int values of a pinned host tensor that the work queued on the current
+    stream writes (a captured graph's last copy), armed by arm_pinned: the
+    host spins on the buffer itself for up to ``spin_s`` (a blocking stream
+    wait wakes the host tens of microseconds after the copy lands), then
+    waits on the stream (timed either way; the wait also surfaces a device
+    error the spin cannot see)."""
+    global blocked_s
+    t0 = time.perf_counter()
+    view = host.numpy()
+    while view[0] < 0 and time.perf_counter() - t0 < spin_s:
+        pass
+    if view[0] < 0:
+        torch.cuda.current_stream().synchronize()
+    blocked_s += time.perf_counter() - t0
+    return [int(v) for v in view.tolist()]
+
+
 class PendingRead:
     """A device-to-host read started early: the values are copied into pinned
     host memory behind the work already queued, an event marks them ready,
