@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void wgrad_skinny_partial_kernel(
 // bytes per load of the scalar form, which left this pass latency-bound),
 // and the waves' sums are combined in wave order through LDS before the
 // chunk partial is written.  kChunk4 pixels per workgroup.
-constexpr int kChunk4 = 512;  // (r5: 128 -> 512, a quarter of the partials for the reduce)
+constexpr int kChunk4 = 128;
 
 __device__ __forceinline__ void skinny_partial4(const float* __restrict__ x,
                                                 const float* __restrict__ g, int P, int Cin,

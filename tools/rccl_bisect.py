@@ -13,8 +13,13 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARMS = [("default", {}), ("conv_stream=0", {"D2MI_CONV_STREAM": "0"}),
+        ("conv_stream_nt=0", {"D2MI_CONV_STREAM_NT": "0"}),
         ("rpn_merge=0", {"D2MI_RPN_MERGE": "0"}), ("roi_bwd_rec=0", {"D2MI_ROI_BWD_REC": "0"}),
-        ("default again", {})]
+        ("roi_heavy=0", {"D2MI_ROI_HEAVY": "0"}), ("nms_scan=0", {"D2MI_NMS_SCAN": "0"}),
+        ("rpn_compact=0", {"D2MI_RPN_COMPACT": "0"}), ("default again", {})]
+if len(sys.argv) > 1:  # a subset by name
+    ARMS = [a for a in ARMS if a[0] in sys.argv[1:]]
+
 
 
 def port():
