@@ -1423,6 +1423,15 @@ static int wg_slots(int cfg) {
 // Cin >= 512), where its deeper staging pipeline pays; the short-K 1x1s
 // (2-8 k-steps) stay on the 3-per-CU kernel, whose prologue / epilogue
 // overlap across workgroups (tools/ws_ab.py, 16 Mask R-CNN shapes).
+// The stride-1 1x1 shapes with K = 256 that the streaming kernel takes
+// (stream1x1_variant: 1.17x into 64 channels, 1.12x into 512 at >= 32 k
+// pixels, profiles/r5_stream_ab_force_tn_rule.log); the tiled plan of these
+// shapes never splits its tail tiles' K, so both kernels round alike.
+static bool stream256_shape(int M, int Cout, int KH, int KW, int Cin) {
+  return KH == 1 && KW == 1 && Cin == 256 && M >= 32768 && (Cout <= 64 || Cout == 512) &&
+         Cout % 4 == 0;
+}
+
 Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool split = true) {
   Plan p;
   p.cfg = Cout <= 32 ? 2 : (Cout <= 64 || !wide_ok ? 1 : 0);
@@ -1466,7 +1475,8 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool spli
   p.tail_kt_per_split = p.nk;
   p.main_m_end = M;
   static const char* tail_env = getenv("D2MI_CONV_TAIL");  // "0": no tail split (A/B)
-  if (p.splits == 1 && p.ntiles > G && p.nk >= 8 && !(tail_env && tail_env[0] == '0')) {
+  if (p.splits == 1 && p.ntiles > G && p.nk >= 8 && !(tail_env && tail_env[0] == '0') &&
+      !stream256_shape(M, Cout, KH, KW, Cin)) {
     const int full = (p.ntiles / G) * G / nN * nN;
     const int tail = p.ntiles - full;
     if (tail > 0 && 2 * tail <= G) {
@@ -1632,7 +1642,11 @@ static int stream1x1_variant(const ConvArgs& a, const Plan& p, int flags) {
   // differently from an aligned one (tests/test_gpu_dp.py's one-rank RCCL
   // equality).  For K <= 128 both kernels sum in the same order: bit-identical.
   if (a.Cin == 64 || a.Cin == 128) return a.Cin == 64 ? 1 : 2;
-  return force ? 3 : 0;
+  // r5b: K = 256 into <= 64 or 512 channels (where it wins) -- make_plan
+  // keeps those shapes' tiles whole (no tail split, stream256_shape), so the
+  // tiled fallback sums K in the stream kernel's order: bit-identical again
+  if (force || stream256_shape(a.M, a.Cout, a.KH, a.KW, a.Cin)) return 3;
+  return 0;
 }
 
 template <int TN, int KMAX>
