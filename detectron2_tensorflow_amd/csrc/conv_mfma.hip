@@ -1475,7 +1475,9 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool spli
   p.tail_kt_per_split = p.nk;
   p.main_m_end = M;
   static const char* tail_env = getenv("D2MI_CONV_TAIL");  // "0": no tail split (A/B)
-  if (p.splits == 1 && p.ntiles > G && p.nk >= 8 && !(tail_env && tail_env[0] == '0') &&
+  // (tuning "conv_tail_mink": the fewest k-steps whose tail tiles are split, A/B)
+  if (p.splits == 1 && p.ntiles > G && p.nk >= std::max(2, tuning(kTuneConvTailMinK)) &&
+      !(tail_env && tail_env[0] == '0') &&
       !stream256_shape(M, Cout, KH, KW, Cin)) {
     const int full = (p.ntiles / G) * G / nN * nN;
     const int tail = p.ntiles - full;
