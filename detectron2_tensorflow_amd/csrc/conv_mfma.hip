@@ -1438,7 +1438,9 @@ Plan make_plan(int M, int Cout, int KH, int KW, int Cin, bool wide_ok, bool spli
   // tuning "conv_ws_mink": the fewest k-steps that go to the WS kernel (A/B)
   if (p.cfg == 0 && split && tuning(kTuneConvWS) > 0 &&
       KH * KW * ((Cin + BK - 1) / BK) >= tuning(kTuneConvWSMinK) &&
-      KH * KW <= 32)  // (the WS stagers keep a 32-bit tap mask per row)
+      KH * KW <= 32 &&  // (the WS stagers keep a 32-bit tap mask per row)
+      // (tuning "conv_ws_mintiles": the fewest 256x128 tiles that go to the WS kernel, A/B)
+      ((M + 255) / 256) * ((Cout + 127) / 128) >= tuning(kTuneConvWSMinTiles))
     p.cfg = 3;
   p.BM = p.cfg == 3 ? 256 : 128;
   p.BN = (p.cfg == 0 || p.cfg == 3) ? 128 : (p.cfg == 1 ? 64 : 32);
