@@ -70,6 +70,37 @@ __device__ inline uint32_t upper_bound_sig(uint32_t lo, uint32_t hi, float s) {
   }
   return a;
 }
+// The same two searches by one whole wave (every lane calls with the same
+// arguments and gets the same result): each round the 64 lanes test the last
+// key of 64 equal chunks of the range, so 2^32 keys take 6 rounds of one
+// sigmoid per lane instead of 32 dependent ones.  gt = false: smallest key in
+// [lo, hi] whose sigmoid is >= s, or hi + 1 (lower_bound_sig); gt = true:
+// smallest key whose sigmoid is > s, or hi + 1.
+__device__ inline uint32_t wave_bound_sig(uint32_t lo, uint32_t hi, float s, bool gt) {
+  const uint64_t lane = threadIdx.x & 63;
+  uint64_t a = lo, b = (uint64_t)hi + 1;  // search [a, b)
+  while (a < b) {
+    const uint64_t step = (b - a + 63) >> 6;
+    uint64_t m = a + (lane + 1) * step - 1;
+    if (m > b - 1) m = b - 1;
+    const float sm = sigmoidf_tf(from_orderable((uint32_t)m));
+    const uint64_t bal = __ballot(gt ? sm > s : sm >= s);  // monotone in the lane
+    if (bal == 0) return (uint32_t)b;  // (only when b = hi + 1: the range never shrinks from above otherwise)
+    const uint64_t f = (uint64_t)(__ffsll((unsigned long long)bal) - 1);
+    if (step == 1) return (uint32_t)(a + f);
+    const uint64_t mf = a + (f + 1) * step - 1 < b - 1 ? a + (f + 1) * step - 1 : b - 1;
+    a = a + f * step;  // the previous chunk's last key failed
+    b = mf + 1;        // mf satisfies: the answer is <= mf
+  }
+  return (uint32_t)a;
+}
+__device__ inline uint32_t wave_lower_bound_sig(uint32_t lo, uint32_t hi, float s) {
+  return wave_bound_sig(lo, hi, s, false);
+}
+// upper_bound_sig by one wave: the key before the first whose sigmoid is > s.
+__device__ inline uint32_t wave_upper_bound_sig(uint32_t lo, uint32_t hi, float s) {
+  return wave_bound_sig(lo, hi, s, true) - 1;
+}
 
 // RetinaNet inference in four launches (retina_post.hip).
 bool retina_fused_eligible(int L, int k, int max_det);

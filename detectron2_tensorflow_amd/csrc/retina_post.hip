@@ -203,12 +203,15 @@ __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restri
   __shared__ uint32_t mx[kWG];
   mx[t] = best;
   __syncthreads();
+  if (t >= 64) return;
+  // (the top 24 bits only: the floor is a heuristic, a key at most 255
+  // steps lower collects a few more candidates and changes no result)
   uint32_t f0 = 0;
-  if (t < 64) {
+  {
     uint32_t vals[kWG / 64];
 #pragma unroll
     for (int j = 0; j < kWG / 64; ++j) vals[j] = mx[j * 64 + t];
-    for (int b = 31; b >= 0; --b) {
+    for (int b = 31; b >= 8; --b) {
       const uint32_t cand = f0 | (1u << b);
       int c = 0;
 #pragma unroll
@@ -216,13 +219,13 @@ __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restri
       if (c >= ts) f0 = cand;
     }
   }
+  uint32_t floor = f0, exact_lo = f0;
+  if (f0 > kKeyNegInf && f0 <= kKeyPosInf) {  // no sigmoid tie across exact_lo
+    const uint32_t lb = wave_lower_bound_sig(kKeyNegInf, f0, sigmoidf_tf(from_orderable(f0)));
+    exact_lo = lb;
+    floor = lb > kKeyNegInf + kWindowMargin ? lb - kWindowMargin : kKeyNegInf;
+  }
   if (t == 0) {
-    uint32_t floor = f0, exact_lo = f0;
-    if (f0 > kKeyNegInf && f0 <= kKeyPosInf) {  // no sigmoid tie across exact_lo
-      const uint32_t lb = lower_bound_sig(kKeyNegInf, f0, sigmoidf_tf(from_orderable(f0)));
-      exact_lo = lb;
-      floor = lb > kKeyNegInf + kWindowMargin ? lb - kWindowMargin : kKeyNegInf;
-    }
     info[s].floor = floor;
     info[s].exact_lo = exact_lo;
     info[s].k = kk;
@@ -442,21 +445,25 @@ __device__ int exact_select(const float* __restrict__ p, int len, int k, uint64_
     __syncthreads();
   }
   const uint32_t u = prefix;
-  if (t == 0) {
-    s_above = 0;
-    s_tie = 0;
-    if (u > kKeyNegInf && u <= kKeyPosInf) {
-      const float su = sigmoidf_tf(from_orderable(u));
-      const uint32_t lo = lower_bound_sig(kKeyNegInf, u, su);
-      s_sig = su;
-      s_sigmode = 1;
-      s_win_lo = lo > kKeyNegInf + kWindowMargin ? lo - kWindowMargin : kKeyNegInf;
-      s_tie_hi = upper_bound_sig(u, kKeyPosInf, su);
-    } else {
-      s_sig = 0.f;
-      s_sigmode = 0;
-      s_win_lo = u;
-      s_tie_hi = u;
+  if (t < 64) {  // (wave 0: the two sigmoid searches 64 keys a round)
+    const bool sm = u > kKeyNegInf && u <= kKeyPosInf;
+    const float su = sm ? sigmoidf_tf(from_orderable(u)) : 0.f;
+    const uint32_t lo = sm ? wave_lower_bound_sig(kKeyNegInf, u, su) : 0u;
+    const uint32_t hi = sm ? wave_upper_bound_sig(u, kKeyPosInf, su) : 0u;
+    if (t == 0) {
+      s_above = 0;
+      s_tie = 0;
+      if (sm) {
+        s_sig = su;
+        s_sigmode = 1;
+        s_win_lo = lo > kKeyNegInf + kWindowMargin ? lo - kWindowMargin : kKeyNegInf;
+        s_tie_hi = hi;
+      } else {
+        s_sig = 0.f;
+        s_sigmode = 0;
+        s_win_lo = u;
+        s_tie_hi = u;
+      }
     }
   }
   __syncthreads();
@@ -523,20 +530,46 @@ __device__ int exact_select(const float* __restrict__ p, int len, int k, uint64_
   return G + min(found, need);
 }
 
-// The k-th smallest (1-based) of the valid values, 8 per thread: radix
-// select, 12 + 12 + 8 bits, histograms in LDS.
+// The k-th smallest (1-based) of the valid values, 8 per thread: a radix
+// select relative to the smallest value, 4,096 bins of 2^sh keys a pass over
+// [lo, lo + span): the candidates' sort keys share their top bits (sigmoids
+// of one exponent or two), so bins taken from the top bits put thousands of
+// LDS atomics on a few words; relative bins spread them, and a span under
+// 2^24 (the usual case) needs two passes instead of three.
 __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8], int k,
                                     uint32_t* hist, uint32_t* part) {
   __shared__ int s_bin;
   __shared__ uint32_t s_lt;
-  const int t = threadIdx.x;
-  uint32_t prefix = 0;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t mn = 0xffffffffu, mx = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (ok[j]) {
+      mn = min(mn, h[j]);
+      mx = max(mx, h[j]);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  }
+  if (lane == 0) {
+    hist[w] = mn;
+    hist[kWG / 64 + w] = mx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kWG / 64; ++j) {
+    mn = min(mn, hist[j]);
+    mx = max(mx, hist[kWG / 64 + j]);
+  }
+  __syncthreads();
+  uint32_t lo = mn;
+  uint64_t span = (uint64_t)mx - mn + 1u;
   int krem = k;
-  for (int pass = 0; pass < 3; ++pass) {
-    const int nbits = pass < 2 ? 12 : 8;
-    const int shift = pass == 0 ? 20 : (pass == 1 ? 8 : 0);
-    const int hs = shift + nbits;
-    const uint32_t mask = (1u << nbits) - 1u;
+  for (;;) {
+    int sh = 0;
+    while ((span + ((1ull << sh) - 1u)) >> sh > 4096u) ++sh;
     for (int i = t; i < 4096; i += kWG) hist[i] = 0;
     if (t == 0) {
       s_bin = 0;
@@ -545,8 +578,8 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (ok[j] && (hs == 32 || (h[j] >> hs) == prefix))
-        atomicAdd(&hist[(h[j] >> shift) & mask], 1u);
+      if (ok[j] && h[j] >= lo && (uint64_t)(h[j] - lo) < span)
+        atomicAdd(&hist[(h[j] - lo) >> sh], 1u);
     __syncthreads();
     uint32_t c4[4], loc = 0;
 #pragma unroll
@@ -568,11 +601,13 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
       }
     }
     __syncthreads();
-    prefix = (prefix << nbits) | (uint32_t)s_bin;
+    const uint64_t off = (uint64_t)s_bin << sh;
+    lo += (uint32_t)off;
     krem -= (int)s_lt;
+    if (sh == 0) return lo;
+    span = min<uint64_t>(span - off, 1ull << sh);
     __syncthreads();
   }
-  return prefix;
 }
 
 __global__ __launch_bounds__(kWG) void retina_finish_kernel(
@@ -616,20 +651,26 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     m += orderable(__uint_as_float((uint32_t)(ent >> 32))) >= xlo ? 1 : 0;
   };
   if (ok) {
+    // the overflow entries (collect's hits past a wave's 8 slots) are loaded
+    // up front, alongside the first batch (their positions come later)
+    constexpr int kOv = 1;  // (1,024 entries up front, the rest after the slots: registers)
+    const uint64_t* osrc = ovf + (size_t)s * kCap;
+    uint64_t ov[kOv];
+#pragma unroll
+    for (int j = 0; j < kOv; ++j) ov[j] = j * kWG + t < xnovf ? osrc[j * kWG + t] : 0ull;
     constexpr int U = 8;  // wave slots per thread per batch (1333x800 P3: 11,812 in two)
     for (int e0 = 0; e0 < nw; e0 += U * kWG) {
       int cc[U], pos[U];
       uint64_t e1[U], e2[U];
+      // the first two entries of every slot load with its count, unconditionally
+      // (a slot's rows always exist; entries past its count are ignored)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = e0 + u * kWG + t;
+        const uint64_t* src = wslot + (size_t)(w0 + min(e, nw - 1));
         cc[u] = e < nw ? min(wcount[w0 + e], kWaveSlots) : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t* src = wslot + (size_t)(w0 + e0 + u * kWG + t);
-        e1[u] = cc[u] > 0 ? src[0] : 0ull;
-        e2[u] = cc[u] > 1 ? src[nslots] : 0ull;
+        e1[u] = src[0];
+        e2[u] = src[nslots];
       }
       // positions: per wave one LDS atomic per batch row (wave prefix of the counts)
 #pragma unroll
@@ -655,8 +696,12 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     }
     __syncthreads();
     const int nreg = s_n;
-    const uint64_t* osrc = ovf + (size_t)s * kCap;
-    for (int i = t; i < xnovf; i += kWG)
+#pragma unroll
+    for (int j = 0; j < kOv; ++j) {
+      const int i = j * kWG + t;
+      if (i < xnovf && nreg + i < kCap) put(nreg + i, ov[j]);
+    }
+    for (int i = kOv * kWG + t; i < xnovf; i += kWG)
       if (nreg + i < kCap) put(nreg + i, osrc[i]);
     if (m) atomicAdd(&s_m, m);
   }
