@@ -97,10 +97,15 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(const SgdTensor* __rest
                                                          const SgdChunk* __restrict__ chunks,
                                                          const float* __restrict__ partial,
                                                          float clip, float momentum, float lr,
-                                                         const float* __restrict__ lr_dev) {
+                                                         const float* __restrict__ lr_dev,
+                                                         int rev) {
   __shared__ float scale_s;
   if (lr_dev) lr = *lr_dev;  // (a captured graph's step: the LR lives on the device)
-  const SgdChunk c = chunks[blockIdx.x];
+  // rev: chunks in reverse order, so that the operands the sum-of-squares pass
+  // read last come first (tuning "sgd_rev", off: no MALL reuse measured,
+  // 151-157 us per step either way, profiles/r5_sgd_rev_ab.log); each chunk's
+  // arithmetic is the same either way
+  const SgdChunk c = chunks[rev ? gridDim.x - 1 - blockIdx.x : blockIdx.x];
   const SgdTensor t = tensors[c.tensor];
   if (threadIdx.x == 0) {
     float ss = 0.f;
@@ -175,7 +180,8 @@ extern "C" int d2mi_momentum_sgd_ex(const void* tensor_table, const void* chunk_
     D2MI_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(sgd_update_kernel, dim3(num_chunks), dim3(256), 0, st, t, c, partial,
-                     clip_norm, momentum, lr, lr_dev);
+                     clip_norm, momentum, lr, lr_dev,
+                     clip_norm > 0.f && tuning(kTuneSgdRev) != 0 ? 1 : 0);  // (tuning "sgd_rev")
   D2MI_LAUNCH_CHECK();
   return 0;
 }
