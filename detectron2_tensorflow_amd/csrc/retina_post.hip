@@ -834,6 +834,41 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 // workgroups per image (one candidate per thread): position = own rank +
 // earlier levels' scores >= s + later levels' scores > s (the concat
 // position breaks ties).  ord[image][position] = level * topk + rank.
+// The merged position of candidate r (r-th of the concatenated level counts)
+// and its level * topk + rank, from the per-level sorted scores sc.
+__device__ __forceinline__ void rank_of(int r, const float* sc, const int* cnt, const int* cum,
+                                        int L, int topk, int& pos, int& val) {
+  int l = 0;
+  while (l + 1 < L && cum[l + 1] <= r) ++l;
+  const int j = r - cum[l];
+  const float sv = sc[l * topk + j];
+  int lo[D2MI_MAX_LEVELS], hi[D2MI_MAX_LEVELS];
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+    lo[m] = 0;
+    hi[m] = (m < L && m != l) ? cnt[m] : 0;
+  }
+  // every level's search advances each step: D2MI_MAX_LEVELS probes in flight
+  for (int step = 0; step < 14; ++step) {
+    float pv[D2MI_MAX_LEVELS];
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m)
+      pv[m] = m < L ? sc[m * topk + min((lo[m] + hi[m]) >> 1, topk - 1)] : 0.f;
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+      if (lo[m] < hi[m]) {
+        const int mid = (lo[m] + hi[m]) >> 1;
+        if (m < l ? pv[m] >= sv : pv[m] > sv) lo[m] = mid + 1;
+        else hi[m] = mid;
+      }
+    }
+  }
+  pos = j;
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) pos += lo[m];
+  val = l * topk + j;
+}
+
 constexpr int kRankT = 256;
 __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
     RetinaGeo g, int topk, const float* __restrict__ cscore, const int32_t* __restrict__ lvl_cnt,
@@ -870,35 +905,9 @@ __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
   __syncthreads();
   const int r = blockIdx.x * kRankT + t;
   if (r >= cum[L]) return;
-  int l = 0;
-  while (l + 1 < L && cum[l + 1] <= r) ++l;
-  const int j = r - cum[l];
-  const float sv = sc[l * topk + j];
-  int lo[D2MI_MAX_LEVELS], hi[D2MI_MAX_LEVELS];
-#pragma unroll
-  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
-    lo[m] = 0;
-    hi[m] = (m < L && m != l) ? cnt[m] : 0;
-  }
-  // every level's search advances each step: D2MI_MAX_LEVELS probes in flight
-  for (int step = 0; step < 14; ++step) {
-    float pv[D2MI_MAX_LEVELS];
-#pragma unroll
-    for (int m = 0; m < D2MI_MAX_LEVELS; ++m)
-      pv[m] = m < L ? sc[m * topk + min((lo[m] + hi[m]) >> 1, topk - 1)] : 0.f;
-#pragma unroll
-    for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
-      if (lo[m] < hi[m]) {
-        const int mid = (lo[m] + hi[m]) >> 1;
-        if (m < l ? pv[m] >= sv : pv[m] > sv) lo[m] = mid + 1;
-        else hi[m] = mid;
-      }
-    }
-  }
-  int pos = j;
-#pragma unroll
-  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) pos += lo[m];
-  ord[o0 + pos] = (uint16_t)(l * topk + j);
+  int pos, val;
+  rank_of(r, sc, cnt, cum, L, topk, pos, val);
+  ord[o0 + pos] = (uint16_t)val;
 }
 
 __global__ __launch_bounds__(kWG) void retina_nms_kernel(
@@ -906,7 +915,7 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
     const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
     const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
     SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
-    int32_t* __restrict__ oc, uint8_t* __restrict__ ov) {
+    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
   extern __shared__ float4 dyn[];
   const uint64_t t_start = stamp(), c_start = cycles();
   const int n = blockIdx.x, t = threadIdx.x;
@@ -922,16 +931,39 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
   int32_t* kept_cl = reinterpret_cast<int32_t*>(kept_sc + max_det);
   float* wsc = reinterpret_cast<float*>(kept_cl + max_det);
   int32_t* wcl = reinterpret_cast<int32_t*>(wsc + kWG);
+  // inl_rank: the merge rank of the level lists in this workgroup (no rank
+  // launch): the image's scores and its order in LDS after the window arrays
+  float* rsc = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(wcl + kWG) + 15) &
+                                        ~(uintptr_t)15);  // (float4 stores; 16 B of slack)
+  uint16_t* lord = reinterpret_cast<uint16_t*>(rsc + capimg);
   __shared__ uint64_t diag[kTile], wsup[kWG / 64];
   __shared__ int s_total, s_nk;
+  __shared__ int rcnt[D2MI_MAX_LEVELS], rcum[D2MI_MAX_LEVELS + 1];
   const size_t o0 = (size_t)n * capimg;
   if (t == 0) {
     int acc = 0;
-    for (int l = 0; l < L; ++l) acc += lvl_cnt[n * L + l];
+    for (int l = 0; l < L; ++l) {
+      rcnt[l] = lvl_cnt[n * L + l];
+      rcum[l] = acc;
+      acc += rcnt[l];
+    }
+    rcum[L] = acc;
     s_total = acc;
     s_nk = 0;
   }
+  if (inl_rank) {
+    const float4* src = reinterpret_cast<const float4*>(cscore + o0);  // capimg % 4 == 0
+    for (int q4 = t; 4 * q4 < capimg; q4 += kWG) reinterpret_cast<float4*>(rsc)[q4] = src[q4];
+  }
   __syncthreads();
+  if (inl_rank) {
+    for (int r = t; r < s_total; r += kWG) {
+      int pos, val;
+      rank_of(r, rsc, rcnt, rcum, L, topk, pos, val);
+      lord[pos] = (uint16_t)val;
+    }
+    __syncthreads();
+  }
   const uint64_t t_ranked = stamp(), c_ranked = cycles();
   const int total = s_total;
   const float off1 = from_orderable(maxc[n]) + 1.f;
@@ -940,7 +972,7 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
     // window: the next 1,024 candidates in score order
     const int wn = min(kWG, total - w0);
     if (t < wn) {
-      const int q = ord[o0 + w0 + t];
+      const int q = inl_rank ? (int)lord[w0 + t] : (int)ord[o0 + w0 + t];
       const float4 c = cbox[o0 + q];
       const int cl = ccls[o0 + q];
       const float off = (float)cl * off1;
@@ -1120,13 +1152,20 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                      o.cscore, o.cbox, o.ccls, o.lvl_cnt, o.maxc, error_word());
   D2MI_LAUNCH_CHECK();
   const int capimg = L * k;
-  hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
-                     (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);
-  D2MI_LAUNCH_CHECK();
-  const size_t lds = (size_t)(max_det + kWG) * (2 * sizeof(float4) + sizeof(float) + sizeof(int32_t));
+  // (tuning "retina_rank": 1 = the merge rank inside the NMS workgroup, 0 = its own launch;
+  // measured: 165.6 vs 124.4 us per call -- one CU's LDS binary searches over ~4.7 k
+  // candidates cost far more than the launch they save, profiles/r5_retina_post_ab_rank*.log)
+  const int inl = tuning(kTuneRetinaRank) != 0 ? 1 : 0;
+  if (!inl) {
+    hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
+                       (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);
+    D2MI_LAUNCH_CHECK();
+  }
+  const size_t lds = (size_t)(max_det + kWG) * (2 * sizeof(float4) + sizeof(float) + sizeof(int32_t)) +
+                     (inl ? 16 + (size_t)capimg * (sizeof(float) + sizeof(uint16_t)) : 0);
   hipLaunchKernelGGL(retina_nms_kernel, dim3(N), dim3(kWG), lds, st, g, k, o.cscore, o.cbox,
                      o.ccls, o.lvl_cnt, o.ord, o.maxc, nms_thresh, max_det, o.info,
-                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid);
+                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

@@ -571,7 +571,7 @@ def _retina_logits(rng, shape, dist):
     return x.astype(F32)
 
 
-@pytest.mark.parametrize("path", ["fused", "fused_exact_select", "unfused"])
+@pytest.mark.parametrize("path", ["fused", "fused_exact_select", "fused_rank_inline", "unfused"])
 @pytest.mark.parametrize("dist", ["normal", "quantized", "saturated", "sparse"])
 def test_retinanet_inference_vs_oracle(dev, dist, path):
     """Dense top-k + decode + NMS vs the oracle.  The distributions drive the
@@ -579,15 +579,20 @@ def test_retinanet_inference_vs_oracle(dev, dist, path):
     and the exact select it falls back to (saturated: the tie group of
     sigmoid == 1 overflows the candidate buffer).  ``path``: the four-launch
     pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
-    its in-workgroup exact select forced on every level (2), and the unfused
-    top-k / sort / mask NMS pipeline (0)."""
+    its in-workgroup exact select forced on every level (2), the same with the
+    merge rank inside the NMS workgroup (tuning "retina_rank" = 1; default: its
+    own launch), and the unfused top-k / sort / mask NMS pipeline (0)."""
     from detectron2_tensorflow_amd.layers import ops as lops
     old = lops.get_tuning("retina_fused")
-    lops.set_tuning("retina_fused", {"fused": 1, "fused_exact_select": 2, "unfused": 0}[path])
+    old_rank = lops.get_tuning("retina_rank")
+    lops.set_tuning("retina_fused", {"fused": 1, "fused_exact_select": 2, "fused_rank_inline": 1,
+                                     "unfused": 0}[path])
+    lops.set_tuning("retina_rank", 1 if path == "fused_rank_inline" else 0)
     try:
         _retinanet_inference_vs_oracle(dev, dist)
     finally:
         lops.set_tuning("retina_fused", old)
+        lops.set_tuning("retina_rank", old_rank)
 
 
 def _retinanet_inference_vs_oracle(dev, dist):
