@@ -61,7 +61,20 @@ const char* d2mi_last_error(void);
  *   "conv_stream"  streaming short-K 1x1 conv (r5) for stride-1 1x1 launches
  *                  of at least this many output pixels; 0 = off;
  *   "roi_bwd_rec"  ROIAlign backward pixel pass over run records (r5, 1) or
- *                  the r4 slot pass (0). */
+ *                  the r4 slot pass (0); 2 / 3 / 5 other pixel x record shapes;
+ *   "retina_fused" RetinaNet post-processing in five launches (1), the same
+ *                  with the exact select forced (2), the unfused pipeline (0);
+ *   "rpn_merge"    RPN proposals' level merge by merge rank (1) or the one-
+ *                  workgroup bitonic sort (0);
+ *   "nms_scan"     fixed-point NMS tile resolve when T <= 64 tiles (1);
+ *   "roi_heavy"    ROIAlign backward: pixels with >= N runs go first (16);
+ *   "rpn_compact"  RPN decode compacts the valid boxes before NMS (1);
+ *   "conv_stream_nt" streaming 1x1's output stores non-temporal (2);
+ *   "conv_nt"      tiled conv final stores non-temporal (0);
+ *   "conv_tail_mink" fewest k-steps whose tail tiles are split along K (8);
+ *   "conv_ws_mintiles" fewest 256x128 tiles that go to the WS conv (0);
+ *   "sgd_rev"      SGD update over its chunks in reverse order (0);
+ *   "retina_rank"  RetinaNet merge rank inside the NMS workgroup (0). */
 int d2mi_set_tuning(const char* key, int value);
 /* Current value of a d2mi_set_tuning key (INT32_MIN for an unknown key). */
 int d2mi_get_tuning(const char* key);
