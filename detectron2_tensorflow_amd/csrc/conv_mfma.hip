@@ -1246,6 +1246,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
+#pragma unroll 4
     for (int s = 0; s < a.splits; ++s) acc += a.partial[(size_t)s * total + i];
     const int ml = (int)(i / a.Cout), co = (int)(i - (int64_t)ml * a.Cout);
     const int m = a.m_base + ml;
@@ -1294,6 +1295,7 @@ __global__ void splitk_reduce_levels_kernel(ConvArgs a) {
        e += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / C4), c = (int)(e - (int64_t)r * C4) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
     for (int sp = 0; sp < a.splits; ++sp) {
       const float4 v = *reinterpret_cast<const float4*>(a.partial + ((size_t)sp * rows + r) * a.Cout + c);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;

@@ -242,6 +242,7 @@ __global__ void wgrad_reduce4_kernel(const float4* __restrict__ partial, int spl
     } else {
       const size_t c = i - total4;
       float s = 0.f;
+#pragma unroll 8  // (loads in flight; the sum stays in split order)
       for (int k = 0; k < splits; ++k) s += pbias[(size_t)k * Cout + c];
       dbias[c] = accum ? dbias[c] + s : s;
     }
@@ -255,11 +256,13 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ partial, int split
        i += (size_t)gridDim.x * blockDim.x) {
     if (i < total) {
       float s = 0.f;
+#pragma unroll 4
       for (int k = 0; k < splits; ++k) s += partial[(size_t)k * total + i];
       dw[i] = accum ? dw[i] + s : s;
     } else if (dbias) {
       const size_t c = i - total;
       float s = 0.f;
+#pragma unroll 8  // (loads in flight; the sum stays in split order)
       for (int k = 0; k < splits; ++k) s += pbias[(size_t)k * Cout + c];
       dbias[c] = accum ? dbias[c] + s : s;
     }

@@ -210,6 +210,7 @@ __global__ __launch_bounds__(256) void wgrad_skinny_reduce_kernel(
   const int k0 = sg * per, k1 = min(chunks, k0 + per);
   float s = 0.f;
   if (o < n)
+#pragma unroll 8  // (loads in flight; the sum stays in chunk order)
     for (int k = k0; k < k1; ++k) s += partial[(size_t)k * n + o];
   red[sg][ol] = s;
   __syncthreads();
@@ -244,6 +245,7 @@ __global__ __launch_bounds__(256) void wgrad_skinny_reduce_levels_kernel(
     const int k0 = sg * per, k1 = min(chunks, k0 + per);
     float s = 0.f;
     if (o < n)
+#pragma unroll 8  // (loads in flight; the sum stays in chunk order)
       for (int k = k0; k < k1; ++k) s += part[(size_t)k * n + o];
     __syncthreads();  // (the previous level's red reads are done)
     red[sg][ol] = s;
