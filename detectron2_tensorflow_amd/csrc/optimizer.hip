@@ -109,8 +109,10 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(const SgdTensor* __rest
   const SgdTensor t = tensors[c.tensor];
   if (threadIdx.x == 0) {
     float ss = 0.f;
-    if (clip > 0.f)
+    if (clip > 0.f) {
+#pragma unroll 8  // (loads in flight; the sum stays in chunk order)
       for (int k = 0; k < t.num_chunks; ++k) ss += partial[t.first_chunk + k];
+    }
     // tf.clip_by_norm: l2norm = sqrt(sum) (0 when sum == 0); t * clip / max(l2norm, clip)
     const float nrm = ss > 0.f ? sqrtf(ss) : 0.f;
     scale_s = clip > 0.f ? fmaxf(nrm, clip) : 0.f;  // divisor; 0 = no clipping
