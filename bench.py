@@ -35,11 +35,6 @@ import os
 import sys
 import time
 
-# before the HIP runtime starts: the hipGraph-replayed step (--graphs) needs
-# the runtime's graph packet capture off (engine/graphed.py); eager steps
-# launch no graphs
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

@@ -31,6 +31,8 @@ _SIGS = {
     "d2mi_last_error": (c_char_p, []),
     "d2mi_error_word_dev": (c_void_p, []),
     "d2mi_clear_errors": (c_int, [P]),
+    "d2mi_graph_census": (c_int, [P, P, c_int]),
+    "d2mi_capture_census": (c_int, [P, P, c_int]),
     "d2mi_roi_align_fwd": (c_int, [P, P, P, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     "d2mi_roi_align_bwd_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int, c_int, c_int]),

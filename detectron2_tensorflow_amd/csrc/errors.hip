@@ -131,6 +131,57 @@ int d2mi_get_tuning(const char* key) {
 
 int32_t* d2mi_error_word_dev(void) { return d2mi::error_word(); }
 
+// Node census of a captured (not yet instantiated) hipGraph: counts[t] = the
+// number of nodes of hipGraphNodeType t, for t < ntypes.  The graphed
+// training step (engine/graphed.py) refuses a capture holding memset nodes
+// while the runtime's graph packet capture is on: those are the nodes whose
+// order against the kernels around them it does not keep (r5).
+int d2mi_graph_census(void* graph, long long* counts, int ntypes) {
+  D2MI_REQUIRE(graph != nullptr && counts != nullptr && ntypes > 0, "bad graph census arguments");
+  for (int t = 0; t < ntypes; ++t) counts[t] = 0;
+  size_t n = 0;
+  D2MI_REQUIRE(hipGraphGetNodes((hipGraph_t)graph, nullptr, &n) == hipSuccess,
+               "hipGraphGetNodes failed");
+  if (n == 0) return 0;
+  hipGraphNode_t* nodes = (hipGraphNode_t*)malloc(n * sizeof(hipGraphNode_t));
+  D2MI_REQUIRE(nodes != nullptr, "out of host memory");
+  int rc = 0;
+  if (hipGraphGetNodes((hipGraph_t)graph, nodes, &n) != hipSuccess) {
+    d2mi::set_error("hipGraphGetNodes failed");
+    rc = -1;
+  }
+  for (size_t i = 0; rc == 0 && i < n; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) {
+      d2mi::set_error("hipGraphNodeGetType failed");
+      rc = -1;
+    } else if ((int)t >= 0 && (int)t < ntypes) {
+      ++counts[(int)t];
+    }
+  }
+  free(nodes);
+  return rc;
+}
+
+// The same census of the graph a stream is capturing into right now (a
+// diagnosis: tools/graph_nodes.py runs it after every op of a capture to name
+// the ops that add memset / memcpy nodes).  Returns 1 when the stream is not
+// capturing (counts all 0).
+int d2mi_capture_census(void* stream, long long* counts, int ntypes) {
+  D2MI_REQUIRE(counts != nullptr && ntypes > 0, "bad capture census arguments");
+  for (int t = 0; t < ntypes; ++t) counts[t] = 0;
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  D2MI_REQUIRE(hipStreamGetCaptureInfo_v2(d2mi::as_stream(stream), &status, &id, &graph, &deps,
+                                          &ndeps) == hipSuccess,
+               "hipStreamGetCaptureInfo_v2 failed");
+  if (status != hipStreamCaptureStatusActive || graph == nullptr) return 1;
+  return d2mi_graph_census((void*)graph, counts, ntypes);
+}
+
 int d2mi_clear_errors(void* stream) {
   int32_t* w = d2mi::error_word();
   D2MI_REQUIRE(w != nullptr, "cannot resolve the device error word");

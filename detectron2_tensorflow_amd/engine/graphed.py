@@ -15,10 +15,20 @@ of the r4 failures were found and fixed:
   zeroed per-GT best IoU (an atomic max) and torch's global-reduction
   semaphores (the box head's bias gradient) kept a previous replay's values
   (tools/graph_diff.py: eager-exact with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0,
-  divergent with it on).  The library now fills with kernels instead of
-  hipMemsetAsync, and the graphed step requires
-  DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before the HIP runtime
-  starts (torch's own memsets remain in the graphs).
+  divergent with it on).
+
+r6 made the captures memset-free instead of turning the runtime's packet
+capture off: the library fills with kernels (d2mi::fill_bytes), and the one
+torch op that still issued a memset -- the reduction behind the box head's
+fc2 / predictor bias gradients, whose cross-block semaphores torch zeroes
+with hipMemsetAsync -- is the library's fixed-order column sum
+(layers/wrappers.py: _LinearBiasFn).  Every capture is censused before it
+is instantiated (d2mi_graph_census; ``census``): 0 memset nodes in A and in
+every B[R] (tools/graph_nodes.py names any op that adds one), and a capture
+that holds one is refused while packet capture is on.  With the runtime's
+defaults the replays are bit-identical to the eager step at 256x320 and at
+the bench's 1333x800 (tests/test_gpu_graphed.py), and the bench runs the
+same with packet capture on or off (profiles/r6b_bench_pkt_*.json).
 
 The eager ``Trainer.step`` enqueues ~550 launches per iteration from Python
 (autograd engine, custom Functions, ctypes): on an MI355X that host work is
@@ -59,6 +69,44 @@ from ..utils import capture, host_sync
 from .trainer import Trainer
 
 
+NODE_KINDS = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",
+              "event_record", "ext_signal", "ext_wait", "mem_alloc", "mem_free",
+              "memcpy_from_symbol", "memcpy_to_symbol", "batch_mem_op")
+
+
+def _census_dict(counts):
+    return {NODE_KINDS[i]: int(c) for i, c in enumerate(counts) if c}
+
+
+def graph_census(g):
+    """{node kind: count} of a captured ``torch.cuda.CUDAGraph(keep_graph=True)``
+    that is not instantiated yet (d2mi_graph_census)."""
+    import ctypes
+    from .. import _C
+    counts = (ctypes.c_longlong * len(NODE_KINDS))()
+    _C.check(_C.lib().d2mi_graph_census(ctypes.c_void_p(g.raw_cuda_graph()), counts,
+                                        len(NODE_KINDS)), "d2mi_graph_census")
+    return _census_dict(counts)
+
+
+def capture_census(device=None):
+    """The same census of the graph the current stream is capturing into
+    (None when it is not capturing; d2mi_capture_census)."""
+    import ctypes
+    from .. import _C
+    counts = (ctypes.c_longlong * len(NODE_KINDS))()
+    rc = _C.lib().d2mi_capture_census(_C.stream_of(device), counts, len(NODE_KINDS))
+    _C.check(min(rc, 0), "d2mi_capture_census")
+    return None if rc == 1 else _census_dict(counts)
+
+
+def packet_capture_on():
+    """Whether the HIP runtime pre-records captured kernels as AQL packets
+    (its default; DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 read at runtime start
+    turns it off)."""
+    return os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1") not in ("0", "false", "False")
+
+
 def _flatten(tree, prefix=()):
     """(path, tensor) leaves of a nested dict of tensors, in key order."""
     out = []
@@ -84,12 +132,6 @@ class GraphedTrainer(Trainer):
 
     def __init__(self, cfg, model, warmup=1, experimental=False, **kwargs):
         """experimental: accepted for the r4 call sites (no longer needed)."""
-        if os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
-            raise RuntimeError(
-                "GraphedTrainer needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before "
-                "the HIP runtime starts: with the runtime's graph packet capture on, memset "
-                "nodes are not ordered against the kernels around them and replays diverge "
-                "(see engine/graphed.py)")
         super().__init__(cfg, model, **kwargs)
         # >= 1: the first eager step makes the per-shape caches, workspaces and
         # the optimizer / fold tables, none of which may be created in a capture
@@ -113,6 +155,9 @@ class GraphedTrainer(Trainer):
         self._stream = None
         self.captures = 0
         self.replays = 0
+        # node kinds of every capture ("A", "B<rows>" -> {kind: count}),
+        # checked before the graph is instantiated (_finish)
+        self.census = {}
         # a directory: every captured graph is written there as a DOT file
         # (hipGraphDebugDotPrint; tools/graph_dump.py) -- a diagnosis that
         # replays nothing
@@ -164,10 +209,26 @@ class GraphedTrainer(Trainer):
 
     # ---------------------------------------------------------------- capture
     def _new_graph(self):
-        g = torch.cuda.CUDAGraph()
+        # keep_graph: the captured hipGraph stays readable until _finish has
+        # taken its node census and instantiated it
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         if self.debug_dump_dir:
             g.enable_debug_mode()
         return g
+
+    def _finish(self, g, name):
+        """Census the capture's nodes, refuse memset nodes while the HIP
+        runtime's graph packet capture is on, instantiate."""
+        census = graph_census(g)
+        self.census[name] = census
+        if census.get("memset", 0) and packet_capture_on():
+            raise RuntimeError(
+                f"graphed step: capture {name} holds {census['memset']} memset node(s) and the "
+                "HIP runtime's graph packet capture is on (DEBUG_CLR_GRAPH_PACKET_CAPTURE is "
+                "not 0): their order against the kernels around them is not kept, and replays "
+                "diverge from the eager step (r5).  tools/graph_nodes.py names the ops that "
+                "issue them")
+        g.instantiate()
 
     def _dump(self, g, name):
         if self.debug_dump_dir:
@@ -203,6 +264,7 @@ class GraphedTrainer(Trainer):
                 if isinstance(v, DeferredMaskLoss):
                     self._count_host.copy_(v.count.reshape(1).to(torch.int64), non_blocking=True)
         self._dump(g, "A")
+        self._finish(g, "A")
         self._keep = []
         capture.flush(self._keep)
         deferred = [v for v in losses.values() if isinstance(v, DeferredMaskLoss)]
@@ -247,6 +309,7 @@ class GraphedTrainer(Trainer):
         capture.flush(keep)
         values = vals
         self._dump(g, f"B{rows}")
+        self._finish(g, f"B{rows}")
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
         self._B[rows] = (g, values, keys, keep)

@@ -45,6 +45,33 @@ class _LinearMFMAFn(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+class _LinearBiasFn(torch.autograd.Function):
+    """torch.addmm(b, x, w) whose backward forms the bias gradient with the
+    library's fixed-order column sum (d2mi_column_sum) instead of torch's
+    reduction: the weight / input gradients are autograd's own addmm formulas
+    (hipBLASLt), but torch's sum over 1,024 rows zeroes its cross-block
+    semaphores with a memset, and a memset node inside the graphed step's
+    capture is not ordered against the kernels around it while the HIP
+    runtime's graph packet capture is on (engine/graphed.py)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = gy.mm(w.t())
+        if ctx.needs_input_grad[1]:
+            gw = x.t().mm(gy)
+        if ctx.needs_input_grad[2]:
+            gb = ops.column_sum(gy)
+        return gx, gw, gb
+
+
 @add_arg_scope
 class Linear(Layer):
     """x @ weights + bias with weights [in_units, out_units] (TF Dense layout).
@@ -83,6 +110,8 @@ class Linear(Layer):
         K, N = self.weights.shape
         if x.is_cuda and K >= self.MFMA_MIN_K and K % 4 == 0 and x.shape[0] > 0:
             ret = _LinearMFMAFn.apply(x.contiguous(), self.weights, self.bias, self._packed())
+        elif self.bias is not None and x.is_cuda and torch.is_grad_enabled():
+            ret = _LinearBiasFn.apply(x, self.weights, self.bias)
         elif self.bias is not None:
             ret = torch.addmm(self.bias, x, self.weights)
         else:

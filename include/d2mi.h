@@ -82,6 +82,15 @@ int d2mi_get_tuning(const char* key);
  * 2 = NMS segment longer than its declared capacity, 4 = top-k capacity. */
 int32_t* d2mi_error_word_dev(void);
 int d2mi_clear_errors(void* stream);
+/* Node census of a captured, not yet instantiated hipGraph (hipGraph_t as
+ * void*): counts[t] = nodes of hipGraphNodeType t for t < ntypes (0 kernel,
+ * 1 memcpy, 2 memset, ...).  No reference counterpart: the graphed training
+ * step (engine/graphed.py, replacing the loop of lib/engine/trainer.py:173-199)
+ * checks its captures with it. */
+int d2mi_graph_census(void* graph, long long* counts, int ntypes);
+/* The same census of the graph `stream` is capturing into now; returns 1
+ * (counts 0) when the stream is not capturing.  A diagnosis (tools/). */
+int d2mi_capture_census(void* stream, long long* counts, int ntypes);
 
 /* -------------------------------------------------------------- ROIAlign
  * Multi-level ROIAlign / crop_and_resize, one launch for all levels.

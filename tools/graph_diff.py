@@ -9,9 +9,6 @@ import argparse
 import os
 import sys
 
-# before the HIP runtime starts: the graphed step needs the runtime's graph
-# packet capture off (engine/graphed.py); nothing else launches graphs
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 import torch
 
