@@ -89,8 +89,9 @@ def parse():
                    help="inference mask output (SEGMENTATION_OUTPUT.FORMAT)")
     p.add_argument("--bucket-mb", type=int, default=32, help="all-reduce bucket size (train)")
     p.add_argument("--graphs", type=int, default=1,
-                   help="train: replay the step from hipGraphs (engine/graphed.py; world size 1 "
-                        "-- other world sizes run the eager step); 0 = the eager Trainer.step")
+                   help="train: replay the step from hipGraphs (engine/graphed.py; at world "
+                        "size > 1 the all-reduces run between the backward and update graphs); "
+                        "0 = the eager Trainer.step")
     p.add_argument("--fixed-rows-steps", type=int, default=10,
                    help="train (default run): after the main timed region, also time this many "
                         "steps with the fixed 256-row mask branch (a second object in the "
@@ -657,7 +658,9 @@ def main():
         if args.mask_fixed_rows and getattr(model, "roi_heads", None) is not None:
             model.roi_heads.mask_compact_rows = False
             PMC_SKIP.update({"roi_align_fwd_mask", "roi_align_bwd"})
-        if args.graphs and world == 1:
+        if args.graphs:
+            # any world size (r6): at world > 1 the bucketed all-reduces run
+            # between the replayed backward graph and the update graph
             from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
             trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         else:

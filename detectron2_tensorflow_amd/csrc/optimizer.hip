@@ -86,6 +86,22 @@ __global__ __launch_bounds__(256) void sgd_sumsq_kernel(const SgdTensor* __restr
         s += g.w * g.w;
       }
       i0 = c.begin + 4 * n4;
+    } else {
+      // operands not 16-B aligned (a gradient that is a view into an
+      // all-reduce bucket, engine/reducer.py): scalar loads, but the float4
+      // body's summation order -- thread k adds elements 4k .. 4k+3 in turn --
+      // so the norm, and the clip factor, do not depend on the alignment
+      const long long n4 = (c.end - c.begin) / 4;
+      for (long long k = threadIdx.x; k < n4; k += blockDim.x) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long long i = c.begin + 4 * k + u;
+          float g = t.g ? t.g[i] : 0.f;
+          if (t.wd != 0.f) g = g + t.wd * t.w[i];
+          s += g * g;
+        }
+      }
+      i0 = c.begin + 4 * n4;
     }
     for (long long i = i0 + threadIdx.x; i < c.end; i += blockDim.x) s += sq_term(t, i);
   }

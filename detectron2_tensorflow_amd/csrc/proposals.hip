@@ -217,7 +217,8 @@ __global__ __launch_bounds__(1024) void rpn_merge_kernel(
 // asc): an entry's position = its own position + the earlier levels' entries
 // whose key is not above its own + the later levels' entries strictly above
 // it -- the desc_key(score, l * post + t) order of rpn_merge_kernel, scores
-// compared as orderable words (-0 < +0, as the key).  Many workgroups per
+// compared as orderable words (-0.0 and +0.0 share one word, so they tie and
+// the concat position decides, as TF compares values).  Many workgroups per
 // image (one entry per thread, every list's score words in LDS) instead of
 // one workgroup's bitonic sort of up to 8,192 keys (61 us per training step).
 constexpr int kMergeT = 256;

@@ -509,7 +509,11 @@ __global__ __launch_bounds__(kRankT) void topk_rank_kernel(
 #pragma unroll
     for (int v = 0; v < kRankW; ++v) rank += part[v * 64 + lane];
     if ((int)rank < kk) {
-      vals_out[(size_t)s * kmax + rank] = from_orderable(~(uint32_t)(mine >> 32));
+      // the value itself, from the candidate's raw bits (not rebuilt from the
+      // key: orderable() gives -0.0 the key of +0.0, and TF's top_k returns
+      // a -0.0 input as -0.0)
+      const float v = key_value(__uint_as_float((uint32_t)(A[i] >> 32)), key_mode);
+      vals_out[(size_t)s * kmax + rank] = v;
       idx_out[(size_t)s * kmax + rank] = (int32_t)(uint32_t)mine;
     }
   }

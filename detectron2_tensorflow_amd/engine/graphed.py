@@ -42,7 +42,7 @@ step.  Here the same step is captured into hipGraphs once and replayed:
 * graph B[R], one per possible mask-branch row count R (a multiple of 32:
   8 graphs for 2 images x 128 foreground slots, all captured right after
   A): the mask branch forward + loss, the total loss, the whole backward (through graph A's retained autograd graph), the all-reduce
-  (world size 1: none) and the fused Momentum-SGD update with the LR read
+  (world size 1: none; see below) and the fused Momentum-SGD update with the LR read
   from the device (``d2mi_momentum_sgd_ex``).
 
 A step is then: copy the batch into the captured input tensors (when the
@@ -58,7 +58,13 @@ freed temporaries.  The caches keyed on parameter versions (folded /
 packed weights) are made stale before A is captured, so A re-folds and
 re-packs every trainable layer at each replay; nothing bumps a version while
 the graphs are in use, and an eager step (``eager_step``) marks them stale
-again first.  A multi-rank job runs the eager step (see __init__).
+again first.
+
+Data parallel (r6): with the bucketed all-reduce active (world > 1) B[R]
+ends after the backward and its bucket copies; the host launches the
+buckets' all-reduces right after launching B[R] (engine/reducer.py, capture
+form), and a last graph U (the update over the reduced buckets) replays
+after them.
 """
 import os
 
@@ -137,12 +143,15 @@ class GraphedTrainer(Trainer):
         # the optimizer / fold tables, none of which may be created in a capture
         self.warmup = max(1, int(warmup))
         self.heads = [m for m in model.modules() if isinstance(m, StandardROIHeads)]
-        # world size 1 only: capturing the bucketed all-reduce was tried over
-        # RCCL at world size 1 and fails (the process group's watchdog queries
-        # the events of collectives recorded inside the capture); gloo cannot
-        # be captured at all.  A multi-rank job runs the eager step.
-        self.enabled = (next(model.parameters()).is_cuda and self.world == 1
-                        and not self.reducer.active)
+        # any world size (r6): the collectives stay outside the graphs.
+        # Capturing the bucketed all-reduce itself fails over RCCL (the
+        # process group's watchdog queries the events of collectives recorded
+        # inside a capture) and gloo cannot be captured at all, so with the
+        # reducer active B[R] ends after the backward's bucket copies, the
+        # host launches the all-reduces after it (engine/reducer.py, capture
+        # form), and one more graph, U, holds the update.
+        self.enabled = next(model.parameters()).is_cuda
+        self._U = None
         self._eager = 0
         self._pool = None
         self._A = None
@@ -302,17 +311,40 @@ class GraphedTrainer(Trainer):
                 seed = self._seed = torch.ones_like(total)
             # retain graph A's autograd graph: a later row count is captured
             # by another backward through it
+            dp = self.reducer.active
+            if dp:
+                self.reducer.begin_capture()
             total.backward(seed, retain_graph=True)
             self.reducer.finish()
-            self.optimizer.step_captured(self._lr_dev)
+            events = self.reducer.end_capture() if dp else None
+            if not dp:
+                self.optimizer.step_captured(self._lr_dev)
             vals.copy_(torch.stack([t.detach() for t in self._loss_terms(out)] + [total.detach()]))
         capture.flush(keep)
         values = vals
         self._dump(g, f"B{rows}")
         self._finish(g, f"B{rows}")
+        if dp and self._U is None:
+            self._capture_update(dev)
         self.optimizer.zero_grad()
         keys = list(out) + ["total_loss"]
-        self._B[rows] = (g, values, keys, keep)
+        self._B[rows] = (g, values, keys, keep, events)
+        self.captures += 1
+
+    def _capture_update(self, dev):
+        """Graph U (reducer active): the fused Momentum-SGD update over the
+        gradients as views of the all-reduced buckets -- the same pointers
+        after every B[R], so one graph serves them all."""
+        keep = []
+        g = self._new_graph()
+        capture.begin(dev)
+        with torch.cuda.graph(g, pool=self._pool, stream=self._stream,
+                              capture_error_mode="thread_local"):
+            self.optimizer.step_captured(self._lr_dev)
+        capture.flush(keep)
+        self._dump(g, "U")
+        self._finish(g, "U")
+        self._U = (g, keep)
         self.captures += 1
 
     # ------------------------------------------------------------------- step
@@ -342,8 +374,14 @@ class GraphedTrainer(Trainer):
             rows = self._deferred.rows_for(nfg)
             for h in self.heads:
                 h.last_mask_rows = rows
-        g, values, keys, _ = self._B[rows]
+        g, values, keys, _, events = self._B[rows]
         g.replay()
+        if events is not None:
+            # the buckets' all-reduces after the replayed backward, then the
+            # update after the last
+            self.reducer.launch_captured(events)
+            self.reducer.wait_captured()
+            self._U[0].replay()
         self.replays += 1
         self.iter += 1
         # (a copy: the next replay rewrites ``values``)

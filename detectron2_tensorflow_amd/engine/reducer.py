@@ -35,6 +35,19 @@ collective), and the end of backward (the compute stream at ``finish()``);
 end of backward, the all-reduce time the backward did NOT hide
 (``exposed_ms``) and the collectives' busy time (reference semantics: the
 clones' gradient sum of model_deploy.py:408-438 happens after the backward).
+
+Graph-replayed steps (engine/graphed.py, r6).  A collective cannot sit
+inside a captured hipGraph here (RCCL inside a capture trips the process
+group's watchdog; gloo cannot be captured at all), so the reducer has a
+capture form: while ``captured`` is set, the hooks' bucket copies are
+captured with the backward but no collective is launched, and ``finish()``
+only points the gradients at the buckets.  At replay the host launches the
+backward graph, then every bucket's all-reduce in order on the side stream
+after it (``launch_captured``), and ``wait_captured`` orders the update
+graph after the last one.  The collectives therefore follow the replayed
+backward instead of overlapping it (the eager hooks overlap them): an
+external event-record node per bucket would restore the overlap, but torch
+refuses external events on ROCm ("External events are disallowed in rocm").
 """
 import torch
 import torch.distributed as dist
@@ -56,6 +69,9 @@ class BucketedAllReduce:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.active = self.world > 1 or (always and dist.is_initialized())
         self.timing = False
+        # capture form (engine/graphed.py): ready buckets record events
+        self.captured = False
+        self._events = None
         self._tl = None
         self.params = [p for p in params if p.requires_grad]
         # partition in registration order starting from the tail bucket (at
@@ -117,6 +133,11 @@ class BucketedAllReduce:
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
             b = self.buckets[self._next]
+            if self.captured:
+                # (the replay launches this bucket's all-reduce: launch_captured)
+                self._events.append(self._next)
+                self._next += 1
+                continue
             tl = self._tl
             if tl is not None:
                 ev = torch.cuda.Event(enable_timing=True)
@@ -140,9 +161,60 @@ class BucketedAllReduce:
             st = self._side = torch.cuda.Stream(device=device)
         return st
 
+    def begin_capture(self):
+        """Arm the capture form for the backward about to be captured."""
+        if self._flat_missing():
+            raise RuntimeError("reducer: the buckets must exist before a capture (run an eager "
+                               "step first)")
+        self.reset()
+        self.captured = True
+        self._events = []
+
+    def end_capture(self):
+        """The buckets completed in the capture just finished, in order."""
+        events, self._events, self.captured = self._events, None, False
+        if len(events) != len(self.buckets):
+            raise RuntimeError(f"reducer: {len(events)} of {len(self.buckets)} buckets became "
+                               "ready in the capture")
+        return events
+
+    def _flat_missing(self):
+        return any(b.flat is None for b in self.buckets)
+
+    def launch_captured(self, events):
+        """At a replay, after the captured backward was launched (on the
+        current stream): every bucket's all-reduce, in order, on the side
+        stream after it."""
+        side = self._side_stream(self.buckets[0].flat.device)
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            for bi in events:
+                b = self.buckets[bi]
+                b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+
+    def wait_captured(self):
+        """The current stream waits for every bucket's all-reduce."""
+        for b in self.buckets:
+            b.work.wait()
+            b.work = None
+
     def finish(self):
-        """Wait for every bucket and expose the averaged gradients as .grad."""
+        """Wait for every bucket and expose the averaged gradients as .grad.
+        In the capture form: no wait (the replay launches the collectives,
+        launch_captured); the gradients become views of the buckets."""
         if not self.active:
+            return
+        if self.captured:
+            for b in self.buckets:
+                if b.pending:
+                    for p, off in zip(b.params, b.offsets):
+                        if p.grad is None:
+                            b.flat[off: off + p.numel()].zero_()
+                    b.pending = 0
+            self._launch_ready()
+            for b in self.buckets:
+                for p, off in zip(b.params, b.offsets):
+                    p.grad = b.flat[off: off + p.numel()].view_as(p)
             return
         if self._tl is not None:
             ev = torch.cuda.Event(enable_timing=True)

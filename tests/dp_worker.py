@@ -13,7 +13,13 @@ ranks used), averaged as the reducer does (g * 1/world, summed), one
 Momentum-SGD update -- model_deploy.py:203-205's mean of the per-clone
 losses -- and saves those parameter vectors too.
 
-    python tests/dp_worker.py <outdir>      (RANK / WORLD_SIZE / MASTER_* in env)
+    python tests/dp_worker.py <outdir> [eager|graphed]   (RANK / WORLD_SIZE / MASTER_* in env)
+
+"graphed" (r6): each rank also trains a second replica of the same model
+with engine/graphed.py's GraphedTrainer on the same batches, right after the
+eager step -- step 0 its eager warm-up, then graph A + B[R] + the update
+graph U replayed, the bucketed all-reduces launched between B[R] and U
+(engine/reducer.py, capture form) -- for 3 steps.
 """
 import os
 import sys
@@ -25,7 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 CATS = {"num_thing_classes": 80, "num_stuff_classes": 53, "stuff_ignore_value": 0}
-STEPS = 2
+STEPS = {"eager": 2, "graphed": 3}
 
 
 def build(cfg, dev, calib_batch):
@@ -52,7 +58,7 @@ def flat(model):
     return torch.cat([p.detach().reshape(-1) for p in model.parameters() if p.requires_grad]).cpu()
 
 
-def main(out):
+def main(out, arm="eager"):
     from detectron2_tensorflow_amd import _C
     from detectron2_tensorflow_amd.config import finalize, get_cfg
     from detectron2_tensorflow_amd.engine import Trainer
@@ -70,14 +76,30 @@ def main(out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     calib = batch_of(0, dev)
     model = build(cfg, dev, calib)
+    steps = STEPS[arm]
     trainer = Trainer(cfg, model)  # broadcasts rank 0's weights
+    if arm == "graphed":
+        # a second replica of the same model, trained by GraphedTrainer on the
+        # same batches right after the eager one each step: bit-identical to it
+        from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
+        model_g = build(cfg, dev, calib)
+        graphed = GraphedTrainer(cfg, model_g, warmup=1)
+        assert graphed.enabled and graphed.reducer.active
     mine = batch_of(rank, dev)
-    for s in range(STEPS):
+    for s in range(steps):
         torch.cuda.manual_seed(seed(s, rank))
         losses = trainer.step(mine)
         rows = getattr(model.roi_heads, "last_mask_rows", None)
-        torch.save({"params": flat(model), "losses": {k: float(v) for k, v in losses.items()},
-                    "mask_rows": rows}, os.path.join(out, f"rank{rank}_step{s}.pt"))
+        rec = {"params": flat(model), "losses": {k: float(v) for k, v in losses.items()},
+               "mask_rows": rows}
+        if arm == "graphed":
+            torch.cuda.manual_seed(seed(s, rank))
+            lg = graphed.step(mine)
+            rec.update(graphed_params=flat(model_g),
+                       graphed_losses={k: float(v) for k, v in lg.items()},
+                       graphed_rows=model_g.roi_heads.last_mask_rows,
+                       replays=graphed.replays, census=graphed.census)
+        torch.save(rec, os.path.join(out, f"rank{rank}_step{s}.pt"))
     _C.raise_on_errors(dev)
     dist.barrier()
     dist.destroy_process_group()
@@ -90,7 +112,7 @@ def main(out):
                       clip_norm=cfg.SOLVER.CLIP_GRADIENTS_BY_NORM)
     lr = build_learning_rate(cfg)
     batches = [batch_of(r, dev) for r in range(world)]
-    for s in range(STEPS):
+    for s in range(steps):
         acc = None
         for r, b in enumerate(batches):
             opt.zero_grad()
@@ -107,4 +129,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:3])

@@ -2,12 +2,14 @@
 
 A child process (never an exec of the test process) initialises
 torch.distributed with the "nccl" backend (RCCL on ROCm) at world size 1 on
-cuda:0 and trains Mask R-CNN R50-FPN at 256x320 for 2 Trainer.steps with the
+cuda:0 and trains Mask R-CNN R50-FPN at 256x320 for 3 Trainer.steps with the
 bucketed all-reduce FORCED on (Trainer(reducer_always=True): the
 post-accumulate-grad hooks, the flat buckets, one RCCL all-reduce per bucket
 on the communicator's stream, finish()'s waits and .grad views), the second
-step with the per-bucket timing events.  It then replays the same 2 steps
-on a second model built from the same seed without the reducer.  An
+step with the per-bucket timing events.  It then replays the same 3 steps
+on a second model built from the same seed without the reducer, and (r6) on
+a third with GraphedTrainer and the RCCL reducer (graph replays, the
+all-reduces launched on the replay's bucket events).  An
 all-reduce of one rank is exact (x * 1.0, summed once), so the two parameter
 vectors must be bit-identical.  Writes <outdir>/rccl.pt.
 
@@ -24,7 +26,7 @@ import torch.distributed as dist  # noqa: E402
 
 from dp_worker import CATS, batch_of, build, flat  # noqa: E402
 
-STEPS = 2
+STEPS = 3
 
 
 def main(out):
@@ -45,10 +47,18 @@ def main(out):
     calib = batch_of(0, dev)
     batch = batch_of(0, dev)
     res = {"backend": backend}
-    for arm in ("rccl", "plain"):
+    from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
+    for arm in ("rccl", "plain", "rccl_graphed"):
         model = build(cfg, dev, calib)
-        trainer = Trainer(cfg, model, bucket_bytes=8 << 20, reducer_always=(arm == "rccl"))
-        assert trainer.reducer.active == (arm == "rccl")
+        if arm == "rccl_graphed":
+            # r6: the graphed step with the RCCL reducer: B[R] records the
+            # buckets' ready events, the host launches the all-reduces on them,
+            # the update graph U replays after (engine/graphed.py)
+            trainer = GraphedTrainer(cfg, model, warmup=1, bucket_bytes=8 << 20,
+                                     reducer_always=True)
+        else:
+            trainer = Trainer(cfg, model, bucket_bytes=8 << 20, reducer_always=(arm == "rccl"))
+        assert trainer.reducer.active == (arm != "plain")
         for s in range(STEPS):
             torch.cuda.manual_seed(1000 * s)
             trainer.reducer.timing = arm == "rccl" and s == STEPS - 1
@@ -59,6 +69,9 @@ def main(out):
         if arm == "rccl":
             res["timeline"] = trainer.reducer.timeline()
             res["buckets"] = len(trainer.reducer.buckets)
+        if arm == "rccl_graphed":
+            res["replays"] = trainer.replays
+            res["census"] = trainer.census
     _C.raise_on_errors(dev)
     dist.destroy_process_group()
     torch.save(res, os.path.join(out, "rccl.pt"))

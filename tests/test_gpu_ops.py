@@ -377,8 +377,11 @@ def test_nms_large_segment_uses_radix_sort_path(dev, n, tied):
 # --------------------------------------------------------------------- top-k
 def test_topk_segments_vs_oracle(dev):
     rng = np.random.default_rng(12)
-    lens = [1, 10, 999, 5000, 9000, 201600, 300000, 300001, 1 << 20]
+    lens = [1, 10, 999, 5000, 9000, 201600, 300000, 300001, 1 << 20, 3001]
     vals = [rng.normal(size=n).astype(F32) for n in lens]
+    # signed zeros: -0.0 ties +0.0 (the index decides) and comes back as -0.0
+    vals[9] = np.round(vals[9] * 0.6).astype(F32)
+    vals[9][(vals[9] == 0) & (rng.uniform(size=lens[9]) < 0.5)] = -0.0
     vals[3] = np.round(vals[3], 1)           # heavy ties
     vals[4][:] = 0.5                          # all tied: ordered-ties path
     vals[6] = np.round(vals[6] * 4) / 4       # ties straddling the threshold bin
@@ -409,7 +412,8 @@ def test_topk_segments_vs_oracle(dev):
                         np.testing.assert_array_equal(i[s, : c[s]], wi)
                 else:
                     np.testing.assert_array_equal(i[s, : c[s]], wi)
-                    np.testing.assert_array_equal(v[s, : c[s]], wv)
+                    np.testing.assert_array_equal(v[s, : c[s]].view(np.int32),
+                                                  np.asarray(wv, F32).view(np.int32))
 
 
 # ------------------------------------------------------------ anchors/deltas
@@ -484,6 +488,9 @@ def _rpn_proposals_vs_oracle(dev, pre, post, min_size, strides, hw, cells, logit
                                      torch.from_numpy(image_hw).to(dev), pre, post, 0.7, min_size)
     np.testing.assert_array_equal(gv.cpu().numpy(), wv)
     np.testing.assert_array_equal(gs.cpu().numpy(), ws)
+    # bit for bit: a -0.0 logit stays a -0.0 score (TF's top_k returns the
+    # input value; assert_array_equal alone treats the two zeros as equal)
+    np.testing.assert_array_equal(gs.cpu().numpy().view(np.int32), ws.astype(F32).view(np.int32))
     assert_boxes_close(gb.cpu().numpy(), wb)
 
 
@@ -707,6 +714,12 @@ def test_conv2d_split_bf16_products_are_f32_class(dev, shape):
     ((2, 40, 52, 64, 256), "r"), ((2, 40, 52, 64, 256), "plain"), ((1, 37, 41, 64, 96), "g"),
     ((2, 33, 40, 128, 512), "gr"), ((2, 33, 40, 128, 128), "plain"), ((1, 29, 31, 128, 192), "r"),
     ((2, 20, 24, 256, 1024), "gr"), ((2, 20, 24, 256, 256), "g"), ((1, 21, 23, 256, 64), "plain"),
+    # K = 256 at >= 32 k pixels into 64 / 512 channels: the stream kernel's
+    # K = 256 variant ON BY DEFAULT (stream1x1_variant: stream256_shape), whose
+    # tiled fallback keeps its tail tiles' K whole -- the shapes above stay
+    # under 32 k pixels, where both arms run the tiled kernel
+    ((2, 128, 160, 256, 64), "r"), ((2, 128, 160, 256, 64), "g"),
+    ((2, 128, 160, 256, 64), "plain"), ((2, 128, 160, 256, 512), "r"),
 ])
 def test_conv1x1_stream_kernel_matches_tiled_and_float64(dev, shape, form):
     """conv1x1_stream_kernel (r5, tuning "conv_stream": the streaming short-K
@@ -746,6 +759,16 @@ def test_conv1x1_stream_kernel_matches_tiled_and_float64(dev, shape, form):
         ops().set_tuning("conv_stream", old)
     np.testing.assert_allclose(outs[1].double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
     assert torch.equal(outs[0], outs[1])
+    if Cin == 256 and N * H * W >= 32768:
+        # and with the stream kernel forced (tuning < 0: every eligible launch
+        # of >= -value pixels), whatever the default selection rule says
+        try:
+            ops().set_tuning("conv_stream", -32768)
+            forced = ops().conv2d_nhwc(x.to(dev), wp, b.to(dev), 1, (0, 0), math_mode="split",
+                                       **kw).cpu()
+        finally:
+            ops().set_tuning("conv_stream", old)
+        assert torch.equal(forced, outs[0])
 
 
 def test_split_bf16x3_is_exact(dev):

@@ -268,6 +268,40 @@ def test_fused_momentum_sgd_matches_foreach_reference(dev):
         torch.testing.assert_close(b.cpu(), a, rtol=1e-5, atol=1e-6)
 
 
+def test_fused_momentum_sgd_unaligned_gradients_are_bit_identical(dev):
+    """Gradients that are views into one flat buffer at offsets that are not
+    16-B aligned (the all-reduce buckets of engine/reducer.py) give the same
+    clipped update, bit for bit, as separate aligned gradients: the norm's
+    scalar fallback sums in the float4 body's order (r6: the one-rank RCCL
+    test drifted by 4e-9 once a third step clipped)."""
+    from detectron2_tensorflow_amd.solver import MomentumSGD
+    g = torch.Generator().manual_seed(3)
+    shapes = [(7,), (3, 3, 64, 64), (1024, 300), (5,), (2, 2, 128, 520)]
+    w0 = [torch.randn(s, generator=g).to(dev) for s in shapes]
+    arms = {}
+    for arm in ("aligned", "views"):
+        ps = [w.clone() for w in w0]
+        opt = MomentumSGD([{"params": ps[:3], "weight_decay": 1e-4},
+                           {"params": ps[3:], "weight_decay": 0.0}], 0.9, 10.0)
+        for step in range(3):
+            gs = [torch.randn(s, generator=torch.Generator().manual_seed(10 * step + i)) * 3.0
+                  for i, s in enumerate(shapes)]
+            if arm == "aligned":
+                for p, gr in zip(ps, gs):
+                    p.grad = gr.to(dev)
+            else:
+                flat = torch.cat([gr.reshape(-1) for gr in gs]).to(dev)
+                off = 0
+                for p, gr in zip(ps, gs):
+                    p.grad = flat[off: off + gr.numel()].view_as(p)
+                    off += gr.numel()
+                assert any(p.grad.data_ptr() % 16 for p in ps)
+            opt.step(0.02)
+        arms[arm] = (ps, opt.accum)
+    for a, b in zip(arms["aligned"][0] + arms["aligned"][1], arms["views"][0] + arms["views"][1]):
+        assert torch.equal(a, b)
+
+
 def test_fused_momentum_sgd_bumps_parameter_versions(dev):
     """Weight caches (packed conv weights, the fused RPN 1x1) key on the
     parameters' version counters: the fused update must bump them."""
