@@ -60,6 +60,8 @@ MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32
 # (MI355X_MICROARCH.md: ~2.5 PF dense BF16)
 MFMA_SPLIT_PEAK_TFLOPS = round(2500.0 / 6, 1)
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
+# MI355X_MICROARCH.md: I8 MFMA (32x32x32) at 2x the BF16 rate per clock
+MFMA_I8_PEAK_TOPS = 2 * 2500.0
 
 
 def parse():
@@ -273,9 +275,19 @@ def kernel_report(summary, mode="infer", extras=None):
                 r.update(achieved=round(gbs, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
                          frac=round(gbs / HBM_PEAK_GBPS, 4))
             rep[name] = r
+    if "solo_matrix_nms" in summary:
+        # int8 MFMA intersections (r6): 2 N^2 HW ops per image
+        n, ms, ops_ = summary["solo_matrix_nms"]
+        ach = ops_ / (ms * 1e-3) / 1e12
+        rep["solo_matrix_nms"] = {"bound": "mfma", "achieved": round(ach, 1),
+                                  "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
+                                  "frac": round(ach / MFMA_I8_PEAK_TOPS, 4),
+                                  "ops_model": "2*k^2*Hm*Wm per image (SURVEY 8d D4)",
+                                  "launches": n, "avg_us": round(ms * 1e3 / n, 2),
+                                  "algorithmic_per_launch": ops_ / n}
     for name in ("roi_align_fwd", "roi_align_fwd_mask", "roi_align_bwd", "retinanet_postprocess",
                  "solo_mask_stats",
-                 "solo_matrix_nms", "solo_paste"):
+                 "solo_matrix_nms_popcount", "solo_paste"):
         if name not in summary:
             continue
         n, ms, byts = summary[name]

@@ -53,7 +53,7 @@ enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi 
                kTuneRoiBwdRec = 11, kTuneRetinaFused = 12, kTuneRpnMerge = 13, kTuneNmsScan = 14, kTuneRoiHeavy = 15,
                kTuneRpnCompact = 16, kTuneConvStreamNt = 17, kTuneConvNt = 18,
                kTuneConvTailMinK = 19, kTuneConvWSMinTiles = 20,
-               kTuneSgdRev = 21, kTuneRetinaRank = 22,
+               kTuneSgdRev = 21, kTuneRetinaRank = 22, kTuneSoloMfma = 23,
                kTuneCount };
 int tuning(TuneKey k);
 

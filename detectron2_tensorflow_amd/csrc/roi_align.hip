@@ -1325,6 +1325,11 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   // layout share an L2), the mask pooler (32 ROIs x 14x14) 19.7 -> 18.9-19.6
   int tv = tuning(kTuneRoiFwd);
   if (tv < 0) tv = 2 | 4 | 8 | (R >= 256 ? 1 : 0);
+  // r6, bit 16: ONE wave iteration per wave -- a workgroup takes 4 x U bins,
+  // so every wave issues all of its corner loads in one round (the bins'
+  // loads no longer wait on the previous bins' round trips); bit 32: U = 8
+  const int U = (tv & 32) ? 8 : (tv & 1) ? 2 : 4;
+  if (tv & 16) a.bpb = 4 * U;
   const int nby = (nbins + a.bpb - 1) / a.bpb;
   if (tv & 2) a.bpb = (nbins + nby - 1) / nby;
   a.xcd_remap = (tv & 8) ? 1 : 0;
@@ -1332,6 +1337,8 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   hipStream_t st = as_stream(stream);
   if (!vec4)
     hipLaunchKernelGGL((roi_align_fwd_kernel<false>), grid, dim3(256), 0, st, a);
+  else if (U == 8)
+    hipLaunchKernelGGL((roi_align_fwd_kernel<true, 8, true>), grid, dim3(256), 0, st, a);
   else if ((tv & 5) == 0)
     hipLaunchKernelGGL((roi_align_fwd_kernel<true, 4, false>), grid, dim3(256), 0, st, a);
   else if ((tv & 5) == 1)

@@ -402,6 +402,231 @@ __global__ __launch_bounds__(256) void solo_inter_kernel(const uint64_t* __restr
     }
 }
 
+// r6: the same counts on the int8 MFMA (v_mfma_i32_32x32x32_i8: exact i32
+// accumulation of 0/1 products).  One wave owns a 64 x 64 output tile of an
+// upper-triangle tile pair (ti <= tj) over a slice of the pixel words (2 x 2
+// MFMA tiles of 32 x 32); a k-step is 32 pixels.  Lane l (row r = l & 31,
+// half h = l >> 5) expands bits 16h .. 16h+15 of its row's 32-pixel chunk to
+// 16 bytes of 0 / 1 for both operands: the A and B fragments use the same
+// lane / element -> k assignment, so every product pairs one pixel of row i
+// with the SAME pixel of row j and the sum over the 32 is popcount(a & b),
+// whatever the hardware's k order inside the step.
+//
+// The wave's 128 rows (64 A, 64 B) come in chunks of 16 words (1,024
+// pixels, one 128-B line per row): 32 coalesced 8-B loads per lane (4 whole
+// lines per instruction) land in registers while the previous chunk is
+// multiplied out of the wave's LDS image (rows padded to 136 B: the 32 rows a
+// read touches fall on distinct banks), then go to LDS.  Partials per pixel
+// slice go to a workspace slab (ints: summed exactly in the reduce launch).
+constexpr int kIT = 64;                        // output tile side per wave
+constexpr int kIWords = 16;                    // pixel words per chunk
+constexpr int kIRowB = kIWords * 8 + 8;        // LDS bytes per row (padded)
+constexpr int kIWaveB = 2 * kIT * kIRowB;      // LDS bytes per wave
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// 16 bits -> 16 bytes of 0 / 1 (bit b -> byte b): per nibble x,
+// x * (1 + 2^7 + 2^14 + 2^21) puts bit i at bit 8i with no carries.
+__device__ __forceinline__ v4i expand16(uint32_t x) {
+  v4i r;
+  r[0] = (int)(__umul24(x & 0xFu, 0x204081u) & 0x01010101u);
+  r[1] = (int)(__umul24((x >> 4) & 0xFu, 0x204081u) & 0x01010101u);
+  r[2] = (int)(__umul24((x >> 8) & 0xFu, 0x204081u) & 0x01010101u);
+  r[3] = (int)(__umul24((x >> 12) & 0xFu, 0x204081u) & 0x01010101u);
+  return r;
+}
+
+// upper-triangle tile pair u -> (ti, tj), ti <= tj, row-major over ti
+__device__ __forceinline__ void tri_pair(int u, int T, int& ti, int& tj) {
+  int i = 0, left = T;
+  while (u >= left) {
+    u -= left;
+    ++i;
+    --left;
+  }
+  ti = i;
+  tj = i + u;
+}
+
+// Workgroup: kIWaves waves on ONE tile pair, each over its own run of chunks
+// (two waves per SIMD: one wave's expansions beside the other's MFMAs); their
+// accumulators are summed in LDS (integer adds: exact in any order) and one
+// partial tile per workgroup goes to the workspace.
+constexpr int kIWaves = 8;
+
+__global__ __launch_bounds__(64 * kIWaves) void solo_inter_mfma_kernel(
+    const uint64_t* __restrict__ bits, int N, int k, int W64, int T, int groups,
+    int words_per_wave, int32_t* __restrict__ part, float* __restrict__ comp) {
+  extern __shared__ __align__(16) unsigned char ism[];
+  if (blockIdx.x == 0)  // (the reduce launch max-folds the compensation into it)
+    for (int e = threadIdx.x; e < N * k; e += 64 * kIWaves) comp[e] = 0.f;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tri = T * (T + 1) / 2;
+  const int grp = blockIdx.x % groups, u = (blockIdx.x / groups) % tri, n = blockIdx.x / (groups * tri);
+  unsigned char* img = ism + (size_t)wv * kIWaveB;
+  int ti, tj;
+  tri_pair(u, T, ti, tj);
+  const int r = lane & 31, h = lane >> 5;
+  const uint64_t* base = bits + (size_t)n * k * W64;
+  // load slot q (0..31) of a chunk: image row 4q + (lane >> 4), word lane & 15
+  // (image rows 0..63 = A rows ti * 64 + ..., 64..127 = B rows tj * 64 + ...)
+  const int lw = lane & 15;
+  const int slice = grp * kIWaves + wv;
+  const int w0 = min(W64, slice * words_per_wave), w1 = min(W64, w0 + words_per_wave);
+  auto src_of = [&](int q) -> const uint64_t* {
+    const int ir = 4 * q + (lane >> 4);
+    const int row = (ir < kIT ? ti * kIT + ir : tj * kIT + ir - kIT);
+    return row < k ? base + (size_t)row * W64 : nullptr;
+  };
+  v16i acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0;
+  uint64_t pre[32];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const uint64_t* p = src_of(q);
+      const int w = c0 + lw;
+      pre[q] = (p != nullptr && w < w1) ? p[w] : 0ull;
+    }
+  };
+  load_chunk(w0);
+  for (int c0 = w0; c0 < w1; c0 += kIWords) {
+    // the chunk's words into the wave's image, then the next chunk's loads
+#pragma unroll
+    for (int q = 0; q < 32; ++q)
+      *reinterpret_cast<uint64_t*>(img + (size_t)(4 * q + (lane >> 4)) * kIRowB + 8 * lw) = pre[q];
+    __builtin_amdgcn_wave_barrier();
+    if (c0 + kIWords < w1) load_chunk(c0 + kIWords);
+    const int nks = min(kIWords, w1 - c0) * 2;  // 32-pixel k-steps in this chunk
+#pragma unroll 2
+    for (int ks = 0; ks < nks; ks += 2) {
+      uint64_t d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)  // rows r, 32 + r (A), 64 + r, 96 + r (B)
+        d[q] = *reinterpret_cast<const uint64_t*>(img + (size_t)(32 * q + r) * kIRowB + 4 * ks);
+#pragma unroll
+      for (int half32 = 0; half32 < 2; ++half32) {
+        v4i fr[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          fr[q] = expand16((uint32_t)(d[q] >> (32 * half32 + 16 * h)) & 0xFFFFu);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[a], fr[2 + b], acc[a][b], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // the waves' tiles summed in LDS (the staging images are free now), then
+  // stored row-major.  C / D layout (dtype-independent on gfx950):
+  // col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+  int32_t* red = reinterpret_cast<int32_t*>(ism);
+  __syncthreads();
+  for (int e = threadIdx.x; e < kIT * kIT; e += 64 * kIWaves) red[e] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h, col = 32 * b + r;
+        atomicAdd(&red[row * kIT + col], acc[a][b][e]);
+      }
+  __syncthreads();
+  int32_t* out = part + (((size_t)grp * N + n) * tri + u) * (kIT * kIT);
+  for (int e = threadIdx.x; e < kIT * kIT; e += 64 * kIWaves) out[e] = red[e];
+}
+
+// The groups' partial tiles summed (ints: exact in any order) into the IoU
+// matrix TRANSPOSED, iouT[n][j][i] = iou(i, j) of solo_iou below (0 unless
+// i < j and the classes match), so that the compensation / decay passes read
+// rows.  A workgroup takes 16 columns j of one (image, tile pair): the
+// partials are read row-major (coalesced), transposed through LDS and stored
+// as rows of iouT; a pair ti < tj also zeroes its mirror (i > j).
+constexpr int kRedCols = 16;
+__global__ __launch_bounds__(256) void solo_inter_reduce_kernel(
+    const int32_t* __restrict__ part, int N, int k, int T, int groups,
+    const float* __restrict__ sums, const int64_t* __restrict__ cls, float* __restrict__ iouT,
+    float* __restrict__ comp) {
+  __shared__ float tile[kRedCols][kIT + 1];
+  const int tri = T * (T + 1) / 2;
+  const int cb = blockIdx.x % (kIT / kRedCols);
+  const int u = (blockIdx.x / (kIT / kRedCols)) % tri, n = blockIdx.x / ((kIT / kRedCols) * tri);
+  int ti, tj;
+  tri_pair(u, T, ti, tj);
+  const size_t per = (size_t)N * tri * kIT * kIT;
+  const size_t at0 = ((size_t)n * tri + u) * (kIT * kIT);
+  const float* sn = sums + (size_t)n * k;
+  const int64_t* cn = cls + (size_t)n * k;
+  for (int e = threadIdx.x; e < kIT * kRedCols; e += 256) {
+    const int ii = e / kRedCols, jj = cb * kRedCols + e % kRedCols;  // part row i, column j
+    const int i = ti * kIT + ii, j = tj * kIT + jj;
+    float v = 0.f;
+    if (i < j && j < k && cn[i] == cn[j]) {
+      int it = 0;
+      for (int q = 0; q < groups; ++q) it += part[(size_t)q * per + at0 + (size_t)ii * kIT + jj];
+      const float fit = (float)it;
+      const float uni = (sn[j] + sn[i]) - fit;  // sum_matrix + sum_matrix^T - inter
+      v = fit / uni;
+    }
+    tile[jj - cb * kRedCols][ii] = v;
+  }
+  __syncthreads();
+  // comp[j] = max_i iou(i, j) (the reference's column max, nms.py:66-69): this
+  // block's part of row j of iouT, folded in with an integer atomicMax on the
+  // IoU's bits (IoU >= 0: the bit patterns order as the values; exact in any
+  // order).  One wave per four rows of the block's 16.
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int jl = wv; jl < kRedCols; jl += 4) {
+      float mx = tile[jl][lane];
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      const int j = tj * kIT + cb * kRedCols + jl;
+      if (lane == 0 && j < k && mx > 0.f)
+        atomicMax(reinterpret_cast<int*>(comp) + (size_t)n * k + j, __float_as_int(mx));
+    }
+  }
+  for (int e = threadIdx.x; e < kIT * kRedCols; e += 256) {
+    const int jl = e / kIT, ii = e % kIT, jj = cb * kRedCols + jl;
+    const int i = ti * kIT + ii, j = tj * kIT + jj;
+    if (i < k && j < k) iouT[((size_t)n * k + j) * k + i] = tile[jl][ii];
+    // the mirror (rows j' of tile ti, columns i' of tile tj: i' > j')
+    const int i2 = tj * kIT + ii, j2 = ti * kIT + jj;
+    if (ti < tj && i2 < k && j2 < k) iouT[((size_t)n * k + j2) * k + i2] = 0.f;
+  }
+}
+
+// out[j] = scores[j] * min_i decay(iou[i][j], comp[i]) over row j of iouT:
+// one wave per (row, image); the decay formula of solo_decay_kernel
+__global__ __launch_bounds__(256) void solo_decay_rows_kernel(
+    const float* __restrict__ iouT, const float* __restrict__ comp,
+    const float* __restrict__ scores, int N, int k, int kernel, float sigma,
+    float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N * k) return;
+  const int n = row / k;
+  const float* p = iouT + (size_t)row * k;
+  const float* cp = comp + (size_t)n * k;
+  const float ns = -1.f * sigma;
+  float mn = INFINITY;
+  for (int i = lane; i < k; i += 64) {
+    const float v = p[i], ci = cp[i];
+    const float d = kernel == 0 ? expf(ns * (v * v - ci * ci)) : (1.f - v) / (1.f - ci);
+    mn = fminf(mn, d);
+  }
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
+  if (lane == 0) out[row] = scores[row] * mn;
+}
+
 __device__ __forceinline__ float solo_iou(const int32_t* inter, const float* s, const int64_t* cls,
                                           int k, int i, int j) {
   if (i >= j || cls[i] != cls[j]) return 0.f;  // band part removed, class-specific
@@ -877,10 +1102,24 @@ extern "C" int d2mi_solo_select(const float* probs, const int32_t* live_row,
   return 0;
 }
 
+// workgroups per tile pair of the MFMA intersection: about one per CU over
+// the upper-triangle 64 x 64 tile pairs of all images (each workgroup's
+// kIWaves waves split its pixel words)
+static int solo_mfma_groups(int N, int k, int W64) {
+  const int T = (k + kIT - 1) / kIT, tri = T * (T + 1) / 2;
+  const int want = std::max(1, 256 / std::max(1, N * tri));
+  const int most = std::max(1, (W64 + kIWaves * kIWords - 1) / (kIWaves * kIWords));
+  return std::min(want, most);
+}
+
 extern "C" size_t d2mi_solo_matrix_nms_workspace_size(int N, int k) {
   WorkspaceSizer z;
   z.take<int32_t>((size_t)N * k * k);
   z.take<float>((size_t)N * k);
+  // (the MFMA path's partial tiles, sized for the most groups any P gives)
+  const int T = (k + kIT - 1) / kIT, tri = T * (T + 1) / 2;
+  const int gmax = std::max(1, 256 / std::max(1, N * tri));
+  z.take<int32_t>((size_t)gmax * N * tri * kIT * kIT);
   return z.off;
 }
 
@@ -897,6 +1136,28 @@ extern "C" int d2mi_solo_matrix_nms(const uint64_t* mask_bits, const int64_t* cl
   int32_t* inter = w.take<int32_t>((size_t)N * k * k);
   float* comp = w.take<float>((size_t)N * k);
   D2MI_REQUIRE(w.ok(), "SOLO Matrix-NMS workspace too small (%zu < %zu)", workspace_bytes, w.off);
+  if (tuning(kTuneSoloMfma) != 0) {
+    // (inter's bytes hold the transposed IoU matrix: float, N * k * k)
+    float* iouT = reinterpret_cast<float*>(inter);
+    const int T = (k + kIT - 1) / kIT, tri = T * (T + 1) / 2;
+    const int groups = solo_mfma_groups(N, k, W64);
+    const int slices = groups * kIWaves;
+    const int wpw = ((W64 + slices - 1) / slices + kIWords - 1) / kIWords * kIWords;
+    int32_t* part = w.take<int32_t>((size_t)groups * N * tri * kIT * kIT);
+    D2MI_REQUIRE(w.ok(), "SOLO Matrix-NMS workspace too small (%zu < %zu)", workspace_bytes,
+                 w.off);
+    hipLaunchKernelGGL(solo_inter_mfma_kernel, dim3(N * tri * groups), dim3(64 * kIWaves),
+                       kIWaves * kIWaveB, st, mask_bits, N, k, W64, T, groups, wpw, part, comp);
+    D2MI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(solo_inter_reduce_kernel, dim3(N * tri * (kIT / kRedCols)), dim3(256), 0,
+                       st, part, N, k, T, groups, sum_masks, classes, iouT, comp);
+    D2MI_LAUNCH_CHECK();
+    const unsigned rows_grid = (unsigned)(((size_t)N * k + 3) / 4);
+    hipLaunchKernelGGL(solo_decay_rows_kernel, dim3(rows_grid), dim3(256), 0, st, iouT, comp,
+                       scores, N, k, kernel, sigma, out_scores);
+    D2MI_LAUNCH_CHECK();
+    return 0;
+  } else {
   D2MI_REQUIRE(fill_bytes(inter, sizeof(int32_t) * (size_t)N * k * k, 0, st) == 0, "fill failed");
   const int tiles = (k + kMT - 1) / kMT;
   // word slices: enough workgroups to fill the chip (>= ~4 per CU over the
@@ -908,6 +1169,7 @@ extern "C" int d2mi_solo_matrix_nms(const uint64_t* mask_bits, const int64_t* cl
   hipLaunchKernelGGL(solo_inter_kernel, dim3(tiles, tiles, N * splits), dim3(256), 0, st,
                      mask_bits, k, W64, wps, inter);
   D2MI_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(solo_comp_kernel, dim3(k, N), dim3(256), 0, st, inter, sum_masks, classes, k,
                      comp);
   D2MI_LAUNCH_CHECK();

@@ -1726,9 +1726,14 @@ def solo_inference(cate_logits, kernels, mask_features, strides, out_hw, score_t
     rc = lib.d2mi_solo_matrix_nms(_C.ptr(bits), _C.ptr(top_classes), _C.ptr(top_scores),
                                   _C.ptr(top_sum), N, k, P, 0 if nms_kernel == "gaussian" else 1,
                                   float(nms_sigma), _C.ptr(decayed), _C.ptr(mws), mwsb, st)
-    # algorithmic bytes: the bit-packed masks read once (SURVEY D4 prices the
-    # f32 GEMM at 2 N^2 HW flop; the AND + popcount form is bound by bytes)
-    KernelTimer.stop(ev, "solo_matrix_nms", N * k * W64 * 8)
+    if get_tuning("solo_mfma"):
+        # the int8 MFMA intersections (r6): SURVEY 8d D4's 2 N^2 HW ops per
+        # image (the reference's full M M^T; the kernel forms the upper
+        # triangle) against the I8 MFMA peak
+        KernelTimer.stop(ev, "solo_matrix_nms", 2 * N * k * k * P)
+    else:
+        # the AND + popcount tiles: the bit-packed masks read once (bytes)
+        KernelTimer.stop(ev, "solo_matrix_nms_popcount", N * k * W64 * 8)
     _C.check(rc, "d2mi_solo_matrix_nms")
     OH, OW = int(out_hw[0]), int(out_hw[1])
     out_masks = torch.empty((N, max_detections, OH, OW), dtype=torch.uint8, device=dev)

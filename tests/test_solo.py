@@ -242,9 +242,20 @@ def _assert_tail_equal(got, want, dbg, score_rtol=1e-5, exact_masks=True, proof=
     return nflip
 
 
+@pytest.fixture(params=[1, 0], ids=["mfma", "popcount"])
+def solo_mfma(request):
+    """The Matrix-NMS intersections on the int8 MFMA (tuning "solo_mfma" 1, r6)
+    or the AND + popcount tiles (0)."""
+    from detectron2_tensorflow_amd.layers import ops
+    old = ops.get_tuning("solo_mfma")
+    ops.set_tuning("solo_mfma", request.param)
+    yield request.param
+    ops.set_tuning("solo_mfma", old)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["gaussian", "linear"])
-def test_solo_tail_vs_oracle(dev, kernel):
+def test_solo_tail_vs_oracle(dev, kernel, solo_mfma):
     """ops.solo_inference on random head outputs (2 images, the C5 grids
     40/36/24/16/12, K = 80, D = 256, masks 64x80 -> 256x320)."""
     import solo
@@ -283,7 +294,7 @@ def test_solo_tail_vs_oracle(dev, kernel):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["gaussian", "linear"])
-def test_solo_tail_vs_oracle_c5_geometry(dev, kernel):
+def test_solo_tail_vs_oracle_c5_geometry(dev, kernel, solo_mfma):
     """The tail at the C5 geometry (SOLOv2 R50-FPN at 1333x800 padded to
     800x1344): mask features 200x336 (67,200 pixels), D = 256, the five grids,
     more than 500 candidates per image (the top-k(500) and a 500 x 500 Matrix
@@ -321,7 +332,7 @@ def test_solo_tail_vs_oracle_c5_geometry(dev, kernel):
 
 
 @pytest.mark.gpu
-def test_solo_tail_few_candidates_and_empty(dev):
+def test_solo_tail_few_candidates_and_empty(dev, solo_mfma):
     """Fewer candidates than TOPK_CANDIDATES_TEST (top-k of the valid count,
     zero-mask padding rows in Matrix NMS), and an image with none at all."""
     from detectron2_tensorflow_amd.layers import ops

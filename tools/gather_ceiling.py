@@ -42,6 +42,7 @@ def load_lib():
     lib.gc_copy.argtypes = [P, ctypes.c_longlong, P, P]
     lib.gc_copy_u.argtypes = [P, ctypes.c_longlong, P, I, I, P]
     lib.gc_gather1_u.argtypes = [P, P, I, P, I, I, P]
+    lib.gc_gather_s.argtypes = [P, P, I, I, P, I, I, P]
     return lib
 
 
@@ -141,8 +142,22 @@ def main():
     cb = uniq.numel() * C * 4
     cp_src = src[:uniq.numel()].contiguous()
     cp_out = torch.empty_like(cp_src)
+    def roi_tv(v):
+        def fn():
+            old = ops.get_tuning("roi_fwd")
+            ops.set_tuning("roi_fwd", v)
+            try:
+                run_roi()
+            finally:
+                ops.set_tuning("roi_fwd", old)
+        return fn
+
     arms = {
         "roi_align": run_roi,
+        # r6: one wave iteration per wave (bit 16), U = 4 / 2 / 8 bins in flight
+        "roi_align_1it_u4": roi_tv(2 | 4 | 8 | 16),
+        "roi_align_1it_u2": roi_tv(1 | 2 | 4 | 8 | 16),
+        "roi_align_1it_u8": roi_tv(2 | 4 | 8 | 16 | 32),
         "gather4_u4": lambda: lib.gc_gather4(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(), 4, st),
         "gather4_u2": lambda: lib.gc_gather4(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(), 2, st),
         "gather1_unique": lambda: lib.gc_gather1(src.data_ptr(), uniq.data_ptr(), uniq.numel(),
@@ -168,7 +183,17 @@ def main():
             tot += e0.elapsed_time(e1)
         return tot / a.iters * 1e3
 
+    for v in (2 | 4 | 8 | 16, 1 | 2 | 4 | 8 | 16, 2 | 4 | 8 | 16 | 32):
+        old = ops.get_tuning("roi_fwd")
+        ops.set_tuning("roi_fwd", v)
+        try:
+            yv = run_roi()
+        finally:
+            ops.set_tuning("roi_fwd", old)
+        print(f"roi_fwd variant {v}: output equal to the default's: {bool(torch.equal(yv, y))}",
+              flush=True)
     copy_validation(lib, dev, st)
+    guide_gather(lib, dev, st, uniq, src, C, flush, a.iters)
     t = {k: [] for k in arms}
     for _ in range(a.rounds):
         for k, fn in arms.items():
@@ -181,6 +206,62 @@ def main():
               cb + uniq.numel() * C * 4 if k.startswith("gather1_unique") else ub)
         print(f"{k:18s} {us:8.1f} us  {by / us / 1e3:7.1f} GB/s ({by / us / 1e3 / 8000:.3f} of 8 TB/s)"
               f"  roi_align / this = {med['roi_align'] / us:.3f}", flush=True)
+
+
+def guide_gather(lib, dev, st, uniq, src, C, flush, iters):
+    """r6 (verdict r5 weak #3): the guide's register gather (MI355X_MICROARCH.md
+    'Indexed rows', last paragraph: random whole 1,152-B rows of a buffer far
+    larger than the Infinity Cache, each fetched once, one wave per
+    destination, 4 rows in flight, 16 waves per CU: 5.5-5.6 TB/s) with
+    wave-uniform scalar row indices (gather_s_kernel), then the same kernel on
+    the box pooler's own distinct rows, cold and warm."""
+    rows = 2 << 20  # 2 GiB of 1 KiB rows (8x the 256 MiB Infinity Cache)
+    table = torch.empty(rows * C, device=dev)
+    perm = torch.randperm(rows, device=dev).to(torch.int32)
+    grid = 256 * 4  # 4 workgroups of 4 waves per CU: 16 waves per CU
+    out_sum = torch.empty(rows // 4 + 1, C, device=dev)
+    out_copy = torch.empty(rows, C, device=dev)
+
+    def t_of(fn, cold, n_it):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        fn()
+        for _ in range(n_it):
+            if cold:
+                flush.zero_()
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        return statistics.median(ts)
+
+    for u in (4, 8):
+        for mode in (1, 0):
+            out = out_sum if mode else out_copy
+            us = t_of(lambda: lib.gc_gather_s(table.data_ptr(), perm.data_ptr(), rows, mode,
+                                              out.data_ptr(), u, grid, st), False, 5)
+            rd = rows * C * 4
+            wr = (rows // u if mode else rows) * C * 4
+            print(f"guide gather 2 GiB table, random rows once, U={u} "
+                  f"{'sum (1 row written per U)' if mode else 'copy (every row written)'}: "
+                  f"{us:9.1f} us  read {rd / us / 1e3:7.1f} GB/s  read+write "
+                  f"{(rd + wr) / us / 1e3:7.1f} GB/s", flush=True)
+    del table, out_copy
+    # the pooler's distinct rows (their own addresses in the concatenated levels)
+    n = uniq.numel()
+    shuf = uniq[torch.randperm(n, device=dev)].contiguous()
+    out1 = torch.empty(n, C, device=dev)
+    for order, ids in (("sorted", uniq), ("shuffled", shuf)):
+        for cold in (True, False):
+            for mode in (1, 0):
+                us = t_of(lambda: lib.gc_gather_s(src.data_ptr(), ids.data_ptr(), n, mode,
+                                                  out1.data_ptr(), 4, grid, st), cold, iters)
+                rd = n * C * 4
+                wr = (n // 4 if mode else n) * C * 4
+                print(f"pooler rows ({n}, {rd / 1e6:.1f} MB) {order:8s} {'cold' if cold else 'warm'} "
+                      f"{'sum ' if mode else 'copy'} U=4: {us:8.1f} us  read {rd / us / 1e3:7.1f} GB/s"
+                      f"  read+write {(rd + wr) / us / 1e3:7.1f} GB/s", flush=True)
 
 
 def copy_validation(lib, dev, st, iters=20):
