@@ -94,6 +94,9 @@ def parse():
                    help="train: replay the step from hipGraphs (engine/graphed.py; at world "
                         "size > 1 the all-reduces run between the backward and update graphs); "
                         "0 = the eager Trainer.step")
+    p.add_argument("--wgrad-side", type=int, default=0,
+                   help="train, graphed: the convs' weight gradients captured on a side stream "
+                        "beside their data gradients (1) or on the step's one stream (0)")
     p.add_argument("--fixed-rows-steps", type=int, default=10,
                    help="train (default run): after the main timed region, also time this many "
                         "steps with the fixed 256-row mask branch (a second object in the "
@@ -674,7 +677,8 @@ def main():
             # any world size (r6): at world > 1 the bucketed all-reduces run
             # between the replayed backward graph and the update graph
             from detectron2_tensorflow_amd.engine.graphed import GraphedTrainer
-            trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
+            trainer = GraphedTrainer(cfg, model, bucket_bytes=args.bucket_mb << 20,
+                                     wgrad_side=bool(args.wgrad_side))
         else:
             trainer = Trainer(cfg, model, bucket_bytes=args.bucket_mb << 20)
         step = lambda: trainer.step(batch)
@@ -787,7 +791,9 @@ def main():
                             "kernel_events_on_timed_step": None if args.no_kernel_timing
                             else f"{sample + 1}/{args.steps}",
                             **({"step_launch": (f"hipGraph replays ({trainer.replays} in warmup + "
-                                                "timed; the kernel-timing step eager)")
+                                                "timed; the kernel-timing step eager)"
+                                                + ("; weight gradients on a side stream"
+                                                   if getattr(trainer, "wgrad_side", False) else ""))
                                 if getattr(trainer, "enabled", False) else "eager"}
                                if args.mode == "train" else {}),
                             **({"mask_format": args.mask_format} if args.mode == "infer" else {})},

@@ -159,7 +159,18 @@ constexpr int kMaxBinsPerBlock = 64, kMinBinsPerBlock = 16, kFwdMinBlocks = 2048
 // the L2 the feature maps are being gathered through); XCD: ROI r taken from
 // a bijective XCD-contiguous remap of blockIdx.x (ROIs that neighbour in the
 // sampled layout -- foreground proposals of one GT -- share an XCD's L2).
-template <bool VEC4, int U = 4, bool NT = false>
+template <bool NTL>
+__device__ __forceinline__ float4 ld_row4(const float4* p) {
+  if constexpr (NTL) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+
+template <bool VEC4, int U = 4, bool NT = false, bool NTL = false>
 __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
   int r = blockIdx.x;
   if (a.xcd_remap) {
@@ -199,10 +210,10 @@ __global__ __launch_bounds__(256) void roi_align_fwd_kernel(RoiArgs a) {
         ok[u] = g.ok && ty.valid && tx.valid;
         ly[u] = ty.lerp;
         lx[u] = tx.lerp;
-        c00[u] = p[((size_t)ty.r0 * g.W + tx.r0) * 64 + lane];
-        c01[u] = p[((size_t)ty.r0 * g.W + tx.r1) * 64 + lane];
-        c10[u] = p[((size_t)ty.r1 * g.W + tx.r0) * 64 + lane];
-        c11[u] = p[((size_t)ty.r1 * g.W + tx.r1) * 64 + lane];
+        c00[u] = ld_row4<NTL>(p + ((size_t)ty.r0 * g.W + tx.r0) * 64 + lane);
+        c01[u] = ld_row4<NTL>(p + ((size_t)ty.r0 * g.W + tx.r1) * 64 + lane);
+        c10[u] = ld_row4<NTL>(p + ((size_t)ty.r1 * g.W + tx.r0) * 64 + lane);
+        c11[u] = ld_row4<NTL>(p + ((size_t)ty.r1 * g.W + tx.r1) * 64 + lane);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1337,7 +1348,12 @@ extern "C" int d2mi_roi_align_fwd(const float* const* feats, const int32_t* dims
   hipStream_t st = as_stream(stream);
   if (!vec4)
     hipLaunchKernelGGL((roi_align_fwd_kernel<false>), grid, dim3(256), 0, st, a);
-  else if (U == 8)
+  else if (tv & 64) {  // r6, bit 64: the corner rows loaded non-temporally
+    if (U == 2)
+      hipLaunchKernelGGL((roi_align_fwd_kernel<true, 2, true, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_kernel<true, 4, true, true>), grid, dim3(256), 0, st, a);
+  } else if (U == 8)
     hipLaunchKernelGGL((roi_align_fwd_kernel<true, 8, true>), grid, dim3(256), 0, st, a);
   else if ((tv & 5) == 0)
     hipLaunchKernelGGL((roi_align_fwd_kernel<true, 4, false>), grid, dim3(256), 0, st, a);

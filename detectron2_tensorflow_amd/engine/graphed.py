@@ -70,6 +70,7 @@ import os
 
 import torch
 
+from ..layers import convolutional
 from ..modeling.roi_heads.roi_heads import DeferredMaskLoss, StandardROIHeads
 from ..utils import capture, host_sync
 from .trainer import Trainer
@@ -136,7 +137,7 @@ class GraphedTrainer(Trainer):
     allocator, workspaces, per-shape caches).  Falls back to the eager step when the
     process group has more than one rank."""
 
-    def __init__(self, cfg, model, warmup=1, experimental=False, **kwargs):
+    def __init__(self, cfg, model, warmup=1, experimental=False, wgrad_side=False, **kwargs):
         """experimental: accepted for the r4 call sites (no longer needed)."""
         super().__init__(cfg, model, **kwargs)
         # >= 1: the first eager step makes the per-shape caches, workspaces and
@@ -152,6 +153,13 @@ class GraphedTrainer(Trainer):
         # form), and one more graph, U, holds the update.
         self.enabled = next(model.parameters()).is_cuda
         self._U = None
+        # r6: capture the backward with every conv's weight gradient on a side
+        # stream (layers/convolutional.py WGRAD_STREAM).  Off by default:
+        # bit-identical, but no faster -- 105.3 / 105.8 vs 105.6 / 106.1 img/s
+        # in alternating bench runs (profiles/r6l_bench_wgrad_side_ab.txt): the
+        # warp-specialised convs hold a whole CU each, so the branches contend
+        self.wgrad_side = bool(wgrad_side)
+        self._wgrad_stream = None
         self._eager = 0
         self._pool = None
         self._A = None
@@ -314,7 +322,16 @@ class GraphedTrainer(Trainer):
             dp = self.reducer.active
             if dp:
                 self.reducer.begin_capture()
-            total.backward(seed, retain_graph=True)
+            # the convs' weight gradients on a side stream beside their data
+            # gradients: forked branches of the captured graph (r6)
+            if self.wgrad_side:
+                if self._wgrad_stream is None:
+                    self._wgrad_stream = torch.cuda.Stream(device=dev)
+                convolutional.WGRAD_STREAM["stream"] = self._wgrad_stream
+            try:
+                total.backward(seed, retain_graph=True)
+            finally:
+                convolutional.WGRAD_STREAM.pop("stream", None)
             self.reducer.finish()
             events = self.reducer.end_capture() if dp else None
             if not dp:

@@ -159,6 +159,28 @@ def _wgrad_shared(acc, x, gy, w_shape, stride, pb, pe, want_bias):
     return gw, gb
 
 
+# r6: {"stream": a side stream} while the graphed training step captures its
+# backward (engine/graphed.py): every MFMA conv's weight gradient is issued
+# there, beside its data gradient, so the replayed graph runs the two
+# concurrently (a replayed graph runs forked branches in parallel,
+# tools/graph_parallel_probe.py).  Empty in eager steps: a per-layer stream
+# fork costs host time there (r2 measured +3.7 %), and a replay pays none.
+WGRAD_STREAM = {}
+
+
+def _wgrad_of(ctx, x, gy, w, stride, pb, pe, want_b):
+    """(weight, bias) gradient of _ConvMFMAFn's backward, None where not needed."""
+    gw = gb = None
+    if ctx.needs_input_grad[1] and ctx.wacc is not None:
+        gw, gb = _wgrad_shared(ctx.wacc, x, gy, w.shape, stride, pb, pe, want_b)
+    else:
+        if ctx.needs_input_grad[1]:
+            gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
+        if want_b and gb is None:
+            gb = ops.column_sum(gy)
+    return gw, gb
+
+
 def _gate_eligible(w_shape, stride, pb, pe):
     KH, KW, _, Cout = w_shape
     return KH == KW and Cout % 4 == 0 and stride == 1 and max(pb, pe) <= KH - 1
@@ -231,6 +253,17 @@ class _ConvMFMAFn(torch.autograd.Function):
             handoff.deposit(ctx.res_grad_to, "g", gres, "residual")  # taken by the conv reading it
             gres = None
         gx = gw = gb = None
+        want_b = has_bias and ctx.needs_input_grad[2]
+        side = WGRAD_STREAM.get("stream")
+        main = None
+        if side is not None and ctx.needs_input_grad[1] and gy.is_cuda:
+            # r6: the weight gradient on the side stream, issued BEFORE the
+            # data gradient, so that the two run concurrently (the replayed
+            # graph has both branches); joined at the end of this backward
+            main = torch.cuda.current_stream(gy.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                gw, gb = _wgrad_of(ctx, x, gy, w, stride, pb, pe, want_b)
         if ctx.needs_input_grad[0] and _join_active(ctx):
             gx = _join_backward(ctx, gy, x, w, stride, pb, pe)
         elif ctx.needs_input_grad[0]:
@@ -268,14 +301,13 @@ class _ConvMFMAFn(torch.autograd.Function):
             if deposit:
                 handoff.deposit(pair, "g", gx, "pair")
                 gx = None
-        want_b = has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1] and ctx.wacc is not None:
-            gw, gb = _wgrad_shared(ctx.wacc, x, gy, w.shape, stride, pb, pe, want_b)
+        if main is not None:
+            main.wait_stream(side)
+            for t in (gw, gb):  # (made on the side stream, used on this one)
+                if t is not None:
+                    t.record_stream(main)
         else:
-            if ctx.needs_input_grad[1]:
-                gw, gb = _wgrad(x, gy, w.shape, stride, pb, pe, want_b)
-            if want_b and gb is None:
-                gb = ops.column_sum(gy)
+            gw, gb = _wgrad_of(ctx, x, gy, w, stride, pb, pe, want_b)
         return (gx, gw, gb, None, None, None, None, gtd, gres, None, None, None, None, None, None,
                 None)
 

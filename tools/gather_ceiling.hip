@@ -132,6 +132,61 @@ __global__ __launch_bounds__(256) void gather_s_kernel(const float4* __restrict_
   }
 }
 
+// r6: the ROIAlign forward's own access pattern in the guide's shape: per
+// output bin its 4 corner rows (idx[4b .. 4b+3], wave-uniform scalar loads),
+// U bins (4U rows) in flight per wave, a persistent grid of 16 waves per CU,
+// the rows summed and one output row stored (non-temporal); NTL: the corner
+// rows loaded non-temporally.
+template <int U, bool NTL>
+__global__ __launch_bounds__(256) void gather4_s_kernel(const float4* __restrict__ src,
+                                                        const int32_t* __restrict__ idx, int nbins,
+                                                        float4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int nw = gridDim.x * 4;
+  const nv4* s4 = reinterpret_cast<const nv4*>(src);
+  nv4* o4 = reinterpret_cast<nv4*>(out);
+  for (int b0 = w * U; b0 < nbins; b0 += nw * U) {
+    int row[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        row[u][c] = __builtin_amdgcn_readfirstlane(idx[4 * min(b0 + u, nbins - 1) + c]);
+    nv4 v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const nv4* q = s4 + (size_t)row[u][c] * 64 + lane;
+        v[u][c] = NTL ? __builtin_nontemporal_load(q) : *q;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (b0 + u < nbins)
+        __builtin_nontemporal_store((v[u][0] + v[u][1]) + (v[u][2] + v[u][3]),
+                                    o4 + (size_t)(b0 + u) * 64 + lane);
+  }
+}
+
+extern "C" int gc_gather4_s(const float* src, const int32_t* idx, int nbins, float* out, int u,
+                            int ntl, int grid, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (u == 4 && ntl)
+    hipLaunchKernelGGL((gather4_s_kernel<4, true>), dim3(grid), dim3(256), 0, st,
+                       (const float4*)src, idx, nbins, (float4*)out);
+  else if (u == 4)
+    hipLaunchKernelGGL((gather4_s_kernel<4, false>), dim3(grid), dim3(256), 0, st,
+                       (const float4*)src, idx, nbins, (float4*)out);
+  else if (ntl)
+    hipLaunchKernelGGL((gather4_s_kernel<2, true>), dim3(grid), dim3(256), 0, st,
+                       (const float4*)src, idx, nbins, (float4*)out);
+  else
+    hipLaunchKernelGGL((gather4_s_kernel<2, false>), dim3(grid), dim3(256), 0, st,
+                       (const float4*)src, idx, nbins, (float4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int gc_gather_s(const float* src, const int32_t* idx, int n, int sum, float* out,
                            int u, int grid, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

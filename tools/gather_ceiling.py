@@ -43,6 +43,7 @@ def load_lib():
     lib.gc_copy_u.argtypes = [P, ctypes.c_longlong, P, I, I, P]
     lib.gc_gather1_u.argtypes = [P, P, I, P, I, I, P]
     lib.gc_gather_s.argtypes = [P, P, I, I, P, I, I, P]
+    lib.gc_gather4_s.argtypes = [P, P, I, P, I, I, I, P]
     return lib
 
 
@@ -158,6 +159,18 @@ def main():
         "roi_align_1it_u4": roi_tv(2 | 4 | 8 | 16),
         "roi_align_1it_u2": roi_tv(1 | 2 | 4 | 8 | 16),
         "roi_align_1it_u8": roi_tv(2 | 4 | 8 | 16 | 32),
+        # r6: corner rows loaded non-temporally (bit 64)
+        "roi_align_ntl_u2": roi_tv(1 | 2 | 4 | 8 | 64),
+        "roi_align_ntl_u4": roi_tv(2 | 4 | 8 | 64),
+        "roi_align_ntl_1it_u4": roi_tv(2 | 4 | 8 | 16 | 64),
+        # r6: the forward's 4-corner pattern in the guide's shape (scalar
+        # corner indices, persistent 16 waves per CU), default / nt loads
+        "gather4_s_u2": lambda: lib.gc_gather4_s(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(),
+                                                 2, 0, 1024, st),
+        "gather4_s_u4": lambda: lib.gc_gather4_s(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(),
+                                                 4, 0, 1024, st),
+        "gather4_s_u2_nt": lambda: lib.gc_gather4_s(src.data_ptr(), idx.data_ptr(), nb,
+                                                    out4.data_ptr(), 2, 1, 1024, st),
         "gather4_u4": lambda: lib.gc_gather4(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(), 4, st),
         "gather4_u2": lambda: lib.gc_gather4(src.data_ptr(), idx.data_ptr(), nb, out4.data_ptr(), 2, st),
         "gather1_unique": lambda: lib.gc_gather1(src.data_ptr(), uniq.data_ptr(), uniq.numel(),
@@ -171,11 +184,17 @@ def main():
     }
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)  # > the 256 MiB MALL
 
-    def timeit(fn):
+    def timeit(fn, cold=True):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         tot = 0.0
         for _ in range(a.iters):
-            flush.zero_()  # cold caches, as in the step (the maps were just written by the FPN)
+            if cold:
+                flush.zero_()  # cold caches
+            else:
+                # warm: the maps rewritten just before, as the FPN writes them in
+                # the step (they then sit in the MALL / L2 as far as they fit)
+                for f in feats:
+                    f.add_(0.0)
             e0.record()
             fn()
             e1.record()
@@ -183,7 +202,8 @@ def main():
             tot += e0.elapsed_time(e1)
         return tot / a.iters * 1e3
 
-    for v in (2 | 4 | 8 | 16, 1 | 2 | 4 | 8 | 16, 2 | 4 | 8 | 16 | 32):
+    for v in (2 | 4 | 8 | 16, 1 | 2 | 4 | 8 | 16, 2 | 4 | 8 | 16 | 32, 1 | 2 | 4 | 8 | 64,
+              2 | 4 | 8 | 64, 2 | 4 | 8 | 16 | 64):
         old = ops.get_tuning("roi_fwd")
         ops.set_tuning("roi_fwd", v)
         try:
@@ -195,17 +215,23 @@ def main():
     copy_validation(lib, dev, st)
     guide_gather(lib, dev, st, uniq, src, C, flush, a.iters)
     t = {k: [] for k in arms}
+    tw = {k: [] for k in arms}
     for _ in range(a.rounds):
         for k, fn in arms.items():
             t[k].append(timeit(fn))
+            tw[k].append(timeit(fn, cold=False))
     med = {k: statistics.median(v) for k, v in t.items()}
+    medw = {k: statistics.median(v) for k, v in tw.items()}
     print(f"box pooler of the step: {y.shape[0]} ROIs x 49 bins, {uniq.numel()} distinct rows "
           f"({cb / 1e6:.1f} MB), unique-bytes model {ub / 1e6:.1f} MB; cold caches per launch")
     for k, us in med.items():
         by = (cb * 2 if k.startswith("copy_unique") else
               cb + uniq.numel() * C * 4 if k.startswith("gather1_unique") else ub)
-        print(f"{k:18s} {us:8.1f} us  {by / us / 1e3:7.1f} GB/s ({by / us / 1e3 / 8000:.3f} of 8 TB/s)"
-              f"  roi_align / this = {med['roi_align'] / us:.3f}", flush=True)
+        uw = medw[k]
+        print(f"{k:20s} cold {us:7.1f} us {by / us / 1e3:7.1f} GB/s ({by / us / 1e3 / 8000:.3f})"
+              f"  roi/this {med['roi_align'] / us:.3f} | maps-rewritten {uw:7.1f} us "
+              f"{by / uw / 1e3:7.1f} GB/s ({by / uw / 1e3 / 8000:.3f}) roi/this "
+              f"{medw['roi_align'] / uw:.3f}", flush=True)
 
 
 def guide_gather(lib, dev, st, uniq, src, C, flush, iters):
