@@ -34,9 +34,10 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
 // retina_fused: RetinaNet inference in four launches (retina_post.hip; 0 the
 // unfused pipeline, 2 the fused one with its in-workgroup exact select forced)
 // rpn_merge: the RPN's per-image concat + top-k as a merge rank (proposals.hip)
-// solo_mfma: the SOLOv2 Matrix-NMS intersections on int8 MFMA (solo.hip, r6;
-// 0 = the AND + popcount tiles)
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 1};
+// solo_mfma: the SOLOv2 Matrix-NMS intersections on int8 MFMA (solo.hip, r6):
+// 2 = bits expanded by an LDS table (default), 1 = by arithmetic, 0 = the AND +
+// popcount tiles
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

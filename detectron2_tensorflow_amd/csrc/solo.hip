@@ -436,6 +436,18 @@ __device__ __forceinline__ v4i expand16(uint32_t x) {
   return r;
 }
 
+// The same by table (r6): an LDS table of the 256 byte values' 8-byte
+// expansions, two lookups per 16 bits (4 VALU + 2 LDS reads instead of 12 VALU)
+__device__ __forceinline__ v4i expand16_lut(uint32_t x, const uint2* __restrict__ lut) {
+  const uint2 lo = lut[x & 0xFFu], hi = lut[(x >> 8) & 0xFFu];
+  v4i r;
+  r[0] = (int)lo.x;
+  r[1] = (int)lo.y;
+  r[2] = (int)hi.x;
+  r[3] = (int)hi.y;
+  return r;
+}
+
 // upper-triangle tile pair u -> (ti, tj), ti <= tj, row-major over ti
 __device__ __forceinline__ void tri_pair(int u, int T, int& ti, int& tj) {
   int i = 0, left = T;
@@ -454,10 +466,19 @@ __device__ __forceinline__ void tri_pair(int u, int T, int& ti, int& tj) {
 // partial tile per workgroup goes to the workspace.
 constexpr int kIWaves = 8;
 
+template <bool LUT>
 __global__ __launch_bounds__(64 * kIWaves) void solo_inter_mfma_kernel(
     const uint64_t* __restrict__ bits, int N, int k, int W64, int T, int groups,
     int words_per_wave, int32_t* __restrict__ part, float* __restrict__ comp) {
   extern __shared__ __align__(16) unsigned char ism[];
+  __shared__ uint2 lut[256];
+  if (LUT) {
+    for (int v = threadIdx.x; v < 256; v += 64 * kIWaves) {
+      const v4i e = expand16((uint32_t)v);
+      lut[v] = make_uint2((uint32_t)e[0], (uint32_t)e[1]);
+    }
+    __syncthreads();
+  }
   if (blockIdx.x == 0)  // (the reduce launch max-folds the compensation into it)
     for (int e = threadIdx.x; e < N * k; e += 64 * kIWaves) comp[e] = 0.f;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -514,7 +535,8 @@ __global__ __launch_bounds__(64 * kIWaves) void solo_inter_mfma_kernel(
         v4i fr[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          fr[q] = expand16((uint32_t)(d[q] >> (32 * half32 + 16 * h)) & 0xFFFFu);
+          fr[q] = LUT ? expand16_lut((uint32_t)(d[q] >> (32 * half32 + 16 * h)) & 0xFFFFu, lut)
+                      : expand16((uint32_t)(d[q] >> (32 * half32 + 16 * h)) & 0xFFFFu);
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -552,27 +574,28 @@ __global__ __launch_bounds__(64 * kIWaves) void solo_inter_mfma_kernel(
 // partials are read row-major (coalesced), transposed through LDS and stored
 // as rows of iouT; a pair ti < tj also zeroes its mirror (i > j).
 constexpr int kRedCols = 16;
+template <int TS>
 __global__ __launch_bounds__(256) void solo_inter_reduce_kernel(
     const int32_t* __restrict__ part, int N, int k, int T, int groups,
     const float* __restrict__ sums, const int64_t* __restrict__ cls, float* __restrict__ iouT,
     float* __restrict__ comp) {
-  __shared__ float tile[kRedCols][kIT + 1];
+  __shared__ float tile[kRedCols][TS + 1];
   const int tri = T * (T + 1) / 2;
-  const int cb = blockIdx.x % (kIT / kRedCols);
-  const int u = (blockIdx.x / (kIT / kRedCols)) % tri, n = blockIdx.x / ((kIT / kRedCols) * tri);
+  const int cb = blockIdx.x % (TS / kRedCols);
+  const int u = (blockIdx.x / (TS / kRedCols)) % tri, n = blockIdx.x / ((TS / kRedCols) * tri);
   int ti, tj;
   tri_pair(u, T, ti, tj);
-  const size_t per = (size_t)N * tri * kIT * kIT;
-  const size_t at0 = ((size_t)n * tri + u) * (kIT * kIT);
+  const size_t per = (size_t)N * tri * TS * TS;
+  const size_t at0 = ((size_t)n * tri + u) * (TS * TS);
   const float* sn = sums + (size_t)n * k;
   const int64_t* cn = cls + (size_t)n * k;
-  for (int e = threadIdx.x; e < kIT * kRedCols; e += 256) {
+  for (int e = threadIdx.x; e < TS * kRedCols; e += 256) {
     const int ii = e / kRedCols, jj = cb * kRedCols + e % kRedCols;  // part row i, column j
-    const int i = ti * kIT + ii, j = tj * kIT + jj;
+    const int i = ti * TS + ii, j = tj * TS + jj;
     float v = 0.f;
     if (i < j && j < k && cn[i] == cn[j]) {
       int it = 0;
-      for (int q = 0; q < groups; ++q) it += part[(size_t)q * per + at0 + (size_t)ii * kIT + jj];
+      for (int q = 0; q < groups; ++q) it += part[(size_t)q * per + at0 + (size_t)ii * TS + jj];
       const float fit = (float)it;
       const float uni = (sn[j] + sn[i]) - fit;  // sum_matrix + sum_matrix^T - inter
       v = fit / uni;
@@ -588,18 +611,19 @@ __global__ __launch_bounds__(256) void solo_inter_reduce_kernel(
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int jl = wv; jl < kRedCols; jl += 4) {
       float mx = tile[jl][lane];
+      if (TS > 64) mx = fmaxf(mx, tile[jl][64 + lane]);
       for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-      const int j = tj * kIT + cb * kRedCols + jl;
+      const int j = tj * TS + cb * kRedCols + jl;
       if (lane == 0 && j < k && mx > 0.f)
         atomicMax(reinterpret_cast<int*>(comp) + (size_t)n * k + j, __float_as_int(mx));
     }
   }
-  for (int e = threadIdx.x; e < kIT * kRedCols; e += 256) {
-    const int jl = e / kIT, ii = e % kIT, jj = cb * kRedCols + jl;
-    const int i = ti * kIT + ii, j = tj * kIT + jj;
+  for (int e = threadIdx.x; e < TS * kRedCols; e += 256) {
+    const int jl = e / TS, ii = e % TS, jj = cb * kRedCols + jl;
+    const int i = ti * TS + ii, j = tj * TS + jj;
     if (i < k && j < k) iouT[((size_t)n * k + j) * k + i] = tile[jl][ii];
     // the mirror (rows j' of tile ti, columns i' of tile tj: i' > j')
-    const int i2 = tj * kIT + ii, j2 = ti * kIT + jj;
+    const int i2 = tj * TS + ii, j2 = ti * TS + jj;
     if (ti < tj && i2 < k && j2 < k) iouT[((size_t)n * k + j2) * k + i2] = 0.f;
   }
 }
@@ -1146,10 +1170,17 @@ extern "C" int d2mi_solo_matrix_nms(const uint64_t* mask_bits, const int64_t* cl
     int32_t* part = w.take<int32_t>((size_t)groups * N * tri * kIT * kIT);
     D2MI_REQUIRE(w.ok(), "SOLO Matrix-NMS workspace too small (%zu < %zu)", workspace_bytes,
                  w.off);
-    hipLaunchKernelGGL(solo_inter_mfma_kernel, dim3(N * tri * groups), dim3(64 * kIWaves),
-                       kIWaves * kIWaveB, st, mask_bits, N, k, W64, T, groups, wpw, part, comp);
+    // tuning "solo_mfma": 2 (default) = bits expanded by an LDS table (r6:
+    // intersections 38.1 -> 31.9 us per call, profiles/r6m_stats_*.csv), 1 = by
+    // arithmetic
+    if (tuning(kTuneSoloMfma) == 2)
+      hipLaunchKernelGGL(solo_inter_mfma_kernel<true>, dim3(N * tri * groups), dim3(64 * kIWaves),
+                         kIWaves * kIWaveB, st, mask_bits, N, k, W64, T, groups, wpw, part, comp);
+    else
+      hipLaunchKernelGGL(solo_inter_mfma_kernel<false>, dim3(N * tri * groups), dim3(64 * kIWaves),
+                         kIWaves * kIWaveB, st, mask_bits, N, k, W64, T, groups, wpw, part, comp);
     D2MI_LAUNCH_CHECK();
-    hipLaunchKernelGGL(solo_inter_reduce_kernel, dim3(N * tri * (kIT / kRedCols)), dim3(256), 0,
+    hipLaunchKernelGGL(solo_inter_reduce_kernel<kIT>, dim3(N * tri * (kIT / kRedCols)), dim3(256), 0,
                        st, part, N, k, T, groups, sum_masks, classes, iouT, comp);
     D2MI_LAUNCH_CHECK();
     const unsigned rows_grid = (unsigned)(((size_t)N * k + 3) / 4);

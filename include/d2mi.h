@@ -75,7 +75,8 @@ const char* d2mi_last_error(void);
  *   "conv_ws_mintiles" fewest 256x128 tiles that go to the WS conv (0);
  *   "sgd_rev"      SGD update over its chunks in reverse order (0);
  *   "retina_rank"  RetinaNet merge rank inside the NMS workgroup (0);
- *   "solo_mfma"    SOLOv2 Matrix-NMS intersections on int8 MFMA (1), 0 = the
+ *   "solo_mfma"    SOLOv2 Matrix-NMS intersections on int8 MFMA: 2 (default)
+ *                  = bits expanded by an LDS table, 1 = by arithmetic; 0 = the
  *                  AND + popcount tiles. */
 int d2mi_set_tuning(const char* key, int value);
 /* Current value of a d2mi_set_tuning key (INT32_MIN for an unknown key). */

@@ -242,10 +242,11 @@ def _assert_tail_equal(got, want, dbg, score_rtol=1e-5, exact_masks=True, proof=
     return nflip
 
 
-@pytest.fixture(params=[1, 0], ids=["mfma", "popcount"])
+@pytest.fixture(params=[2, 1, 0], ids=["mfma_lut", "mfma", "popcount"])
 def solo_mfma(request):
-    """The Matrix-NMS intersections on the int8 MFMA (tuning "solo_mfma" 1, r6)
-    or the AND + popcount tiles (0)."""
+    """The Matrix-NMS intersections on the int8 MFMA (tuning "solo_mfma" 2:
+    bits expanded by an LDS table, the default; 1: by arithmetic; r6) or the
+    AND + popcount tiles (0)."""
     from detectron2_tensorflow_amd.layers import ops
     old = ops.get_tuning("solo_mfma")
     ops.set_tuning("solo_mfma", request.param)
