@@ -4,9 +4,12 @@ with the same weights and image.
 
 Op-level parity is exact (test_gpu_ops.py).  End to end, the fp32 convs on
 MFMA vs torch-CPU differ in summation order (~1e-6 relative), which can
-reorder near-tied proposals; the bar here is therefore statistical: RPN
-proposal sets and final detections agree on >= 95% of entries, scores within
-1e-3 and masks within 1e-3 where the detection matches.
+reorder near-tied proposals; the bar of the whole-pipeline test is therefore
+statistical: RPN proposal sets and final detections agree on >= 95% of
+entries, scores within 1e-3 and masks within 1e-3 where the detection
+matches.  The stage-wise tests at 1333x800 (Faster R-CNN, C2; Mask R-CNN,
+r6) compare every stage against the oracle on the model's own inputs to that
+stage, with exact decisions.
 """
 import os
 
@@ -293,3 +296,120 @@ def test_faster_rcnn_c2_1333x800_vs_oracle_on_its_own_heads(dev):
             g0 = i
         assert_boxes_close(h["boxes"][n][k:], wbx[k:])
         assert k >= 20  # a realistic survivor count (score injection)
+
+
+def test_mask_rcnn_1333x800_vs_oracle_on_its_own_heads(dev):
+    """Mask R-CNN R50-FPN inference at the bench geometry (2 synthetic
+    1333x800 images, BASELINE.md score injection), stage by stage against the
+    oracle on the model's OWN intermediate outputs -- the exact counterpart of
+    the statistical 256x320 end-to-end test above:
+    (1) the RPN proposals equal find_top_rpn_proposals on the model's RPN-head
+    outputs (scores / valid flags bit-exact); (2) the detections equal
+    fast_rcnn_inference on its box-head outputs (classes / valid flags exact);
+    (3) the mask pooler's 14x14 features equal the oracle ROIPooler
+    (poolers.py:134-180) on the model's own p2..p5 and detection boxes
+    (<= 1e-5 relative); (4) the mask logits equal a float64 restatement of
+    the mask head on those pooled features (1e-4, the north_star bar); (5) the
+    returned 28x28 masks are the sigmoid of the predicted class's logits,
+    zeroed on invalid slots (mask_head.py:71-106)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_pipeline as cp
+    import oracle
+    import torch.nn.functional as F
+    from test_gpu_ops import assert_boxes_close
+    from detectron2_tensorflow_amd.utils.synthetic import calibrate_rcnn_scores, synthetic_images
+    model = _model(dev, mask=True)
+    batch = synthetic_images(2, 800, 1333, 1000, dev)
+    calibrate_rcnn_scores(model, batch)
+    model.eval()
+    cap = {}
+    pg, rh = model.proposal_generator, model.roi_heads
+    hooks = [pg.rpn_head.register_forward_hook(lambda m, i, o: cap.__setitem__("rpn", o)),
+             pg.register_forward_hook(lambda m, i, o: cap.__setitem__("props", o[0])),
+             rh.box_predictor.register_forward_hook(lambda m, i, o: cap.__setitem__("box", o)),
+             model.neck.register_forward_hook(lambda m, i, o: cap.__setitem__("fpn", o)),
+             rh.mask_head.register_forward_hook(
+                 lambda m, i, o: cap.__setitem__("mask", (i[0].detach().clone(), o[1].detach().clone())))]
+    try:
+        with torch.no_grad():
+            a = model.inference(batch)["instances"]
+    finally:
+        for hk in hooks:
+            hk.remove()
+    h = {k: v.cpu().numpy() for k, v in a.items()}
+    N, D = h["is_valid"].shape
+    image_hw = batch["image_shape"].cpu().numpy()
+    # (1) proposals
+    props = cap["props"]
+    pboxes = props.boxes.cpu().numpy()
+    pscores = props.get_field("objectness_logits").cpu().numpy()
+    pvalid = props.get_field("is_valid").cpu().numpy()
+    lg, dl = [[t.detach().contiguous().cpu().numpy() for t in lst] for lst in cap["rpn"][1:]]
+    ag = pg.anchor_generator
+    cells = [np.asarray(c.cpu() if torch.is_tensor(c) else c, np.float32) for c in ag.cell_anchors]
+    wprops = []
+    for x, d, st, c in zip(lg, dl, ag.strides, cells):
+        anc = oracle.grid_anchors(x.shape[1], x.shape[2], st, c)
+        wprops.append(oracle.apply_deltas(d.reshape(-1, 4), np.tile(anc, (N, 1)), (1, 1, 1, 1))
+                      .reshape(N, -1, 4))
+    wb, ws, wv = oracle.find_top_rpn_proposals(
+        wprops, [x.reshape(N, -1) for x in lg], image_hw, pg.nms_thresh,
+        pg.pre_nms_topk[False], pg.post_nms_topk[False], float(pg.min_box_side_len))
+    np.testing.assert_array_equal(pvalid, wv)
+    np.testing.assert_array_equal(pscores, ws)
+    assert_boxes_close(pboxes, wb)
+    # (2) detections (tie groups compared as sets, as the C2 test)
+    logits, deltas = (t.detach().cpu().numpy() for t in cap["box"])
+    P = pboxes.shape[1]
+    rows = np.nonzero(pvalid.reshape(-1))[0]
+    dec = oracle.apply_deltas(deltas[rows], pboxes.reshape(-1, 4)[rows], rh.box2box_transform.weights)
+    want = oracle.fast_rcnn_inference(dec, oracle.softmax(logits[rows]), rows // P, rows % P, P,
+                                      image_hw, rh.test_score_thresh, rh.test_nms_thresh, D,
+                                      rh.test_nms_cls_agnostic)
+    for n in range(N):
+        wbx, wsc, wc, wvd, _ = want[n]
+        np.testing.assert_array_equal(h["is_valid"][n], wvd)
+        np.testing.assert_allclose(h["scores"][n], wsc, rtol=2e-6, atol=1e-7)
+        k = int(wvd.sum())
+        assert k >= 20
+        g0 = 0
+        for i in range(1, k + 1):
+            if i < k and wsc[g0] - wsc[i] <= 1e-7 + 2e-6 * abs(wsc[g0]):
+                continue
+            key = lambda c, b: np.lexsort((b[:, 3], b[:, 2], b[:, 1], b[:, 0], c))  # noqa: E731
+            gc, gb = h["classes"][n][g0:i], h["boxes"][n][g0:i]
+            og, oo = key(gc, np.round(gb, 2)), key(wc[g0:i], np.round(wbx[g0:i], 2))
+            np.testing.assert_array_equal(gc[og], wc[g0:i][oo])
+            assert_boxes_close(gb[og], wbx[g0:i][oo])
+            g0 = i
+    # (3) the mask pooler on the model's own maps and detection boxes
+    pooled, mlogits = cap["mask"]
+    feats = [cap["fpn"][f].detach().cpu().numpy() for f in rh.in_features]
+    boxes = h["boxes"].reshape(-1, 4)
+    img = np.repeat(np.arange(N, dtype=np.int32), D)
+    scales = [float(v) for v in rh.mask_pooler.scales]
+    R = rh.mask_pooler.output_size
+    want_x, _ = oracle.roi_pooler(feats, boxes, img, R, scales, rh.mask_pooler.sampling_ratio)
+    got_x = pooled.cpu().numpy().reshape(want_x.shape)
+    scale = max(1.0, float(np.abs(want_x).max()))
+    assert np.abs(got_x - want_x).max() <= 1e-5 * scale
+    # (4) mask logits vs a float64 restatement of the head on those features
+    ref = cp.CPUReference(model)
+    mh = ref.m.double().roi_heads.mask_head
+    with torch.no_grad():
+        y = pooled.cpu().double()
+        for c in mh.convs:
+            y = cp._conv(y, c)
+        y = F.conv_transpose2d(y.permute(0, 3, 1, 2), mh.deconv.weights.permute(3, 2, 0, 1),
+                               mh.deconv.bias, stride=mh.deconv.stride)
+        y = cp._conv(torch.relu(y).permute(0, 2, 3, 1), mh.predictor)
+    err = (mlogits.cpu().double() - y).abs().max().item()
+    assert err <= 1e-4 * max(y.abs().max().item(), 1.0), err
+    # (5) the masks: sigmoid of the predicted class's logits, zero where invalid
+    ml = mlogits.cpu()
+    cls = torch.from_numpy(h["classes"].reshape(-1)).long().clamp(min=0)
+    want_m = torch.sigmoid(ml[torch.arange(ml.shape[0]), :, :, cls])
+    want_m = want_m * torch.from_numpy(h["is_valid"].reshape(-1))[:, None, None].float()
+    got_m = a["masks"].cpu().reshape(want_m.shape)
+    assert torch.allclose(got_m, want_m, rtol=0, atol=2e-7), float((got_m - want_m).abs().max())
