@@ -67,7 +67,10 @@ MFMA_I8_PEAK_TOPS = 2 * 2500.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    # (30: the one eager step that carries the per-launch HIP events -- the
+    # live roofline -- is one of the timed steps; among 10 it weighed ~1 % of
+    # the line, among 30 a third of that; 30 steps still take < 1 s)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--batch", type=int, default=2, help="images per GPU per step")
     p.add_argument("--model", default="mask_rcnn_R_50_FPN", choices=sorted(CONFIGS))

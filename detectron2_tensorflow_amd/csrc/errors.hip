@@ -21,13 +21,13 @@ const char* const kTuneNames[kTuneCount] = {"conv_ws",   "roi_fwd",  "wgrad_ws",
                                             "conv_epi",  "wgrad_ws1", "wgrad_xcd",
                                             "conv_xcd",  "wgrad_inc", "conv_ws_mink",
                                             "roi_pix_grid", "conv_stream", "roi_bwd_rec",
-                                            "retina_fused", "rpn_merge", "nms_scan", "roi_heavy", "rpn_compact", "conv_stream_nt", "conv_nt", "conv_tail_mink", "conv_ws_mintiles", "sgd_rev", "retina_rank", "solo_mfma"};
+                                            "retina_fused", "rpn_merge", "nms_scan", "roi_heavy", "rpn_compact", "conv_stream_nt", "conv_nt", "conv_tail_mink", "conv_ws_mintiles", "sgd_rev", "retina_rank", "solo_mfma", "retina_var"};
 const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D2MI_WGRAD_WS",
                                           "D2MI_CONV_EPI",  "D2MI_WGRAD_WS1", "D2MI_WGRAD_XCD",
                                           "D2MI_CONV_XCD",  "D2MI_WGRAD_INC", "D2MI_CONV_WS_MINK",
                                           "D2MI_ROI_PIX_GRID", "D2MI_CONV_STREAM",
                                           "D2MI_ROI_BWD_REC", "D2MI_RETINA_FUSED",
-                                          "D2MI_RPN_MERGE", "D2MI_NMS_SCAN", "D2MI_ROI_HEAVY", "D2MI_RPN_COMPACT", "D2MI_CONV_STREAM_NT", "D2MI_CONV_NT", "D2MI_CONV_TAIL_MINK", "D2MI_CONV_WS_MINTILES", "D2MI_SGD_REV", "D2MI_RETINA_RANK", "D2MI_SOLO_MFMA"};
+                                          "D2MI_RPN_MERGE", "D2MI_NMS_SCAN", "D2MI_ROI_HEAVY", "D2MI_RPN_COMPACT", "D2MI_CONV_STREAM_NT", "D2MI_CONV_NT", "D2MI_CONV_TAIL_MINK", "D2MI_CONV_WS_MINTILES", "D2MI_SGD_REV", "D2MI_RETINA_RANK", "D2MI_SOLO_MFMA", "D2MI_RETINA_VAR"};
 // defaults: measured per shape and in the training step
 // conv_stream: the streaming 1x1 for launches of >= 8192 output pixels (r5 in-step A/B:
 // -0.85 %, profiles/r5_ab_inproc_conv_stream.log); roi_bwd_rec: run records (-0.41 %);
@@ -36,8 +36,9 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
 // rpn_merge: the RPN's per-image concat + top-k as a merge rank (proposals.hip)
 // solo_mfma: the SOLOv2 Matrix-NMS intersections on int8 MFMA (solo.hip, r6):
 // 2 = bits expanded by an LDS table (default), 1 = by arithmetic, 0 = the AND +
-// popcount tiles
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2};
+// popcount tiles; retina_var: the r6 RetinaNet finish (compaction, early
+// select bound, DPP / permlane bitonic: 208; 0 = the r5 form)
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 208};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

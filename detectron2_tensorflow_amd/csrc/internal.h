@@ -54,6 +54,7 @@ enum TuneKey { kTuneConvWS = 0, kTuneRoiFwd = 1, kTuneWgradWS = 2, kTuneConvEpi 
                kTuneRpnCompact = 16, kTuneConvStreamNt = 17, kTuneConvNt = 18,
                kTuneConvTailMinK = 19, kTuneConvWSMinTiles = 20,
                kTuneSgdRev = 21, kTuneRetinaRank = 22, kTuneSoloMfma = 23,
+               kTuneRetinaVar = 24,
                kTuneCount };
 int tuning(TuneKey k);
 

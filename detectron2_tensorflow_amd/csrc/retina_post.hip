@@ -50,6 +50,8 @@ constexpr int kCV = 4;                    // float4 per collect thread per chunk
 constexpr int kChunk4 = kCT * kCV;        // float4 per chunk (16 KB)
 constexpr int kWaveSlots = 8;             // candidate slots per (chunk, wave)
 constexpr int kTile = 64;                 // NMS tile
+constexpr int kPT = 1024;                 // compact: wave slots per part (one per thread)
+constexpr int kPartCap = kPT * kWaveSlots;  // compact: entries a part can hold
 
 struct SegInfo {
   uint32_t floor;     // collect keys >= floor
@@ -60,6 +62,7 @@ struct SegInfo {
   int32_t pad;
   uint64_t ts[10];    // wall-clock stamps of the phases (tools/retina_post_ab.py --debug)
   uint64_t cyc[10];   // shader-clock stamps at the same points (the clock the phases ran at)
+  uint64_t sub[8];    // stamps inside the sort (4) and the NMS (4) phases (tools/retina_post_ab.py)
 };
 
 struct RetinaGeo {
@@ -67,6 +70,7 @@ struct RetinaGeo {
   int32_t anchors[D2MI_MAX_LEVELS];     // H W A
   int32_t chunk0[D2MI_MAX_LEVELS + 1];  // per-image prefix of collect chunks
   int32_t L, N, K;
+  int32_t part0[D2MI_MAX_LEVELS + 1];   // per-image prefix of compact parts (kPT wave slots each)
 };
 
 __device__ __forceinline__ const float* seg_ptr(const float* base, const Levels& lv, int n, int l,
@@ -114,23 +118,82 @@ __device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t* part
 __device__ uint64_t bitonic1024(uint64_t v, uint64_t* lds) {
   const int t = threadIdx.x;
   int buf = 0;
-  for (int size = 2; size <= kWG; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      uint64_t o;
-      if (stride < 64) {
-        o = (uint64_t)__shfl_xor((unsigned long long)v, stride);
-      } else {
-        uint64_t* b = lds + buf * kWG;
-        b[t] = v;
-        __syncthreads();
-        o = b[t ^ stride];
-        buf ^= 1;
-      }
-      const bool up = (t & size) == 0, low = (t & stride) == 0;
-      const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
-      v = (low == up) ? mn : mx;
+  auto step = [&](int size, int stride) {
+    uint64_t o;
+    if (stride < 64) {
+      o = (uint64_t)__shfl_xor((unsigned long long)v, stride);
+    } else {
+      uint64_t* b = lds + buf * kWG;
+      b[t] = v;
+      __syncthreads();
+      o = b[t ^ stride];
+      buf ^= 1;
     }
+    const bool up = (t & size) == 0, low = (t & stride) == 0;
+    const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
+    v = (low == up) ? mn : mx;
+  };
+  for (int size = 2; size <= kWG; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) step(size, stride);
+  return v;
+}
+
+// The same sort with the exchanges at strides < 64 done in VALU lane
+// permutations (tuning retina_var 128): DPP quad / row / half-row mirrors for
+// strides 1 - 8, v_permlane16_swap / v_permlane32_swap (gfx950) for 16 and
+// 32 -- no LDS crossbar round trip and no address arithmetic -- and the
+// compare-exchange as one 64-bit compare and a select; fully unrolled.  The
+// shuffle form runs ~25 VALU per stage per wave, which at 16 waves per CU is
+// what bound it (11.5 us for 55 stages, profiles/r6s_retina_post_ab.log).
+template <int S>
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
+  if constexpr (S == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  } else if constexpr (S == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  } else if constexpr (S == 4) {  // half-row mirror (p ^ 7), then quad reverse (p ^ 3)
+    const int h = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp(h, 0x1B, 0xF, 0xF, false);
+  } else if constexpr (S == 8) {  // row mirror (p ^ 15), then half-row mirror (p ^ 7)
+    const int m = __builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x141, 0xF, 0xF, false);
+  } else if constexpr (S == 16) {  // odd rows of the first operand <-> even rows of the second
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((threadIdx.x >> 4) & 1) ? r[0] : r[1];
+  } else {  // S == 32: upper half of the first operand <-> lower half of the second
+    static_assert(S == 32, "lane_xor32: strides 1 - 32");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return ((threadIdx.x >> 5) & 1) ? r[0] : r[1];
   }
+}
+
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic_strides(uint64_t& v, uint64_t* lds, int& buf) {
+  const int t = threadIdx.x;
+  uint64_t o;
+  if constexpr (STRIDE >= 64) {
+    uint64_t* b = lds + buf * kWG;
+    b[t] = v;
+    __syncthreads();
+    o = b[t ^ STRIDE];
+    buf ^= 1;
+  } else {
+    o = ((uint64_t)lane_xor32<STRIDE>((uint32_t)(v >> 32)) << 32) | lane_xor32<STRIDE>((uint32_t)v);
+  }
+  const bool want_min = ((t & SIZE) == 0) == ((t & STRIDE) == 0);
+  // (branch-free: take the partner's key when it is on the wanted side; on
+  // equal keys either choice is the same key)
+  v = ((o < v) == want_min) ? o : v;
+  if constexpr (STRIDE > 1) bitonic_strides<SIZE, STRIDE / 2>(v, lds, buf);
+}
+template <int SIZE>
+__device__ __forceinline__ void bitonic_sizes(uint64_t& v, uint64_t* lds, int& buf) {
+  bitonic_strides<SIZE, SIZE / 2>(v, lds, buf);
+  if constexpr (SIZE < kWG) bitonic_sizes<SIZE * 2>(v, lds, buf);
+}
+__device__ __forceinline__ uint64_t bitonic1024_lanes(uint64_t v, uint64_t* lds) {
+  int buf = 0;
+  bitonic_sizes<2>(v, lds, buf);
   return v;
 }
 
@@ -352,6 +415,38 @@ __global__ __launch_bounds__(kCT) void retina_collect_kernel(
   }
 }
 
+// ---------------------------------------------------------------- compact
+// (tuning retina_var 16) Many workgroups per segment: part p of segment s
+// compacts the slot entries of kPT wave slots into its own region (no
+// atomics, so nothing to zero first) and writes its count; the finish then
+// gathers ~k x 4 contiguous entries instead of every wave slot's count.
+__global__ __launch_bounds__(kPT) void retina_compact_kernel(RetinaGeo g,
+                                                             const int32_t* __restrict__ wcount,
+                                                             const uint64_t* __restrict__ wslot,
+                                                             uint64_t* __restrict__ cand,
+                                                             int32_t* __restrict__ pcnt) {
+  const int s = blockIdx.y, n = s / g.L, l = s - n * g.L;
+  const int part = blockIdx.x;
+  if (part >= g.part0[l + 1] - g.part0[l]) return;
+  __shared__ uint32_t sp[kPT / 64];
+  const int t = threadIdx.x;
+  const int cpi = g.chunk0[g.L];
+  const int w0 = (n * cpi + g.chunk0[l]) * kCW;
+  const int nw = (g.chunk0[l + 1] - g.chunk0[l]) * kCW;
+  const size_t nslots = (size_t)g.N * cpi * kCW;
+  const int e = part * kPT + t;
+  const int slot = w0 + min(e, nw - 1);
+  const int c = e < nw ? min(wcount[slot], kWaveSlots) : 0;
+  const uint64_t e1 = wslot[slot];  // (loaded with the count: a slot's rows always exist)
+  const uint32_t incl = wg_inclusive_scan((uint32_t)c, sp);
+  const int pos = (int)incl - c;
+  const int gp = n * g.part0[g.L] + g.part0[l] + part;
+  uint64_t* dst = cand + (size_t)gp * kPartCap;
+  if (c > 0) dst[pos] = e1;
+  for (int j = 1; j < c; ++j) dst[pos + j] = wslot[(size_t)j * nslots + slot];
+  if (t == kPT - 1) pcnt[gp] = (int)incl;
+}
+
 // ----------------------------------------------------------------- finish
 // f(index, value) over a segment by the whole workgroup: aligned float4 body
 // (8 loads in flight per thread), scalar head and tail.
@@ -536,10 +631,14 @@ __device__ int exact_select(const float* __restrict__ p, int len, int k, uint64_
 // of one exponent or two), so bins taken from the top bits put thousands of
 // LDS atomics on a few words; relative bins spread them, and a span under
 // 2^24 (the usual case) needs two passes instead of three.
+//
+// cap > 0: stop at the first bin whose end leaves at most cap values at or
+// below it (and at least k): any such bound serves the caller, which sorts
+// the values at or below it (usually one pass instead of three).
 __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8], int k,
-                                    uint32_t* hist, uint32_t* part) {
+                                    uint32_t* hist, uint32_t* part, int cap = 0) {
   __shared__ int s_bin;
-  __shared__ uint32_t s_lt;
+  __shared__ uint32_t s_lt, s_in;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t mn = 0xffffffffu, mx = 0u;
 #pragma unroll
@@ -595,6 +694,7 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
         if ((uint32_t)krem <= acc + c4[j]) {
           s_bin = 4 * t + j;
           s_lt = acc;
+          s_in = c4[j];
           break;
         }
         acc += c4[j];
@@ -602,6 +702,9 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
     }
     __syncthreads();
     const uint64_t off = (uint64_t)s_bin << sh;
+    // (below: values under lo from earlier passes, k - krem of them)
+    if (cap > 0 && (k - krem) + (int)(s_lt + s_in) <= cap)
+      return (uint32_t)((uint64_t)lo + min<uint64_t>(off + (1ull << sh), span) - 1u);
     lo += (uint32_t)off;
     krem -= (int)s_lt;
     if (sh == 0) return lo;
@@ -614,9 +717,10 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     const float* __restrict__ base_a, const float* __restrict__ base_b, Levels lv, RetinaGeo g,
     int topk, float thresh, DeltaCfg dc, SegInfo* __restrict__ info,
     const int32_t* __restrict__ wcount, const uint64_t* __restrict__ wslot,
-    const uint64_t* __restrict__ ovf, float* __restrict__ cscore, float4* __restrict__ cbox,
-    int32_t* __restrict__ ccls, int32_t* __restrict__ lvl_cnt, uint32_t* __restrict__ maxc,
-    int32_t* __restrict__ err) {
+    const uint64_t* __restrict__ ovf, const uint64_t* __restrict__ cand,
+    const int32_t* __restrict__ pcnt, int compact, float* __restrict__ cscore,
+    float4* __restrict__ cbox, int32_t* __restrict__ ccls, int32_t* __restrict__ lvl_cnt,
+    uint32_t* __restrict__ maxc, int32_t* __restrict__ err, int early, int lanes) {
   extern __shared__ uint64_t sk[];  // kCap entries
   __shared__ uint32_t hist[4096];
   __shared__ uint32_t part[kWG / 64];
@@ -658,8 +762,53 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     uint64_t ov[kOv];
 #pragma unroll
     for (int j = 0; j < kOv; ++j) ov[j] = j * kWG + t < xnovf ? osrc[j * kWG + t] : 0ull;
+    if (compact) {
+      // the compacted parts: counts (one per part), their prefix by wave 0,
+      // then every entry in one round of loads (<= kCap: 8 per thread)
+      __shared__ int s_pre[65];
+      const int np = g.part0[l + 1] - g.part0[l];
+      const int gp0 = n * g.part0[g.L] + g.part0[l];
+      if (t < 64) {
+        int tot = 0;
+        for (int p0 = 0; p0 < np; p0 += 64) {
+          const int c = p0 + t < np ? pcnt[gp0 + p0 + t] : 0;
+          int incl = c;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (t >= o) incl += y;
+          }
+          if (p0 + t < np && p0 + t < 64) s_pre[p0 + t] = tot + incl - c;
+          tot += __shfl(incl, 63);
+        }
+        if (t == 0) {
+          s_pre[min(np, 64)] = tot;
+          s_n = tot;
+        }
+      }
+      __syncthreads();
+      const int tot = s_n;
+      if (np <= 64 && tot + xnovf <= kCap) {
+        uint64_t ent[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = j * kWG + t;
+          ent[j] = 0ull;
+          if (i < tot) {
+            int p = 0;
+            while (p + 1 < np && s_pre[p + 1] <= i) ++p;
+            ent[j] = cand[(size_t)(gp0 + p) * kPartCap + (i - s_pre[p])];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j * kWG + t < tot) put(j * kWG + t, ent[j]);
+      } else if (t == 0) {
+        s_n = kCap + 1;  // (more parts than the prefix holds, or too many: the exact select)
+      }
+    }
     constexpr int U = 8;  // wave slots per thread per batch (1333x800 P3: 11,812 in two)
-    for (int e0 = 0; e0 < nw; e0 += U * kWG) {
+    for (int e0 = 0; e0 < (compact ? 0 : nw); e0 += U * kWG) {
       int cc[U], pos[U];
       uint64_t e1[U], e2[U];
       // the first two entries of every slot load with its count, unconditionally
@@ -721,6 +870,7 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
   uint64_t kv[8];
   uint32_t hi[8];
   bool valid[8];
+
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int i = j * kWG + t;
@@ -737,18 +887,22 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
   __syncthreads();
   // the kk smallest keys: all keys whose score word is <= the kk-th smallest
   // one, when at most 1,024 (ties beyond that: the general sort)
-  const uint32_t thr32 = nc <= kWG ? 0xffffffffu : wg_kth_smallest(hi, valid, kk, hist, part);
+  const uint64_t t_keys = stamp();
+  const uint32_t thr32 = nc <= kWG ? 0xffffffffu
+                                    : wg_kth_smallest(hi, valid, kk, hist, part, early ? kWG : 0);
+  const uint64_t t_kth = stamp();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int pos = wave_append(valid[j] && hi[j] <= thr32, &s_le);
     if (pos >= 0 && pos < kWG) sk[pos] = kv[j];
   }
   __syncthreads();
+  const uint64_t t_app = stamp();
   const int nle = s_le;
   if (nle <= kWG) {
     const uint64_t v = t < nle ? sk[t] : ~0ull;
     __syncthreads();
-    const uint64_t sv = bitonic1024(v, sk + kWG);
+    const uint64_t sv = lanes ? bitonic1024_lanes(v, sk + kWG) : bitonic1024(v, sk + kWG);
     sk[t] = sv;
   } else {  // more than 1,024 keys tie at the k-th score: bitonic over all of them
 #pragma unroll
@@ -820,6 +974,10 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     info[s].cyc[4] = c_cand;
     info[s].cyc[5] = c_sorted;
     info[s].cyc[6] = cycles();
+    info[s].sub[0] = t_keys;
+    info[s].sub[1] = t_kth;
+    info[s].sub[2] = t_app;
+    info[s].sub[3] = nle;
   }
 }
 
@@ -910,15 +1068,15 @@ __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
   ord[o0 + pos] = (uint16_t)val;
 }
 
-__global__ __launch_bounds__(kWG) void retina_nms_kernel(
-    RetinaGeo g, int topk, const float* __restrict__ cscore, const float4* __restrict__ cbox,
-    const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
-    const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
-    SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
-    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
-  extern __shared__ float4 dyn[];
+// Greedy NMS of image n's merged candidates by one workgroup (dyn: the LDS
+// the kernel below declares).
+__device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int topk, const float* cscore,
+                          const float4* cbox, const int32_t* ccls, const int32_t* lvl_cnt,
+                          const uint16_t* ord, const uint32_t* maxc, float thr, int max_det,
+                          SegInfo* info, float4* __restrict__ ob, float* __restrict__ os,
+                          int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
   const uint64_t t_start = stamp(), c_start = cycles();
-  const int n = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int L = g.L, capimg = L * topk;
   // LDS: kept (offset box, box, score, class) [max_det], the window's
@@ -968,6 +1126,8 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
   const int total = s_total;
   const float off1 = from_orderable(maxc[n]) + 1.f;
   int nk = 0;
+  uint64_t t_win = 0, t_tile1 = 0;
+  int ntiles = 0;
   for (int w0 = 0; w0 < total && nk < max_det; w0 += kWG) {
     // window: the next 1,024 candidates in score order
     const int wn = min(kWG, total - w0);
@@ -982,7 +1142,9 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
       wcl[t] = cl;
     }
     __syncthreads();
+    if (w0 == 0) t_win = stamp();
     for (int t0 = 0; t0 < wn && nk < max_det; t0 += kTile) {
+      ++ntiles;
       const int rem = wn - t0;
       const float4 cb = lane < rem ? wobox[t0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       bool sup = false;
@@ -1025,8 +1187,10 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
       }
       __syncthreads();
       nk = s_nk;
+      if (ntiles == 1) t_tile1 = stamp();
     }
   }
+  const uint64_t t_loop = stamp();
   for (int i = t; i < max_det; i += kWG) {
     const size_t o = (size_t)n * max_det + i;
     const bool k = i < nk;
@@ -1042,7 +1206,22 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
     info[n * L].cyc[7] = c_start;
     info[n * L].cyc[8] = c_ranked;
     info[n * L].cyc[9] = cycles();
+    info[n * L].sub[4] = t_win;
+    info[n * L].sub[5] = ntiles;
+    info[n * L].sub[6] = t_tile1;
+    info[n * L].sub[7] = t_loop;
   }
+}
+
+__global__ __launch_bounds__(kWG) void retina_nms_kernel(
+    RetinaGeo g, int topk, const float* __restrict__ cscore, const float4* __restrict__ cbox,
+    const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
+    const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
+    SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
+    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
+  extern __shared__ float4 dyn[];
+  nms_image(blockIdx.x, dyn, g, topk, cscore, cbox, ccls, lvl_cnt, ord, maxc, thr, max_det, info, ob,
+            os, oc, ov, inl_rank);
 }
 
 struct FusedWs {
@@ -1056,9 +1235,11 @@ struct FusedWs {
   int32_t* lvl_cnt;
   uint32_t* maxc;
   uint16_t* ord;
+  uint64_t* cand;
+  int32_t* pcnt;
 };
 template <typename WS>
-void fused_layout(WS& w, FusedWs* o, int N, int L, int k, int chunks) {
+void fused_layout(WS& w, FusedWs* o, int N, int L, int k, int chunks, int parts) {
   const int S = N * L;
   const size_t C = (size_t)N * L * k;
   auto a0 = w.template take<SegInfo>(S);
@@ -1071,9 +1252,12 @@ void fused_layout(WS& w, FusedWs* o, int N, int L, int k, int chunks) {
   auto a7 = w.template take<int32_t>(S);
   auto a8 = w.template take<uint32_t>(N);
   auto a9 = w.template take<uint16_t>(C);
+  auto a10 = w.template take<uint64_t>((size_t)parts * kPartCap);
+  auto a11 = w.template take<int32_t>((size_t)parts);
   if (o)
     *o = FusedWs{(SegInfo*)a0, (int32_t*)a1, (uint64_t*)a2, (uint64_t*)a3, (float*)a4,
-                 (float4*)a5, (int32_t*)a6, (int32_t*)a7, (uint32_t*)a8, (uint16_t*)a9};
+                 (float4*)a5, (int32_t*)a6, (int32_t*)a7, (uint32_t*)a8, (uint16_t*)a9,
+                 (uint64_t*)a10, (int32_t*)a11};
 }
 struct SizerP {
   WorkspaceSizer z;
@@ -1091,6 +1275,7 @@ bool make_geo(RetinaGeo& g, const int32_t* level_hw, int L, int A, int K, int N)
   g.N = N;
   g.K = K;
   g.chunk0[0] = 0;
+  g.part0[0] = 0;
   for (int l = 0; l < L; ++l) {
     const int64_t anchors = (int64_t)level_hw[2 * l] * level_hw[2 * l + 1] * A;
     const int64_t len = anchors * K;
@@ -1100,6 +1285,7 @@ bool make_geo(RetinaGeo& g, const int32_t* level_hw, int L, int A, int K, int N)
     const int64_t c = g.chunk0[l] + (len + 3 + 4LL * kChunk4 - 1) / (4LL * kChunk4);
     if (c * N >= (1ll << 31) / kCW) return false;
     g.chunk0[l + 1] = (int32_t)c;
+    g.part0[l + 1] = g.part0[l] + (int32_t)(((c - g.chunk0[l]) * kCW + kPT - 1) / kPT);
   }
   return true;
 }
@@ -1114,7 +1300,7 @@ size_t retina_fused_workspace_size(int N, int L, const int32_t* level_hw, int A,
   RetinaGeo g;
   if (!make_geo(g, level_hw, L, A, K, N)) return 0;
   SizerP s;
-  fused_layout(s, nullptr, N, L, k, N * g.chunk0[L]);
+  fused_layout(s, nullptr, N, L, k, N * g.chunk0[L], N * g.part0[L]);
   return s.z.off;
 }
 
@@ -1125,16 +1311,26 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
+  // tuning "retina_var" (r6 bits; default 208 = 16 + 64 + 128, 0 = the r5
+  // form): 16 = the wave slots compacted by many workgroups before the
+  // finish (one launch more), 64 = the finish's select stops at the first
+  // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
+  // DPP / permlane lane permutations; 4 = floor and finish launched twice
+  // (both idempotent: the stamps then time warm second launches)
+  const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
   D2MI_REQUIRE(make_geo(g, level_hw, L, lv.A, K, N), "RetinaNet level too large");
   const int chunks = N * g.chunk0[L];
   Workspace w(workspace, workspace_bytes);
   FusedWs o;
-  fused_layout(w, &o, N, L, k, chunks);
+  fused_layout(w, &o, N, L, k, chunks, N * g.part0[L]);
   D2MI_REQUIRE(w.ok(), "retinanet workspace too small (%zu < %zu)", workspace_bytes, w.off);
-  hipLaunchKernelGGL(retina_floor_kernel, dim3(S), dim3(kWG), 0, st, cls[0], lv, g, k,
-                     force_exact ? 1 : 0, o.info, o.maxc);
-  D2MI_LAUNCH_CHECK();
+  const int reps = (var & 4) ? 2 : 1;
+  for (int rep = 0; rep < reps; ++rep) {
+    hipLaunchKernelGGL(retina_floor_kernel, dim3(S), dim3(kWG), 0, st, cls[0], lv, g, k,
+                       force_exact ? 1 : 0, o.info, o.maxc);
+    D2MI_LAUNCH_CHECK();
+  }
   // persistent collect grid: the workgroups the device holds at once
   static int resident = 0;
   if (!resident) {
@@ -1147,15 +1343,26 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   hipLaunchKernelGGL(retina_collect_kernel, dim3(std::min(chunks, resident)), dim3(kCT), 0, st, cls[0],
                      lv, g, o.info, o.wcount, o.wslot, o.ovf);
   D2MI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(retina_finish_kernel, dim3(S), dim3(kWG), kCap * sizeof(uint64_t), st, cls[0],
-                     box[0], lv, g, k, score_thresh, dc, o.info, o.wcount, o.wslot, o.ovf,
-                     o.cscore, o.cbox, o.ccls, o.lvl_cnt, o.maxc, error_word());
-  D2MI_LAUNCH_CHECK();
+  const int compact = (var & 16) ? 1 : 0;
+  if (compact) {
+    int maxp = 0;
+    for (int l = 0; l < L; ++l) maxp = std::max(maxp, g.part0[l + 1] - g.part0[l]);
+    hipLaunchKernelGGL(retina_compact_kernel, dim3(std::max(1, maxp), S), dim3(kPT), 0, st, g,
+                       o.wcount, o.wslot, o.cand, o.pcnt);
+    D2MI_LAUNCH_CHECK();
+  }
+  for (int rep = 0; rep < reps; ++rep) {
+    hipLaunchKernelGGL(retina_finish_kernel, dim3(S), dim3(kWG), kCap * sizeof(uint64_t), st, cls[0],
+                       box[0], lv, g, k, score_thresh, dc, o.info, o.wcount, o.wslot, o.ovf, o.cand,
+                       o.pcnt, compact, o.cscore, o.cbox, o.ccls, o.lvl_cnt, o.maxc, error_word(),
+                       (var & 64) ? 1 : 0, (var & 128) ? 1 : 0);
+    D2MI_LAUNCH_CHECK();
+  }
   const int capimg = L * k;
+  const int inl = tuning(kTuneRetinaRank) != 0 ? 1 : 0;
   // (tuning "retina_rank": 1 = the merge rank inside the NMS workgroup, 0 = its own launch;
   // measured: 165.6 vs 124.4 us per call -- one CU's LDS binary searches over ~4.7 k
   // candidates cost far more than the launch they save, profiles/r5_retina_post_ab_rank*.log)
-  const int inl = tuning(kTuneRetinaRank) != 0 ? 1 : 0;
   if (!inl) {
     hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
                        (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);

@@ -578,7 +578,8 @@ def _retina_logits(rng, shape, dist):
     return x.astype(F32)
 
 
-@pytest.mark.parametrize("path", ["fused", "fused_exact_select", "fused_rank_inline", "unfused"])
+@pytest.mark.parametrize("path", ["fused", "fused_exact_select", "fused_rank_inline", "fused_r5",
+                                  "unfused"])
 @pytest.mark.parametrize("dist", ["normal", "quantized", "saturated", "sparse"])
 def test_retinanet_inference_vs_oracle(dev, dist, path):
     """Dense top-k + decode + NMS vs the oracle.  The distributions drive the
@@ -588,18 +589,25 @@ def test_retinanet_inference_vs_oracle(dev, dist, path):
     pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
     its in-workgroup exact select forced on every level (2), the same with the
     merge rank inside the NMS workgroup (tuning "retina_rank" = 1; default: its
-    own launch), and the unfused top-k / sort / mask NMS pipeline (0)."""
+    own launch), the r5 form of the finish (tuning "retina_var" = 0; the
+    default 208 compacts the wave slots with many workgroups before the
+    finish, stops the finish's select at the first bound leaving <= 1,024
+    keys and runs its bitonic exchanges in DPP / permlane lane permutations),
+    and the unfused top-k / sort / mask NMS pipeline (0)."""
     from detectron2_tensorflow_amd.layers import ops as lops
     old = lops.get_tuning("retina_fused")
     old_rank = lops.get_tuning("retina_rank")
+    old_var = lops.get_tuning("retina_var")
     lops.set_tuning("retina_fused", {"fused": 1, "fused_exact_select": 2, "fused_rank_inline": 1,
-                                     "unfused": 0}[path])
+                                     "fused_r5": 1, "unfused": 0}[path])
     lops.set_tuning("retina_rank", 1 if path == "fused_rank_inline" else 0)
+    lops.set_tuning("retina_var", 0 if path == "fused_r5" else old_var)
     try:
         _retinanet_inference_vs_oracle(dev, dist)
     finally:
         lops.set_tuning("retina_fused", old)
         lops.set_tuning("retina_rank", old_rank)
+        lops.set_tuning("retina_var", old_var)
 
 
 def _retinanet_inference_vs_oracle(dev, dist):

@@ -7,6 +7,8 @@ in one process: outputs compared exactly, times as medians of interleaved
 rounds, and the fraction of HBM for the 129 MB of scores read once.
 
     python tools/retina_post_ab.py [--iters 20] [--rounds 5] [--dist normal]
+    python tools/retina_post_ab.py --vars 0,1,2 --debug   # fused-path variants
+                                    # (tuning "retina_var"; 4 = warm relaunches)
 """
 import argparse
 import os
@@ -54,11 +56,12 @@ def seg_debug(run, cls, N):
         ops.set_tuning("retina_fused", old)
     torch.cuda.synchronize()
     L = len(cls)
-    sz = 184  # sizeof(SegInfo)
+    sz = 248  # sizeof(SegInfo)
     raw = keep[-1][:N * L * sz].cpu()
     i32 = raw.view(torch.int32).view(N * L, sz // 4)
     ts = raw.view(torch.int64).view(N * L, sz // 8)[:, 3:13]
     cy = raw.view(torch.int64).view(N * L, sz // 8)[:, 13:23]
+    sub = raw.view(torch.int64).view(N * L, sz // 8)[:, 23:31]
     mhz = lambda a, b: (int(cy[s, b]) - int(cy[s, a])) / max(1, int(ts[s, b]) - int(ts[s, a])) * 100  # noqa
     t0 = int(ts[:, 0].min())
     us = lambda a, b: (int(b) - int(a)) / 100.0  # noqa: E731
@@ -72,10 +75,15 @@ def seg_debug(run, cls, N):
                 f"keys >= floor {int((keys >= f).sum())}"
                 f" | floor {us(r[0], r[1]):.1f} us [{us(t0, r[0]):.1f}..{us(t0, r[1]):.1f}]"
                 f" | finish at {us(t0, r[2]):.1f}: gather {us(r[2], r[3]):.1f} select {us(r[3], r[4]):.1f}"
-                f" sort {us(r[4], r[5]):.1f} decode {us(r[5], r[6]):.1f} (end {us(t0, r[6]):.1f})"
+                f" sort {us(r[4], r[5]):.1f} [keys {us(r[4], sub[s, 0]):.1f} kth {us(sub[s, 0], sub[s, 1]):.1f}"
+                f" append {us(sub[s, 1], sub[s, 2]):.1f} bitonic({int(sub[s, 3])}) {us(sub[s, 2], r[5]):.1f}]"
+                f" decode {us(r[5], r[6]):.1f} (end {us(t0, r[6]):.1f})"
                 f" | clock MHz floor {mhz(0, 1):.0f} finish {mhz(2, 6):.0f}")
         if l == 0:
-            line += (f" | nms at {us(t0, r[7]):.1f}: counts {us(r[7], r[8]):.1f} scan {us(r[8], r[9]):.1f}"
+            line += (f" | nms at {us(t0, r[7]):.1f}: counts {us(r[7], r[8]):.1f} window {us(r[8], sub[s, 4]):.1f}"
+                     f" scan({int(sub[s, 5])} tiles) {us(sub[s, 4], r[9]):.1f} [first tile"
+                     f" {us(sub[s, 4], sub[s, 6]):.1f} rest {us(sub[s, 6], sub[s, 7]):.1f}"
+                     f" outputs {us(sub[s, 7], r[9]):.1f}]"
                      f" (end {us(t0, r[9]):.1f}) nms clock {mhz(7, 9):.0f} MHz")
         print(line, flush=True)
 
@@ -86,6 +94,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--dist", default="normal", choices=["normal", "saturated"])
     ap.add_argument("--arms", default="0,1", help="retina_fused values to time")
+    ap.add_argument("--vars", default="",
+                    help="time the fused path under these tuning retina_var values instead")
     ap.add_argument("--debug", action="store_true",
                     help="print the fused path's per-segment floor state (workspace head)")
     a = ap.parse_args()
@@ -105,24 +115,34 @@ def main():
     cells = [cell_anchors(s) for s in (32, 64, 128, 256, 512)]
     nbytes = 4 * sum(t.numel() for t in cls)
     run = lambda: ops.retinanet_inference(cls, box, strides, cells, K, 1000, 0.05, 0.5, 100)  # noqa
-    arms = [int(v) for v in a.arms.split(",")]
+    key = "retina_var" if a.vars else "retina_fused"
+    arms = [int(v) for v in (a.vars or a.arms).split(",")]
     if a.debug:
-        seg_debug(run, cls, N)
-    old = ops.get_tuning("retina_fused")
+        for arm in (arms if a.vars else [0]):
+            if a.vars:
+                print(f"-- retina_var={arm}", flush=True)
+                ops.set_tuning("retina_var", arm)
+            seg_debug(run, cls, N)
+        if a.vars:
+            ops.set_tuning("retina_var", 0)
+        arms = [v for v in arms if not v & 4]  # (relaunch arms: stamps only)
+    old = ops.get_tuning(key)
+    if a.vars:
+        ops.set_tuning("retina_fused", 1)
     outs = {}
     for arm in arms:
-        ops.set_tuning("retina_fused", arm)
+        ops.set_tuning(key, arm)
         outs[arm] = [t.clone() for t in run()]
     torch.cuda.synchronize()
     ref = outs[arms[0]]
     for arm in arms[1:]:
         same = all(torch.equal(x, y) for x, y in zip(ref, outs[arm]))
-        print(f"retina_fused={arm} outputs equal to retina_fused={arms[0]}: {same} "
+        print(f"{key}={arm} outputs equal to {key}={arms[0]}: {same} "
               f"(valid {int(outs[arm][3].sum())} vs {int(ref[3].sum())})", flush=True)
     times = {arm: [] for arm in arms}
     for _ in range(a.rounds):
         for arm in arms:
-            ops.set_tuning("retina_fused", arm)
+            ops.set_tuning(key, arm)
             run()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -132,10 +152,10 @@ def main():
             e1.record()
             e1.synchronize()
             times[arm].append(e0.elapsed_time(e1) / a.iters * 1e3)
-    ops.set_tuning("retina_fused", old)
+    ops.set_tuning(key, old)
     for arm in arms:
         m = statistics.median(times[arm])
-        print(f"retina_fused={arm}: {m:8.1f} us per call  ({nbytes / m / 1e6 / 8:.3f} of HBM for "
+        print(f"{key}={arm}: {m:8.1f} us per call  ({nbytes / m / 1e6 / 8:.3f} of HBM for "
               f"{nbytes / 1e6:.1f} MB of scores)  rounds {[round(v, 1) for v in times[arm]]}",
               flush=True)
 
