@@ -36,9 +36,10 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
 // rpn_merge: the RPN's per-image concat + top-k as a merge rank (proposals.hip)
 // solo_mfma: the SOLOv2 Matrix-NMS intersections on int8 MFMA (solo.hip, r6):
 // 2 = bits expanded by an LDS table (default), 1 = by arithmetic, 0 = the AND +
-// popcount tiles; retina_var: the r6 RetinaNet finish (compaction, early
-// select bound, DPP / permlane bitonic: 208; 0 = the r5 form)
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 208};
+// popcount tiles; retina_var: the r6 RetinaNet post (compaction, early
+// select bound, DPP / permlane bitonic and select, NMS IoU only where boxes
+// meet: 1744; 0 = the r5 form)
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 1744};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

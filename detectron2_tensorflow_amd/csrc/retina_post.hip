@@ -94,14 +94,31 @@ __device__ __forceinline__ int wave_append(bool hit, int* counter) {
   return hit ? base + __popcll(b & ((1ull << lane) - 1ull)) : -1;
 }
 
+// Inclusive scan of one value across the wave in DPP row shifts and row
+// broadcasts (no LDS crossbar round trips): within rows of 16, then row 15
+// into rows 1 and 3, then lane 31 into rows 2 and 3.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
 // Inclusive scan of one value per thread over the workgroup (part: 16 words).
-__device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t* part) {
+__device__ __forceinline__ uint32_t wg_inclusive_scan(uint32_t v, uint32_t* part, bool dpp = false) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t incl = v;
+  if (dpp) {
+    incl = wave_incl_scan_dpp(v);
+  } else {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
   }
   if (lane == 63) part[w] = incl;
   __syncthreads();
@@ -636,7 +653,7 @@ __device__ int exact_select(const float* __restrict__ p, int len, int k, uint64_
 // below it (and at least k): any such bound serves the caller, which sorts
 // the values at or below it (usually one pass instead of three).
 __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8], int k,
-                                    uint32_t* hist, uint32_t* part, int cap = 0) {
+                                    uint32_t* hist, uint32_t* part, int cap = 0, bool dpp = false) {
   __shared__ int s_bin;
   __shared__ uint32_t s_lt, s_in;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -647,10 +664,25 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
       mn = min(mn, h[j]);
       mx = max(mx, h[j]);
     }
+  if (dpp) {  // (the lane permutations of bitonic1024_lanes)
+    mn = min(mn, lane_xor32<32>(mn));
+    mx = max(mx, lane_xor32<32>(mx));
+    mn = min(mn, lane_xor32<16>(mn));
+    mx = max(mx, lane_xor32<16>(mx));
+    mn = min(mn, lane_xor32<8>(mn));
+    mx = max(mx, lane_xor32<8>(mx));
+    mn = min(mn, lane_xor32<4>(mn));
+    mx = max(mx, lane_xor32<4>(mx));
+    mn = min(mn, lane_xor32<2>(mn));
+    mx = max(mx, lane_xor32<2>(mx));
+    mn = min(mn, lane_xor32<1>(mn));
+    mx = max(mx, lane_xor32<1>(mx));
+  } else {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    for (int o = 32; o > 0; o >>= 1) {
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    }
   }
   if (lane == 0) {
     hist[w] = mn;
@@ -686,7 +718,7 @@ __device__ uint32_t wg_kth_smallest(const uint32_t (&h)[8], const bool (&ok)[8],
       c4[j] = hist[4 * t + j];
       loc += c4[j];
     }
-    const uint32_t incl = wg_inclusive_scan(loc, part);
+    const uint32_t incl = wg_inclusive_scan(loc, part, dpp);
     const uint32_t before = incl - loc;
     if ((uint32_t)krem > before && (uint32_t)krem <= incl) {
       uint32_t acc = before;
@@ -720,7 +752,7 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
     const uint64_t* __restrict__ ovf, const uint64_t* __restrict__ cand,
     const int32_t* __restrict__ pcnt, int compact, float* __restrict__ cscore,
     float4* __restrict__ cbox, int32_t* __restrict__ ccls, int32_t* __restrict__ lvl_cnt,
-    uint32_t* __restrict__ maxc, int32_t* __restrict__ err, int early, int lanes) {
+    uint32_t* __restrict__ maxc, int32_t* __restrict__ err, int early, int lanes, int lanes_kth) {
   extern __shared__ uint64_t sk[];  // kCap entries
   __shared__ uint32_t hist[4096];
   __shared__ uint32_t part[kWG / 64];
@@ -889,7 +921,8 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
   // one, when at most 1,024 (ties beyond that: the general sort)
   const uint64_t t_keys = stamp();
   const uint32_t thr32 = nc <= kWG ? 0xffffffffu
-                                    : wg_kth_smallest(hi, valid, kk, hist, part, early ? kWG : 0);
+                                    : wg_kth_smallest(hi, valid, kk, hist, part, early ? kWG : 0,
+                                                      lanes_kth != 0);
   const uint64_t t_kth = stamp();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -1068,14 +1101,22 @@ __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
   ord[o0 + pos] = (uint16_t)val;
 }
 
+// Corner-normalised boxes with a positive-area intersection (the only case
+// in which tf_iou can exceed a non-negative threshold).
+__device__ __forceinline__ bool boxes_meet(float4 a, float4 b) {
+  return fminf(a.z, b.z) > fmaxf(a.x, b.x) && fminf(a.w, b.w) > fmaxf(a.y, b.y);
+}
+
 // Greedy NMS of image n's merged candidates by one workgroup (dyn: the LDS
 // the kernel below declares).
 __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int topk, const float* cscore,
                           const float4* cbox, const int32_t* ccls, const int32_t* lvl_cnt,
                           const uint16_t* ord, const uint32_t* maxc, float thr, int max_det,
                           SegInfo* info, float4* __restrict__ ob, float* __restrict__ os,
-                          int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
+                          int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank,
+                          int fast_iou) {
   const uint64_t t_start = stamp(), c_start = cycles();
+  const bool fast = fast_iou != 0 && thr >= 0.f;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int L = g.L, capimg = L * topk;
@@ -1136,7 +1177,12 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
       const float4 c = cbox[o0 + q];
       const int cl = ccls[o0 + q];
       const float off = (float)cl * off1;
-      wobox[t] = make_float4(c.x + off, c.y + off, c.z + off, c.w + off);
+      const float4 ob4 = make_float4(c.x + off, c.y + off, c.z + off, c.w + off);
+      // (fast: stored corner-normalised -- tf_iou normalises its inputs, so
+      // its value on these is the same bits)
+      wobox[t] = fast ? make_float4(fminf(ob4.x, ob4.z), fminf(ob4.y, ob4.w), fmaxf(ob4.x, ob4.z),
+                                    fmaxf(ob4.y, ob4.w))
+                      : ob4;
       wbox[t] = c;
       wsc[t] = cscore[o0 + q];
       wcl[t] = cl;
@@ -1148,7 +1194,16 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
       const int rem = wn - t0;
       const float4 cb = lane < rem ? wobox[t0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       bool sup = false;
-      for (int i = w; i < nk; i += kWG / 64) sup = sup || (tf_iou(kept_obox[i], cb) > thr);
+      // (fast: the IoU only where the normalised boxes intersect -- elsewhere
+      // it is 0 or NaN, never > thr >= 0 -- and per row only when some lane does)
+      if (fast) {
+        for (int i = w; i < nk; i += kWG / 64) {
+          const float4 kb = kept_obox[i];
+          if (!sup && boxes_meet(kb, cb)) sup = tf_iou(kb, cb) > thr;
+        }
+      } else {
+        for (int i = w; i < nk; i += kWG / 64) sup = sup || (tf_iou(kept_obox[i], cb) > thr);
+      }
       const uint64_t ws = __ballot(sup);
       if (lane == 0) wsup[w] = ws;
       constexpr int RPW = kTile / (kWG / 64);  // tile rows per wave
@@ -1156,7 +1211,14 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
       for (int rr = 0; rr < RPW; ++rr) {
         const int r = w * RPW + rr;
         const bool live = r < rem && lane > r && lane < rem;
-        const uint64_t d = __ballot(live && tf_iou(wobox[t0 + r], cb) > thr);
+        uint64_t d;
+        if (fast) {
+          const float4 rb = wobox[t0 + r];
+          const bool meet = live && boxes_meet(rb, cb);
+          d = __ballot(meet) ? __ballot(meet && tf_iou(rb, cb) > thr) : 0ull;
+        } else {
+          d = __ballot(live && tf_iou(wobox[t0 + r], cb) > thr);
+        }
         if (lane == 0) diag[r] = d;
       }
       __syncthreads();
@@ -1218,10 +1280,10 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
     const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
     const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
     SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
-    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank) {
+    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank, int fast_iou) {
   extern __shared__ float4 dyn[];
   nms_image(blockIdx.x, dyn, g, topk, cscore, cbox, ccls, lvl_cnt, ord, maxc, thr, max_det, info, ob,
-            os, oc, ov, inl_rank);
+            os, oc, ov, inl_rank, fast_iou);
 }
 
 struct FusedWs {
@@ -1311,11 +1373,13 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 208 = 16 + 64 + 128, 0 = the r5
-  // form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 1744 = 16 + 64 + 128 + 512 + 1024,
+  // 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
-  // DPP / permlane lane permutations; 4 = floor and finish launched twice
+  // DPP / permlane lane permutations, 512 = the finish's k-th select with
+  // DPP / permlane reductions and scans, 1024 = the NMS's IoU only where
+  // boxes intersect (exact); 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1355,7 +1419,7 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
     hipLaunchKernelGGL(retina_finish_kernel, dim3(S), dim3(kWG), kCap * sizeof(uint64_t), st, cls[0],
                        box[0], lv, g, k, score_thresh, dc, o.info, o.wcount, o.wslot, o.ovf, o.cand,
                        o.pcnt, compact, o.cscore, o.cbox, o.ccls, o.lvl_cnt, o.maxc, error_word(),
-                       (var & 64) ? 1 : 0, (var & 128) ? 1 : 0);
+                       (var & 64) ? 1 : 0, (var & 128) ? 1 : 0, (var & 512) ? 1 : 0);
     D2MI_LAUNCH_CHECK();
   }
   const int capimg = L * k;
@@ -1372,7 +1436,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                      (inl ? 16 + (size_t)capimg * (sizeof(float) + sizeof(uint16_t)) : 0);
   hipLaunchKernelGGL(retina_nms_kernel, dim3(N), dim3(kWG), lds, st, g, k, o.cscore, o.cbox,
                      o.ccls, o.lvl_cnt, o.ord, o.maxc, nms_thresh, max_det, o.info,
-                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl);
+                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl,
+                     (var & 1024) ? 1 : 0);
   D2MI_LAUNCH_CHECK();
   return 0;
 }
