@@ -1114,9 +1114,11 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
                           const uint16_t* ord, const uint32_t* maxc, float thr, int max_det,
                           SegInfo* info, float4* __restrict__ ob, float* __restrict__ os,
                           int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank,
-                          int fast_iou) {
+                          int fast_iou, int fp_resolve) {
   const uint64_t t_start = stamp(), c_start = cycles();
   const bool fast = fast_iou != 0 && thr >= 0.f;
+  const bool fp = fp_resolve != 0;
+  __shared__ uint64_t colpart[kWG];  // (fp) per wave, per lane: column bits of the wave's rows
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int L = g.L, capimg = L * topk;
@@ -1167,7 +1169,7 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
   const int total = s_total;
   const float off1 = from_orderable(maxc[n]) + 1.f;
   int nk = 0;
-  uint64_t t_win = 0, t_tile1 = 0;
+  uint64_t t_win = 0, t_tile1 = 0, t_a = 0, t_b = 0, t_c = 0;
   int ntiles = 0;
   for (int w0 = 0; w0 < total && nk < max_det; w0 += kWG) {
     // window: the next 1,024 candidates in score order
@@ -1207,35 +1209,71 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
       const uint64_t ws = __ballot(sup);
       if (lane == 0) wsup[w] = ws;
       constexpr int RPW = kTile / (kWG / 64);  // tile rows per wave
+      uint64_t colp = 0;  // (fp: this lane's column bits of the wave's rows)
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr) {
         const int r = w * RPW + rr;
         const bool live = r < rem && lane > r && lane < rem;
         uint64_t d;
+        bool p;
         if (fast) {
           const float4 rb = wobox[t0 + r];
           const bool meet = live && boxes_meet(rb, cb);
-          d = __ballot(meet) ? __ballot(meet && tf_iou(rb, cb) > thr) : 0ull;
+          p = __ballot(meet) ? (meet && tf_iou(rb, cb) > thr) : false;
         } else {
-          d = __ballot(live && tf_iou(wobox[t0 + r], cb) > thr);
+          p = live && tf_iou(wobox[t0 + r], cb) > thr;
         }
+        d = __ballot(p);
+        colp |= p ? (1ull << r) : 0ull;
         if (lane == 0) diag[r] = d;
       }
+      if (fp) colpart[w * 64 + lane] = colp;
+      if (ntiles == 1) t_a = stamp();
       __syncthreads();
+      if (ntiles == 1) t_b = stamp();
       if (w == 0) {
         uint64_t removed = 0;
 #pragma unroll
         for (int vv = 0; vv < kWG / 64; ++vv) removed |= wsup[vv];
         if (rem < 64) removed |= ~((1ull << rem) - 1ull);
-        const uint64_t my_diag = diag[lane];
         uint64_t keptm = 0;
         int k2 = nk;
-        for (int r = 0; r < kTile; ++r) {
-          if (k2 >= max_det) break;
-          if (!((removed >> r) & 1ull)) {
-            keptm |= 1ull << r;
-            ++k2;
-            removed |= readlane64(my_diag, r);
+        if (fp) {
+          // (retina_var 2048) the kept set as the fixed point of a ballot
+          // over the column words (nms.hip's r5 scan): lane c is row c, kept
+          // iff alive and no kept row < c suppresses it; row c is final after
+          // c + 1 rounds, and the greedy set is the only fixed point
+          uint64_t colD = 0;
+#pragma unroll
+          for (int vv = 0; vv < kWG / 64; ++vv) colD |= colpart[vv * 64 + lane];
+          const bool alive = !((removed >> lane) & 1ull);
+          uint64_t K = __ballot(alive);
+          for (int it = 0; it <= 64; ++it) {
+            const uint64_t K2 = __ballot(alive && (colD & K) == 0ull);
+            if (K2 == K) break;
+            K = K2;
+          }
+          const int room = max_det - nk;
+          if (__popcll(K) > room) {  // the greedy stops at max_det: its first room rows
+            uint64_t kk2 = 0, rest = K;
+            for (int q = 0; q < room; ++q) {
+              const uint64_t low = rest & (~rest + 1ull);
+              kk2 |= low;
+              rest ^= low;
+            }
+            K = kk2;
+          }
+          keptm = K;
+          k2 = nk + __popcll(K);
+        } else {
+          const uint64_t my_diag = diag[lane];
+          for (int r = 0; r < kTile; ++r) {
+            if (k2 >= max_det) break;
+            if (!((removed >> r) & 1ull)) {
+              keptm |= 1ull << r;
+              ++k2;
+              removed |= readlane64(my_diag, r);
+            }
           }
         }
         if ((keptm >> lane) & 1ull) {
@@ -1246,6 +1284,7 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
           kept_cl[pos] = wcl[t0 + lane];
         }
         if (lane == 0) s_nk = k2;
+        if (ntiles == 1) t_c = stamp();
       }
       __syncthreads();
       nk = s_nk;
@@ -1272,6 +1311,11 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
     info[n * L].sub[5] = ntiles;
     info[n * L].sub[6] = t_tile1;
     info[n * L].sub[7] = t_loop;
+    if (L > 1) {  // (first tile: diag rows done, after the barrier, resolved)
+      info[n * L + 1].sub[4] = t_a;
+      info[n * L + 1].sub[5] = t_b;
+      info[n * L + 1].sub[6] = t_c;
+    }
   }
 }
 
@@ -1280,10 +1324,10 @@ __global__ __launch_bounds__(kWG) void retina_nms_kernel(
     const int32_t* __restrict__ ccls, const int32_t* __restrict__ lvl_cnt,
     const uint16_t* __restrict__ ord, const uint32_t* __restrict__ maxc, float thr, int max_det,
     SegInfo* __restrict__ info, float4* __restrict__ ob, float* __restrict__ os,
-    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank, int fast_iou) {
+    int32_t* __restrict__ oc, uint8_t* __restrict__ ov, int inl_rank, int fast_iou, int fp_resolve) {
   extern __shared__ float4 dyn[];
   nms_image(blockIdx.x, dyn, g, topk, cscore, cbox, ccls, lvl_cnt, ord, maxc, thr, max_det, info, ob,
-            os, oc, ov, inl_rank, fast_iou);
+            os, oc, ov, inl_rank, fast_iou, fp_resolve);
 }
 
 struct FusedWs {
@@ -1373,13 +1417,14 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 1744 = 16 + 64 + 128 + 512 + 1024,
-  // 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 3792 = 16 + 64 + 128 + 512 + 1024 +
+  // 2048, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
   // DPP / permlane lane permutations, 512 = the finish's k-th select with
   // DPP / permlane reductions and scans, 1024 = the NMS's IoU only where
-  // boxes intersect (exact); 4 = floor and finish launched twice
+  // boxes intersect (exact), 2048 = the NMS tile resolved as a ballot fixed
+  // point over column words; 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1437,7 +1482,7 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   hipLaunchKernelGGL(retina_nms_kernel, dim3(N), dim3(kWG), lds, st, g, k, o.cscore, o.cbox,
                      o.ccls, o.lvl_cnt, o.ord, o.maxc, nms_thresh, max_det, o.info,
                      reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl,
-                     (var & 1024) ? 1 : 0);
+                     (var & 1024) ? 1 : 0, (var & 2048) ? 1 : 0);
   D2MI_LAUNCH_CHECK();
   return 0;
 }

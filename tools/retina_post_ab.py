@@ -83,7 +83,9 @@ def seg_debug(run, cls, N):
             line += (f" | nms at {us(t0, r[7]):.1f}: counts {us(r[7], r[8]):.1f} window {us(r[8], sub[s, 4]):.1f}"
                      f" scan({int(sub[s, 5])} tiles) {us(sub[s, 4], r[9]):.1f} [first tile"
                      f" {us(sub[s, 4], sub[s, 6]):.1f} rest {us(sub[s, 6], sub[s, 7]):.1f}"
-                     f" outputs {us(sub[s, 7], r[9]):.1f}]"
+                     f" outputs {us(sub[s, 7], r[9]):.1f}] first tile: rows"
+                     f" {us(sub[s, 4], sub[s + 1, 4]):.1f} barrier {us(sub[s + 1, 4], sub[s + 1, 5]):.1f}"
+                     f" resolve {us(sub[s + 1, 5], sub[s + 1, 6]):.1f}"
                      f" (end {us(t0, r[9]):.1f}) nms clock {mhz(7, 9):.0f} MHz")
         print(line, flush=True)
 
