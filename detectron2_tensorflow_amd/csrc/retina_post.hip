@@ -50,6 +50,7 @@ constexpr int kCV = 4;                    // float4 per collect thread per chunk
 constexpr int kChunk4 = kCT * kCV;        // float4 per chunk (16 KB)
 constexpr int kWaveSlots = 8;             // candidate slots per (chunk, wave)
 constexpr int kTile = 64;                 // NMS tile
+constexpr int kRankWin = 128;             // NMS window ranked in the NMS workgroup (retina_var 4096)
 constexpr int kPT = 1024;                 // compact: wave slots per part (one per thread)
 constexpr int kPartCap = kPT * kWaveSlots;  // compact: entries a part can hold
 
@@ -1060,6 +1061,43 @@ __device__ __forceinline__ void rank_of(int r, const float* sc, const int* cnt, 
   val = l * topk + j;
 }
 
+// The same rank restricted to merged positions < cap (the NMS's windowed rank,
+// retina_var 4096): every other level is searched only over its first cap
+// entries (a count of cap already puts the candidate at or past cap), so
+// ceil(log2(cap + 1)) rounds, and the rounds stay a loop: this runs once per
+// call from a cold instruction cache, where unrolled code costs more than
+// the loop (about 0.3-0.5 us per KB, profiles/r5_icache_probe.log).
+__device__ __forceinline__ void rank_of_capped(int r, const float* sc, const int* cnt, const int* cum,
+                                               int L, int topk, int cap, int& pos, int& val) {
+  int l = 0;
+  while (l + 1 < L && cum[l + 1] <= r) ++l;
+  const int j = r - cum[l];
+  const float sv = sc[l * topk + j];
+  int lo[D2MI_MAX_LEVELS], hi[D2MI_MAX_LEVELS];
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+    lo[m] = 0;
+    hi[m] = (m < L && m != l) ? min(cnt[m], cap) : 0;
+  }
+  const int rounds = 32 - __clz(cap);
+#pragma unroll 1
+  for (int step = 0; step < rounds; ++step) {
+#pragma unroll
+    for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
+      if (lo[m] < hi[m]) {
+        const int mid = (lo[m] + hi[m]) >> 1;
+        const float pv = sc[m * topk + mid];
+        if (m < l ? pv >= sv : pv > sv) lo[m] = mid + 1;
+        else hi[m] = mid;
+      }
+    }
+  }
+  pos = j;
+#pragma unroll
+  for (int m = 0; m < D2MI_MAX_LEVELS; ++m) pos += lo[m];
+  val = l * topk + j;
+}
+
 constexpr int kRankT = 256;
 __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
     RetinaGeo g, int topk, const float* __restrict__ cscore, const int32_t* __restrict__ lvl_cnt,
@@ -1157,7 +1195,7 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
     for (int q4 = t; 4 * q4 < capimg; q4 += kWG) reinterpret_cast<float4*>(rsc)[q4] = src[q4];
   }
   __syncthreads();
-  if (inl_rank) {
+  if (inl_rank == 1) {
     for (int r = t; r < s_total; r += kWG) {
       int pos, val;
       rank_of(r, rsc, rcnt, rcum, L, topk, pos, val);
@@ -1171,11 +1209,28 @@ __device__ __forceinline__ void nms_image(int n, float4* dyn, RetinaGeo g, int t
   int nk = 0;
   uint64_t t_win = 0, t_tile1 = 0, t_a = 0, t_b = 0, t_c = 0;
   int ntiles = 0;
-  for (int w0 = 0; w0 < total && nk < max_det; w0 += kWG) {
-    // window: the next 1,024 candidates in score order
-    const int wn = min(kWG, total - w0);
+  // inl_rank 2 (retina_var 4096): windows of kRankWin candidates, each ranked
+  // here just before it is used -- a candidate at position j of its level's
+  // list has j candidates above it, so a window [w0, w0 + W) only holds
+  // candidates with j < w0 + W; the NMS usually ends inside the first window
+  const int wsize = inl_rank == 2 ? kRankWin : kWG;
+  for (int w0 = 0; w0 < total && nk < max_det; w0 += wsize) {
+    // window: the next wsize candidates in score order
+    const int wn = min(wsize, total - w0);
+    if (inl_rank == 2) {
+      const int lim = w0 + wsize;  // list positions that can land in this window
+      for (int idx = t; idx < L * lim; idx += kWG) {
+        const int l = idx / lim, j = idx - l * lim;
+        if (j < rcnt[l]) {
+          int pos, val;
+          rank_of_capped(rcum[l] + j, rsc, rcnt, rcum, L, topk, lim, pos, val);
+          if (pos >= w0 && pos < lim) lord[pos - w0] = (uint16_t)val;
+        }
+      }
+      __syncthreads();
+    }
     if (t < wn) {
-      const int q = inl_rank ? (int)lord[w0 + t] : (int)ord[o0 + w0 + t];
+      const int q = inl_rank == 2 ? (int)lord[t] : inl_rank ? (int)lord[w0 + t] : (int)ord[o0 + w0 + t];
       const float4 c = cbox[o0 + q];
       const int cl = ccls[o0 + q];
       const float off = (float)cl * off1;
@@ -1417,14 +1472,15 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 3792 = 16 + 64 + 128 + 512 + 1024 +
-  // 2048, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 7888 = 16 + 64 + 128 + 512 + 1024 +
+  // 2048 + 4096, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
   // DPP / permlane lane permutations, 512 = the finish's k-th select with
   // DPP / permlane reductions and scans, 1024 = the NMS's IoU only where
   // boxes intersect (exact), 2048 = the NMS tile resolved as a ballot fixed
-  // point over column words; 4 = floor and finish launched twice
+  // point over column words, 4096 = no rank launch: the NMS ranks each
+  // 128-candidate window itself; 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1472,16 +1528,19 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   // (tuning "retina_rank": 1 = the merge rank inside the NMS workgroup, 0 = its own launch;
   // measured: 165.6 vs 124.4 us per call -- one CU's LDS binary searches over ~4.7 k
   // candidates cost far more than the launch they save, profiles/r5_retina_post_ab_rank*.log)
-  if (!inl) {
+  // (retina_var 4096: no rank launch -- the NMS ranks each 128-candidate
+  // window itself, inl_rank 2)
+  const int inl_arg = inl ? 1 : ((var & 4096) ? 2 : 0);
+  if (!inl_arg) {
     hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
                        (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);
     D2MI_LAUNCH_CHECK();
   }
   const size_t lds = (size_t)(max_det + kWG) * (2 * sizeof(float4) + sizeof(float) + sizeof(int32_t)) +
-                     (inl ? 16 + (size_t)capimg * (sizeof(float) + sizeof(uint16_t)) : 0);
+                     (inl_arg ? 16 + (size_t)capimg * (sizeof(float) + sizeof(uint16_t)) : 0);
   hipLaunchKernelGGL(retina_nms_kernel, dim3(N), dim3(kWG), lds, st, g, k, o.cscore, o.cbox,
                      o.ccls, o.lvl_cnt, o.ord, o.maxc, nms_thresh, max_det, o.info,
-                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl,
+                     reinterpret_cast<float4*>(out_boxes), out_scores, out_classes, out_valid, inl_arg,
                      (var & 1024) ? 1 : 0, (var & 2048) ? 1 : 0);
   D2MI_LAUNCH_CHECK();
   return 0;
