@@ -828,8 +828,14 @@ __global__ __launch_bounds__(kWG) void retina_finish_kernel(
           const int i = j * kWG + t;
           ent[j] = 0ull;
           if (i < tot) {
+            // the part holding entry i: the last p with s_pre[p] <= i (empty
+            // parts repeat a prefix), by binary search -- six LDS rounds for
+            // all eight entries together (the r6 linear walk was up to np
+            // dependent rounds per entry)
             int p = 0;
-            while (p + 1 < np && s_pre[p + 1] <= i) ++p;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+              if (p + step < np && s_pre[p + step] <= i) p += step;
             ent[j] = cand[(size_t)(gp0 + p) * kPartCap + (i - s_pre[p])];
           }
         }
