@@ -39,8 +39,9 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
 // popcount tiles; retina_var: the r6 RetinaNet post (compaction, early
 // select bound, DPP / permlane bitonic and select, NMS IoU only where boxes
 // meet, NMS tiles resolved as a ballot fixed point, the merge rank done by
-// the NMS per 128-candidate window: 7888; 0 = the r5 form)
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 7888};
+// the NMS per 128-candidate window, the floor's radix select: 16080; 0 = the
+// r5 form)
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 16080};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

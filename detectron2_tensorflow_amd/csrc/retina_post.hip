@@ -218,7 +218,7 @@ __device__ __forceinline__ uint64_t bitonic1024_lanes(uint64_t v, uint64_t* lds)
 // ------------------------------------------------------------------ floor
 __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restrict__ base,
                                                            Levels lv, RetinaGeo g, int topk,
-                                                           int force_exact,
+                                                           int force_exact, int radix,
                                                            SegInfo* __restrict__ info,
                                                            uint32_t* __restrict__ maxc) {
   const uint64_t t_start = stamp(), c_start = cycles();
@@ -282,12 +282,61 @@ __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restri
   // value that at least ts maxima reach), by wave 0 alone: ballot counts, no
   // further barriers
   __shared__ uint32_t mx[kWG];
+  uint32_t f0 = 0;
+  if (radix) {
+    // (retina_var 8192) the same value -- the ts-th largest maximum with its
+    // low 8 bits cleared -- by a radix select over the whole workgroup: three
+    // 8-bit passes of LDS histogram atomics, each bin searched from the top by
+    // wave 0 (4 bins per lane, one DPP scan), instead of wave 0's 24 rounds
+    // of 16 compare-ballots
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_pref, s_krem;
+    if (t == 0) {
+      s_pref = 0;
+      s_krem = (uint32_t)ts;
+    }
+    for (int pass = 0; pass < 3; ++pass) {
+      const int sh = 24 - 8 * pass;
+      if (t < 256) hist[t] = 0;
+      __syncthreads();
+      const uint32_t pref = s_pref;
+      if (pass == 0 || (best >> (sh + 8)) == pref) atomicAdd(&hist[(best >> sh) & 255u], 1u);
+      __syncthreads();
+      if (t < 64) {
+        const uint32_t krem = s_krem;
+        uint32_t c4[4], loc = 0;  // lane t: bins 255 - 4t .. 252 - 4t
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c4[j] = hist[255 - (4 * t + j)];
+          loc += c4[j];
+        }
+        const uint32_t incl = wave_incl_scan_dpp(loc);
+        const uint64_t hitm = __ballot(incl >= krem);
+        const int first = hitm ? __ffsll((unsigned long long)hitm) - 1 : 63;
+        if (t == first) {
+          uint32_t acc = incl - loc;
+          int bin = 252 - 4 * t;
+          for (int j = 0; j < 4; ++j) {
+            if (acc + c4[j] >= krem) {
+              bin = 255 - (4 * t + j);
+              break;
+            }
+            acc += c4[j];
+          }
+          s_pref = (pref << 8) | (uint32_t)bin;
+          s_krem = krem - acc;
+        }
+      }
+      __syncthreads();
+    }
+    f0 = s_pref << 8;
+    if (t >= 64) return;
+  } else {
   mx[t] = best;
   __syncthreads();
   if (t >= 64) return;
   // (the top 24 bits only: the floor is a heuristic, a key at most 255
   // steps lower collects a few more candidates and changes no result)
-  uint32_t f0 = 0;
   {
     uint32_t vals[kWG / 64];
 #pragma unroll
@@ -299,6 +348,7 @@ __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restri
       for (int j = 0; j < kWG / 64; ++j) c += __popcll(__ballot(vals[j] >= cand));
       if (c >= ts) f0 = cand;
     }
+  }
   }
   uint32_t floor = f0, exact_lo = f0;
   if (f0 > kKeyNegInf && f0 <= kKeyPosInf) {  // no sigmoid tie across exact_lo
@@ -1478,15 +1528,16 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 7888 = 16 + 64 + 128 + 512 + 1024 +
-  // 2048 + 4096, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 16080 = 16 + 64 + 128 + 512 + 1024 +
+  // 2048 + 4096 + 8192, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
   // DPP / permlane lane permutations, 512 = the finish's k-th select with
   // DPP / permlane reductions and scans, 1024 = the NMS's IoU only where
   // boxes intersect (exact), 2048 = the NMS tile resolved as a ballot fixed
   // point over column words, 4096 = no rank launch: the NMS ranks each
-  // 128-candidate window itself; 4 = floor and finish launched twice
+  // 128-candidate window itself, 8192 = the floor's ts-th maximum by a
+  // radix select over the workgroup; 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1499,7 +1550,7 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   const int reps = (var & 4) ? 2 : 1;
   for (int rep = 0; rep < reps; ++rep) {
     hipLaunchKernelGGL(retina_floor_kernel, dim3(S), dim3(kWG), 0, st, cls[0], lv, g, k,
-                       force_exact ? 1 : 0, o.info, o.maxc);
+                       force_exact ? 1 : 0, (var & 8192) ? 1 : 0, o.info, o.maxc);
     D2MI_LAUNCH_CHECK();
   }
   // persistent collect grid: the workgroups the device holds at once

@@ -589,14 +589,15 @@ def test_retinanet_inference_vs_oracle(dev, dist, path):
     pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
     its in-workgroup exact select forced on every level (2), the same with the
     merge rank inside the NMS workgroup (tuning "retina_rank" = 1; default: its
-    own launch), the r5 form (tuning "retina_var" = 0; the default 7888
+    own launch), the r5 form (tuning "retina_var" = 0; the default 16080
     compacts the wave slots with many workgroups before the finish, stops the
     finish's select at the first bound leaving <= 1,024 keys, runs its bitonic
     exchanges, reductions and scans in DPP / permlane lane permutations,
     computes the NMS IoU only where the boxes intersect, resolves each NMS
     tile as a ballot fixed point and ranks the merged candidates inside the
-    NMS workgroup one 128-candidate window at a time), and the unfused top-k /
-    sort / mask NMS pipeline (0)."""
+    NMS workgroup one 128-candidate window at a time, and selects the floor by
+    a workgroup radix select), and the unfused top-k / sort / mask NMS
+    pipeline (0)."""
     from detectron2_tensorflow_amd.layers import ops as lops
     old = lops.get_tuning("retina_fused")
     old_rank = lops.get_tuning("retina_rank")
