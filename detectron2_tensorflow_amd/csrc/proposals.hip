@@ -240,14 +240,27 @@ __global__ __launch_bounds__(kMergeT) void rpn_merge_rank_kernel(
     cum[L] = acc;
   }
   __syncthreads();
-  for (int q = t; q < L * post; q += kMergeT) {
-    const int l = q / post, i = q - l * post;
-    uint32_t w = 0;
-    if (i < cnt[l]) {
-      const int s = n * L + l;
-      w = orderable(tvals[(size_t)s * k + keep[(size_t)s * post + i]]);
+  // every level's kept score words into LDS: 8 entries per thread per round,
+  // their keep indices loaded together and then their scores (two dependent
+  // load rounds per 8 entries instead of per entry)
+  for (int q0 = t; q0 < L * post; q0 += 8 * kMergeT) {
+    int ix[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + u * kMergeT;
+      const int l = q / post, i = q - l * post;
+      ix[u] = (q < L * post && i < cnt[l]) ? keep[(size_t)(n * L + l) * post + i] : -1;
     }
-    sw[q] = w;
+    uint32_t w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + u * kMergeT;
+      const int l = q / post;
+      w[u] = ix[u] >= 0 ? orderable(tvals[(size_t)(n * L + l) * k + ix[u]]) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (q0 + u * kMergeT < L * post) sw[q0 + u * kMergeT] = w[u];
   }
   __syncthreads();
   const int r = blockIdx.x * kMergeT + t;
@@ -268,10 +281,16 @@ __global__ __launch_bounds__(kMergeT) void rpn_merge_rank_kernel(
 #pragma unroll
   for (int m = 0; m < D2MI_MAX_LEVELS; ++m) {
     lo[m] = 0;
-    hi[m] = (m < L && m != l) ? cnt[m] : 0;
+    // (only positions < post are kept: a level searched over its first post
+    // entries -- a count of post already puts this entry past the cut -- in
+    // ceil(log2(post + 1)) rounds, kept as a loop: r6, 14 unrolled rounds
+    // before; the same cut for every entry whose position is < post)
+    hi[m] = (m < L && m != l) ? min(cnt[m], post) : 0;
   }
+  const int rounds = 32 - __clz(post);
   // earlier levels: entries with word >= mine come first; later: word > mine
-  for (int step = 0; step < 14; ++step) {
+#pragma unroll 1
+  for (int step = 0; step < rounds; ++step) {
     uint32_t pv[D2MI_MAX_LEVELS];
 #pragma unroll
     for (int m = 0; m < D2MI_MAX_LEVELS; ++m)
