@@ -1255,11 +1255,74 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 }
 
 // float4 form (Cout % 4 == 0, 16-B aligned partial / y): same split order.
+// epilogue() on four consecutive channels of one row (Cout % 4 == 0, co % 4
+// == 0): the same operations in the same order per channel, with the bias,
+// top-down, residual and gate operands read as one float4 each (r6: the
+// per-channel form issued four scalar loads of each)
+__device__ __forceinline__ float4 epilogue4(const ConvArgs& a, const Geo& g, float4 acc, int m,
+                                            int co) {
+  float4 v = acc;
+  if (a.bias) {
+    const float4 b = *reinterpret_cast<const float4*>(a.bias + co);
+    v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+  } else {
+    v = make_float4(v.x + 0.f, v.y + 0.f, v.z + 0.f, v.w + 0.f);
+  }
+  const bool relu = (a.flags & kRelu) != 0, after = (a.flags & kReluAfterResidual) != 0;
+  if (relu && !after) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  if (a.topdown) {
+    const int n = m / (g.OH * g.OW);
+    const int rem = m - n * g.OH * g.OW;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
+    const float4 t = *reinterpret_cast<const float4*>(
+        a.topdown + (((size_t)n * a.tdH + (oh >> 1)) * a.tdW + (ow >> 1)) * a.Cout + co);
+    v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
+  }
+  if (a.residual) {
+    const float4 r = *reinterpret_cast<const float4*>(a.residual + (size_t)m * a.Cout + co);
+    v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+  }
+  if (relu && after) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  if (g.gate) {
+    const float4 q = *reinterpret_cast<const float4*>(g.gate + (size_t)m * a.Cout + co);
+    if (!(q.x > 0.f)) v.x = 0.f;
+    if (!(q.y > 0.f)) v.y = 0.f;
+    if (!(q.z > 0.f)) v.z = 0.f;
+    if (!(q.w > 0.f)) v.w = 0.f;
+  }
+  return v;
+}
+
+// The split-K sum in split order + the epilogue, one float4 of channels per
+// thread and step.  32-bit row / channel arithmetic when the slab has < 2^31
+// float4s (every training shape; the 64-bit division cost more VALU than the
+// loads it indexed), the float4 epilogue operands, and the split loads eight
+// at a time.
 __global__ void splitk_reduce4_kernel(ConvArgs a) {
   const Geo g = geo_of(a);
   const int64_t total = (int64_t)(a.m_end - a.m_base) * a.Cout;
   const int64_t total4 = total / 4;
   const float4* p4 = reinterpret_cast<const float4*>(a.partial);
+  if (total4 < (1ll << 31) - (int64_t)gridDim.x * blockDim.x) {
+    const int t4 = (int)total4, C4 = a.Cout >> 2;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < t4; i += gridDim.x * blockDim.x) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+      for (int s = 0; s < a.splits; ++s) {
+        const float4 v = p4[(size_t)s * t4 + i];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      const int ml = i / C4, co = 4 * (i - ml * C4);
+      const int m = a.m_base + ml;
+      const float4 o = epilogue4(a, g, acc, m, co);
+      if (a.nt_store) st4_nt(a.y + (size_t)m * a.Cout + co, o);
+      else *reinterpret_cast<float4*>(a.y + (size_t)m * a.Cout + co) = o;
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1813,7 +1876,11 @@ static int conv_core(const float* x, const float* w_packed, const float* bias,
     D2MI_LAUNCH_CHECK();
     if (c.splits > 1) {
       const int64_t total = (int64_t)(c.m_end - c.m_base) * Cout;
-      if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+      // (the float4 epilogue reads bias / top-down / residual / gate as float4s)
+      const uintptr_t ops4 = (uintptr_t)c.bias | (uintptr_t)c.topdown | (uintptr_t)c.residual |
+                             (uintptr_t)c.gate;
+      if (Cout % 4 == 0 && ((uintptr_t)c.partial & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+          (ops4 & 15) == 0) {
         const int gr = (int)std::min<int64_t>((total / 4 + 255) / 256, 8192);
         hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(gr), dim3(256), 0, st, c);
       } else {

@@ -20,17 +20,20 @@
 namespace d2mi {
 namespace {
 
+// I: the element index type -- uint32_t when the tensor has < 2^31 float4s
+// (r6: the int64 divisions and remainders were most of these HBM passes'
+// instructions), int64_t otherwise
+template <typename I>
 __global__ void upsample2x_grad_kernel(const float4* __restrict__ gy, int N, int OH, int OW,
                                        int C4, int TH, int TW, float4* __restrict__ gtd) {
-  const int64_t total = (int64_t)N * TH * TW * C4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4);
-    int64_t p = i / C4;
-    const int tw = (int)(p % TW);
-    p /= TW;
-    const int th = (int)(p % TH);
-    const int n = (int)(p / TH);
+  const I total = (I)N * TH * TW * C4;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (I)C4);
+    I p = i / (I)C4;
+    const int tw = (int)(p % (I)TW);
+    p /= (I)TW;
+    const int th = (int)(p % (I)TH);
+    const int n = (int)(p / (I)TH);
     const int h0 = 2 * th, w0 = 2 * tw;
     const float4* row = gy + (((int64_t)n * OH + h0) * OW + w0) * C4 + c;
     float4 s = row[0];
@@ -51,19 +54,19 @@ __global__ void upsample2x_grad_kernel(const float4* __restrict__ gy, int N, int
   }
 }
 
+template <typename I>
 __global__ void stride_scatter_kernel(const float4* __restrict__ g, const float4* __restrict__ add,
                                       const float4* __restrict__ add2,
                                       const float4* __restrict__ gate, int N, int H, int W, int C4,
                                       int stride, int GH, int GW, float4* __restrict__ out) {
-  const int64_t total = (int64_t)N * H * W * C4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4);
-    int64_t p = i / C4;
-    const int w = (int)(p % W);
-    p /= W;
-    const int h = (int)(p % H);
-    const int n = (int)(p / H);
+  const I total = (I)N * H * W * C4;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (I)C4);
+    I p = i / (I)C4;
+    const int w = (int)(p % (I)W);
+    p /= (I)W;
+    const int h = (int)(p % (I)H);
+    const int n = (int)(p / (I)H);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (h % stride == 0 && w % stride == 0)
       v = g[(((int64_t)n * GH + h / stride) * GW + w / stride) * C4 + c];
@@ -87,6 +90,9 @@ __global__ void stride_scatter_kernel(const float4* __restrict__ g, const float4
 }
 
 int grid_for(int64_t total) { return (int)std::min<int64_t>((total + 255) / 256, 16384); }
+// 32-bit element indices suffice: the index never passes 2^31 (total + one
+// grid stride)
+bool narrow_index(int64_t total) { return total + 256ll * grid_for(total) < (1ll << 31); }
 
 }  // namespace
 }  // namespace d2mi
@@ -100,9 +106,14 @@ extern "C" int d2mi_upsample2x_grad(const float* gy, int N, int OH, int OW, int 
                "gy / gtd must be 16-byte aligned");
   const int TH = (OH + 1) / 2, TW = (OW + 1) / 2;
   const int64_t total = (int64_t)N * TH * TW * (C / 4);
-  hipLaunchKernelGGL(upsample2x_grad_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     as_stream(stream), reinterpret_cast<const float4*>(gy), N, OH, OW, C / 4, TH,
-                     TW, reinterpret_cast<float4*>(gtd));
+  if (narrow_index(total))
+    hipLaunchKernelGGL(upsample2x_grad_kernel<uint32_t>, dim3(grid_for(total)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(gy), N, OH, OW, C / 4, TH,
+                       TW, reinterpret_cast<float4*>(gtd));
+  else
+    hipLaunchKernelGGL(upsample2x_grad_kernel<int64_t>, dim3(grid_for(total)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(gy), N, OH, OW, C / 4, TH,
+                       TW, reinterpret_cast<float4*>(gtd));
   D2MI_LAUNCH_CHECK();
   return 0;
 }
@@ -118,11 +129,18 @@ extern "C" int d2mi_stride_scatter_ex(const float* g, const float* add, const fl
                "g / add / add2 / gate / out must be 16-byte aligned");
   const int GH = (H - 1) / stride + 1, GW = (W - 1) / stride + 1;
   const int64_t total = (int64_t)N * H * W * (C / 4);
-  hipLaunchKernelGGL(stride_scatter_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     as_stream(stream), reinterpret_cast<const float4*>(g),
-                     reinterpret_cast<const float4*>(add), reinterpret_cast<const float4*>(add2),
-                     reinterpret_cast<const float4*>(gate), N, H, W, C / 4, stride, GH, GW,
-                     reinterpret_cast<float4*>(out));
+  if (narrow_index(total))
+    hipLaunchKernelGGL(stride_scatter_kernel<uint32_t>, dim3(grid_for(total)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(g),
+                       reinterpret_cast<const float4*>(add), reinterpret_cast<const float4*>(add2),
+                       reinterpret_cast<const float4*>(gate), N, H, W, C / 4, stride, GH, GW,
+                       reinterpret_cast<float4*>(out));
+  else
+    hipLaunchKernelGGL(stride_scatter_kernel<int64_t>, dim3(grid_for(total)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(g),
+                       reinterpret_cast<const float4*>(add), reinterpret_cast<const float4*>(add2),
+                       reinterpret_cast<const float4*>(gate), N, H, W, C / 4, stride, GH, GW,
+                       reinterpret_cast<float4*>(out));
   D2MI_LAUNCH_CHECK();
   return 0;
 }
