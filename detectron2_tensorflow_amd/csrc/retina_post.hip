@@ -1157,7 +1157,7 @@ __device__ __forceinline__ void rank_of_capped(int r, const float* sc, const int
 constexpr int kRankT = 256;
 __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
     RetinaGeo g, int topk, const float* __restrict__ cscore, const int32_t* __restrict__ lvl_cnt,
-    uint16_t* __restrict__ ord) {
+    uint16_t* __restrict__ ord, int rolled) {
   extern __shared__ float sc[];  // [capimg]
   __shared__ int cnt[D2MI_MAX_LEVELS], cum[D2MI_MAX_LEVELS + 1];
   const int n = blockIdx.y, t = threadIdx.x;
@@ -1191,7 +1191,10 @@ __global__ __launch_bounds__(kRankT) void retina_rank_kernel(
   const int r = blockIdx.x * kRankT + t;
   if (r >= cum[L]) return;
   int pos, val;
-  rank_of(r, sc, cnt, cum, L, topk, pos, val);
+  // (retina_var 32: the rounds as a loop, ceil(log2(topk + 1)) of them --
+  // every list holds <= topk, so the cap changes no position)
+  if (rolled) rank_of_capped(r, sc, cnt, cum, L, topk, topk, pos, val);
+  else rank_of(r, sc, cnt, cum, L, topk, pos, val);
   ord[o0 + pos] = (uint16_t)val;
 }
 
@@ -1528,8 +1531,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 16080 = 16 + 64 + 128 + 512 + 1024 +
-  // 2048 + 4096 + 8192, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 12016 = 16 + 32 + 64 + 128 + 512 +
+  // 1024 + 2048 + 8192, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
   // DPP / permlane lane permutations, 512 = the finish's k-th select with
@@ -1537,7 +1540,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   // boxes intersect (exact), 2048 = the NMS tile resolved as a ballot fixed
   // point over column words, 4096 = no rank launch: the NMS ranks each
   // 128-candidate window itself, 8192 = the floor's ts-th maximum by a
-  // radix select over the workgroup; 4 = floor and finish launched twice
+  // radix select over the workgroup, 32 = the rank launch's search rounds
+  // capped and kept as a loop; 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1590,7 +1594,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   const int inl_arg = inl ? 1 : ((var & 4096) ? 2 : 0);
   if (!inl_arg) {
     hipLaunchKernelGGL(retina_rank_kernel, dim3((capimg + kRankT - 1) / kRankT, N), dim3(kRankT),
-                       (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord);
+                       (size_t)capimg * sizeof(float), st, g, k, o.cscore, o.lvl_cnt, o.ord,
+                       (var & 32) ? 1 : 0);
     D2MI_LAUNCH_CHECK();
   }
   const size_t lds = (size_t)(max_det + kWG) * (2 * sizeof(float4) + sizeof(float) + sizeof(int32_t)) +

@@ -579,7 +579,7 @@ def _retina_logits(rng, shape, dist):
 
 
 @pytest.mark.parametrize("path", ["fused", "fused_exact_select", "fused_rank_inline", "fused_r5",
-                                  "unfused"])
+                                  "fused_rank_windowed", "unfused"])
 @pytest.mark.parametrize("dist", ["normal", "quantized", "saturated", "sparse"])
 def test_retinanet_inference_vs_oracle(dev, dist, path):
     """Dense top-k + decode + NMS vs the oracle.  The distributions drive the
@@ -589,23 +589,23 @@ def test_retinanet_inference_vs_oracle(dev, dist, path):
     pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
     its in-workgroup exact select forced on every level (2), the same with the
     merge rank inside the NMS workgroup (tuning "retina_rank" = 1; default: its
-    own launch), the r5 form (tuning "retina_var" = 0; the default 16080
+    own launch), the r5 form (tuning "retina_var" = 0; the default 12016
     compacts the wave slots with many workgroups before the finish, stops the
     finish's select at the first bound leaving <= 1,024 keys, runs its bitonic
     exchanges, reductions and scans in DPP / permlane lane permutations,
     computes the NMS IoU only where the boxes intersect, resolves each NMS
-    tile as a ballot fixed point and ranks the merged candidates inside the
-    NMS workgroup one 128-candidate window at a time, and selects the floor by
-    a workgroup radix select), and the unfused top-k / sort / mask NMS
+    tile as a ballot fixed point, selects the floor by a workgroup radix
+    select and loops the rank launch's rounds), the same with the merge rank
+    windowed inside the NMS (16080), and the unfused top-k / sort / mask NMS
     pipeline (0)."""
     from detectron2_tensorflow_amd.layers import ops as lops
     old = lops.get_tuning("retina_fused")
     old_rank = lops.get_tuning("retina_rank")
     old_var = lops.get_tuning("retina_var")
     lops.set_tuning("retina_fused", {"fused": 1, "fused_exact_select": 2, "fused_rank_inline": 1,
-                                     "fused_r5": 1, "unfused": 0}[path])
+                                     "fused_r5": 1, "fused_rank_windowed": 1, "unfused": 0}[path])
     lops.set_tuning("retina_rank", 1 if path == "fused_rank_inline" else 0)
-    lops.set_tuning("retina_var", 0 if path == "fused_r5" else old_var)
+    lops.set_tuning("retina_var", {"fused_r5": 0, "fused_rank_windowed": 16080}.get(path, old_var))
     try:
         _retinanet_inference_vs_oracle(dev, dist)
     finally:

@@ -98,6 +98,9 @@ def main():
     ap.add_argument("--arms", default="0,1", help="retina_fused values to time")
     ap.add_argument("--vars", default="",
                     help="time the fused path under these tuning retina_var values instead")
+    ap.add_argument("--from-model", action="store_true",
+                    help="the head outputs of bench.py's calibrated RetinaNet R101-FPN on its "
+                         "synthetic batch (the in-model score distribution) instead of iid logits")
     ap.add_argument("--debug", action="store_true",
                     help="print the fused path's per-segment floor state (workspace head)")
     a = ap.parse_args()
@@ -108,7 +111,22 @@ def main():
     hw = [(100, 168), (50, 84), (25, 42), (13, 21), (7, 11)]
     strides = [8, 16, 32, 64, 128]
     cls, box = [], []
-    for h, w in hw:
+    if a.from_model:
+        import bench
+        sys.argv = [sys.argv[0], "--model", "retinanet_R_101_FPN", "--mode", "infer"]
+        bargs = bench.parse()
+        _, model = bench.build(bargs, dev)
+        batch = bench.synthetic_batch(bargs, dev, 0)
+        bench.calibrate_scores(model, batch)
+        with torch.no_grad():
+            det = model.detector
+            feats = model.neck(model.backbone(model.preprocess_image(batch).tensor))
+            c_out, b_out = det.head([feats[f] for f in det.in_features])
+        cls = [t.contiguous() for t in c_out]
+        box = [t.contiguous() for t in b_out]
+        N = cls[0].shape[0]
+        print("from model: levels", [tuple(t.shape) for t in cls], flush=True)
+    for h, w in ([] if a.from_model else hw):
         x = torch.randn(N, h, w, A * K, generator=g) - 3.0
         if a.dist == "saturated":
             x = torch.where(torch.rand(x.shape, generator=g) < 0.2, x + 30.0, x)
