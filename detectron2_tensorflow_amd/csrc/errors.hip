@@ -39,10 +39,11 @@ const char* const kTuneEnv[kTuneCount] = {"D2MI_CONV_WS",   "D2MI_ROI_FWD",   "D
 // popcount tiles; retina_var: the r6 RetinaNet post (compaction, early
 // select bound, DPP / permlane bitonic and select, NMS IoU only where boxes
 // meet, NMS tiles resolved as a ballot fixed point, the floor's radix select,
-// the rank launch's rounds looped: 12016; 0 = the r5 form; + 4096, the rank
+// the rank launch's rounds looped, small levels' floor samples spread over the
+// level: 12018; 0 = the r5 form; + 4096, the rank
 // inside the NMS per 128-candidate window, is faster on iid logits and slower
 // on a model's head outputs, where the NMS needs several windows)
-const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 12016};
+const int kTuneDefault[kTuneCount] = {2, -1, 1, 1, 6, 1, 1, 1, 16, 8192, 8192, 1, 1, 1, 1, 16, 1, 2, 0, 8, 0, 0, 0, 2, 12018};
 int g_tune[kTuneCount];
 bool g_tune_set[kTuneCount];
 }  // namespace

@@ -219,6 +219,7 @@ __device__ __forceinline__ uint64_t bitonic1024_lanes(uint64_t v, uint64_t* lds)
 __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restrict__ base,
                                                            Levels lv, RetinaGeo g, int topk,
                                                            int force_exact, int radix,
+                                                           int spread,
                                                            SegInfo* __restrict__ info,
                                                            uint32_t* __restrict__ maxc) {
   const uint64_t t_start = stamp(), c_start = cycles();
@@ -266,6 +267,19 @@ __global__ __launch_bounds__(kWG) void retina_floor_kernel(const float* __restri
     }
     const int64_t e = (int64_t)full * kRunStride + t;  // the last run, one key per thread
     if (e < len) best = max(best, orderable(p[e]));
+  } else if (spread) {
+    // (few runs, retina_var 2) the same number of samples,
+    // spread evenly over the whole segment: on a model's outputs the first
+    // 1,024 keys of a small level are one or two anchor positions, and P7's
+    // floor from them left 9,969 keys above it -- past the candidate buffer,
+    // so the exact select ran (44 us on the critical path)
+    int64_t ns = 0;
+    for (int r = 0; r < nruns; ++r) ns += min<int64_t>(kRun, len - (int64_t)r * kRunStride);
+    const int64_t stride = max<int64_t>(1, len / ns);
+    for (int r = 0; r < nruns; ++r) {
+      const int64_t i = (int64_t)r * kRun + t;
+      if (i < ns) best = max(best, orderable(p[i * stride]));
+    }
   } else {  // (few runs: one sample per thread and run, so the maxima are the samples)
     for (int r = 0; r < nruns; ++r) {
       const int64_t e = (int64_t)r * kRunStride + t;
@@ -1531,8 +1545,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
                     size_t workspace_bytes, hipStream_t st, bool force_exact) {
   const int L = lv.L, S = N * L;
   D2MI_REQUIRE(retina_fused_eligible(L, k, max_det), "fused RetinaNet sizes out of range");
-  // tuning "retina_var" (r6 bits; default 12016 = 16 + 32 + 64 + 128 + 512 +
-  // 1024 + 2048 + 8192, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
+  // tuning "retina_var" (r6 bits; default 12018 = 2 + 16 + 32 + 64 + 128 +
+  // 512 + 1024 + 2048 + 8192, 0 = the r5 form): 16 = the wave slots compacted by many workgroups before the
   // finish (one launch more), 64 = the finish's select stops at the first
   // bound that leaves <= 1,024 keys, 128 = the finish's bitonic exchanges in
   // DPP / permlane lane permutations, 512 = the finish's k-th select with
@@ -1541,7 +1555,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   // point over column words, 4096 = no rank launch: the NMS ranks each
   // 128-candidate window itself, 8192 = the floor's ts-th maximum by a
   // radix select over the workgroup, 32 = the rank launch's search rounds
-  // capped and kept as a loop; 4 = floor and finish launched twice
+  // capped and kept as a loop, 2 = a small level's floor samples spread over
+  // the whole level; 4 = floor and finish launched twice
   // (both idempotent: the stamps then time warm second launches)
   const int var = tuning(kTuneRetinaVar);
   RetinaGeo g;
@@ -1554,7 +1569,8 @@ int retinanet_fused(const float* const* cls, const float* const* box, const Leve
   const int reps = (var & 4) ? 2 : 1;
   for (int rep = 0; rep < reps; ++rep) {
     hipLaunchKernelGGL(retina_floor_kernel, dim3(S), dim3(kWG), 0, st, cls[0], lv, g, k,
-                       force_exact ? 1 : 0, (var & 8192) ? 1 : 0, o.info, o.maxc);
+                       force_exact ? 1 : 0, (var & 8192) ? 1 : 0, (var & 2) ? 1 : 0, o.info,
+                       o.maxc);
     D2MI_LAUNCH_CHECK();
   }
   // persistent collect grid: the workgroups the device holds at once

@@ -78,7 +78,7 @@ const char* d2mi_last_error(void);
  *   "solo_mfma"    SOLOv2 Matrix-NMS intersections on int8 MFMA: 2 (default)
  *                  = bits expanded by an LDS table, 1 = by arithmetic; 0 = the
  *                  AND + popcount tiles;
- *   "retina_var"   RetinaNet fused-path variants (bits; default 12016, 0 = the
+ *   "retina_var"   RetinaNet fused-path variants (bits; default 12018, 0 = the
  *                  r5 form): 16 = the wave slots compacted by many workgroups
  *                  before the finish, 64 = the finish's k-th select stopped at
  *                  the first bound leaving <= 1,024 keys, 128 = its bitonic
@@ -89,8 +89,9 @@ const char* d2mi_last_error(void);
  *                  4096 = no rank launch (the NMS ranks each 128-candidate
  *                  window; off by default), 8192 = the floor's ts-th maximum
  *                  by a workgroup radix select, 32 = the rank launch's search
- *                  rounds capped and looped, 4 = floor and finish launched
- *                  twice (measurement only). */
+ *                  rounds capped and looped, 2 = a small level's floor
+ *                  samples spread over the level, 4 = floor and finish
+ *                  launched twice (measurement only). */
 int d2mi_set_tuning(const char* key, int value);
 /* Current value of a d2mi_set_tuning key (INT32_MIN for an unknown key). */
 int d2mi_get_tuning(const char* key);

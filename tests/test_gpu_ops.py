@@ -589,13 +589,14 @@ def test_retinanet_inference_vs_oracle(dev, dist, path):
     pipeline (csrc/retina_post.hip, tuning "retina_fused" = 1), the same with
     its in-workgroup exact select forced on every level (2), the same with the
     merge rank inside the NMS workgroup (tuning "retina_rank" = 1; default: its
-    own launch), the r5 form (tuning "retina_var" = 0; the default 12016
+    own launch), the r5 form (tuning "retina_var" = 0; the default 12018
     compacts the wave slots with many workgroups before the finish, stops the
     finish's select at the first bound leaving <= 1,024 keys, runs its bitonic
     exchanges, reductions and scans in DPP / permlane lane permutations,
     computes the NMS IoU only where the boxes intersect, resolves each NMS
     tile as a ballot fixed point, selects the floor by a workgroup radix
-    select and loops the rank launch's rounds), the same with the merge rank
+    select spreading a small level's samples over the level, and loops the
+    rank launch's rounds), the same with the merge rank
     windowed inside the NMS (16080), and the unfused top-k / sort / mask NMS
     pipeline (0)."""
     from detectron2_tensorflow_amd.layers import ops as lops
