@@ -135,6 +135,7 @@ _SIGS = {
                                     c_float, c_float, P, P, P, c_size_t, P]),
     "d2mi_stem_pool": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_stem_conv": (c_int, [P, P, c_int, c_int, c_int, P, P]),
+    "d2mi_preprocess_images": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_rpn_loss_blocks": (c_int, []),
     "d2mi_rpn_loss_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P]),
     "d2mi_rpn_loss_bwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P, P,

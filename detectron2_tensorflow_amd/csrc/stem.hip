@@ -205,10 +205,75 @@ __global__ __launch_bounds__(kStemThreads) void stem_conv_kernel(const float* __
     }
 }
 
+// The input pipeline ahead of the stem in one pass (lib/modeling/meta_arch/
+// rcnn.py:146-157 preprocess_image, structures/image_list.py:89-100):
+// (image - mean) / std per channel, the channel flip to BGR, and the zero
+// pad to the size divisibility -- one read of the image, one write of the
+// padded map (torch's form: a subtract, a divide, a flip gather, a fill and a
+// copy, five launches of ~12 us each over the whole image per step).  The
+// same two IEEE operations per value, so the result is the same bits.
+// grid (row chunks, N * OHp): one padded output row per blockIdx.y, FOUR
+// consecutive output floats per thread (a float4 store when the row is a
+// whole number of float4s); the input row (W * 3 floats) is read by scalars.
+template <bool VEC>
+__global__ __launch_bounds__(256) void preprocess_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ stdv, int H,
+                                                         int W, int OHp, int OWp, int flip,
+                                                         float* __restrict__ out) {
+  const int row = blockIdx.y;  // n * OHp + y
+  const int n = row / OHp, y = row - n * OHp;
+  const int f0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  const int rowf = OWp * 3;
+  if (f0 >= rowf) return;
+  const float m[3] = {mean[0], mean[1], mean[2]};
+  const float s[3] = {stdv[0], stdv[1], stdv[2]};
+  const float* xr = x + ((size_t)n * H + y) * W * 3;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = f0 + k;
+    const int px = f / 3, c = f - 3 * px;
+    const int cs = flip ? 2 - c : c;
+    // (the register arrays by a selected constant: no dynamic index into scratch)
+    const float mc = cs == 0 ? m[0] : (cs == 1 ? m[1] : m[2]);
+    const float sc = cs == 0 ? s[0] : (cs == 1 ? s[1] : s[2]);
+    v[k] = (y < H && px < W && f < rowf) ? (xr[(size_t)px * 3 + cs] - mc) / sc : 0.f;
+  }
+  float* orow = out + (size_t)row * rowf;
+  if (VEC) {
+    *reinterpret_cast<float4*>(orow + f0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (f0 + k < rowf) orow[f0 + k] = v[k];
+  }
+}
+
 }  // namespace
 }  // namespace d2mi
 
 using namespace d2mi;
+
+extern "C" int d2mi_preprocess_images(const float* x, const float* mean, const float* stdv, int N,
+                                      int H, int W, int OHp, int OWp, int flip, float* out,
+                                      void* stream) {
+  D2MI_REQUIRE(N > 0 && H > 0 && W > 0 && OHp >= H && OWp >= W, "bad preprocess shape");
+  D2MI_REQUIRE(x && mean && stdv && out && x != out, "preprocess: null or aliased operand");
+  D2MI_REQUIRE((long long)N * OHp < 65536 && (long long)OWp * 3 < (1LL << 30),
+               "preprocess: too many rows or a row too long");
+  const int rowf = OWp * 3;
+  const dim3 grid((unsigned)((rowf / 4 + 1 + 255) / 256), (unsigned)(N * OHp));
+  const bool vec = rowf % 4 == 0 && ((uintptr_t)out & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(preprocess_kernel<true>, grid, dim3(256), 0, as_stream(stream), x, mean,
+                       stdv, H, W, OHp, OWp, flip ? 1 : 0, out);
+  else
+    hipLaunchKernelGGL(preprocess_kernel<false>, grid, dim3(256), 0, as_stream(stream), x, mean,
+                       stdv, H, W, OHp, OWp, flip ? 1 : 0, out);
+  D2MI_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int d2mi_stem_conv(const float* x, const uint16_t* w3, int N, int H, int W, float* y,
                               void* stream) {

@@ -1249,6 +1249,31 @@ def stem_conv(x, w3):
     return y
 
 
+# Device images preprocessed by d2mi_preprocess_images (False: torch's
+# subtract / divide / flip / pad, five launches; tests compare;
+# D2MI_FUSED_PREPROCESS=0 for a bench A/B).
+FUSED_PREPROCESS = os.environ.get("D2MI_FUSED_PREPROCESS", "1") != "0"
+
+
+def preprocess_images(x, mean, std, flip, size_divisibility=0):
+    """d2mi_preprocess_images: (x - mean) / std, the BGR channel flip and the
+    zero pad to size_divisibility in one pass (rcnn.py:146-157 +
+    image_list.py:89-100); x [N, H, W, 3] NHWC f32 -> [N, Hp, Wp, 3]."""
+    x = _f32c(x)
+    mean, std = _f32c(mean), _f32c(std)
+    _C.require_device(x, mean, std)
+    N, H, W, C = x.shape
+    if C != 3 or mean.numel() != 3 or std.numel() != 3:
+        raise ValueError(f"preprocess takes 3 channels and 3 means / stds, got {tuple(x.shape)}")
+    s = int(size_divisibility)
+    Hp, Wp = (H + (-H) % s, W + (-W) % s) if s > 0 else (H, W)
+    out = torch.empty((N, Hp, Wp, 3), dtype=torch.float32, device=x.device)
+    rc = _C.lib().d2mi_preprocess_images(_C.ptr(x), _C.ptr(mean), _C.ptr(std), N, H, W, Hp, Wp,
+                                         int(bool(flip)), _C.ptr(out), _C.stream_of(x.device))
+    _C.check(rc, "d2mi_preprocess_images")
+    return out
+
+
 def stem_pool(y, shift=None):
     """relu(y + shift) -> zero pad 1 -> 3x3 / 2 VALID max pool, NHWC
     (d2mi_stem_pool): the ResNet stem tail in one pass (no gradient)."""

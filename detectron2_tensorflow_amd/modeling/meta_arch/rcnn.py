@@ -37,7 +37,15 @@ class _Preprocess:
         self.input_format = cfg.MODEL.INPUT_FORMAT
 
     def preprocess_image(self, batched_inputs):
-        images = (batched_inputs["image"] - self.pixel_mean) / self.pixel_std
+        from ...layers import ops
+        x = batched_inputs["image"]
+        if x.is_cuda and ops.FUSED_PREPROCESS and x.dim() == 4 and x.shape[-1] == 3:
+            # one launch: normalise, flip, pad (d2mi_preprocess_images)
+            images = ops.preprocess_images(x, self.pixel_mean, self.pixel_std,
+                                           self.input_format == "BGR", self.neck.size_divisibility)
+            shapes = batched_inputs["image_shape"].to(device=images.device, dtype=torch.int32)
+            return ImageList.from_tensors(images, shapes, 0)
+        images = (x - self.pixel_mean) / self.pixel_std
         if self.input_format == "BGR":
             images = images.flip(-1)
         shapes = batched_inputs["image_shape"].to(device=images.device, dtype=torch.int32)

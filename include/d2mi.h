@@ -788,6 +788,14 @@ int d2mi_stem_pool(const float* y, const float* shift, int N, int H, int W, int 
  * frozen stem. */
 int d2mi_stem_conv(const float* x, const uint16_t* w3, int N, int H, int W, float* y,
                    void* stream);
+/* The preprocessing ahead of it (lib/modeling/meta_arch/rcnn.py:146-157
+ * preprocess_image + structures/image_list.py:89-100 with pad value 0):
+ * x [N,H,W,3] NHWC f32 0-255 RGB -> out [N,OHp,OWp,3], out = (x - mean[c]) /
+ * std[c] (mean / std: 3 device floats), channels reversed when flip (BGR
+ * input format), zeros at rows >= H and columns >= W.  One launch; the same
+ * IEEE subtract and divide per value as the unfused form. */
+int d2mi_preprocess_images(const float* x, const float* mean, const float* stdv, int N, int H,
+                           int W, int OHp, int OWp, int flip, float* out, void* stream);
 
 /* ------------------------------------------------ resampling gradients
  * d2mi_upsample2x_grad: adjoint of the FPN top-down nearest 2x upsample

@@ -1567,6 +1567,36 @@ def test_stem_conv_mfma_vs_float64(dev, shape):
     np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5 * scale)
 
 
+@pytest.mark.parametrize("shape,div,flip", [((2, 37, 45), 32, True), ((1, 29, 30), 0, False),
+                                            ((3, 64, 64), 32, True), ((2, 800, 1333), 32, True)])
+def test_preprocess_images_bit_exact(dev, shape, div, flip):
+    """d2mi_preprocess_images (normalise, BGR flip, zero pad to the size
+    divisibility in one launch) vs the reference's three steps in float32 on
+    the CPU (rcnn.py:146-157, image_list.py:89-100; the form of
+    oracle/cpu_pipeline.py) -- bit-identical, odd sizes (partial float4 rows,
+    no pad, pad on both axes) and the bench geometry, and vs torch's own
+    GPU launches of the same steps."""
+    N, H, W = shape
+    g = torch.Generator().manual_seed(H * W + N)
+    x = torch.rand(N, H, W, 3, generator=g) * 255.0
+    mean = torch.tensor([123.675, 116.28, 103.53])
+    std = torch.tensor([58.395, 57.12, 57.375])
+    ref = (x - mean) / std
+    if flip:
+        ref = ref.flip(-1)
+    if div:
+        ref = torch.nn.functional.pad(ref, (0, 0, 0, (-W) % div, 0, (-H) % div))
+    got = ops().preprocess_images(x.to(dev), mean.to(dev), std.to(dev), flip, div)
+    assert got.shape == ref.shape
+    assert torch.equal(got.cpu(), ref)
+    # the GPU torch form the fused op replaces: the same bits
+    t = (x.to(dev) - mean.to(dev)) / std.to(dev)
+    t = t.flip(-1) if flip else t
+    if div:
+        t = torch.nn.functional.pad(t, (0, 0, 0, (-W) % div, 0, (-H) % div))
+    assert torch.equal(got, t)
+
+
 def test_stem_mfma_conv_matches_miopen_stem(dev):
     from detectron2_tensorflow_amd.modeling.backbone.resnet import Stem, resnet_arg_scope
     torch.manual_seed(0)
