@@ -136,6 +136,8 @@ _SIGS = {
     "d2mi_stem_pool": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "d2mi_stem_conv": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "d2mi_preprocess_images": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_roi_gt_classes": (c_int, [P, P, P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "d2mi_roi_sample_take": (c_int, [P, P, P, P, P, P] + [c_int] * 6 + [P] * 13),
     "d2mi_rpn_loss_blocks": (c_int, []),
     "d2mi_rpn_loss_fwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P]),
     "d2mi_rpn_loss_bwd": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_float, P, P, P,

@@ -543,6 +543,74 @@ def subsample(labels, num_samples, num_pos, bg_label, seed, order_slots=0):
     return pos, neg
 
 
+# The ROI heads' label / take / mask-prep glue on d2mi_roi_gt_classes and
+# d2mi_roi_sample_take (False: torch's gathers, selects, argsort; tests compare;
+# D2MI_FUSED_SAMPLE_TAKE=0 for a bench A/B).
+FUSED_SAMPLE_TAKE = os.environ.get("D2MI_FUSED_SAMPLE_TAKE", "1") != "0"
+
+
+def roi_gt_classes(labels, matches, gt_classes, pvalid, num_classes):
+    """d2mi_roi_gt_classes: the training class of every proposal, [N, M] int64
+    (roi_heads.py:160-216): the matched GT class for label 1, num_classes
+    (background) for 0, -1 for ignored rows and invalid proposal slots."""
+    _C.require_device(labels, matches, gt_classes, pvalid)
+    if labels.dtype is not torch.int64 or matches.dtype is not torch.int64:
+        raise ValueError("roi_gt_classes: labels / matches must be int64")
+    labels, matches = labels.contiguous(), matches.contiguous()
+    if gt_classes.dtype not in (torch.int32, torch.int64):
+        gt_classes = gt_classes.to(torch.int64)
+    gt_classes = gt_classes.contiguous()
+    pv = pvalid.to(torch.bool).contiguous()
+    N, M = labels.shape
+    G = gt_classes.shape[1]
+    out = torch.empty((N, M), dtype=torch.int64, device=labels.device)
+    rc = _C.lib().d2mi_roi_gt_classes(_C.ptr(labels), _C.ptr(matches), _C.ptr(gt_classes),
+                                      int(gt_classes.dtype is torch.int64), _C.ptr(pv), N, M, G,
+                                      int(num_classes), _C.ptr(out), _C.stream_of(labels.device))
+    _C.check(rc, "d2mi_roi_gt_classes")
+    return out
+
+
+def roi_sample_take(order, valid, boxes, gt_classes, matches, gt_boxes, num_classes, mask_slots):
+    """d2mi_roi_sample_take: the sampled dict of label_and_sample_proposals
+    (boxes, gt_classes, gt_index, gt_boxes [N, S(, 4)]) and, mask_slots = F >
+    0, the mask branch's inputs over the first F slots per image in stable
+    foreground-first order: ((boxes, classes, fg, image, mask index, gt boxes),
+    fg [N*F] in slot order, count [1] int64)."""
+    _C.require_device(order, valid, boxes, gt_classes, matches, gt_boxes)
+    order, valid = order.contiguous(), valid.to(torch.bool).contiguous()
+    boxes, gt_boxes = _f32c(boxes), _f32c(gt_boxes)
+    gt_classes, matches = gt_classes.contiguous(), matches.contiguous()
+    N, S = order.shape
+    M, G, F = boxes.shape[1], gt_boxes.shape[1], int(mask_slots)
+    dev = order.device
+    s_boxes = torch.empty((N, S, 4), dtype=torch.float32, device=dev)
+    s_cls = torch.empty((N, S), dtype=torch.int64, device=dev)
+    s_gidx = torch.empty((N, S), dtype=torch.int64, device=dev)
+    s_gtb = torch.empty((N, S, 4), dtype=torch.float32, device=dev)
+    R = N * F
+    m = None
+    if F:
+        m = (torch.empty((R, 4), dtype=torch.float32, device=dev),
+             torch.empty((R,), dtype=torch.int64, device=dev),
+             torch.empty((R,), dtype=torch.bool, device=dev),
+             torch.empty((R,), dtype=torch.int32, device=dev),
+             torch.empty((R,), dtype=torch.int64, device=dev),
+             torch.empty((R, 4), dtype=torch.float32, device=dev),
+             torch.empty((R,), dtype=torch.bool, device=dev),
+             torch.empty((1,), dtype=torch.int64, device=dev))
+    mp = [_C.ptr(t) for t in m] if m else [None] * 8
+    rc = _C.lib().d2mi_roi_sample_take(_C.ptr(order), _C.ptr(valid), _C.ptr(boxes),
+                                       _C.ptr(gt_classes), _C.ptr(matches), _C.ptr(gt_boxes), N,
+                                       M, S, G, F, int(num_classes), _C.ptr(s_boxes),
+                                       _C.ptr(s_cls), _C.ptr(s_gidx), _C.ptr(s_gtb), *mp,
+                                       _C.stream_of(dev))
+    _C.check(rc, "d2mi_roi_sample_take")
+    sampled = {"boxes": s_boxes, "gt_classes": s_cls, "gt_index": s_gidx, "gt_boxes": s_gtb,
+               "is_valid": valid}
+    return sampled, ((m[:6], m[6], m[7]) if m else None)
+
+
 # ------------------------------------------------------------ anchors/deltas
 def grid_anchors(H, W, stride, cell_anchors, device):
     """DefaultAnchorGenerator.grid_anchors for one level -> [H*W*A, 4]."""

@@ -9,7 +9,7 @@ values the reference's SparseBoxList.to_dense produces.
 """
 import torch
 
-from ...layers import ShapeSpec
+from ...layers import ShapeSpec, ops
 from ...structures import BoxList
 from ...utils import capture, host_sync
 from ...utils.registry import Registry
@@ -101,12 +101,26 @@ class ROIHeads(Layer):
         matches, labels = match_boxes(self.proposal_matcher, gt_boxes, gvalid, boxes,
                                       crowd=crowd, difficult=difficult)
         K = self.num_classes
+        S = self.batch_size_per_image
+        if boxes.is_cuda and FUSED_ORDER and ops.FUSED_SAMPLE_TAKE:
+            # two launches for the glue (d2mi_roi_gt_classes, d2mi_roi_sample_take),
+            # the mask branch's fg-first inputs and foreground count included
+            gt_classes = ops.roi_gt_classes(labels, matches, targets["gt_classes"], pvalid, K)
+            _, _, order, valid = subsample_labels(gt_classes, S, self.positive_sample_fraction, K,
+                                                  order_slots=S)
+            F_ = (int(S * self.positive_sample_fraction)
+                  if getattr(self, "mask_on", False) and getattr(self, "mask_compact_rows", False)
+                  else 0)
+            sampled, mprep = ops.roi_sample_take(order, valid, boxes, gt_classes, matches,
+                                                 gt_boxes, K, F_)
+            if mprep is not None:
+                sampled["_mask_prep"] = mprep
+            return sampled
         gcls = torch.gather(targets["gt_classes"].long(), 1, matches)
         # label 1 -> the matched GT class, 0 -> background K, -1 -> ignored;
         # invalid proposal slots -> -1
         gt_classes = torch.where(labels == 1, gcls, torch.where(labels == 0, K, labels))
         gt_classes = torch.where(pvalid, gt_classes, -1)
-        S = self.batch_size_per_image
         if boxes.is_cuda and FUSED_ORDER:
             # fused: the sampled rows come back in fg-first, index order
             _, _, order, valid = subsample_labels(gt_classes, S, self.positive_sample_fraction, K,
@@ -138,10 +152,10 @@ class DeferredMaskLoss:
     that row count (``compute(rows)``, run once per distinct row count at
     capture time).  The eager trainer never sees one (defer_mask_loss False)."""
 
-    def __init__(self, heads, feats, sampled, targets, share, fg, prep=None):
+    def __init__(self, heads, feats, sampled, targets, share, fg, prep=None, count=None):
         self.heads, self.feats, self.sampled, self.targets = heads, feats, sampled, targets
         self.share, self.fg, self.prep = share, fg, prep
-        self.count = fg.sum()
+        self.count = fg.sum() if count is None else count
         self.slots = fg.numel()
 
     def rows_for(self, nfg):
@@ -210,20 +224,29 @@ class StandardROIHeads(ROIHeads):
             # the mask branch's foreground count is read while the box branch
             # is enqueued (the device never idles at the read)
             pending = None
-            fg = self._mask_fg(sampled) if self.mask_on else None  # (once per step)
+            # (d2mi_roi_sample_take: the mask branch's fg-first inputs, fg and
+            # the foreground count made with the sampled rows)
+            fused = sampled.pop("_mask_prep", None)
+            fg = (fused[1] if fused is not None
+                  else self._mask_fg(sampled) if self.mask_on else None)  # (once per step)
+            count = fused[2] if fused is not None else None
             defer = self.mask_on and self.mask_compact_rows and self.defer_mask_loss
             prep = None
             if self.mask_on and self.mask_compact_rows:
                 if not defer:
-                    pending = host_sync.start_read(fg.sum())
+                    pending = host_sync.start_read(count if count is not None else fg.sum())
                 # (deferred too, r5: in a replayed step these small gathers are
                 # issued inside graph A, under the box branch's kernels, not at
                 # graph B's head where the host's per-node submission outran them)
-                prep = self._mask_prep(sampled, targets, fg) if self.MASK_PREP_EARLY else None
+                if fused is not None:
+                    gm = targets["gt_masks"]
+                    prep = (fused[0], gm.reshape(gm.shape[0] * gm.shape[1], *gm.shape[2:]), fg)
+                elif self.MASK_PREP_EARLY:
+                    prep = self._mask_prep(sampled, targets, fg)
             losses = self._box_losses(feats, sampled, share)
             if defer:
                 losses["loss_mask"] = DeferredMaskLoss(self, feats, sampled, targets, share, fg,
-                                                       prep)
+                                                       prep, count)
             elif self.mask_on:
                 losses["loss_mask"] = self._mask_loss(feats, sampled, targets, share, pending, fg,
                                                       prep=prep)

@@ -797,6 +797,32 @@ int d2mi_stem_conv(const float* x, const uint16_t* w3, int N, int H, int W, floa
 int d2mi_preprocess_images(const float* x, const float* mean, const float* stdv, int N, int H,
                            int W, int OHp, int OWp, int flip, float* out, void* stream);
 
+/* ------------------------------------------------ ROI-head sampling glue
+ * (lib/modeling/roi_heads/roi_heads.py:100-232 label_and_sample_proposals,
+ * :35-62 select_foreground_proposals)
+ * d2mi_roi_gt_classes: out [N,M] int64 = -1 where !pvalid, else the matched
+ * GT class gt_cls[n][matches] (gt_cls [N,G], int64 when gt_cls_64 else
+ * int32) for label 1, K (background) for label 0, the label (-1) otherwise;
+ * labels / matches [N,M] int64 (d2mi_match_boxes), pvalid [N,M] bool.
+ * d2mi_roi_sample_take: the sampled slots in the sampler's order (order [N,S]
+ * int64, d2mi_subsample): s_boxes [N,S,4] = boxes[n][order], s_cls =
+ * gt_classes[n][order], s_gidx = matches[n][order], s_gtb [N,S,4] =
+ * gt_boxes[n][s_gidx]; and (F > 0) the mask branch's rows over the first F
+ * slots of each image (R = N*F rows, row i = slot (i / F, i % F)): fg_all[i]
+ * = valid && s_cls < K, count[0] = the number of foreground rows, and
+ * m_boxes / m_cls / m_fg / m_img (the image, int32) / m_mind (s_gidx + n*G) /
+ * m_gtb [R(,4)] in stable foreground-first order.  One workgroup; box arrays
+ * 16-byte aligned. */
+int d2mi_roi_gt_classes(const int64_t* labels, const int64_t* matches, const void* gt_cls,
+                        int gt_cls_64, const uint8_t* pvalid, int N, int M, int G, int K,
+                        int64_t* out, void* stream);
+int d2mi_roi_sample_take(const int64_t* order, const uint8_t* valid, const float* boxes,
+                         const int64_t* gt_classes, const int64_t* matches, const float* gt_boxes,
+                         int N, int M, int S, int G, int F, int K, float* s_boxes, int64_t* s_cls,
+                         int64_t* s_gidx, float* s_gtb, float* m_boxes, int64_t* m_cls,
+                         uint8_t* m_fg, int32_t* m_img, int64_t* m_mind, float* m_gtb,
+                         uint8_t* fg_all, int64_t* count, void* stream);
+
 /* ------------------------------------------------ resampling gradients
  * d2mi_upsample2x_grad: adjoint of the FPN top-down nearest 2x upsample
  * (lib/modeling/backbone/fpn.py:138-149): gy [N,OH,OW,C] -> gtd

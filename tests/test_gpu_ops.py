@@ -1692,3 +1692,76 @@ def test_fused_subsample_pairwise_co_inclusion(dev):
     assert np.all(np.abs(off - p2) < 5 * sd), (off.min(), off.max(), p2)
     near = np.array([co[i, i + 1] for i in range(n - 1)])
     assert abs(near.mean() - p2) < 5 * sd / math.sqrt(n - 1) + 1e-3, (near.mean(), p2)
+
+
+def _mask_rcnn_cfg():
+    from detectron2_tensorflow_amd.config import get_cfg
+    cfg = get_cfg()
+    cfg.merge_from_file(os.path.join(os.path.dirname(__file__), "..", "configs",
+                                     "COCO-InstanceSegmentation", "mask_rcnn_R_50_FPN_1x.yaml"))
+    return cfg
+
+
+@pytest.mark.parametrize("case", ["mixed", "empty_gt_image", "few_proposals"])
+def test_roi_sample_take_matches_torch_glue(dev, case):
+    """d2mi_roi_gt_classes + d2mi_roi_sample_take (label_and_sample_proposals'
+    glue and the mask branch's fg-first inputs, roi_heads.py:100-232 / :35-62)
+    vs the torch form of the same steps on the same sampler draw: every
+    sampled field, the six fg-first mask inputs, the foreground flags and the
+    count equal (pure data movement); with crowd / difficult GT, invalid
+    proposal slots, an image with no valid GT, and fewer proposals than slots."""
+    from detectron2_tensorflow_amd.layers import ShapeSpec
+    from detectron2_tensorflow_amd.modeling.roi_heads.roi_heads import StandardROIHeads
+    from detectron2_tensorflow_amd.structures import BoxList
+    cfg = _mask_rcnn_cfg()
+    heads = StandardROIHeads(cfg, {f"p{i}": ShapeSpec(channels=256, stride=2 ** i)
+                                   for i in range(2, 6)}).to(dev)
+    rng = np.random.default_rng({"mixed": 1, "empty_gt_image": 2, "few_proposals": 3}[case])
+    N, G = 2, 7
+    P = 300 if case == "few_proposals" else 1000
+    gt = np.stack([rand_boxes(rng, G, 800, 1333) for _ in range(N)])
+    props = np.stack([rand_boxes(rng, P, 800, 1333) for _ in range(N)])
+    near = rng.integers(0, G, (N, P // 3))
+    props[:, :P // 3] = (np.take_along_axis(gt, near[..., None], 1)
+                         + rng.normal(0, 6, (N, P // 3, 4))).astype(F32)
+    pvalid = np.ones((N, P), bool)
+    pvalid[1, P - 120:] = False
+    gvalid = np.ones((N, G), bool)
+    gvalid[0, 5:] = False
+    if case == "empty_gt_image":
+        gvalid[1] = False
+    crowd = np.zeros((N, G), bool)
+    crowd[0, 2] = True
+    diff = np.zeros((N, G), bool)
+    diff[1, 3] = True
+    pl = BoxList(torch.from_numpy(props).to(dev))
+    pl.add_field("is_valid", torch.from_numpy(pvalid).to(dev))
+    targets = {"gt_boxes": torch.from_numpy(gt).to(dev),
+               # (int32 GT classes in one case: the kernel reads either width)
+               "gt_classes": torch.from_numpy(rng.integers(0, 80, (N, G)).astype(
+                   np.int32 if case == "few_proposals" else np.int64)).to(dev),
+               "is_valid": torch.from_numpy(gvalid).to(dev),
+               "gt_is_crowd": torch.from_numpy(crowd).to(dev),
+               "gt_difficult": torch.from_numpy(diff).to(dev),
+               "gt_masks": torch.rand(N, G, 56, 56, device=dev)}
+    from detectron2_tensorflow_amd.layers import ops as lops
+    try:
+        lops.FUSED_SAMPLE_TAKE = False
+        torch.manual_seed(11)
+        ref = heads.label_and_sample_proposals(pl, targets)
+        lops.FUSED_SAMPLE_TAKE = True
+        torch.manual_seed(11)
+        got = heads.label_and_sample_proposals(pl, targets)
+    finally:
+        lops.FUSED_SAMPLE_TAKE = True
+    fused = got.pop("_mask_prep")
+    assert sorted(got) == sorted(ref)
+    for k in ref:
+        assert got[k].dtype == ref[k].dtype and torch.equal(got[k], ref[k]), k
+    ts, _, fg = heads._mask_prep(ref, targets)
+    for a, b in zip(fused[0], ts):
+        assert a.dtype == b.dtype and torch.equal(a, b)
+    assert torch.equal(fused[1], fg)
+    assert int(fused[2].item()) == int(fg.sum().item())
+    if case == "empty_gt_image":
+        assert not bool(fg[fg.numel() // 2:].any())
