@@ -37,12 +37,12 @@ def main():
             "aten::flip", "aten::sum", "aten::eq", "aten::sort", "aten::random_",
             "aten::constant_pad_nd", "aten::masked_fill_", "aten::index_put_")
     ev = [e for e in prof.key_averages(group_by_input_shape=True, group_by_stack_n=6)
-          if e.key in keep and getattr(e, "device_time_total", e.cuda_time_total) > 0]
-    ev.sort(key=lambda e: -getattr(e, "device_time_total", e.cuda_time_total))
-    total = sum(getattr(e, "device_time_total", e.cuda_time_total) for e in ev)
+          if e.key in keep and e.device_time_total > 0]
+    ev.sort(key=lambda e: -e.device_time_total)
+    total = sum(e.device_time_total for e in ev)
     print(f"torch ops with device time in one eager step: {total / 1e3:.1f} ms")
     for e in ev[:40]:
-        t = getattr(e, "device_time_total", e.cuda_time_total)
+        t = e.device_time_total
         print(f"\n{t:8.1f} us  x{e.count:3d}  {e.key}  {e.input_shapes}")
         for fr in (e.stack or [])[:6]:
             print("      ", fr)
