@@ -224,6 +224,16 @@ class _ConvMFMAFn(torch.autograd.Function):
         ctx.res_grad_to = res_grad_to if residual is not None else None
         ctx.grad_from = grad_from
         ctx.pair_grad = pair_grad
+        # FPN top-down hand-off (modeling/necks/fpn.py TD_HANDOFF): the merged
+        # map's output conv (pair_grad {"td": True}) and the finer lateral that
+        # reads it as its top-down input -- both MFMA convs, registered here
+        if pair_grad is not None and pair_grad.get("td"):
+            pair_grad["mfma"] = True
+        tdp = getattr(topdown, "_d2mi_td_pair", None) if topdown is not None else None
+        ctx.td_pair = (tdp if tdp is not None and tdp.get("mfma") and topdown.requires_grad
+                       else None)
+        if ctx.td_pair is not None:
+            ctx.td_pair["lat_mfma"] = True
         ctx.join = join
         ctx.wacc = wacc  # a weight shared by several calls: _wgrad_shared
         # the producer's ReLU tag, used if a join is registered by backward time
@@ -248,6 +258,16 @@ class _ConvMFMAFn(torch.autograd.Function):
             N, OH, OW, C = gy.shape
             g = F.pad(gy, (0, 0, 0, OW % 2, 0, OH % 2))
             gtd = g.reshape(N, (OH + 1) // 2, 2, (OW + 1) // 2, 2, C).sum((2, 4))
+        if gtd is not None and ctx.td_pair is not None and ctx.needs_input_grad[7]:
+            # the merged map's other reader is its output conv: first of the
+            # two leaves its gradient, the second adds it (the output conv in
+            # its dgrad epilogue) -- autograd's sum of the two, no add launch
+            other = ctx.td_pair.pop("g", None)
+            if other is None:
+                handoff.deposit(ctx.td_pair, "g", gtd, "FPN top-down")
+                gtd = None
+            else:
+                gtd = gtd + other
         gres = gy if has_res and ctx.needs_input_grad[8] else None
         if gres is not None and ctx.res_grad_to is not None:
             handoff.deposit(ctx.res_grad_to, "g", gres, "residual")  # taken by the conv reading it
@@ -269,6 +289,8 @@ class _ConvMFMAFn(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             add = ctx.grad_from.pop("g", None) if ctx.grad_from is not None else None
             pair = ctx.pair_grad
+            if pair is not None and pair.get("td") and not pair.get("lat_mfma"):
+                pair = None  # (an FPN output conv whose map no MFMA lateral reads)
             deposit = False
             deferred = None
             gated = ctx.in_info is not None and _gate_eligible(w.shape, stride, pb, pe)

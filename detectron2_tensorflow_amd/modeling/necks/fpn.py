@@ -109,12 +109,26 @@ class FPN(Layer):
             return None  # a third reader (P6 from C5)
         return getattr(feats, "_d2mi_pair", None)
 
+    # A merged map read by its output conv and, as the top-down input, by the
+    # next finer lateral: the two backwards hand its gradient over (the second
+    # adds it; the output conv inside its dgrad epilogue) instead of an
+    # autograd add of two full maps (layers/convolutional.py ctx.td_pair).
+    TD_HANDOFF = os.environ.get("D2MI_FPN_TD", "1") != "0"
+
+    def _out(self, out, prev, fused):
+        if not (fused and self.TD_HANDOFF and torch.is_grad_enabled() and prev.requires_grad):
+            return out(prev)
+        td = {"td": True}
+        y = out(prev, pair_grad=td)
+        prev._d2mi_td_pair = td  # (read by the finer lateral's forward)
+        return y
+
     def call(self, bottom_up_features):
         names = self.in_features[::-1]
         x = [bottom_up_features[f] for f in names]
-        prev = self.lateral_convs[0](x[0], join=self._join_of(names[0], x[0]))
-        results = [self.output_convs[0](prev)]
         fused = self.fuse_type == "sum" and self.norm == ""
+        prev = self.lateral_convs[0](x[0], join=self._join_of(names[0], x[0]))
+        results = [self._out(self.output_convs[0], prev, fused)]
         for name, feats, lat, out in zip(names[1:], x[1:], self.lateral_convs[1:],
                                          self.output_convs[1:]):
             if fused:
@@ -124,7 +138,7 @@ class FPN(Layer):
                 prev = lat(feats) + upsample(prev, 2)
                 if self.fuse_type == "avg":
                     prev = prev / 2
-            results.insert(0, out(prev))
+            results.insert(0, self._out(out, prev, fused))
         if self.top_block is not None:
             src = bottom_up_features.get(self.top_block.in_feature)
             if src is None:

@@ -610,6 +610,50 @@ def test_fpn_join_engages_and_matches_plain_step(dev, monkeypatch):
         assert torch.equal(grads[True][n], grads[False][n]), n
 
 
+def test_fpn_topdown_handoff_engages_and_matches_plain_step(dev, monkeypatch):
+    """The FPN merged maps P5..P3 (inner) are read by their output conv and by
+    the next finer lateral's fused top-down add: with FPN.TD_HANDOFF the two
+    backwards hand the gradient over (the output conv adds it in its dgrad
+    epilogue) -- engaged at three levels, and the step's gradients equal those
+    of the autograd add (TD_HANDOFF False), bit for bit."""
+    from detectron2_tensorflow_amd.layers import convolutional as conv_mod
+    from detectron2_tensorflow_amd.modeling import build_model
+    from detectron2_tensorflow_amd.modeling.necks.fpn import FPN
+    from detectron2_tensorflow_amd.utils.synthetic import (calibrate_rcnn_scores,
+                                                           synthetic_train_batch)
+    cfg = _cfg(True)
+    torch.manual_seed(0)
+    model = build_model(cfg).to(dev).train()
+    batch = synthetic_train_batch(2, 256, 320, 5, dev)
+    calibrate_rcnn_scores(model, batch)
+    deposits = []
+    real = conv_mod.handoff.deposit
+
+    def counted(d, key, value, what):
+        deposits.append(what)
+        return real(d, key, value, what)
+
+    monkeypatch.setattr(conv_mod.handoff, "deposit", counted)
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    grads = {}
+    for td in (True, False):
+        monkeypatch.setattr(FPN, "TD_HANDOFF", td)
+        model.zero_grad(set_to_none=True)
+        deposits.clear()
+        torch.manual_seed(1)  # the same subsampling draws in both passes
+        losses = model(batch)
+        sum(losses.values()).backward()
+        # (one deposit per hand-off level, by whichever of the two runs first)
+        n_td = sum(1 for w in deposits if w in ("FPN top-down", "pair"))
+        grads[td] = ({n: p.grad.clone() for n, p in model.named_parameters()
+                      if p.grad is not None}, n_td)
+    assert grads[True][1] - grads[False][1] == 3, (grads[True][1], grads[False][1])
+    g1, g0 = grads[True][0], grads[False][0]
+    assert g1.keys() == g0.keys() and g1
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n
+
+
 @pytest.mark.parametrize("one_launch", [True, False])
 def test_rpn_head_level_weight_grad_accumulator_is_exact(dev, monkeypatch, one_launch):
     """The RPN head's fused 1x1 and its shared 3x3 accumulate their weight /
