@@ -70,7 +70,10 @@ def parse():
     # (30: the one eager step that carries the per-launch HIP events -- the
     # live roofline -- is one of the timed steps; among 10 it weighed ~1 % of
     # the line, among 30 a third of that; 30 steps still take < 1 s)
-    p.add_argument("--steps", type=int, default=30)
+    # (60: the one event-timed sample step -- eager, HIP events around every
+    # hot launch, ~6 ms more than a replay -- is 1/60 of the timed region;
+    # at 30 steps it cost the line 1.1 %, profiles/r6aw_sample_step_cost.txt)
+    p.add_argument("--steps", type=int, default=60)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--batch", type=int, default=2, help="images per GPU per step")
     p.add_argument("--model", default="mask_rcnn_R_50_FPN", choices=sorted(CONFIGS))

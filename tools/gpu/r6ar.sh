@@ -2,4 +2,4 @@
 # where (tools/torch_op_census.py: torch.profiler, stacks, device time)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u tools/torch_op_census.py > gpurun_out/r6ar_torch_op_census.txt 2>&1
+timeout -k 10 400 python -u tools/torch_op_census.py > gpurun_out/${CENSUS_OUT:-r6ar_torch_op_census.txt} 2>&1
