@@ -328,6 +328,53 @@ def test_nms_segmented_vs_oracle_with_ties(dev, thr, nms_scan):
         np.testing.assert_array_equal(k.cpu().numpy(), want_k)
 
 
+@pytest.mark.parametrize("thr", [0.5, 0.7, 0.3])
+def test_nms_iou_at_the_threshold_is_exact(dev, thr, nms_scan):
+    """Box pairs whose IoU is the threshold to within a few ulps -- exactly
+    equal (not suppressed: TF's test is IoU > thr), a few ulps either side,
+    and random shapes at the threshold up to their coordinates' rounding: the
+    float32 quotient's rounding decides every pair, and the kept sets equal
+    the oracle's.  (r6 measured a division-free form of this test -- a
+    reciprocal estimate outside a 2^-18 margin, exact by construction and
+    green here -- at no gain in the RetinaNet or training step,
+    profiles/r6ay_iou_fast_ab.txt, and did not keep it.)"""
+    rng = np.random.default_rng(int(thr * 100))
+    pairs = []
+    # IoU of [y, x, y + h, x + w] and [y, x + dx, y + h, x + w + dx] is
+    # (w - dx) / (w + dx): integer w = a m, dx = b m with (a - b) / (a + b) =
+    # thr hit the threshold's float exactly; the second box's x corners then
+    # move 0 .. 3 ulps either way (IoU a few ulps off the threshold)
+    a, b = {0.5: (3, 1), 0.7: (17, 3), 0.3: (13, 7)}[thr]
+    for _ in range(2000):
+        m = int(rng.integers(1, 12))
+        h, w, dx = F32(rng.integers(1, 200)), F32(a * m), F32(b * m)
+        y0, x0 = F32(rng.integers(0, 4000)), F32(rng.integers(0, 4000))
+        x1, x2 = F32(x0 + dx), F32(x0 + w + dx)
+        for _k in range(int(rng.integers(0, 4))):
+            step = np.inf if rng.integers(0, 2) else -np.inf
+            x1, x2 = np.nextafter(x1, F32(step)), np.nextafter(x2, F32(-step))
+        pairs.append([[y0, x0, y0 + h, x0 + w], [y0, x1, y0 + h, x2]])
+    # and random shapes at the threshold up to the coordinates' rounding
+    for _ in range(1000):
+        h, w = F32(rng.uniform(1, 200)), F32(rng.uniform(1, 200))
+        dx = F32(w * (1 - thr) / (1 + thr))
+        y0, x0 = F32(rng.uniform(0, 5000)), F32(rng.uniform(0, 5000))
+        pairs.append([[y0, x0, y0 + h, x0 + w], [y0, x0 + dx, y0 + h, x0 + w + dx]])
+    boxes = np.asarray(pairs, F32).reshape(-1, 4)
+    n = boxes.shape[0]
+    scores = np.linspace(1.0, 0.0, n, dtype=F32)
+    lens = [64, 1000, 2000, n - 3064]  # several segments, the same pairs order
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    want_k, want_n = oracle.nms_batched(boxes, scores, off, 2000, thr)
+    k, m = ops().nms_segments(torch.from_numpy(boxes).to(dev), torch.from_numpy(scores).to(dev),
+                              torch.from_numpy(off).to(dev), 2000, thr, seg_capacity=max(lens))
+    np.testing.assert_array_equal(m.cpu().numpy(), want_n)
+    np.testing.assert_array_equal(k.cpu().numpy(), want_k)
+    # the pairs do straddle the threshold: some second boxes kept, some not
+    kept = int(want_n.sum())
+    assert n // 2 < kept < n, kept
+
+
 @pytest.mark.parametrize("cap", [2000, 4096, 4160])
 def test_nms_suppression_chains_and_truncation(dev, cap, nms_scan):
     """Chains of boxes each overlapping the next above the threshold (the
