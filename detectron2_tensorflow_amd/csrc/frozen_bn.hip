@@ -328,6 +328,43 @@ __global__ __launch_bounds__(256) void fold_bn_bwd_many_kernel(
   const bool live = co < Cout;
   const int per = (rows + kRowChunks - 1) / kRowChunks;
   const int r0 = chunk * per, r1 = min(rows, r0 + per);
+  if (!e.ggamma) {
+    // no gamma gradient (FrozenBN: gamma is a constant): only gw = gw_eff *
+    // scale -- the sum of gw_eff * w (and so the read of w) is not needed;
+    // float4 rows where aligned, 16 threads per 64-channel row
+    if (!e.gw) return;
+    const bool al = ((reinterpret_cast<uintptr_t>(e.gw_eff) | reinterpret_cast<uintptr_t>(e.gw)) &
+                     15) == 0;
+    if (Cout % 4 == 0 && al) {
+      const int t = threadIdx.x, cq = t & 15, ri = t >> 4;
+      const int c4 = cot * 64 + 4 * cq;
+      if (c4 >= Cout) return;
+      float sc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float inv = bn_inv(e.var, e.eps, c4 + q);
+        sc[q] = e.gamma ? inv * e.gamma[c4 + q] : inv;
+      }
+#pragma unroll 4
+      for (int r = r0 + ri; r < r1; r += 16) {
+        const size_t o = (size_t)r * Cout + c4;
+        const float4 g = e.gw_eff ? *reinterpret_cast<const float4*>(e.gw_eff + o)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(e.gw + o) =
+            make_float4(g.x * sc[0], g.y * sc[1], g.z * sc[2], g.w * sc[3]);
+      }
+      return;
+    }
+    if (!live) return;
+    const float inv = bn_inv(e.var, e.eps, co);
+    const float scale = e.gamma ? inv * e.gamma[co] : inv;
+#pragma unroll 8
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const float g = e.gw_eff ? e.gw_eff[(size_t)r * Cout + co] : 0.f;
+      e.gw[(size_t)r * Cout + co] = g * scale;
+    }
+    return;
+  }
   float scale = 0.f;
   if (live) {
     const float inv = bn_inv(e.var, e.eps, co);
@@ -358,7 +395,8 @@ __global__ void fold_bn_bwd_many_finish_kernel(const d2mi_fold_entry* __restrict
   const int Cout = e.Cout, co = g - e.co_begin;
   const float* partial = ws + e.partial_offset;
   float gs = 0.f;
-  for (int k = 0; k < kRowChunks; ++k) gs += partial[(size_t)k * Cout + co];
+  if (e.ggamma)  // (the partials exist only then: fold_bn_bwd_many_kernel)
+    for (int k = 0; k < kRowChunks; ++k) gs += partial[(size_t)k * Cout + co];
   const float inv = bn_inv(e.var, e.eps, co);
   const float scale = e.gamma ? inv * e.gamma[co] : inv;
   const float gb = e.gb_eff ? e.gb_eff[co] : 0.f;

@@ -1040,11 +1040,14 @@ def test_fold_frozen_bn_forward_backward(dev, with_bias):
                                    atol=1e-3, err_msg=name)
 
 
-def test_fold_frozen_bn_many_bit_identical_to_per_conv(dev):
+@pytest.mark.parametrize("frozen_affine", [False, True])
+def test_fold_frozen_bn_many_bit_identical_to_per_conv(dev, frozen_affine):
     """d2mi_fold_frozen_bn_many / _bwd_many (one table-driven launch for every
     conv) give the per-conv fold's w_eff, b_eff, packed and all four
     gradients bit for bit -- mixed shapes (ci / co tails, 7x7 stem, Cout 2048),
-    entries with and without bias / packed / a gradient."""
+    entries with and without bias / packed / a gradient; frozen_affine: gamma
+    and beta constants (FrozenBN, the training step's case: the batched
+    backward then skips the gamma sums and the read of w, float4 rows)."""
     g = torch.Generator().manual_seed(11)
     shapes = [(7, 7, 3, 64), (1, 1, 64, 256), (3, 3, 60, 36), (1, 1, 1024, 2048), (3, 3, 128, 128),
               (1, 1, 256, 16)]
@@ -1057,7 +1060,8 @@ def test_fold_frozen_bn_many_bit_identical_to_per_conv(dev):
         grads.append((r(kh, kw, ci, co), r(co) if i != 4 else None))
 
     def run(batched):
-        leaves = [[t.to(dev).requires_grad_(k < 4) if t is not None else None
+        trainable = (0, 1) if frozen_affine else (0, 1, 2, 3)
+        leaves = [[t.to(dev).requires_grad_(k in trainable) if t is not None else None
                    for k, t in enumerate(ts)] for ts, _, _ in entries]
         if batched:
             outs = ops().fold_frozen_bn_many([(*lv, eps, pk) for lv, (_, eps, pk)
@@ -1081,7 +1085,7 @@ def test_fold_frozen_bn_many_bit_identical_to_per_conv(dev):
         assert (pa is None) == (pb is None) and (pa is None or torch.equal(pa, pb))
     for xa, xb in zip(la, lb):
         for ta, tb in zip(xa[:4], xb[:4]):
-            if ta is not None:
+            if ta is not None and ta.requires_grad:
                 assert torch.equal(ta.grad, tb.grad)
 
 
